@@ -1,0 +1,232 @@
+"""Generate golden vectors by importing the REFERENCE implementation (this container only).
+
+    cd /tmp && python /root/repo/tests/golden/make_golden.py        # writes tests/golden/*.npz
+
+Recipe: `import transformers` first, then stub `torchvision`/`torchvision.models` with empty
+modules (only the reference's resnet/mobilenet branches use them — never executed here), put
+`/root/reference` on sys.path, run from a scratch CWD (the reference's config import mkdirs ./outputs) with
+bytecode writing off.  VideoMAE weights cannot be fetched offline: a random-geometry `VideoMAEModel` is saved to
+a local directory and `video_backbone` points at it (the `"/" in vb` branch, `models.py:154`).  All parameters
+are then overwritten with `seeded.seeded_state_dict` so fixtures need not store weights.
+
+Each fixture stores: the config overrides (JSON), the state_dict key list with shapes, the inputs, and the
+reference's outputs / gradients (full tensors when small, per-parameter norms + sums when large).
+"""
+from __future__ import annotations
+
+import json
+import os
+import sys
+import tempfile
+import types
+
+sys.dont_write_bytecode = True
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, HERE)
+sys.path.insert(0, os.path.join(REPO, 'crossmodal-imu-video-ood-har_amd'))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import transformers  # noqa: E402,F401  (must precede the torchvision stub)
+
+tv = types.ModuleType('torchvision')
+tv.models = types.ModuleType('torchvision.models')
+sys.modules.setdefault('torchvision', tv)
+sys.modules.setdefault('torchvision.models', tv.models)
+sys.path.insert(0, '/root/reference')
+
+from seeded import seeded_input, seeded_state_dict  # noqa: E402
+from cmhar.config import Config  # noqa: E402
+
+SCRATCH = tempfile.mkdtemp(prefix='cmhar_golden_')
+os.chdir(SCRATCH)
+
+from src.models.models import CrossModalModel, IMUClassifier, IMUEncoder  # noqa: E402
+from src.models.losses import SigmoidContrastiveLoss  # noqa: E402
+from src.train.trainer import CrossModalTrainer  # noqa: E402
+from transformers import VideoMAEConfig, VideoMAEModel  # noqa: E402
+
+torch.set_num_threads(8)
+
+
+def make_cfg(overrides):
+    cfg = Config()
+    for sect, kv in overrides.items():
+        for k, v in kv.items():
+            setattr(getattr(cfg, sect), k, v)
+    return cfg
+
+
+def local_videomae(hidden, layers, heads, inter, image, frames, use_mean_pooling=True, patch=16):
+    d = tempfile.mkdtemp(prefix='videomae_', dir=SCRATCH)
+    m = VideoMAEModel(VideoMAEConfig(hidden_size=hidden, num_hidden_layers=layers, num_attention_heads=heads,
+                                     intermediate_size=inter, image_size=image, num_frames=frames,
+                                     use_mean_pooling=use_mean_pooling, patch_size=patch))
+    m.save_pretrained(d)
+    return d
+
+
+def sd_meta(sd):
+    keys = list(sd.keys())
+    return {'keys': json.dumps(keys), 'shapes': json.dumps([list(sd[k].shape) for k in keys])}
+
+
+def grads_of(module, full_limit=200_000):
+    out = {}
+    for n, p in module.named_parameters():
+        g = p.grad
+        if g is None:
+            out[f'gnone.{n}'] = np.array(1)
+            continue
+        if p.numel() <= full_limit:
+            out[f'grad.{n}'] = g.detach().numpy().copy()
+        else:
+            out[f'gnorm.{n}'] = np.array(g.detach().double().norm().item())
+            out[f'gsum.{n}'] = np.array(g.detach().double().sum().item())
+            out[f'gsample.{n}'] = g.detach().reshape(-1)[::997].numpy().copy()
+    return out
+
+
+def save(name, **arrays):
+    path = os.path.join(HERE, name + '.npz')
+    np.savez_compressed(path, **arrays)
+    print(f'wrote {path}  ({os.path.getsize(path) / 1024:.1f} KiB)')
+
+
+# ---------------------------------------------------------------------------------------------------------
+def g1_imu_encoder():
+    """IMUEncoder at the north-star IMU geometry (W=200 → 13 tokens), dropout 0; fwd + param grads."""
+    ov = {'data': {'imu_window_size': 200}, 'model': {'imu_dropout': 0.0}}
+    cfg = make_cfg(ov)
+    torch.manual_seed(0)
+    enc = IMUEncoder(cfg)
+    sd = seeded_state_dict(enc.state_dict(), seed=1)
+    enc.load_state_dict(sd, strict=True)
+    enc.train()
+    x = seeded_input(11, (4, 6, 200))
+    r = seeded_input(12, (4, 128))
+    cls, tok = enc(x)
+    ((cls * r).sum() + 0.1 * tok.pow(2).sum()).backward()
+    save('g1_imu_encoder', config=json.dumps(ov), seed=1, x=x.numpy(), r=r.numpy(), cls=cls.detach().numpy(),
+         tokens=tok.detach().numpy(), **sd_meta(sd), **grads_of(enc, full_limit=20_000))
+
+
+def tiny_overrides(vdir, imu_w=64):
+    return {'data': {'imu_window_size': imu_w, 'video_frames_per_window': 4, 'video_resize': (16, 16)},
+            'model': {'imu_d_model': 32, 'imu_nhead': 4, 'imu_num_layers': 2, 'imu_dropout': 0.0,
+                      'video_backbone': vdir, 'video_d_model': 48, 'projection_hidden_dim': 64,
+                      'projection_dim': 32, 'classifier_hidden_dims': [48, 24], 'num_classes': 7,
+                      'videomae_hidden_size': 64, 'videomae_num_layers': 2, 'videomae_num_heads': 4,
+                      'videomae_intermediate_size': 128, 'videomae_num_frames': 4, 'videomae_image_size': 16,
+                      'videomae_patch_size': 8},
+            'training': {'pretrain_lr': 1e-4, 'pretrain_weight_decay': 0.01, 'pretrain_epochs': 10,
+                         'pretrain_warmup_epochs': 5}}
+
+
+def g2_crossmodal_tiny():
+    """Whole CrossModalModel + SigmoidContrastiveLoss with a tiny VideoMAE; fwd, grads, 2 trainer steps."""
+    vdir = local_videomae(64, 2, 4, 128, 16, 4, patch=8)
+    ov = tiny_overrides(vdir)
+    cfg = make_cfg(ov)
+    torch.manual_seed(0)
+    model = CrossModalModel(cfg)
+    sd = seeded_state_dict(model.state_dict(), seed=2)
+    model.load_state_dict(sd, strict=True)
+    model.train()
+    B = 6
+    imu = seeded_input(21, (B, 6, 64))
+    video = seeded_input(22, (B, 4, 3, 16, 16))
+    loss_fn = SigmoidContrastiveLoss(learnable=True)
+    a, b = model(imu, video)
+    logits = (a @ b.T) * loss_fn.temperature.exp() + loss_fn.bias
+    loss = loss_fn(a, b)
+    loss.backward()
+    bn = {f'bn.{k}': v.numpy().copy() for k, v in model.state_dict().items() if 'running' in k or 'num_batches' in k}
+    out = dict(config=json.dumps({k: {kk: (list(vv) if isinstance(vv, tuple) else vv) for kk, vv in d.items()}
+                                  for k, d in ov.items()}),
+               seed=2, imu=imu.numpy(), video=video.numpy(), imu_proj=a.detach().numpy(),
+               video_proj=b.detach().numpy(), logits=logits.detach().numpy(), loss=np.array(loss.item()),
+               loss_grad_temperature=np.array(loss_fn.temperature.grad.item()),
+               loss_grad_bias=np.array(loss_fn.bias.grad.item()), **sd_meta(sd), **grads_of(model), **bn)
+    # Two CrossModalTrainer steps (trainer.py:130-144): AdamW lr=1e-5 at step 0 (LinearLR 0.1x), clip 1.0.
+    model2 = CrossModalModel(cfg)
+    model2.load_state_dict(sd, strict=True)
+    loss_fn2 = SigmoidContrastiveLoss(learnable=True)
+    trainer = CrossModalTrainer(model2, loss_fn2, cfg, device='cpu')
+    batches = [{'imu': imu, 'video': video},
+               {'imu': seeded_input(23, (B, 6, 64)), 'video': seeded_input(24, (B, 4, 3, 16, 16))}]
+    mean_loss = trainer.train_epoch(batches)
+    out['step_imu2'] = batches[1]['imu'].numpy()
+    out['step_video2'] = batches[1]['video'].numpy()
+    out['step_mean_loss'] = np.array(mean_loss)
+    for k, v in model2.state_dict().items():
+        out[f'after.{k}'] = v.detach().numpy().copy()
+    out['after_loss_temperature'] = np.array(loss_fn2.temperature.item())
+    save('g2_crossmodal_tiny', **out)
+
+
+def g3_siglip():
+    """SigmoidContrastiveLoss at B=32×256 (pins the all-pairs softplus degeneracy)."""
+    torch.manual_seed(0)
+    loss_fn = SigmoidContrastiveLoss(learnable=True)
+    a = torch.nn.functional.normalize(seeded_input(31, (32, 256)), dim=1).requires_grad_(True)
+    b = torch.nn.functional.normalize(seeded_input(32, (32, 256)), dim=1).requires_grad_(True)
+    loss = loss_fn(a, b)
+    loss.backward()
+    save('g3_siglip', a=a.detach().numpy(), b=b.detach().numpy(), loss=np.array(loss.item()),
+         grad_a=a.grad.numpy(), grad_b=b.grad.numpy(), grad_temperature=np.array(loss_fn.temperature.grad.item()),
+         grad_bias=np.array(loss_fn.bias.grad.item()))
+
+
+def g4_classifier():
+    """IMUClassifier (tiny IMU encoder) logits in train and eval mode + grads in train mode."""
+    vdir = local_videomae(64, 2, 4, 128, 16, 4, patch=8)
+    ov = tiny_overrides(vdir)
+    ov['model']['classifier_dropout'] = 0.0          # train-mode logits must be deterministic
+    cfg = make_cfg(ov)
+    torch.manual_seed(0)
+    enc = IMUEncoder(cfg)
+    clf = IMUClassifier(enc, cfg, freeze_encoder=False)
+    sd = seeded_state_dict(clf.state_dict(), seed=4)
+    clf.load_state_dict(sd, strict=True)
+    x = seeded_input(41, (8, 6, 64))
+    clf.train()
+    lt = clf(x)
+    lt.pow(2).mean().backward()
+    clf.eval()
+    with torch.no_grad():
+        le = clf(x)
+    save('g4_classifier', config=json.dumps({k: {kk: (list(vv) if isinstance(vv, tuple) else vv)
+                                                 for kk, vv in d.items()} for k, d in ov.items()}),
+         seed=4, x=x.numpy(), logits_train=lt.detach().numpy(), logits_eval=le.numpy(), **sd_meta(sd),
+         **grads_of(clf))
+
+
+def g5_videomae_base(frames=16, image=224, B=1):
+    """VideoMAE-B geometry (hidden 768, 12 layers) VideoEncoder forward at the metric's clip shape."""
+    vdir = local_videomae(768, 12, 12, 3072, image, frames)
+    ov = {'data': {'video_frames_per_window': frames, 'video_resize': (image, image)},
+          'model': {'video_backbone': vdir, 'imu_dropout': 0.0}}
+    cfg = make_cfg(ov)
+    from src.models.models import VideoEncoder
+    torch.manual_seed(0)
+    venc = VideoEncoder(cfg)
+    sd = seeded_state_dict(venc.state_dict(), seed=5)
+    venc.load_state_dict(sd, strict=True)
+    venc.eval()
+    video = seeded_input(51, (B, frames, 3, image, image))
+    with torch.no_grad():
+        hs = venc.backbone(pixel_values=video).last_hidden_state
+        feat = venc(video)
+    save(f'g5_videomae_base_{frames}x{image}', seed=5, video_seed=51, video_shape=np.array(video.shape),
+         feat=feat.numpy(), token0=hs[:, 0].numpy(), last_row=hs[:, -1].numpy(),
+         hs_mean=np.array(hs.double().mean().item()), hs_absmean=np.array(hs.double().abs().mean().item()),
+         **sd_meta(sd))
+
+
+if __name__ == '__main__':
+    which = sys.argv[1:] or ['g1', 'g2', 'g3', 'g4', 'g5']
+    for w in which:
+        {'g1': g1_imu_encoder, 'g2': g2_crossmodal_tiny, 'g3': g3_siglip, 'g4': g4_classifier,
+         'g5': lambda: g5_videomae_base(16, 224, 1)}[w]()
