@@ -1,0 +1,124 @@
+"""ctypes binding of the cmhar C ABI (include/cmhar.h) — the only compute path of this package.
+
+The library is built in-tree (`make -C crossmodal-imu-video-ood-har_amd`, or `__graft_entry__.build()`) as
+`cmhar/libcmhar.so`.  There is deliberately NO fallback: if the library is missing or a kernel rejects its
+arguments, the call raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get('CMHAR_LIB', os.path.join(_HERE, 'libcmhar.so'))
+
+F32, BF16 = 0, 1
+ACT_NONE, ACT_GELU, ACT_RELU, ACT_DGELU, ACT_DRELU = 0, 1, 2, 3, 4
+
+vp, i32, i64, f32, u64 = C.c_void_p, C.c_int, C.c_long, C.c_float, C.c_ulonglong
+
+
+class Epilogue(C.Structure):
+    _fields_ = [('bias', vp), ('residual', vp), ('ldr', i64), ('aux_in', vp), ('lda', i64), ('aux_out', vp),
+                ('ldo', i64), ('rowadd', vp), ('rowadd_mod', i32), ('rowadd_ld', i32), ('act', i32),
+                ('alpha', f32), ('beta', f32), ('pdrop', f32), ('pad_', i32), ('seed', u64)]
+
+
+_SIGS = {
+    'cmhar_version': (i32, []),
+    'cmhar_gemm_bf16': (i32, [i32, i32, i32, i32, i32, vp, i64, vp, i64, vp, i64, C.POINTER(Epilogue), i32, vp, vp]),
+    'cmhar_gemm_generic': (i32, [i32, i32, i32, i32, i32, i32, vp, i64, i64, i64, vp, i64, i64, i64, vp, i64, i64,
+                                 C.POINTER(Epilogue), vp]),
+    'cmhar_attention_fwd': (i32, [i32, i32, i32, i32, i32, i32, vp, i64, vp, i64, vp, i64, vp, i64, vp, f32, f32, u64,
+                                  vp]),
+    'cmhar_attention_bwd': (i32, [i32, i32, i32, i32, i32, i32, vp, i64, vp, i64, vp, i64, vp, i64, vp, i64, vp, vp,
+                                  vp, i64, vp, i64, vp, i64, f32, f32, u64, vp]),
+    'cmhar_layernorm_fwd': (i32, [i32, i32, i32, vp, i64, vp, i64, f32, u64, vp, i64, vp, i64, vp, vp, vp, vp, f32,
+                                  vp]),
+    'cmhar_layernorm_bwd_ws': (i64, [i32, i32]),
+    'cmhar_layernorm_bwd': (i32, [i32, i32, i32, vp, i64, vp, i64, vp, vp, vp, vp, i64, vp, i64, vp, i64, f32, u64,
+                                  vp, vp, f32, vp, vp]),
+    'cmhar_colsum_ws': (i64, [i32, i32]),
+    'cmhar_colsum': (i32, [i32, i32, i32, vp, i64, vp, f32, f32, vp, i64, vp]),
+    'cmhar_batchnorm_fwd': (i32, [i32, i32, vp, vp, vp, vp, vp, vp, vp, vp, i32, f32, f32, i32, vp, vp]),
+    'cmhar_batchnorm_bwd': (i32, [i32, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, f32, vp]),
+    'cmhar_l2normalize_fwd': (i32, [i32, i32, vp, vp, vp, f32, vp]),
+    'cmhar_l2normalize_bwd': (i32, [i32, i32, vp, vp, vp, vp, f32, vp]),
+    'cmhar_siglip_ws': (i64, [i32, i32]),
+    'cmhar_siglip_loss': (i32, [i32, i32, i32, vp, vp, vp, vp, vp, vp, i32, i32, vp, i32, i32, vp, vp, vp, vp]),
+    'cmhar_tubelet_im2col': (i32, [i32, i32, i32, i32, i32, i32, i32, i32, vp, vp, vp]),
+    'cmhar_imu_embed_fwd': (i32, [i32, i32, i32, i32, i32, i32, i32, i32, vp, C.POINTER(vp), C.POINTER(vp), vp, vp,
+                                  vp, vp]),
+    'cmhar_imu_embed_bwd': (i32, [i32, i32, i32, i32, i32, i32, i32, i32, i32, vp, vp, vp, vp, C.POINTER(vp),
+                                  C.POINTER(vp), vp]),
+    'cmhar_copy2d': (i32, [i32, i32, i32, i32, vp, i64, vp, i64, f32, f32, f32, u64, vp]),
+    'cmhar_mt_grad_norm': (i32, [vp, vp, i32, vp, vp, f32, i32, vp]),
+    'cmhar_mt_adamw': (i32, [vp, vp, i32, f32, f32, f32, f32, f32, f32, f32, vp, vp]),
+    'cmhar_mt_cast_bf16': (i32, [vp, vp, i32, vp]),
+}
+
+EXPORTED = tuple(_SIGS)
+
+_lib = None
+
+
+def lib():
+    """Load libcmhar.so (raises if it is missing — there is no fallback path)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f'cmhar HIP library not found at {LIB_PATH}; build it with '
+                               f'`make -C crossmodal-imu-video-ood-har_amd` (or __graft_entry__.build())')
+        L = C.CDLL(LIB_PATH)
+        for name, (res, args) in _SIGS.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def call(name, *args):
+    rc = getattr(lib(), name)(*args)
+    if rc != 0:
+        raise RuntimeError(f'{name} failed with code {rc}')
+    return rc
+
+
+def ptr(t):
+    return None if t is None else t.data_ptr()
+
+
+def stream(device=None):
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def dtype_code(dt):
+    if dt == torch.float32:
+        return F32
+    if dt == torch.bfloat16:
+        return BF16
+    raise TypeError(f'unsupported dtype {dt}')
+
+
+def epilogue(bias=None, residual=None, aux_in=None, aux_out=None, rowadd=None, rowadd_mod=1, act=ACT_NONE,
+             alpha=1.0, beta=0.0, pdrop=0.0, seed=0):
+    e = Epilogue()
+    e.bias = ptr(bias)
+    e.residual = ptr(residual)
+    e.ldr = residual.stride(0) if residual is not None else 0
+    e.aux_in = ptr(aux_in)
+    e.lda = aux_in.stride(0) if aux_in is not None else 0
+    e.aux_out = ptr(aux_out)
+    e.ldo = aux_out.stride(0) if aux_out is not None else 0
+    e.rowadd = ptr(rowadd)
+    e.rowadd_mod = rowadd_mod
+    e.rowadd_ld = rowadd.stride(0) if rowadd is not None else 0
+    e.act = act
+    e.alpha = alpha
+    e.beta = beta
+    e.pdrop = pdrop
+    e.seed = seed
+    return e

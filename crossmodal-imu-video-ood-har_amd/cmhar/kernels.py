@@ -1,0 +1,345 @@
+"""Tensor-level wrappers over the cmhar C ABI.
+
+Every wrapper validates shapes, strides, dtypes and alignment on the host BEFORE launching (a malformed launch
+of a hand-written kernel can fault the GPU), passes raw device pointers + the caller's current HIP stream, and
+raises on any non-zero return code.  No wrapper has a torch fallback.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import math
+
+import torch
+
+from . import _lib as L
+from ._lib import call, ptr
+
+# ------------------------------------------------------------------------------------------------------------
+# optional launch tracer: HIP events recorded on the launching stream around selected kernels (bench.py uses it
+# to measure the dominant kernel's average duration live over the timed region)
+# ------------------------------------------------------------------------------------------------------------
+class Tracer:
+    def __init__(self):
+        self.active = False
+        self.records = []      # (kernel symbol, flops, bytes, start_event, end_event)
+
+    def begin(self):
+        if not self.active:
+            return None
+        ev = torch.cuda.Event(enable_timing=True)
+        ev.record()
+        return ev
+
+    def end(self, ev0, name, flops, nbytes):
+        if ev0 is None:
+            return
+        ev1 = torch.cuda.Event(enable_timing=True)
+        ev1.record()
+        self.records.append((name, flops, nbytes, ev0, ev1))
+
+    def summary(self):
+        """{symbol: (launches, total_ms, total_flops, total_bytes)} — call after synchronising."""
+        out = {}
+        for name, fl, nb, e0, e1 in self.records:
+            n, ms, f, b = out.get(name, (0, 0.0, 0, 0))
+            out[name] = (n + 1, ms + e0.elapsed_time(e1), f + fl, b + nb)
+        return out
+
+
+TRACE = Tracer()
+
+_GEMM_SYMBOL = {0: 'gemm_bf16_kernel<true,true,{o}>', 1: 'gemm_bf16_kernel<true,false,{o}>',
+                2: 'gemm_bf16_kernel<false,false,{o}>'}
+
+# ------------------------------------------------------------------------------------------------------------
+# workspaces (one growing fp32 buffer per (device, stream))
+# ------------------------------------------------------------------------------------------------------------
+_WS = {}
+
+
+def workspace(nfloats: int, device) -> torch.Tensor:
+    st = torch.cuda.current_stream(device)
+    key = (str(device), st.cuda_stream)
+    buf = _WS.get(key)
+    if buf is None or buf.numel() < nfloats:
+        buf = torch.empty(max(int(nfloats), 1 << 16), dtype=torch.float32, device=device)
+        _WS[key] = buf
+    return buf
+
+
+def _check_2d(t, name):
+    if t.dim() != 2:
+        raise ValueError(f'{name}: expected a 2-D matrix, got {tuple(t.shape)}')
+    if t.stride(1) != 1:
+        raise ValueError(f'{name}: inner dimension must be contiguous (stride {t.stride()})')
+    if not t.is_cuda:
+        raise ValueError(f'{name}: must be a device tensor')
+
+
+def _check_bf16_operand(t, name):
+    if t.data_ptr() % 16 or t.stride(0) % 8:
+        raise ValueError(f'{name}: bf16 MFMA operands need 16-B aligned rows (ptr {t.data_ptr() % 16}, '
+                         f'ld {t.stride(0)})')
+
+
+def _splits_for(M, N, K):
+    tiles = math.ceil(M / 128) * math.ceil(N / 128)
+    if tiles >= 384 or K < 1024:
+        return 1
+    return max(1, min(32, round(512 / tiles), K // 256))
+
+
+# ------------------------------------------------------------------------------------------------------------
+# GEMM: C = A·B in one of three layouts (see include/cmhar.h)
+# ------------------------------------------------------------------------------------------------------------
+def gemm(layout: int, a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, *, bias=None, residual=None,
+         aux_in=None, aux_out=None, rowadd=None, rowadd_mod=1, act=L.ACT_NONE, alpha=1.0, beta=0.0, splits=None,
+         pdrop=0.0, seed=0):
+    """layout 0: out[M,N] = a[M,K]·b[N,K]ᵀ;  1: a[M,K]·b[K,N];  2: a[K,M]ᵀ·b[K,N]."""
+    for t, n in ((a, 'A'), (b, 'B'), (out, 'C')):
+        _check_2d(t, n)
+    if layout == 0:
+        M, K = a.shape
+        N = b.shape[0]
+        ok = b.shape[1] == K
+    elif layout == 1:
+        M, K = a.shape
+        N = b.shape[1]
+        ok = b.shape[0] == K
+    elif layout == 2:
+        K, M = a.shape
+        N = b.shape[1]
+        ok = b.shape[0] == K
+    else:
+        raise ValueError(layout)
+    if not ok or tuple(out.shape) != (M, N):
+        raise ValueError(f'gemm layout {layout}: shapes A{tuple(a.shape)} B{tuple(b.shape)} C{tuple(out.shape)}')
+    if a.dtype != b.dtype:
+        raise TypeError('A and B must share a dtype')
+    for t, n in ((bias, 'bias'), (rowadd, 'rowadd')):
+        if t is not None and (t.dtype != torch.float32 or not t.is_contiguous() and t.dim() == 1):
+            raise TypeError(f'{n} must be fp32')
+    if bias is not None and bias.numel() != N:
+        raise ValueError('bias length')
+    for t, n in ((residual, 'residual'), (aux_in, 'aux_in'), (aux_out, 'aux_out')):
+        if t is not None:
+            _check_2d(t, n)
+            if tuple(t.shape) != (M, N) or t.dtype != out.dtype:
+                raise ValueError(f'{n} must be [{M},{N}] {out.dtype}')
+    if rowadd is not None and (rowadd.dim() != 2 or rowadd.shape[1] != N or rowadd.stride(1) != 1):
+        raise ValueError('rowadd must be [mod, N]')
+    if beta != 0.0 and out.dtype != torch.float32:
+        raise ValueError('beta accumulation only for fp32 outputs')
+    epi = L.epilogue(bias, residual, aux_in, aux_out, rowadd, rowadd_mod, act, alpha, beta, pdrop, seed)
+    st = L.stream(out.device)
+    if a.dtype == torch.bfloat16:
+        _check_bf16_operand(a, 'A')
+        _check_bf16_operand(b, 'B')
+        if K % 8 or (layout >= 1 and N % 8) or (layout == 2 and M % 8):
+            raise ValueError('bf16 GEMM needs K (and the row-contraction operand widths) to be multiples of 8')
+        if out.dtype not in (torch.bfloat16, torch.float32):
+            raise TypeError('out dtype')
+        s = _splits_for(M, N, K) if splits is None else splits
+        ws = None
+        if s > 1:
+            ws = workspace(s * M * N, out.device)
+        ev = TRACE.begin()
+        call('cmhar_gemm_bf16', layout, L.dtype_code(out.dtype), M, N, K, ptr(a), a.stride(0), ptr(b), b.stride(0),
+             ptr(out), out.stride(0), C.byref(epi), s, ptr(ws), st)
+        if ev is not None:
+            name = _GEMM_SYMBOL[layout].format(o='float' if (s > 1 or out.dtype == torch.float32) else 'bf16')
+            if s > 1:
+                name += '+splitk_reduce'
+            TRACE.end(ev, name, 2 * M * N * K, 2 * (M * K + N * K) + out.element_size() * M * N)
+    else:
+        if layout == 0:
+            sam, sak, sbk, sbn = a.stride(0), 1, 1, b.stride(0)
+        elif layout == 1:
+            sam, sak, sbk, sbn = a.stride(0), 1, b.stride(0), 1
+        else:
+            sam, sak, sbk, sbn = 1, a.stride(0), b.stride(0), 1
+        call('cmhar_gemm_generic', L.dtype_code(a.dtype), L.dtype_code(out.dtype), M, N, K, 1, ptr(a), sam, sak, 0,
+             ptr(b), sbk, sbn, 0, ptr(out), out.stride(0), 0, C.byref(epi), st)
+    return out
+
+
+def linear(x, w, bias=None, *, residual=None, act=L.ACT_NONE, aux_out=None, rowadd=None, rowadd_mod=1,
+           out=None, out_dtype=None, pdrop=0.0, seed=0):
+    """y = dropout(act(x·wᵀ + bias [+ rowadd])) [+ residual]  — nn.Linear forward (+ fused activation)."""
+    M, N = x.shape[0], w.shape[0]
+    if out is None:
+        out = torch.empty(M, N, dtype=out_dtype or x.dtype, device=x.device)
+    return gemm(0, x, w, out, bias=bias, residual=residual, act=act, aux_out=aux_out, rowadd=rowadd,
+                rowadd_mod=rowadd_mod, pdrop=pdrop, seed=seed)
+
+
+def linear_dgrad(dy, w, *, act=L.ACT_NONE, aux_in=None, residual=None, out=None, beta=0.0, pdrop=0.0, seed=0):
+    """dx = (dy·w) [* dropmask] [* act'(aux_in)] [+ residual]."""
+    M, K = dy.shape[0], w.shape[1]
+    if out is None:
+        out = torch.empty(M, K, dtype=dy.dtype, device=dy.device)
+    return gemm(1, dy, w, out, act=act, aux_in=aux_in, residual=residual, beta=beta, pdrop=pdrop, seed=seed)
+
+
+def linear_wgrad(dy, x, *, out=None, beta=0.0):
+    """dW[N,K] (fp32) = dyᵀ·x."""
+    N, K = dy.shape[1], x.shape[1]
+    if out is None:
+        out = torch.empty(N, K, dtype=torch.float32, device=dy.device)
+    return gemm(2, dy, x, out, beta=beta)
+
+
+def colsum(x, out=None, *, alpha=1.0, beta=0.0):
+    """out[n] (fp32) = alpha Σ_m x[m, n] + beta out[n]  — bias gradients."""
+    _check_2d(x, 'x')
+    M, N = x.shape
+    if out is None:
+        out = torch.empty(N, dtype=torch.float32, device=x.device)
+    n = L.lib().cmhar_colsum_ws(M, N)
+    ws = workspace(n, x.device)
+    call('cmhar_colsum', L.dtype_code(x.dtype), M, N, ptr(x), x.stride(0), ptr(out), alpha, beta, ptr(ws), ws.numel(),
+         L.stream(x.device))
+    return out
+
+
+# ------------------------------------------------------------------------------------------------------------
+# attention
+# ------------------------------------------------------------------------------------------------------------
+def _head_view_ok(t, B, L_, H, D, name):
+    _check_2d(t, name)
+    if t.shape[0] != B * L_ or t.shape[1] < H * D:
+        raise ValueError(f'{name}: expected [{B * L_}, >={H * D}] got {tuple(t.shape)}')
+
+
+def attention_fwd(q, k, v, out, lse, *, B, H, Lq, Lk, D, scale, pdrop=0.0, seed=0):
+    for t, n, Lx in ((q, 'q', Lq), (k, 'k', Lk), (v, 'v', Lk), (out, 'o', Lq)):
+        _head_view_ok(t, B, Lx, H, D, n)
+    if lse.numel() < B * H * Lq or lse.dtype != torch.float32:
+        raise ValueError('lse workspace')
+    dt = L.dtype_code(q.dtype)
+    if dt == L.BF16:
+        if D != 64 or pdrop != 0.0:
+            raise ValueError('bf16 flash attention supports head dim 64 without dropout')
+        for t, n in ((q, 'q'), (k, 'k'), (v, 'v'), (out, 'o')):
+            _check_bf16_operand(t, n)
+    ev = TRACE.begin() if dt == L.BF16 else None
+    call('cmhar_attention_fwd', dt, B, H, Lq, Lk, D, ptr(q), q.stride(0), ptr(k), k.stride(0), ptr(v), v.stride(0),
+         ptr(out), out.stride(0), ptr(lse), scale, pdrop, seed, L.stream(q.device))
+    TRACE.end(ev, 'attn_fwd_bf16', 4 * B * H * Lq * Lk * D, 2 * (B * Lq + 2 * B * Lk + B * Lq) * H * D)
+    return out
+
+
+def attention_bwd(q, k, v, o, do, lse, dq, dk, dv, *, B, H, Lq, Lk, D, scale, pdrop=0.0, seed=0):
+    for t, n, Lx in ((q, 'q', Lq), (k, 'k', Lk), (v, 'v', Lk), (o, 'o', Lq), (do, 'do', Lq), (dq, 'dq', Lq),
+                     (dk, 'dk', Lk), (dv, 'dv', Lk)):
+        _head_view_ok(t, B, Lx, H, D, n)
+    dt = L.dtype_code(q.dtype)
+    if dt == L.BF16:
+        for t, n in ((q, 'q'), (k, 'k'), (v, 'v'), (o, 'o'), (do, 'do'), (dq, 'dq'), (dk, 'dk'), (dv, 'dv')):
+            _check_bf16_operand(t, n)
+    delta = workspace(B * H * Lq, q.device)
+    ev = TRACE.begin() if dt == L.BF16 else None
+    call('cmhar_attention_bwd', dt, B, H, Lq, Lk, D, ptr(q), q.stride(0), ptr(k), k.stride(0), ptr(v), v.stride(0),
+         ptr(o), o.stride(0), ptr(do), do.stride(0), ptr(lse), ptr(delta), ptr(dq), dq.stride(0), ptr(dk),
+         dk.stride(0), ptr(dv), dv.stride(0), scale, pdrop, seed, L.stream(q.device))
+    TRACE.end(ev, 'attn_bwd_bf16(delta+dq+dkdv)', 14 * B * H * Lq * Lk * D, 2 * (6 * B * Lq + 4 * B * Lk) * H * D)
+
+
+# ------------------------------------------------------------------------------------------------------------
+# norms
+# ------------------------------------------------------------------------------------------------------------
+def layernorm_fwd(a, gamma, beta, eps, *, b=None, pdrop=0.0, seed=0, h_out=None, out=None, mean=None, rstd=None):
+    _check_2d(a, 'a')
+    M, N = a.shape
+    if N > 1024:
+        raise ValueError('LayerNorm width > 1024')
+    if out is None:
+        out = torch.empty_like(a, memory_format=torch.contiguous_format)
+    if mean is None:
+        mean = torch.empty(M, dtype=torch.float32, device=a.device)
+    if rstd is None:
+        rstd = torch.empty(M, dtype=torch.float32, device=a.device)
+    if b is not None and (tuple(b.shape) != (M, N) or b.dtype != a.dtype):
+        raise ValueError('b shape')
+    call('cmhar_layernorm_fwd', L.dtype_code(a.dtype), M, N, ptr(a), a.stride(0), ptr(b),
+         b.stride(0) if b is not None else 0, pdrop, seed, ptr(h_out), h_out.stride(0) if h_out is not None else 0,
+         ptr(out), out.stride(0), ptr(gamma), ptr(beta), ptr(mean), ptr(rstd), eps, L.stream(a.device))
+    return out, mean, rstd
+
+
+def layernorm_bwd(dy, h, gamma, mean, rstd, dgamma, dbeta, *, dres=None, dh=None, db_out=None, pdrop=0.0, seed=0,
+                  beta_acc=0.0):
+    M, N = h.shape
+    if dh is None:
+        dh = torch.empty_like(h, memory_format=torch.contiguous_format)
+    n = L.lib().cmhar_layernorm_bwd_ws(M, N)
+    ws = workspace(n, h.device)
+    call('cmhar_layernorm_bwd', L.dtype_code(h.dtype), M, N, ptr(dy), dy.stride(0), ptr(h), h.stride(0), ptr(gamma),
+         ptr(mean), ptr(rstd), ptr(dres), dres.stride(0) if dres is not None else 0, ptr(dh), dh.stride(0),
+         ptr(db_out), db_out.stride(0) if db_out is not None else 0, pdrop, seed, ptr(dgamma), ptr(dbeta), beta_acc,
+         ptr(ws), L.stream(h.device))
+    return dh
+
+
+def batchnorm_fwd(x, w, b, rmean, rvar, training, momentum, eps, relu, num_batches_tracked=None):
+    B, Cc = x.shape
+    y = torch.empty_like(x)
+    sm = torch.empty(Cc, dtype=torch.float32, device=x.device)
+    sr = torch.empty(Cc, dtype=torch.float32, device=x.device)
+    call('cmhar_batchnorm_fwd', B, Cc, ptr(x), ptr(y), ptr(w), ptr(b), ptr(rmean), ptr(rvar), ptr(sm), ptr(sr),
+         int(training), momentum, eps, int(relu), ptr(num_batches_tracked), L.stream(x.device))
+    return y, sm, sr
+
+
+def batchnorm_bwd(x, y, dy, w, sm, sr, training, relu):
+    B, Cc = x.shape
+    dx = torch.empty_like(x)
+    dw = torch.empty(Cc, dtype=torch.float32, device=x.device)
+    db = torch.empty(Cc, dtype=torch.float32, device=x.device)
+    call('cmhar_batchnorm_bwd', B, Cc, ptr(x), ptr(y), ptr(dy.contiguous()), ptr(w), ptr(sm), ptr(sr), ptr(dx),
+         ptr(dw), ptr(db), int(training), int(relu), 0.0, L.stream(x.device))
+    return dx, dw, db
+
+
+def l2normalize_fwd(x, eps=1e-12):
+    M, N = x.shape
+    y = torch.empty_like(x)
+    nrm = torch.empty(M, dtype=torch.float32, device=x.device)
+    call('cmhar_l2normalize_fwd', M, N, ptr(x), ptr(y), ptr(nrm), eps, L.stream(x.device))
+    return y, nrm
+
+
+def l2normalize_bwd(y, dy, nrm, eps=1e-12):
+    M, N = y.shape
+    dx = torch.empty_like(y)
+    call('cmhar_l2normalize_bwd', M, N, ptr(y), ptr(dy.contiguous()), ptr(nrm), ptr(dx), eps, L.stream(y.device))
+    return dx
+
+
+def copy2d(src, dst, alpha=1.0, beta=0.0, pdrop=0.0, seed=0):
+    """dst = alpha * src * dropmask + beta * dst (casts / gathers / adds / dropout)."""
+    _check_2d(src, 'src')
+    _check_2d(dst, 'dst')
+    if src.shape != dst.shape:
+        raise ValueError('copy2d shape')
+    call('cmhar_copy2d', L.dtype_code(src.dtype), L.dtype_code(dst.dtype), src.shape[0], src.shape[1], ptr(src),
+         src.stride(0), ptr(dst), dst.stride(0), alpha, beta, pdrop, seed, L.stream(src.device))
+    return dst
+
+
+def tubelet_im2col(video, tub, P, out_dtype):
+    if video.dtype != torch.float32 or video.dim() != 5 or not video.is_contiguous():
+        raise ValueError('video must be a contiguous fp32 (B,T,C,H,W) tensor')
+    B, T, Cc, H, W = video.shape
+    if T % tub or H % P or W % P or P % 8:
+        raise ValueError(f'video {tuple(video.shape)} incompatible with tubelet {tub} patch {P}')
+    Lt = (T // tub) * (H // P) * (W // P)
+    out = torch.empty(B * Lt, Cc * tub * P * P, dtype=out_dtype, device=video.device)
+    call('cmhar_tubelet_im2col', L.dtype_code(out_dtype), B, T, Cc, H, W, tub, P, ptr(video), ptr(out),
+         L.stream(video.device))
+    return out
+
+
+def ptr_array(tensors):
+    arr = (C.c_void_p * len(tensors))(*[t.data_ptr() for t in tensors])
+    return arr

@@ -1,0 +1,158 @@
+"""Drop-in replacements for the reference's `src/models/models.py` API, running on the cmhar HIP library.
+
+    from cmhar.models import IMUEncoder, VideoEncoder, ProjectionHead, CrossModalModel, IMUClassifier
+
+Constructor signatures, attributes, forward() outputs and state_dict() keys match the reference
+(`models.py:16-348`), so `CrossModalTrainer` / `ClassificationTrainer` / `Evaluator` (src/train/trainer.py,
+src/eval/evaluator.py) and checkpoints written by the reference work unchanged.  Compute runs in
+`config.model.compute_dtype` ('bf16': MFMA bf16 with fp32 accumulation for the VideoMAE backbone — the FLOP-heavy
+part; 'fp32': exact fp32 everywhere, the parity mode).  The IMU encoder, heads, normalisation and loss are always
+fp32 (they are latency- not FLOP-bound).
+"""
+from __future__ import annotations
+
+import math
+import os
+import warnings
+
+import torch
+import torch.nn as nn
+
+from . import kernels as K
+from .heads import ProjectionHead, l2_normalize, run_head, _Seeds
+from .imu import IMUEncoder, PatchEmbedding
+from .videomae import VideoMAEBackbone, default_videomae_config, run_backbone
+
+__all__ = ['PatchEmbedding', 'IMUEncoder', 'VideoEncoder', 'ProjectionHead', 'CrossModalModel', 'IMUClassifier']
+
+
+class _LinearFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias):
+        ctx.save_for_backward(x, weight)
+        ctx.has_bias = bias is not None
+        return K.linear(x, weight.detach(), None if bias is None else bias.detach())
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        dy = dy.contiguous()
+        dx = K.linear_dgrad(dy, w.detach()) if ctx.needs_input_grad[0] else None
+        dw = K.linear_wgrad(dy, x) if ctx.needs_input_grad[1] else None
+        db = K.colsum(dy) if ctx.has_bias and ctx.needs_input_grad[2] else None
+        return dx, dw, db
+
+
+def linear_fp32(x, lin: nn.Linear):
+    x = x.contiguous().float()
+    if torch.is_grad_enabled() and (x.requires_grad or lin.weight.requires_grad):
+        return _LinearFn.apply(x, lin.weight, lin.bias)
+    return K.linear(x, lin.weight.detach(), None if lin.bias is None else lin.bias.detach())
+
+
+def _videomae_geometry(config):
+    m, d = config.model, config.data
+    frames = m.videomae_num_frames or d.video_frames_per_window
+    image = m.videomae_image_size or (d.video_resize[0] if isinstance(d.video_resize, (tuple, list)) else d.video_resize)
+    return default_videomae_config(image_size=image, patch_size=m.videomae_patch_size, num_frames=frames,
+                                   tubelet_size=m.videomae_tubelet_size, hidden_size=m.videomae_hidden_size,
+                                   num_hidden_layers=m.videomae_num_layers, num_attention_heads=m.videomae_num_heads,
+                                   intermediate_size=m.videomae_intermediate_size,
+                                   layer_norm_eps=m.videomae_layer_norm_eps, qkv_bias=m.videomae_qkv_bias,
+                                   use_mean_pooling=m.videomae_use_mean_pooling)
+
+
+class VideoEncoder(nn.Module):
+    """models.py:137-216 (VideoMAE branch).  A local HF-format directory is loaded (config.json +
+    safetensors / .bin via weights-only loaders); a hub name cannot be fetched offline, so the VideoMAE
+    architecture is built from `config.model.videomae_*` / the data geometry with HF's random init."""
+
+    def __init__(self, config):
+        super().__init__()
+        self.config = config
+        model_cfg = config.model
+        vb = model_cfg.video_backbone
+        self.is_videomae = False
+        dt = getattr(model_cfg, 'compute_dtype', 'bf16')
+        if isinstance(vb, str) and ('videomae' in vb.lower() or '/' in vb):
+            self.is_videomae = True
+            if os.path.isdir(vb) and os.path.exists(os.path.join(vb, 'config.json')):
+                self.backbone = VideoMAEBackbone.from_pretrained(vb, compute_dtype=dt)
+            else:
+                if model_cfg.video_pretrained and not os.path.isdir(vb):
+                    warnings.warn(f'VideoMAE checkpoint {vb!r} is not available offline; using a randomly '
+                                  f'initialised backbone of the configured geometry')
+                self.backbone = VideoMAEBackbone(_videomae_geometry(config), compute_dtype=dt)
+            self.feature_dim = self.backbone.config.hidden_size
+        elif vb in ('resnet18', 'mobilenet_v2'):
+            raise NotImplementedError(f'{vb}: per-frame 2-D CNN backbones are not on the accelerated path '
+                                      f'(torchvision is absent; see DESIGN.md scope)')
+        else:
+            raise ValueError(f'Backbone inconnu: {vb}')
+        self.projection = nn.Linear(self.feature_dim, model_cfg.video_d_model)
+
+    def forward(self, x):
+        """x (B, T, C, H, W) → (B, video_d_model)."""
+        if x.dim() != 5:
+            raise ValueError(f'expected (B, T, C, H, W) video, got {tuple(x.shape)}')
+        feat = run_backbone(self.backbone, x, token0_only=True)   # last_hidden_state[:, 0]  (models.py:201)
+        return linear_fp32(feat, self.projection)                 # models.py:202
+
+
+class CrossModalModel(nn.Module):
+    """models.py:239-291."""
+
+    def __init__(self, config):
+        super().__init__()
+        self.config = config
+        model_cfg = config.model
+        self.imu_encoder = IMUEncoder(config)
+        self.video_encoder = VideoEncoder(config)
+        self.imu_proj = ProjectionHead(model_cfg.imu_d_model, model_cfg.projection_hidden_dim,
+                                       model_cfg.projection_dim)
+        self.video_proj = ProjectionHead(model_cfg.video_d_model, model_cfg.projection_hidden_dim,
+                                         model_cfg.projection_dim)
+        self.temperature = nn.Parameter(torch.ones([]) * math.log(10))
+        self.bias = nn.Parameter(torch.ones([]) * -10)
+
+    def forward(self, imu, video):
+        imu_feat, _ = self.imu_encoder(imu)
+        video_feat = self.video_encoder(video)
+        imu_proj = self.imu_proj(imu_feat)
+        video_proj = self.video_proj(video_feat)
+        return l2_normalize(imu_proj), l2_normalize(video_proj)
+
+
+class IMUClassifier(nn.Module):
+    """models.py:296-348."""
+
+    def __init__(self, imu_encoder, config, freeze_encoder=False):
+        super().__init__()
+        self.imu_encoder = imu_encoder
+        self.config = config
+        model_cfg = config.model
+        if freeze_encoder:
+            for param in self.imu_encoder.parameters():
+                param.requires_grad = False
+        layers = []
+        in_dim = model_cfg.imu_d_model
+        for hidden_dim in model_cfg.classifier_hidden_dims:
+            layers.extend([nn.Linear(in_dim, hidden_dim), nn.BatchNorm1d(hidden_dim), nn.ReLU(inplace=True),
+                           nn.Dropout(model_cfg.classifier_dropout)])
+            in_dim = hidden_dim
+        layers.append(nn.Linear(in_dim, model_cfg.num_classes))
+        self.classifier = nn.Sequential(*layers)
+        self._seeds = _Seeds()
+
+    def forward(self, imu):
+        with torch.set_grad_enabled(self.training or not self.freeze_encoder):
+            imu_feat, _ = self.imu_encoder(imu)
+        return run_head(self.classifier, imu_feat, self.training, self._seeds)
+
+    @property
+    def freeze_encoder(self):
+        return not next(self.imu_encoder.parameters()).requires_grad
+
+    def unfreeze_encoder(self):
+        for param in self.imu_encoder.parameters():
+            param.requires_grad = True

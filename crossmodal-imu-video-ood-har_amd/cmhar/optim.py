@@ -1,0 +1,132 @@
+"""Gradient clipping and AdamW as multi-tensor HIP launches (replaces `torch.nn.utils.clip_grad_norm_` and
+`torch.optim.AdamW.step` as used by `CrossModalTrainer`, src/train/trainer.py:74-78,140-141).
+
+Both are HBM-bound passes over the 88.4 M fp32 parameters.  `clip_grad_norm_` = one sum-of-squares launch over
+a chunk table + one tiny final launch (total norm and clip coefficient stay on the device: no host sync) + one
+in-place scale launch.  `FusedAdamW.step` = one launch that reads p, g, m, v and writes p, m, v and the
+parameter's compute shadow (bf16 weight pack / fp32 bias pack, see cmhar.weights) in the same pass, with
+torch.optim.AdamW's arithmetic (step scalars computed on the host in double precision, as torch does).
+"""
+from __future__ import annotations
+
+import math
+from typing import Iterable, List
+
+import numpy as np
+import torch
+
+from . import _lib as L
+from .weights import MT_TENSOR, chunk_list, to_device_bytes
+
+
+class _Table:
+    """Device tensor + chunk tables for a list of parameters, rebuilt only when a pointer changes."""
+
+    def __init__(self):
+        self.key = None
+        self.dev_t = self.dev_c = None
+        self.nchunks = 0
+
+    def get(self, rows, device):
+        key = tuple(tuple(int(x) for x in r) for r in rows)
+        if key != self.key:
+            tab = np.zeros(len(rows), dtype=MT_TENSOR)
+            for i, r in enumerate(rows):
+                tab[i] = r
+            ch = chunk_list([r[6] for r in rows])
+            self.dev_t = to_device_bytes(tab, device)
+            self.dev_c = to_device_bytes(ch, device)
+            self.nchunks = len(ch)
+            self.key = key
+        return self.dev_t, self.dev_c, self.nchunks
+
+
+_NORM_TABLES = {}
+
+
+def clip_grad_norm_(parameters, max_norm: float, norm_type: float = 2.0, error_if_nonfinite: bool = False,
+                    foreach=None) -> torch.Tensor:
+    """torch.nn.utils.clip_grad_norm_ (L2): returns the total norm as a 0-dim DEVICE tensor (no sync)."""
+    if norm_type != 2.0:
+        raise NotImplementedError('only the L2 norm is on the accelerated path')
+    if isinstance(parameters, torch.Tensor):
+        parameters = [parameters]
+    params = [p for p in parameters if p.grad is not None]
+    if not params:
+        return torch.tensor(0.0)
+    dev = params[0].grad.device
+    rows = [(p.data_ptr(), p.grad.data_ptr(), 0, 0, 0, 0, p.grad.numel(), 0.0, 1.0) for p in params]
+    tab = _NORM_TABLES.setdefault(str(dev), _Table())
+    t, c, n = tab.get(rows, dev)
+    part = torch.empty(max(n, 1), dtype=torch.float32, device=dev)
+    out = torch.empty(2, dtype=torch.float32, device=dev)
+    L.call('cmhar_mt_grad_norm', t.data_ptr(), c.data_ptr(), n, part.data_ptr(), out.data_ptr(), float(max_norm), 1,
+           L.stream(dev))
+    return out[0]
+
+
+class FusedAdamW(torch.optim.Optimizer):
+    """torch.optim.AdamW (amsgrad=False, maximize=False) as one multi-tensor HIP launch per step.
+
+    State layout matches torch (`state[p] = {'step', 'exp_avg', 'exp_avg_sq'}`), so optimizer state dicts
+    interchange.  `shadow_sources`: modules whose `_packs` (cmhar.weights.PackedWeights) hold compute copies of
+    parameters; those copies are rewritten in the same pass."""
+
+    def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-2, shadow_sources=()):
+        defaults = dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay)
+        super().__init__(params, defaults)
+        self.shadow_sources = list(shadow_sources)
+        self._tables = {}
+
+    def _slots(self):
+        slots = {}
+        packs = []
+        for m in self.shadow_sources:
+            pk = getattr(m, '_packs', None)
+            if pk is not None:
+                slots.update(pk.slots)
+                packs.append(pk)
+        return slots, packs
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        loss = None
+        if closure is not None:
+            with torch.enable_grad():
+                loss = closure()
+        slots, packs = self._slots()
+        for gi, group in enumerate(self.param_groups):
+            b1, b2 = group['betas']
+            lr, eps, wd = group['lr'], group['eps'], group['weight_decay']
+            rows = []
+            steps = set()
+            dev = None
+            for p in group['params']:
+                if p.grad is None:
+                    continue
+                if p.grad.is_sparse or p.grad.dtype != torch.float32 or p.dtype != torch.float32:
+                    raise RuntimeError('FusedAdamW handles dense fp32 parameters and gradients')
+                st = self.state[p]
+                if len(st) == 0:
+                    st['step'] = torch.tensor(0.0)
+                    st['exp_avg'] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                    st['exp_avg_sq'] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                st['step'] += 1
+                steps.add(int(st['step'].item()))
+                bf, cp = slots.get(p, (0, 0))
+                rows.append((p.data_ptr(), p.grad.data_ptr(), st['exp_avg'].data_ptr(),
+                             st['exp_avg_sq'].data_ptr(), bf, cp, p.numel(), float(wd), 1.0))
+                dev = p.device
+            if not rows:
+                continue
+            if len(steps) != 1:
+                raise RuntimeError('parameters of one group at different step counts')
+            step = steps.pop()
+            bc1 = 1.0 - b1 ** step
+            bc2 = 1.0 - b2 ** step
+            t, c, n = self._tables.setdefault(gi, _Table()).get(rows, dev)
+            L.call('cmhar_mt_adamw', t.data_ptr(), c.data_ptr(), n, float(lr), float(1.0 - b1), float(b2),
+                   float(1.0 - b2), float(eps), float(lr / bc1), float(math.sqrt(bc2)), None, L.stream(dev))
+        for pk in packs:
+            pk.mark_fresh()
+        return loss

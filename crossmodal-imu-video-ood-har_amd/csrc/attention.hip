@@ -1,0 +1,649 @@
+// Attention for the VideoMAE blocks (third-party transformers modeling_videomae.py:209-258: softmax(QKᵀ/√d)V,
+// no mask, no dropout) and for the IMU encoder's nn.MultiheadAttention (attention-prob dropout p).
+//
+// bf16 flash path (head dim 64, MFMA 32x32x16 bf16):
+//   fwd   one wave = 32 queries, 4 waves/WG share double-buffered 64-key K/V tiles in LDS.  Scores are computed
+//         transposed, Sᵀ = K·Qᵀ, so each lane owns one query row (lane&31) and the online softmax is lane-local
+//         (+1 cross-half exchange); P stays in registers and is the B operand of Oᵀ = Vᵀ·Pᵀ, whose accumulator
+//         again has the query on the lane, so the rescale by exp(m_old - m_new) is a per-lane scalar.
+//   bwd   two kernels, no atomics: dK/dV (key-block outer: S and dP with the KEY on the lane, so their
+//         accumulators feed dVᵀ += dOᵀP and dKᵀ += QᵀdS directly) and dQ (query-block outer, like fwd).
+//         Row constants (-lse, -delta) are folded into the accumulators before the MFMA chains.
+// fp32 path (any head dim <= 64): exact-f32 scalar kernels with the same algorithm, used by the fp32 parity mode
+// and the tiny IMU attention (L = 13, d = 16), including counter-hash dropout regenerated in backward.
+#include "common.h"
+
+namespace {
+
+constexpr float LOG2E = 1.4426950408889634f;
+
+// [64 rows][64 bf16] image, 128-B rows; 16-B chunk XOR-swizzle that is conflict-free for both the row reads
+// (ds_read_b128) and the transposed reads (ds_read_b64_tr_b16) of every kernel below (tools/lds_banks.py).
+__device__ __forceinline__ int att_off(int row, int chunk) {
+  const int f = (((row >> 1) & 1) << 2) | ((row >> 3) & 3);
+  return row * 128 + ((chunk ^ f) << 4);
+}
+
+// Stage a [64][64] bf16 tile (rows r0.. of a [rows][ld] matrix, column offset col0) into registers: 2 chunks/thread.
+struct Tile64 {
+  uint4_t r[2];
+  __device__ __forceinline__ void load(const bf16* __restrict__ base, long ld, int r0, int rows_total, int tid) {
+#pragma unroll
+    for (int it = 0; it < 2; ++it) {
+      const int c = it * 256 + tid;
+      const int row = c >> 3, ch = c & 7;
+      if (r0 + row < rows_total) r[it] = *(const uint4_t*)(base + (long)(r0 + row) * ld + ch * 8);
+      else r[it] = uint4_t{0u, 0u, 0u, 0u};
+    }
+  }
+  __device__ __forceinline__ void store(char* lds, int tid) const {
+#pragma unroll
+    for (int it = 0; it < 2; ++it) {
+      const int c = it * 256 + tid;
+      *(uint4_t*)(lds + att_off(c >> 3, c & 7)) = r[it];
+    }
+  }
+};
+
+// Row fragment for a 32x32x16 A operand: lane holds row (r0 + lane&31), cols 16t + 8(lane>>5) .. +8.
+__device__ __forceinline__ bf16x8 row_frag(const char* lds, int r0, int t, int lane) {
+  return *(const bf16x8*)(lds + att_off(r0 + (lane & 31), 2 * t + (lane >> 5)));
+}
+
+// Transposed fragment: lane holds element j of column c = c0 + (lane&31) over rows
+//   r0 + 16s + 8(j>>2) + 4h + (j&3)   (h = lane>>5) — the k order of an MFMA accumulator reused as operand.
+__device__ __forceinline__ bf16x8 tr_frag(const char* lds, int r0, int s, int c0, int lane) {
+  const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3, h = g >> 1;
+  const int col = c0 + 16 * (g & 1) + 4 * p;
+  const int ch = col >> 3, hb = (col & 7) * 2;
+  const int ra = r0 + 16 * s + 4 * h + q;
+  short4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(short4_t, lds + att_off(ra, ch) + hb));
+  short4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(short4_t, lds + att_off(ra + 8, ch) + hb));
+  short8_t v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+// Accumulator registers 8s..8s+7 → bf16 operand fragment.
+__device__ __forceinline__ bf16x8 pack8(const floatx16& a, int s) {
+  bf16x8 v;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] = (bf16)a[8 * s + j];
+  return v;
+}
+
+// accumulator register r of lane-half h ↔ row index (r&3) + 8(r>>2) + 4h
+__device__ __forceinline__ int acc_row(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
+
+__device__ __forceinline__ float xhalf(float v) { return __shfl_xor(v, 32); }
+
+// ---------------------------------------------------------------------------------------------------------------
+// forward
+// ---------------------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256, 2) void attn_fwd_bf16(int H, int Lq, int Lk, const bf16* __restrict__ Q, long ldq,
+                                                        const bf16* __restrict__ K, long ldk,
+                                                        const bf16* __restrict__ V, long ldv, bf16* __restrict__ O,
+                                                        long ldo, float* __restrict__ lse, float scale) {
+  __shared__ __attribute__((aligned(16))) char smem[4 * 8192];
+#define Ks(buf) (smem + 8192 * (buf))
+#define Vs(buf) (smem + 16384 + 8192 * (buf))
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5;
+  const int hd = blockIdx.y, b = blockIdx.z;
+  const int q0 = blockIdx.x * 128 + wave * 32;
+  const bf16* Qb = Q + (long)b * Lq * ldq + hd * 64;
+  const bf16* Kb = K + (long)b * Lk * ldk + hd * 64;
+  const bf16* Vb = V + (long)b * Lk * ldv + hd * 64;
+  const float c = scale * LOG2E;
+
+  const int myq = min(q0 + (lane & 31), Lq - 1);
+  bf16x8 qf[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) qf[t] = *(const bf16x8*)(Qb + (long)myq * ldq + 16 * t + 8 * h);
+
+  floatx16 o[2];
+#pragma unroll
+  for (int d = 0; d < 2; ++d)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) o[d][r] = 0.f;
+  float m = -INFINITY, l = 0.f;
+
+  const int nt = (Lk + 63) / 64;
+  Tile64 tk, tv;
+  tk.load(Kb, ldk, 0, Lk, tid);
+  tv.load(Vb, ldv, 0, Lk, tid);
+  tk.store(Ks(0), tid);
+  tv.store(Vs(0), tid);
+  __syncthreads();
+  for (int kt = 0; kt < nt; ++kt) {
+    const int cur = kt & 1;
+    const bool more = kt + 1 < nt;
+    if (more) {
+      tk.load(Kb, ldk, (kt + 1) * 64, Lk, tid);
+      tv.load(Vb, ldv, (kt + 1) * 64, Lk, tid);
+    }
+    floatx16 s[2];
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) s[kb][r] = 0.f;
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+        s[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag(Ks(cur), kb * 32, t, lane), qf[t], s[kb], 0, 0, 0);
+    }
+    float mt = -INFINITY;
+    const int kbase = kt * 64;
+    const bool partial = kbase + 64 > Lk;
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        float v = s[kb][r] * c;
+        if (partial && kbase + kb * 32 + acc_row(r, h) >= Lk) v = -INFINITY;
+        s[kb][r] = v;
+        mt = fmaxf(mt, v);
+      }
+    mt = fmaxf(mt, xhalf(mt));
+    const float mn = fmaxf(m, mt);
+    const float alpha = exp2f(m - mn);
+    m = mn;
+    l *= alpha;
+#pragma unroll
+    for (int d = 0; d < 2; ++d)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) o[d][r] *= alpha;
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float p = exp2f(s[kb][r] - mn);
+        s[kb][r] = p;
+        l += p;
+      }
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int ss = 0; ss < 2; ++ss) {
+        const bf16x8 pb = pack8(s[kb], ss);
+#pragma unroll
+        for (int d = 0; d < 2; ++d)
+          o[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_frag(Vs(cur), kb * 32, ss, d * 32, lane), pb, o[d], 0, 0, 0);
+      }
+    if (more) {
+      tk.store(Ks(cur ^ 1), tid);
+      tv.store(Vs(cur ^ 1), tid);
+    }
+    __syncthreads();
+  }
+  l += xhalf(l);
+  const float inv = 1.f / l;
+  const int q = q0 + (lane & 31);
+  if (q < Lq) {
+    bf16* orow = O + ((long)b * Lq + q) * ldo + hd * 64;
+#pragma unroll
+    for (int d = 0; d < 2; ++d)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        bf16x4 v;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] = (bf16)(o[d][4 * g + j] * inv);
+        *(bf16x4*)(orow + d * 32 + 8 * g + 4 * h) = v;
+      }
+    if (h == 0) lse[((long)b * H + hd) * Lq + q] = m + log2f(l);   // log2-domain LSE of (scale*log2e)*s
+  }
+}
+
+// δ[q] = Σ_d dO[q,d]·O[q,d] per (b, h, q); one wave per 64 queries x 1 head... simple: one thread per (q, head).
+__global__ void attn_bwd_delta(int H, int Lq, const bf16* __restrict__ O, long ldo, const bf16* __restrict__ dO,
+                               long lddo, float* __restrict__ delta, int B) {
+  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long total = (long)B * H * Lq;
+  if (idx >= total) return;
+  const int q = idx % Lq;
+  const int hd = (idx / Lq) % H;
+  const int b = idx / ((long)Lq * H);
+  const bf16* o = O + ((long)b * Lq + q) * ldo + hd * 64;
+  const bf16* g = dO + ((long)b * Lq + q) * lddo + hd * 64;
+  float s = 0.f;
+#pragma unroll
+  for (int c = 0; c < 8; ++c) {
+    const bf16x8 a = *(const bf16x8*)(o + 8 * c), d = *(const bf16x8*)(g + 8 * c);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s += (float)a[j] * (float)d[j];
+  }
+  delta[idx] = s;   // layout [(b*H + h)*Lq + q]
+}
+
+// dK, dV: one wave = 32 keys (K, V fragments in registers as B operands), q tiles of 64 staged in LDS.
+__global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_bf16(int H, int Lq, int Lk, const bf16* __restrict__ Q,
+                                                             long ldq, const bf16* __restrict__ K, long ldk,
+                                                             const bf16* __restrict__ V, long ldv,
+                                                             const bf16* __restrict__ dO, long lddo,
+                                                             const float* __restrict__ lse,
+                                                             const float* __restrict__ delta, bf16* __restrict__ dK,
+                                                             long lddk, bf16* __restrict__ dV, long lddv, float scale) {
+  __shared__ __attribute__((aligned(16))) char smem[4 * 8192 + 2 * 2 * 64 * 4];
+#define Qs(buf) (smem + 8192 * (buf))
+#define Gs(buf) (smem + 16384 + 8192 * (buf))
+  float* Ls = (float*)(smem + 32768);          // [2][64] lse
+  float* Ds = Ls + 128;                         // [2][64] delta
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5;
+  const int hd = blockIdx.y, b = blockIdx.z;
+  const int k0 = blockIdx.x * 128 + wave * 32;
+  const bf16* Qb = Q + (long)b * Lq * ldq + hd * 64;
+  const bf16* Gb = dO + (long)b * Lq * lddo + hd * 64;
+  const float* lseb = lse + ((long)b * H + hd) * Lq;
+  const float* delb = delta + ((long)b * H + hd) * Lq;
+  const float c = scale * LOG2E;
+
+  const int myk = min(k0 + (lane & 31), Lk - 1);
+  bf16x8 kf[4], vf[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    kf[t] = *(const bf16x8*)(K + ((long)b * Lk + myk) * ldk + hd * 64 + 16 * t + 8 * h);
+    vf[t] = *(const bf16x8*)(V + ((long)b * Lk + myk) * ldv + hd * 64 + 16 * t + 8 * h);
+  }
+  floatx16 dk[2], dv[2];
+#pragma unroll
+  for (int d = 0; d < 2; ++d)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) { dk[d][r] = 0.f; dv[d][r] = 0.f; }
+
+  const int nt = (Lq + 63) / 64;
+  Tile64 tq, tg;
+  float lv = 0.f, dv_ = 0.f;
+  auto load_rows = [&](int qt) {
+    tq.load(Qb, ldq, qt * 64, Lq, tid);
+    tg.load(Gb, lddo, qt * 64, Lq, tid);
+    if (tid < 64) {
+      const int q = qt * 64 + tid;
+      lv = q < Lq ? lseb[q] : INFINITY;
+      dv_ = q < Lq ? delb[q] : 0.f;
+    }
+  };
+  auto store_rows = [&](int buf) {
+    tq.store(Qs(buf), tid);
+    tg.store(Gs(buf), tid);
+    if (tid < 64) { Ls[buf * 64 + tid] = lv; Ds[buf * 64 + tid] = dv_; }
+  };
+  load_rows(0);
+  store_rows(0);
+  __syncthreads();
+  for (int qt = 0; qt < nt; ++qt) {
+    const int cur = qt & 1;
+    const bool more = qt + 1 < nt;
+    if (more) load_rows(qt + 1);
+    const float* L_ = Ls + cur * 64;
+    const float* D_ = Ds + cur * 64;
+#pragma unroll
+    for (int qb = 0; qb < 2; ++qb) {
+      // S = Q·Kᵀ (key on lane), pre-loaded with -lse/c so that p = exp2(c*acc)
+      floatx16 s, dp;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int q = qb * 32 + acc_row(r, h);
+        s[r] = -L_[q] / c;
+        dp[r] = -D_[q];
+      }
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag(Qs(cur), qb * 32, t, lane), kf[t], s, 0, 0, 0);
+        dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag(Gs(cur), qb * 32, t, lane), vf[t], dp, 0, 0, 0);
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float p = exp2f(s[r] * c);
+        s[r] = p;
+        dp[r] = p * dp[r];   // dS = P ∘ (dP − δ)
+      }
+#pragma unroll
+      for (int ss = 0; ss < 2; ++ss) {
+        const bf16x8 pb = pack8(s, ss), db = pack8(dp, ss);
+#pragma unroll
+        for (int d = 0; d < 2; ++d) {
+          dv[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_frag(Gs(cur), qb * 32, ss, d * 32, lane), pb, dv[d], 0, 0, 0);
+          dk[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_frag(Qs(cur), qb * 32, ss, d * 32, lane), db, dk[d], 0, 0, 0);
+        }
+      }
+    }
+    if (more) store_rows(cur ^ 1);
+    __syncthreads();
+  }
+  const int key = k0 + (lane & 31);
+  if (key < Lk) {
+    bf16* krow = dK + ((long)b * Lk + key) * lddk + hd * 64;
+    bf16* vrow = dV + ((long)b * Lk + key) * lddv + hd * 64;
+#pragma unroll
+    for (int d = 0; d < 2; ++d)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        bf16x4 a, v;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) { a[j] = (bf16)(dk[d][4 * g + j] * scale); v[j] = (bf16)dv[d][4 * g + j]; }
+        *(bf16x4*)(krow + d * 32 + 8 * g + 4 * h) = a;
+        *(bf16x4*)(vrow + d * 32 + 8 * g + 4 * h) = v;
+      }
+  }
+}
+
+// dQ: one wave = 32 queries (Q, dO fragments in registers), K/V tiles of 64 keys in LDS.
+__global__ __launch_bounds__(256, 2) void attn_bwd_dq_bf16(int H, int Lq, int Lk, const bf16* __restrict__ Q, long ldq,
+                                                           const bf16* __restrict__ K, long ldk,
+                                                           const bf16* __restrict__ V, long ldv,
+                                                           const bf16* __restrict__ dO, long lddo,
+                                                           const float* __restrict__ lse,
+                                                           const float* __restrict__ delta, bf16* __restrict__ dQ,
+                                                           long lddq, float scale) {
+  __shared__ __attribute__((aligned(16))) char smem[4 * 8192];
+#define Ks(buf) (smem + 8192 * (buf))
+#define Vs(buf) (smem + 16384 + 8192 * (buf))
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5;
+  const int hd = blockIdx.y, b = blockIdx.z;
+  const int q0 = blockIdx.x * 128 + wave * 32;
+  const bf16* Kb = K + (long)b * Lk * ldk + hd * 64;
+  const bf16* Vb = V + (long)b * Lk * ldv + hd * 64;
+  const float c = scale * LOG2E;
+  const int myq = min(q0 + (lane & 31), Lq - 1);
+  bf16x8 qf[4], gf[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    qf[t] = *(const bf16x8*)(Q + ((long)b * Lq + myq) * ldq + hd * 64 + 16 * t + 8 * h);
+    gf[t] = *(const bf16x8*)(dO + ((long)b * Lq + myq) * lddo + hd * 64 + 16 * t + 8 * h);
+  }
+  const float L2 = lse[((long)b * H + hd) * Lq + myq];
+  const float Dl = delta[((long)b * H + hd) * Lq + myq];
+  floatx16 dq[2];
+#pragma unroll
+  for (int d = 0; d < 2; ++d)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) dq[d][r] = 0.f;
+  const int nt = (Lk + 63) / 64;
+  Tile64 tk, tv;
+  tk.load(Kb, ldk, 0, Lk, tid);
+  tv.load(Vb, ldv, 0, Lk, tid);
+  tk.store(Ks(0), tid);
+  tv.store(Vs(0), tid);
+  __syncthreads();
+  for (int kt = 0; kt < nt; ++kt) {
+    const int cur = kt & 1;
+    const bool more = kt + 1 < nt;
+    if (more) {
+      tk.load(Kb, ldk, (kt + 1) * 64, Lk, tid);
+      tv.load(Vb, ldv, (kt + 1) * 64, Lk, tid);
+    }
+    const int kbase = kt * 64;
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+      floatx16 s, dp;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) { s[r] = -L2 / c; dp[r] = -Dl; }
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag(Ks(cur), kb * 32, t, lane), qf[t], s, 0, 0, 0);
+        dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag(Vs(cur), kb * 32, t, lane), gf[t], dp, 0, 0, 0);
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        float p = exp2f(s[r] * c);
+        if (kbase + kb * 32 + acc_row(r, h) >= Lk) p = 0.f;
+        dp[r] = p * dp[r];
+      }
+#pragma unroll
+      for (int ss = 0; ss < 2; ++ss) {
+        const bf16x8 db = pack8(dp, ss);
+#pragma unroll
+        for (int d = 0; d < 2; ++d)
+          dq[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_frag(Ks(cur), kb * 32, ss, d * 32, lane), db, dq[d], 0, 0, 0);
+      }
+    }
+    if (more) {
+      tk.store(Ks(cur ^ 1), tid);
+      tv.store(Vs(cur ^ 1), tid);
+    }
+    __syncthreads();
+  }
+  const int q = q0 + (lane & 31);
+  if (q < Lq) {
+    bf16* row = dQ + ((long)b * Lq + q) * lddq + hd * 64;
+#pragma unroll
+    for (int d = 0; d < 2; ++d)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        bf16x4 v;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] = (bf16)(dq[d][4 * g + j] * scale);
+        *(bf16x4*)(row + d * 32 + 8 * g + 4 * h) = v;
+      }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------------------------
+// exact fp32 path (any head dim <= 64), with optional attention-prob dropout (nn.MultiheadAttention semantics)
+// ---------------------------------------------------------------------------------------------------------------
+__device__ __forceinline__ unsigned hash4(unsigned long long seed, unsigned a, unsigned b, unsigned c) {
+  unsigned long long x = seed ^ (0x9E3779B97F4A7C15ull * (a + 1)) ^ (0xC2B2AE3D27D4EB4Full * (b + 1)) ^
+                         (0x165667B19E3779F9ull * (c + 1));
+  x ^= x >> 33; x *= 0xff51afd7ed558ccdull; x ^= x >> 33; x *= 0xc4ceb9fe1a85ec53ull; x ^= x >> 33;
+  return (unsigned)x;
+}
+// keep-mask for attention prob (bh, q, k): keep iff hash >= p * 2^32
+__device__ __forceinline__ float drop_scale(unsigned long long seed, float p, unsigned bh, unsigned q, unsigned k) {
+  if (p <= 0.f) return 1.f;
+  const float u = (float)hash4(seed, bh, q, k) * 2.3283064365386963e-10f;
+  return u >= p ? 1.f / (1.f - p) : 0.f;
+}
+
+template <int D>
+__global__ void attn_fwd_f32(int H, int Lq, int Lk, const float* __restrict__ Q, long ldq, const float* __restrict__ K,
+                             long ldk, const float* __restrict__ V, long ldv, float* __restrict__ O, long ldo,
+                             float* __restrict__ lse, float scale, float pdrop, unsigned long long seed) {
+  const int hd = blockIdx.y, b = blockIdx.z;
+  const int q = blockIdx.x * blockDim.x + threadIdx.x;
+  __shared__ float sK[64][D], sV[64][D];
+  float qv[D], o[D];
+  const bool active = q < Lq;
+  const int qq = active ? q : 0;
+#pragma unroll
+  for (int d = 0; d < D; ++d) { qv[d] = Q[((long)b * Lq + qq) * ldq + hd * D + d] * scale; o[d] = 0.f; }
+  float m = -INFINITY, l = 0.f;
+  const unsigned bh = b * H + hd;
+  for (int k0 = 0; k0 < Lk; k0 += 64) {
+    __syncthreads();
+    for (int i = threadIdx.x; i < 64 * D; i += blockDim.x) {
+      const int kk = i / D, d = i % D;
+      const bool ok = k0 + kk < Lk;
+      sK[kk][d] = ok ? K[((long)b * Lk + k0 + kk) * ldk + hd * D + d] : 0.f;
+      sV[kk][d] = ok ? V[((long)b * Lk + k0 + kk) * ldv + hd * D + d] : 0.f;
+    }
+    __syncthreads();
+    const int kn = min(64, Lk - k0);
+    for (int kk = 0; kk < kn; ++kk) {
+      float s = 0.f;
+#pragma unroll
+      for (int d = 0; d < D; ++d) s = fmaf(qv[d], sK[kk][d], s);
+      const float mn = fmaxf(m, s);
+      const float alpha = __expf(m - mn);
+      const float p = __expf(s - mn);
+      l = l * alpha + p;
+      const float pd = p * drop_scale(seed, pdrop, bh, qq, k0 + kk);
+#pragma unroll
+      for (int d = 0; d < D; ++d) o[d] = o[d] * alpha + pd * sV[kk][d];
+      m = mn;
+    }
+  }
+  if (active) {
+#pragma unroll
+    for (int d = 0; d < D; ++d) O[((long)b * Lq + q) * ldo + hd * D + d] = o[d] / l;
+    lse[((long)bh) * Lq + q] = m + __logf(l);     // natural-log LSE of scale*s
+  }
+}
+
+template <int D>
+__global__ void attn_bwd_dq_f32(int H, int Lq, int Lk, const float* __restrict__ Q, long ldq, const float* __restrict__ K,
+                                long ldk, const float* __restrict__ V, long ldv, const float* __restrict__ O, long ldo,
+                                const float* __restrict__ dO, long lddo, const float* __restrict__ lse,
+                                float* __restrict__ delta_out, float* __restrict__ dQ, long lddq, float scale,
+                                float pdrop, unsigned long long seed) {
+  const int hd = blockIdx.y, b = blockIdx.z;
+  const int q = blockIdx.x * blockDim.x + threadIdx.x;
+  __shared__ float sK[64][D], sV[64][D];
+  const bool active = q < Lq;
+  const int qq = active ? q : 0;
+  const unsigned bh = b * H + hd;
+  float qv[D], g[D], dq[D];
+  float delta = 0.f;
+#pragma unroll
+  for (int d = 0; d < D; ++d) {
+    qv[d] = Q[((long)b * Lq + qq) * ldq + hd * D + d] * scale;
+    g[d] = dO[((long)b * Lq + qq) * lddo + hd * D + d];
+    delta += g[d] * O[((long)b * Lq + qq) * ldo + hd * D + d];
+    dq[d] = 0.f;
+  }
+  const float L = lse[(long)bh * Lq + qq];
+  for (int k0 = 0; k0 < Lk; k0 += 64) {
+    __syncthreads();
+    for (int i = threadIdx.x; i < 64 * D; i += blockDim.x) {
+      const int kk = i / D, d = i % D;
+      const bool ok = k0 + kk < Lk;
+      sK[kk][d] = ok ? K[((long)b * Lk + k0 + kk) * ldk + hd * D + d] : 0.f;
+      sV[kk][d] = ok ? V[((long)b * Lk + k0 + kk) * ldv + hd * D + d] : 0.f;
+    }
+    __syncthreads();
+    const int kn = min(64, Lk - k0);
+    for (int kk = 0; kk < kn; ++kk) {
+      float s = 0.f, dp = 0.f;
+#pragma unroll
+      for (int d = 0; d < D; ++d) { s = fmaf(qv[d], sK[kk][d], s); dp = fmaf(g[d], sV[kk][d], dp); }
+      const float p = __expf(s - L);
+      const float ds = p * (dp * drop_scale(seed, pdrop, bh, qq, k0 + kk) - delta);
+#pragma unroll
+      for (int d = 0; d < D; ++d) dq[d] = fmaf(ds, sK[kk][d], dq[d]);
+    }
+  }
+  if (active) {
+#pragma unroll
+    for (int d = 0; d < D; ++d) dQ[((long)b * Lq + q) * lddq + hd * D + d] = dq[d] * scale;
+    delta_out[(long)bh * Lq + q] = delta;
+  }
+}
+
+template <int D>
+__global__ void attn_bwd_dkdv_f32(int H, int Lq, int Lk, const float* __restrict__ Q, long ldq,
+                                  const float* __restrict__ K, long ldk, const float* __restrict__ V, long ldv,
+                                  const float* __restrict__ dO, long lddo, const float* __restrict__ lse,
+                                  const float* __restrict__ delta, float* __restrict__ dK, long lddk,
+                                  float* __restrict__ dV, long lddv, float scale, float pdrop,
+                                  unsigned long long seed) {
+  const int hd = blockIdx.y, b = blockIdx.z;
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  __shared__ float sQ[64][D], sG[64][D], Ls[64], Ds[64];
+  const bool active = k < Lk;
+  const int kk = active ? k : 0;
+  const unsigned bh = b * H + hd;
+  float kv[D], vv[D], dk[D], dv[D];
+#pragma unroll
+  for (int d = 0; d < D; ++d) {
+    kv[d] = K[((long)b * Lk + kk) * ldk + hd * D + d];
+    vv[d] = V[((long)b * Lk + kk) * ldv + hd * D + d];
+    dk[d] = 0.f;
+    dv[d] = 0.f;
+  }
+  for (int q0 = 0; q0 < Lq; q0 += 64) {
+    __syncthreads();
+    for (int i = threadIdx.x; i < 64 * D; i += blockDim.x) {
+      const int qi = i / D, d = i % D;
+      const bool ok = q0 + qi < Lq;
+      sQ[qi][d] = ok ? Q[((long)b * Lq + q0 + qi) * ldq + hd * D + d] * scale : 0.f;
+      sG[qi][d] = ok ? dO[((long)b * Lq + q0 + qi) * lddo + hd * D + d] : 0.f;
+    }
+    for (int i = threadIdx.x; i < 64; i += blockDim.x) {
+      const bool ok = q0 + i < Lq;
+      Ls[i] = ok ? lse[(long)bh * Lq + q0 + i] : 0.f;
+      Ds[i] = ok ? delta[(long)bh * Lq + q0 + i] : 0.f;
+    }
+    __syncthreads();
+    const int qn = min(64, Lq - q0);
+    for (int qi = 0; qi < qn; ++qi) {
+      float s = 0.f, dp = 0.f;
+#pragma unroll
+      for (int d = 0; d < D; ++d) { s = fmaf(sQ[qi][d], kv[d], s); dp = fmaf(sG[qi][d], vv[d], dp); }
+      const float p = __expf(s - Ls[qi]);
+      const float ms = drop_scale(seed, pdrop, bh, q0 + qi, kk);
+      const float ds = p * (dp * ms - Ds[qi]);
+#pragma unroll
+      for (int d = 0; d < D; ++d) {
+        dv[d] = fmaf(p * ms, sG[qi][d], dv[d]);
+        dk[d] = fmaf(ds, sQ[qi][d], dk[d]);     // Qs already carries the scale
+      }
+    }
+  }
+  if (active) {
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      dK[((long)b * Lk + k) * lddk + hd * D + d] = dk[d];
+      dV[((long)b * Lk + k) * lddv + hd * D + d] = dv[d];
+    }
+  }
+}
+
+#undef Ks
+#undef Vs
+#undef Qs
+#undef Gs
+}  // namespace
+
+// ----------------------------------------------------------------------------------------------------------------
+// C ABI.  Tensors are [B*L, ld] row-major with head h at columns h*D .. h*D+D-1.
+// lse / delta: fp32 [B*H*Lq] workspaces owned by the caller.
+// ----------------------------------------------------------------------------------------------------------------
+extern "C" int cmhar_attention_fwd(int dtype, int B, int H, int Lq, int Lk, int D, const void* Q, long ldq,
+                                   const void* K, long ldk, const void* V, long ldv, void* O, long ldo, float* lse,
+                                   float scale, float pdrop, unsigned long long seed, hipStream_t st) {
+  if (B <= 0 || Lq <= 0) return 0;
+  if (dtype == CMHAR_BF16) {
+    if (D != 64 || pdrop != 0.f) return -1;
+    dim3 grid(cdiv(Lq, 128), H, B);
+    attn_fwd_bf16<<<grid, 256, 0, st>>>(H, Lq, Lk, (const bf16*)Q, ldq, (const bf16*)K, ldk, (const bf16*)V, ldv,
+                                        (bf16*)O, ldo, lse, scale);
+  } else {
+    dim3 grid(cdiv(Lq, 64), H, B);
+#define F(DD) attn_fwd_f32<DD><<<grid, 64, 0, st>>>(H, Lq, Lk, (const float*)Q, ldq, (const float*)K, ldk, \
+                                                    (const float*)V, ldv, (float*)O, ldo, lse, scale, pdrop, seed)
+    switch (D) { case 16: F(16); break; case 32: F(32); break; case 64: F(64); break; case 8: F(8); break; default: return -1; }
+#undef F
+  }
+  CMHAR_CHECK_LAUNCH();
+  return 0;
+}
+
+// Backward.  delta: fp32 [B*H*Lq] workspace (written here).
+extern "C" int cmhar_attention_bwd(int dtype, int B, int H, int Lq, int Lk, int D, const void* Q, long ldq,
+                                   const void* K, long ldk, const void* V, long ldv, const void* O, long ldo,
+                                   const void* dO, long lddo, const float* lse, float* delta, void* dQ, long lddq,
+                                   void* dK, long lddk, void* dV, long lddv, float scale, float pdrop,
+                                   unsigned long long seed, hipStream_t st) {
+  if (B <= 0 || Lq <= 0) return 0;
+  if (dtype == CMHAR_BF16) {
+    if (D != 64 || pdrop != 0.f) return -1;
+    const long n = (long)B * H * Lq;
+    attn_bwd_delta<<<cdiv(n, 256), 256, 0, st>>>(H, Lq, (const bf16*)O, ldo, (const bf16*)dO, lddo, delta, B);
+    attn_bwd_dq_bf16<<<dim3(cdiv(Lq, 128), H, B), 256, 0, st>>>(H, Lq, Lk, (const bf16*)Q, ldq, (const bf16*)K, ldk,
+                                                                (const bf16*)V, ldv, (const bf16*)dO, lddo, lse, delta,
+                                                                (bf16*)dQ, lddq, scale);
+    attn_bwd_dkdv_bf16<<<dim3(cdiv(Lk, 128), H, B), 256, 0, st>>>(H, Lq, Lk, (const bf16*)Q, ldq, (const bf16*)K, ldk,
+                                                                  (const bf16*)V, ldv, (const bf16*)dO, lddo, lse,
+                                                                  delta, (bf16*)dK, lddk, (bf16*)dV, lddv, scale);
+  } else {
+#define F(DD)                                                                                                      \
+  attn_bwd_dq_f32<DD><<<dim3(cdiv(Lq, 64), H, B), 64, 0, st>>>(H, Lq, Lk, (const float*)Q, ldq, (const float*)K,     \
+                                                               ldk, (const float*)V, ldv, (const float*)O, ldo,     \
+                                                               (const float*)dO, lddo, lse, delta, (float*)dQ,      \
+                                                               lddq, scale, pdrop, seed);                           \
+  attn_bwd_dkdv_f32<DD><<<dim3(cdiv(Lk, 64), H, B), 64, 0, st>>>(H, Lq, Lk, (const float*)Q, ldq, (const float*)K,   \
+                                                                 ldk, (const float*)V, ldv, (const float*)dO, lddo, \
+                                                                 lse, delta, (float*)dK, lddk, (float*)dV, lddv,    \
+                                                                 scale, pdrop, seed)
+    switch (D) { case 16: F(16); break; case 32: F(32); break; case 64: F(64); break; case 8: F(8); break; default: return -1; }
+#undef F
+  }
+  CMHAR_CHECK_LAUNCH();
+  return 0;
+}

@@ -1,0 +1,91 @@
+// Shared device helpers for the cmhar HIP library (gfx950 / CDNA4 only).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef __bf16 bf16;
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+typedef __attribute__((ext_vector_type(4))) short short4_t;
+typedef __attribute__((ext_vector_type(8))) short short8_t;
+typedef __attribute__((ext_vector_type(4))) float floatx4;
+typedef __attribute__((ext_vector_type(16))) float floatx16;
+typedef __attribute__((ext_vector_type(4))) unsigned uint4_t;
+typedef __attribute__((ext_vector_type(2))) unsigned uint2_t;
+
+#define LDS_PTR(T, p) ((__attribute__((address_space(3))) T*)(p))
+
+// dtype codes used across the C ABI
+enum { CMHAR_F32 = 0, CMHAR_BF16 = 1 };
+
+// activation / epilogue codes
+enum {
+  ACT_NONE = 0,
+  ACT_GELU = 1,        // out = gelu_erf(acc + bias); aux_out (optional) = acc + bias
+  ACT_RELU = 2,        // out = relu(acc + bias)
+  ACT_DGELU = 3,       // out = acc * gelu_erf'(aux_in)
+  ACT_DRELU = 4,       // out = acc * (aux_in > 0)
+};
+
+// The epilogue struct is part of the C ABI (include/cmhar.h); every extern "C" definition in csrc/ is checked
+// against its declaration there because each translation unit includes the header.
+#include "cmhar.h"
+typedef CmharEpilogue Epilogue;
+
+__device__ __forceinline__ float bf2f(bf16 x) { return (float)x; }
+__device__ __forceinline__ bf16 f2bf(float x) { return (bf16)x; }
+
+template <typename T> __device__ __forceinline__ float to_f(T x);
+template <> __device__ __forceinline__ float to_f<float>(float x) { return x; }
+template <> __device__ __forceinline__ float to_f<bf16>(bf16 x) { return (float)x; }
+template <typename T> __device__ __forceinline__ T from_f(float x);
+template <> __device__ __forceinline__ float from_f<float>(float x) { return x; }
+template <> __device__ __forceinline__ bf16 from_f<bf16>(float x) { return (bf16)x; }
+
+__device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
+__device__ __forceinline__ float gelu_erf_grad(float x) {
+  const float cdf = 0.5f * (1.0f + erff(x * 0.70710678118654752f));
+  const float pdf = 0.39894228040143268f * __expf(-0.5f * x * x);
+  return cdf + x * pdf;
+}
+
+// Counter-hash dropout mask shared by every kernel that applies or regenerates an element dropout:
+// keep (m, n) iff hash(seed, m, n) / 2^32 >= p; kept values are scaled by 1/(1-p) (nn.Dropout semantics).
+__device__ __forceinline__ unsigned drop_hash(unsigned long long seed, unsigned long long a, unsigned b) {
+  unsigned long long x = seed ^ (0x9E3779B97F4A7C15ull * (a + 1)) ^ (0xC2B2AE3D27D4EB4Full * (b + 1));
+  x ^= x >> 33; x *= 0xff51afd7ed558ccdull; x ^= x >> 33; x *= 0xc4ceb9fe1a85ec53ull; x ^= x >> 33;
+  return (unsigned)x;
+}
+__device__ __forceinline__ float drop_mask(unsigned long long seed, float p, long row, int col) {
+  if (p <= 0.f) return 1.f;
+  const float u = (float)drop_hash(seed, (unsigned long long)row, (unsigned)col) * 2.3283064365386963e-10f;
+  return u >= p ? 1.f / (1.f - p) : 0.f;
+}
+
+// Apply the epilogue to one accumulator element at (m, n).  OutT = float or bf16.
+template <typename OutT>
+__device__ __forceinline__ void epilogue_store(const Epilogue& e, OutT* __restrict__ C, long ldc, int m, int n,
+                                               float acc) {
+  float v = e.alpha * acc;
+  if (e.bias) v += e.bias[n];
+  if (e.rowadd) v += e.rowadd[(long)(m % e.rowadd_mod) * e.rowadd_ld + n];
+  switch (e.act) {
+    case ACT_GELU:
+      if (e.aux_out) ((OutT*)e.aux_out)[(long)m * e.ldo + n] = from_f<OutT>(v);
+      v = gelu_erf(v);
+      break;
+    case ACT_RELU: v = v > 0.f ? v : 0.f; break;
+    case ACT_DGELU: v *= gelu_erf_grad(to_f<OutT>(((const OutT*)e.aux_in)[(long)m * e.lda + n])); break;
+    case ACT_DRELU: v = to_f<OutT>(((const OutT*)e.aux_in)[(long)m * e.lda + n]) > 0.f ? v : 0.f; break;
+    default: break;
+  }
+  if (e.pdrop > 0.f) v *= drop_mask(e.seed, e.pdrop, m, n);
+  if (e.residual) v += to_f<OutT>(((const OutT*)e.residual)[(long)m * e.ldr + n]);
+  OutT* p = C + (long)m * ldc + n;
+  if (e.beta != 0.f) v += e.beta * to_f<OutT>(*p);
+  *p = from_f<OutT>(v);
+}
+
+#define CMHAR_CHECK_LAUNCH() do { hipError_t _e = hipGetLastError(); if (_e != hipSuccess) return (int)_e; } while (0)
+
+static inline int cdiv(long a, long b) { return (int)((a + b - 1) / b); }

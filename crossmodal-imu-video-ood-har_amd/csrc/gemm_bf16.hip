@@ -1,0 +1,222 @@
+// bf16 MFMA GEMM for gfx950 with fused epilogues — the VideoMAE Linear / tubelet-conv hot path.
+//
+// C[m,n] = epilogue( sum_k A(m,k) * B(k,n) ), bf16 operands, fp32 accumulation in MFMA accumulators.
+// Operand layouts are template parameters so that ONE kernel body covers the three GEMMs of a Linear:
+//   forward  Y  = X  · Wᵀ : A = X  [M][K] (K-contiguous), B = W  [N][K] (K-contiguous)
+//   dgrad    dX = dY · W  : A = dY [M][N] (K-contiguous), B = W  [N][K] (N-contiguous: contraction on rows)
+//   wgrad    dW = dYᵀ· X  : A = dY [M][N] (M-contiguous), B = X  [M][K] (K-contiguous ... along rows)
+// K-contiguous tiles are read with ds_read_b128; row-contraction tiles with the gfx950 transposing
+// ds_read_b64_tr_b16, so no operand is ever transposed in HBM.
+//
+// Tile 128x128x64, 256 threads = 4 waves (2x2, 64x64 per wave = 4x4 mfma_f32_16x16x32_bf16), LDS double buffer
+// (2 x 32 KiB), register-staged global->LDS copy with XOR-swizzled images (bank-conflict-free for both read
+// kinds), one barrier per K-tile, XCD-aware block remap.  Split-K writes fp32 partial slabs that
+// cmhar_splitk_reduce combines with the epilogue.
+#include "common.h"
+
+namespace {
+
+constexpr int BM = 128, BN = 128, BK = 64, NT = 256;
+
+// K-contiguous image: [128 rows][64 k] = 8 chunks of 16 B per row; chunk ^= (row>>1)&7.
+__device__ __forceinline__ int kc_off(int row, int chunk) { return row * 128 + ((chunk ^ ((row >> 1) & 7)) << 4); }
+// Row-contraction image: [64 k][128 cols] = 16 chunks per row; chunk ^= 2*((k&3) | ((k>>3)&1)<<2).
+__device__ __forceinline__ int mc_swz(int k) { return ((k & 3) | (((k >> 3) & 1) << 2)) << 1; }
+__device__ __forceinline__ int mc_off(int k, int chunk) { return k * 256 + ((chunk ^ mc_swz(k)) << 4); }
+
+template <bool KC>
+struct Stage {
+  uint4_t r[4];
+  // Load this operand's tile (rows r0.., k0..) into registers; rows = M or N index.
+  __device__ __forceinline__ void load(const bf16* __restrict__ P, long ld, int rows_total, int r0, int k0,
+                                       int kend, int tid) {
+#pragma unroll
+    for (int it = 0; it < 4; ++it) {
+      const int c = it * NT + tid;
+      int row, kk;
+      if (KC) { row = c >> 3; kk = (c & 7) * 8; } else { kk = c >> 4; row = (c & 15) * 8; }
+      const int gr = r0 + row, gk = k0 + kk;
+      bool ok = KC ? (gr < rows_total && gk < kend) : (gk < kend && gr < rows_total);
+      const bf16* src = KC ? (P + (long)gr * ld + gk) : (P + (long)gk * ld + gr);
+      if (ok) r[it] = *(const uint4_t*)src;
+      else r[it] = uint4_t{0u, 0u, 0u, 0u};
+    }
+  }
+  __device__ __forceinline__ void store(char* lds, int tid) const {
+#pragma unroll
+    for (int it = 0; it < 4; ++it) {
+      const int c = it * NT + tid;
+      int off;
+      if (KC) off = kc_off(c >> 3, c & 7); else off = mc_off(c >> 4, c & 15);
+      *(uint4_t*)(lds + off) = r[it];
+    }
+  }
+};
+
+// Fragment of 16 rows (r0 + lane&15) x 32 k (kk*32 + 8*(lane>>4) + j) for the 16x16x32 MFMA.
+template <bool KC>
+__device__ __forceinline__ bf16x8 frag(const char* lds, int r0, int kk, int lane) {
+  if (KC) {
+    const int row = r0 + (lane & 15);
+    const int chunk = kk * 4 + (lane >> 4);
+    return *(const bf16x8*)(lds + kc_off(row, chunk));
+  } else {
+    const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+    const int chunk = (r0 >> 3) + (p >> 1);
+    short4_t lo, hi;
+    {
+      const int k = kk * 32 + 8 * g + q;
+      lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(short4_t, lds + mc_off(k, chunk) + (p & 1) * 8));
+    }
+    {
+      const int k = kk * 32 + 8 * g + 4 + q;
+      hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(short4_t, lds + mc_off(k, chunk) + (p & 1) * 8));
+    }
+    short8_t v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    return __builtin_bit_cast(bf16x8, v);
+  }
+}
+
+__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
+  const int q = nwg / 8, r = nwg % 8, xcd = bid % 8;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8;
+}
+
+template <bool A_KC, bool B_KC, typename OutT>
+__global__ __launch_bounds__(NT, 2) void gemm_bf16_kernel(int M, int N, int K, const bf16* __restrict__ A, long lda,
+                                                          const bf16* __restrict__ B, long ldb,
+                                                          OutT* __restrict__ C, long ldc, Epilogue e, int klen,
+                                                          long split_stride, int raw_out) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  // stage buffers: A at smem + 16K*buf, B at smem + 32K + 16K*buf
+#define As(buf) (smem + 16384 * (buf))
+#define Bs(buf) (smem + 32768 + 16384 * (buf))
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wr = wave >> 1, wc = wave & 1;
+  const int tiles_n = (N + BN - 1) / BN, tiles_m = (M + BM - 1) / BM;
+  const int bid = xcd_remap(blockIdx.x, tiles_m * tiles_n);
+  // column-major tile order within a split: consecutive blocks share the same B (weight) panel
+  const int tn = bid / tiles_m, tm = bid % tiles_m;
+  const int bm = tm * BM, bn = tn * BN;
+  const int kbeg = blockIdx.z * klen;
+  const int kend = min(K, kbeg + klen);
+  C += (long)blockIdx.z * split_stride;
+
+  floatx4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+  Stage<A_KC> sa;
+  Stage<B_KC> sb;
+  const int nk = (kend - kbeg + BK - 1) / BK;
+  if (nk > 0) {
+    sa.load(A, lda, M, bm, kbeg, kend, tid);
+    sb.load(B, ldb, N, bn, kbeg, kend, tid);
+    sa.store(As(0), tid);
+    sb.store(Bs(0), tid);
+  }
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    const bool more = kt + 1 < nk;
+    if (more) {
+      sa.load(A, lda, M, bm, kbeg + (kt + 1) * BK, kend, tid);
+      sb.load(B, ldb, N, bn, kbeg + (kt + 1) * BK, kend, tid);
+    }
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      bf16x8 af[4], bfr[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) af[i] = frag<A_KC>(As(cur), wr * 64 + i * 16, kk, lane);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bfr[j] = frag<B_KC>(Bs(cur), wc * 64 + j * 16, kk, lane);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+    if (more) {
+      sa.store(As(cur ^ 1), tid);
+      sb.store(Bs(cur ^ 1), tid);
+    }
+    __syncthreads();
+  }
+
+  // epilogue: lane holds rows 4*(lane>>4)+r, column lane&15 of each 16x16 block
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = bm + wr * 64 + i * 16 + 4 * (lane >> 4) + r;
+        const int n = bn + wc * 64 + j * 16 + (lane & 15);
+        if (m < M && n < N) {
+          if (raw_out) ((float*)C)[(long)m * ldc + n] = acc[i][j][r];
+          else epilogue_store<OutT>(e, C, ldc, m, n, acc[i][j][r]);
+        }
+      }
+}
+
+#undef As
+#undef Bs
+
+// Sum split-K fp32 partial slabs and apply the epilogue.
+template <typename OutT>
+__global__ void splitk_reduce_kernel(int M, int N, int splits, const float* __restrict__ P, long split_stride,
+                                     OutT* __restrict__ C, long ldc, Epilogue e) {
+  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long total = (long)M * N;
+  if (idx >= total) return;
+  const int m = (int)(idx / N), n = (int)(idx % N);
+  float s = 0.f;
+  for (int z = 0; z < splits; ++z) s += P[z * split_stride + idx];
+  epilogue_store<OutT>(e, C, ldc, m, n, s);
+}
+
+template <bool AK, bool BKc, typename OutT>
+int launch(int M, int N, int K, const bf16* A, long lda, const bf16* B, long ldb, OutT* C, long ldc,
+           const Epilogue& e, int splits, float* ws, hipStream_t st) {
+  const int tiles = cdiv(M, BM) * cdiv(N, BN);
+  int klen = K;
+  if (splits > 1) klen = cdiv(cdiv(K, splits), BK) * BK;
+  const int nsplit = cdiv(K, klen);
+  dim3 grid(tiles, 1, nsplit);
+  const size_t lds = 65536;
+  if (nsplit == 1) {
+    gemm_bf16_kernel<AK, BKc, OutT><<<grid, NT, lds, st>>>(M, N, K, A, lda, B, ldb, C, ldc, e, klen, 0, 0);
+  } else {
+    if (!ws) return -2;
+    const long ss = (long)M * N;
+    gemm_bf16_kernel<AK, BKc, float><<<grid, NT, lds, st>>>(M, N, K, A, lda, B, ldb, ws, N, e, klen, ss, 1);
+    const long total = (long)M * N;
+    splitk_reduce_kernel<OutT><<<cdiv(total, 256), 256, 0, st>>>(M, N, nsplit, ws, ss, C, ldc, e);
+  }
+  CMHAR_CHECK_LAUNCH();
+  return 0;
+}
+
+}  // namespace
+
+// layout: 0 = NT (A K-contig, B K-contig: Y = X Wᵀ), 1 = NN (A K-contig, B N-contig: dX = dY W),
+//         2 = TN (A M-contig, B N-contig: dW = dYᵀ X).  ws: fp32 workspace of splits*M*N floats when splits > 1.
+extern "C" int cmhar_gemm_bf16(int layout, int out_dtype, int M, int N, int K, const void* A, long lda, const void* B,
+                               long ldb, void* C, long ldc, const Epilogue* epi, int splits, void* ws,
+                               hipStream_t stream) {
+  if (M <= 0 || N <= 0) return 0;
+  const bf16* a = (const bf16*)A;
+  const bf16* b = (const bf16*)B;
+  float* w = (float*)ws;
+#define DISPATCH(AK, BKc)                                                                                     \
+  return out_dtype == CMHAR_BF16 ? launch<AK, BKc, bf16>(M, N, K, a, lda, b, ldb, (bf16*)C, ldc, *epi, splits, w, stream) \
+                                 : launch<AK, BKc, float>(M, N, K, a, lda, b, ldb, (float*)C, ldc, *epi, splits, w, stream)
+  switch (layout) {
+    case 0: DISPATCH(true, true);
+    case 1: DISPATCH(true, false);
+    case 2: DISPATCH(false, false);
+    default: return -1;
+  }
+#undef DISPATCH
+}

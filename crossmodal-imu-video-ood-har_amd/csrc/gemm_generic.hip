@@ -1,0 +1,80 @@
+// Generic strided GEMM with fp32 accumulation (VALU FMA, LDS-tiled).
+//
+// Used for (a) the exact-fp32 parity mode of every Linear on the path and (b) the small, latency-bound
+// GEMMs of the IMU encoder / projection heads (M = batch*13 or batch rows), where an MFMA tile would idle.
+// C[m,n] = epilogue( sum_k A[m*sam + k*sak] * B[k*sbk + n*sbn] ), batched over blockIdx.z.
+#include "common.h"
+
+namespace {
+
+constexpr int TM = 64, TN = 64, TK = 16;
+
+template <typename TIn, typename TOut>
+__global__ __launch_bounds__(256) void gemm_generic_kernel(
+    int M, int N, int K, const TIn* __restrict__ A, long sam, long sak, long sAb, const TIn* __restrict__ B,
+    long sbk, long sbn, long sBb, TOut* __restrict__ C, long ldc, long sCb, Epilogue e) {
+  __shared__ float As[TK][TM + 4];
+  __shared__ float Bs[TK][TN + 4];
+  const int tid = threadIdx.x;
+  const int bm = blockIdx.y * TM, bn = blockIdx.x * TN;
+  A += blockIdx.z * sAb;
+  B += blockIdx.z * sBb;
+  C += blockIdx.z * sCb;
+  const int tr = tid / 16, tc = tid % 16;   // 16x16 threads, 4x4 outputs each
+  float acc[4][4] = {};
+  for (int k0 = 0; k0 < K; k0 += TK) {
+    for (int i = tid; i < TM * TK; i += 256) {
+      // A tile: choose the faster-varying index along the contiguous dimension
+      int mm, kk;
+      if (sak == 1) { mm = i / TK; kk = i % TK; } else { kk = i / TM; mm = i % TM; }
+      const int gm = bm + mm, gk = k0 + kk;
+      As[kk][mm] = (gm < M && gk < K) ? to_f<TIn>(A[gm * sam + gk * sak]) : 0.f;
+    }
+    for (int i = tid; i < TN * TK; i += 256) {
+      int nn, kk;
+      if (sbn == 1) { kk = i / TN; nn = i % TN; } else { nn = i / TK; kk = i % TK; }
+      const int gn = bn + nn, gk = k0 + kk;
+      Bs[kk][nn] = (gn < N && gk < K) ? to_f<TIn>(B[gk * sbk + gn * sbn]) : 0.f;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int kk = 0; kk < TK; ++kk) {
+      float a[4], b[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) { a[i] = As[kk][tr + 16 * i]; b[i] = Bs[kk][tc + 16 * i]; }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = fmaf(a[i], b[j], acc[i][j]);
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int m = bm + tr + 16 * i, n = bn + tc + 16 * j;
+      if (m < M && n < N) epilogue_store<TOut>(e, C, ldc, m, n, acc[i][j]);
+    }
+}
+
+}  // namespace
+
+extern "C" int cmhar_gemm_generic(int in_dtype, int out_dtype, int M, int N, int K, int batch, const void* A,
+                                  long sam, long sak, long sAb, const void* B, long sbk, long sbn, long sBb, void* C,
+                                  long ldc, long sCb, const Epilogue* epi, hipStream_t stream) {
+  if (M <= 0 || N <= 0 || batch <= 0) return 0;
+  Epilogue e = *epi;
+  dim3 grid(cdiv(N, TN), cdiv(M, TM), batch);
+#define LAUNCH(TI, TO)                                                                                     \
+  gemm_generic_kernel<TI, TO><<<grid, 256, 0, stream>>>(M, N, K, (const TI*)A, sam, sak, sAb, (const TI*)B, \
+                                                        sbk, sbn, sBb, (TO*)C, ldc, sCb, e)
+  if (in_dtype == CMHAR_F32 && out_dtype == CMHAR_F32) LAUNCH(float, float);
+  else if (in_dtype == CMHAR_BF16 && out_dtype == CMHAR_BF16) LAUNCH(bf16, bf16);
+  else if (in_dtype == CMHAR_BF16 && out_dtype == CMHAR_F32) LAUNCH(bf16, float);
+  else if (in_dtype == CMHAR_F32 && out_dtype == CMHAR_BF16) LAUNCH(float, bf16);
+  else return -1;
+#undef LAUNCH
+  CMHAR_CHECK_LAUNCH();
+  return 0;
+}

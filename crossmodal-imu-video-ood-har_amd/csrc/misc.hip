@@ -1,0 +1,311 @@
+// Data-movement kernels around the hot path: tubelet patch extraction (VideoMAE Conv3d as GEMM), the IMU
+// PatchTST embedding, strided copies with dtype conversion, and the multi-tensor optimizer step
+// (clip_grad_norm_ + AdamW, trainer.py:138-141) with fused bf16 shadow-weight refresh.
+#include "common.h"
+
+namespace {
+
+// video (B, T, C, H, W) fp32 → patches [B*L][C*tub*P*P] (row order (t', h', w'), column order (c, dt, dy, dx) —
+// the flatten order of Conv3d weight [hidden, C, tub, P, P], modeling_videomae.py:159-168).
+template <typename TO>
+__global__ void tubelet_im2col_kernel(int B, int T, int C, int H, int W, int tub, int P, const float* __restrict__ v,
+                                      TO* __restrict__ out) {
+  const int Tp = T / tub, Hp = H / P, Wp = W / P;
+  const long L = (long)Tp * Hp * Wp;
+  const int K = C * tub * P * P;
+  const int groups = P / 8;                  // 8 consecutive dx per thread
+  const long total = (long)B * L * C * tub * P * groups;
+  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= total) return;
+  long r = idx;
+  const int gx = r % groups; r /= groups;
+  const int dy = r % P; r /= P;
+  const int dt = r % tub; r /= tub;
+  const int c = r % C; r /= C;
+  const long tok = r % L;
+  const int b = r / L;
+  const int wp = tok % Wp, hp = (tok / Wp) % Hp, tp = tok / ((long)Wp * Hp);
+  const float* src = v + ((((long)b * T + tp * tub + dt) * C + c) * H + hp * P + dy) * W + wp * P + gx * 8;
+  TO* dst = out + ((long)b * L + tok) * K + ((c * tub + dt) * P + dy) * P + gx * 8;
+  const floatx4 x0 = *(const floatx4*)src, x1 = *(const floatx4*)(src + 4);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) { dst[j] = from_f<TO>(x0[j]); dst[4 + j] = from_f<TO>(x1[j]); }
+}
+
+struct PtrTable8 { const float* p[8]; };
+struct MutPtrTable8 { float* p[8]; };
+
+// IMU PatchTST embedding + CLS + positional table, truncated to T tokens (models.py:40-49, 115-123).
+// token 0 = cls + pos[0]; token 1+t (t < T-1) = channel c = t / N, patch n = t % N.
+__global__ void imu_embed_fwd_kernel(int B, int C, int L, int N, int P, int S, int D, int T,
+                                     const float* __restrict__ x, PtrTable8 w, PtrTable8 bias,
+                                     const float* __restrict__ cls, const float* __restrict__ pos,
+                                     float* __restrict__ out) {
+  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (long)B * T * D) return;
+  const int d = idx % D;
+  const int tok = (idx / D) % T;
+  const int b = idx / ((long)D * T);
+  float v;
+  if (tok == 0) v = cls[d];
+  else {
+    const int t = tok - 1, c = t / N, n = t % N;
+    const float* xs = x + ((long)b * C + c) * L + (long)n * S;
+    const float* wr = w.p[c] + (long)d * P;
+    v = bias.p[c][d];
+    for (int p = 0; p < P; ++p) v = fmaf(xs[p], wr[p], v);
+  }
+  out[idx] = v + pos[(long)tok * D + d];
+}
+
+// Gradients: dcls, dpos[0:T] (rest of the table untouched → zero), dW_c, db_c (channels without live tokens → 0).
+__global__ void imu_embed_bwd_kernel(int B, int C, int L, int N, int P, int S, int D, int T, int Tpos,
+                                     const float* __restrict__ x, const float* __restrict__ dout,
+                                     float* __restrict__ dcls, float* __restrict__ dpos, MutPtrTable8 dw,
+                                     MutPtrTable8 db) {
+  const int d = blockIdx.x * blockDim.x + threadIdx.x;
+  if (d >= D) return;
+  const int which = blockIdx.y;   // 0: cls/pos, 1..C: channel which-1
+  if (which == 0) {
+    for (int tok = 0; tok < Tpos; ++tok) {
+      float s = 0.f;
+      if (tok < T)
+        for (int b = 0; b < B; ++b) s += dout[((long)b * T + tok) * D + d];
+      dpos[(long)tok * D + d] = s;
+      if (tok == 0) dcls[d] = s;
+    }
+    return;
+  }
+  const int c = which - 1;
+  float gb = 0.f;
+  float gw[32];
+  for (int p = 0; p < P && p < 32; ++p) gw[p] = 0.f;
+  for (int n = 0; n < N; ++n) {
+    const int tok = 1 + c * N + n;
+    if (tok >= T) break;
+    for (int b = 0; b < B; ++b) {
+      const float g = dout[((long)b * T + tok) * D + d];
+      gb += g;
+      const float* xs = x + ((long)b * C + c) * L + (long)n * S;
+      for (int p = 0; p < P && p < 32; ++p) gw[p] = fmaf(g, xs[p], gw[p]);
+    }
+  }
+  db.p[c][d] = gb;
+  for (int p = 0; p < P && p < 32; ++p) dw.p[c][(long)d * P + p] = gw[p];
+}
+
+// dst = alpha * src * dropmask(seed, p, r, c) + beta * dst   (dropout forward/backward, casts, adds, gathers)
+template <typename TI, typename TO>
+__global__ void copy2d_kernel(int rows, int cols, const TI* __restrict__ src, long lds, TO* __restrict__ dst,
+                              long ldd, float alpha, float beta, float pdrop, unsigned long long seed) {
+  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (long)rows * cols) return;
+  const int r = idx / cols, c = idx % cols;
+  float v = alpha * to_f<TI>(src[(long)r * lds + c]);
+  if (pdrop > 0.f) v *= drop_mask(seed, pdrop, r, c);
+  TO* d = dst + (long)r * ldd + c;
+  if (beta != 0.f) v += beta * to_f<TO>(*d);
+  *d = from_f<TO>(v);
+}
+
+// ---------------------------------------------------------------------------------------------------------------
+// multi-tensor optimizer kernels.  Tensor table entries + a chunk list (built on the host once per step).
+// ---------------------------------------------------------------------------------------------------------------
+struct MTTensor {
+  float* p;
+  const float* g;
+  float* m;
+  float* v;
+  bf16* pbf;      // optional bf16 compute shadow (nullable)
+  float* pcopy;   // optional fp32 compute copy (nullable), e.g. a slice of a packed QKV bias
+  long n;
+  float wd;       // per-tensor weight decay
+  float lr_scale; // per-group lr multiplier
+};
+struct MTChunk {
+  int t;
+  int pad;
+  long start;
+  long len;
+};
+
+__global__ __launch_bounds__(256) void mt_sqnorm_kernel(const MTTensor* __restrict__ tens,
+                                                        const MTChunk* __restrict__ chunks, float* __restrict__ part) {
+  const MTChunk ch = chunks[blockIdx.x];
+  const float* g = tens[ch.t].g;
+  float s = 0.f;
+  if (g) {
+    for (long i = ch.start + threadIdx.x * 4; i < ch.start + ch.len; i += 1024) {
+      if (i + 3 < ch.start + ch.len) {
+        const floatx4 x = *(const floatx4*)(g + i);
+        s += x[0] * x[0] + x[1] * x[1] + x[2] * x[2] + x[3] * x[3];
+      } else {
+        for (long j = i; j < ch.start + ch.len; ++j) s += g[j] * g[j];
+      }
+    }
+  }
+  __shared__ float red[256];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) part[blockIdx.x] = red[0];
+}
+
+// total norm → out[0] = norm, out[1] = clip coefficient clamped to 1 (torch clip_grad_norm_ semantics).
+__global__ void mt_norm_final_kernel(int nparts, const float* __restrict__ part, float* __restrict__ out,
+                                     float max_norm) {
+  __shared__ double red[256];
+  double s = 0.0;
+  for (int i = threadIdx.x; i < nparts; i += 256) s += part[i];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    const float n = (float)sqrt(red[0]);
+    out[0] = n;
+    out[1] = fminf(max_norm / (n + 1e-6f), 1.f);
+  }
+}
+
+__global__ __launch_bounds__(256) void mt_scale_kernel(const MTTensor* __restrict__ tens,
+                                                       const MTChunk* __restrict__ chunks,
+                                                       const float* __restrict__ coef) {
+  const MTChunk ch = chunks[blockIdx.x];
+  float* g = (float*)tens[ch.t].g;
+  if (!g) return;
+  const float c = coef[1];
+  for (long i = ch.start + threadIdx.x; i < ch.start + ch.len; i += 256) g[i] *= c;
+}
+
+// torch.optim.AdamW math order (lerp for exp_avg, mul+addcmul for exp_avg_sq, denom = sqrt(v)/sqrt(bc2) + eps,
+// p *= 1 - lr*wd, p += -step_size * m/denom).  All step scalars are computed by the host in double precision, as
+// torch does in Python floats.  Optional grad scale from device memory (clip coefficient, out[1]); bf16 shadow.
+__global__ __launch_bounds__(256) void mt_adamw_kernel(const MTTensor* __restrict__ tens,
+                                                       const MTChunk* __restrict__ chunks, float lr, float omb1,
+                                                       float beta2, float omb2, float eps, float step_size,
+                                                       float bc2_sqrt, const float* __restrict__ gscale) {
+  const MTChunk ch = chunks[blockIdx.x];
+  const MTTensor T = tens[ch.t];
+  if (!T.g) return;
+  const float gs = gscale ? gscale[1] : 1.f;
+  const float ss = step_size * T.lr_scale;
+  const float decay = 1.f - lr * T.lr_scale * T.wd;
+  for (long i = ch.start + threadIdx.x; i < ch.start + ch.len; i += 256) {
+    const float g = T.g[i] * gs;
+    float p = T.p[i] * decay;
+    float m = T.m[i];
+    m = m + omb1 * (g - m);
+    const float v = beta2 * T.v[i] + omb2 * (g * g);
+    const float denom = sqrtf(v) / bc2_sqrt + eps;
+    p = p + (-ss) * (m / denom);
+    T.p[i] = p;
+    T.m[i] = m;
+    T.v[i] = v;
+    if (T.pbf) T.pbf[i] = (bf16)p;
+    if (T.pcopy) T.pcopy[i] = p;
+  }
+}
+
+__global__ __launch_bounds__(256) void mt_cast_kernel(const MTTensor* __restrict__ tens,
+                                                      const MTChunk* __restrict__ chunks) {
+  const MTChunk ch = chunks[blockIdx.x];
+  const MTTensor T = tens[ch.t];
+  for (long i = ch.start + threadIdx.x; i < ch.start + ch.len; i += 256) {
+    const float x = T.p[i];
+    if (T.pbf) T.pbf[i] = (bf16)x;
+    if (T.pcopy) T.pcopy[i] = x;
+  }
+}
+
+}  // namespace
+
+extern "C" int cmhar_tubelet_im2col(int out_dtype, int B, int T, int C, int H, int W, int tub, int P,
+                                    const float* video, void* out, hipStream_t st) {
+  if (P % 8 != 0 || T % tub || H % P || W % P) return -1;
+  const long total = (long)B * (T / tub) * (H / P) * (W / P) * C * tub * P * (P / 8);
+  if (total == 0) return 0;
+  if (out_dtype == CMHAR_BF16)
+    tubelet_im2col_kernel<bf16><<<cdiv(total, 256), 256, 0, st>>>(B, T, C, H, W, tub, P, video, (bf16*)out);
+  else
+    tubelet_im2col_kernel<float><<<cdiv(total, 256), 256, 0, st>>>(B, T, C, H, W, tub, P, video, (float*)out);
+  CMHAR_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int cmhar_imu_embed_fwd(int B, int C, int L, int N, int P, int S, int D, int T, const float* x,
+                                   const float* const* w, const float* const* bias, const float* cls, const float* pos,
+                                   float* out, hipStream_t st) {
+  if (C > 8 || P > 32) return -1;
+  PtrTable8 tw{}, tb{};
+  for (int c = 0; c < C; ++c) { tw.p[c] = w[c]; tb.p[c] = bias[c]; }
+  const long total = (long)B * T * D;
+  imu_embed_fwd_kernel<<<cdiv(total, 256), 256, 0, st>>>(B, C, L, N, P, S, D, T, x, tw, tb, cls, pos, out);
+  CMHAR_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int cmhar_imu_embed_bwd(int B, int C, int L, int N, int P, int S, int D, int T, int Tpos, const float* x,
+                                   const float* dout, float* dcls, float* dpos, float* const* dw, float* const* db,
+                                   hipStream_t st) {
+  if (C > 8 || P > 32) return -1;
+  MutPtrTable8 tw{}, tb{};
+  for (int c = 0; c < C; ++c) { tw.p[c] = dw[c]; tb.p[c] = db[c]; }
+  imu_embed_bwd_kernel<<<dim3(cdiv(D, 64), C + 1), 64, 0, st>>>(B, C, L, N, P, S, D, T, Tpos, x, dout, dcls, dpos,
+                                                                 tw, tb);
+  CMHAR_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int cmhar_copy2d(int in_dtype, int out_dtype, int rows, int cols, const void* src, long lds, void* dst,
+                            long ldd, float alpha, float beta, float pdrop, unsigned long long seed,
+                            hipStream_t st) {
+  const long total = (long)rows * cols;
+  if (total == 0) return 0;
+  const int g = cdiv(total, 256);
+#define C2(TI, TO)                                                                                          \
+  copy2d_kernel<TI, TO><<<g, 256, 0, st>>>(rows, cols, (const TI*)src, lds, (TO*)dst, ldd, alpha, beta, pdrop, \
+                                           seed)
+  if (in_dtype == CMHAR_F32 && out_dtype == CMHAR_F32) C2(float, float);
+  else if (in_dtype == CMHAR_F32 && out_dtype == CMHAR_BF16) C2(float, bf16);
+  else if (in_dtype == CMHAR_BF16 && out_dtype == CMHAR_F32) C2(bf16, float);
+  else C2(bf16, bf16);
+#undef C2
+  CMHAR_CHECK_LAUNCH();
+  return 0;
+}
+
+// Multi-tensor entry points: `tens` / `chunks` are DEVICE arrays (MTTensor / MTChunk layouts above).
+extern "C" int cmhar_mt_grad_norm(const void* tens, const void* chunks, int nchunks, float* part, float* out,
+                                  float max_norm, int apply_clip, hipStream_t st) {
+  if (nchunks <= 0) return 0;
+  mt_sqnorm_kernel<<<nchunks, 256, 0, st>>>((const MTTensor*)tens, (const MTChunk*)chunks, part);
+  mt_norm_final_kernel<<<1, 256, 0, st>>>(nchunks, part, out, max_norm);
+  if (apply_clip) mt_scale_kernel<<<nchunks, 256, 0, st>>>((const MTTensor*)tens, (const MTChunk*)chunks, out);
+  CMHAR_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int cmhar_mt_adamw(const void* tens, const void* chunks, int nchunks, float lr, float omb1, float beta2,
+                              float omb2, float eps, float step_size, float bc2_sqrt, const float* gscale,
+                              hipStream_t st) {
+  if (nchunks <= 0) return 0;
+  mt_adamw_kernel<<<nchunks, 256, 0, st>>>((const MTTensor*)tens, (const MTChunk*)chunks, lr, omb1, beta2, omb2, eps,
+                                           step_size, bc2_sqrt, gscale);
+  CMHAR_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int cmhar_mt_cast_bf16(const void* tens, const void* chunks, int nchunks, hipStream_t st) {
+  if (nchunks <= 0) return 0;
+  mt_cast_kernel<<<nchunks, 256, 0, st>>>((const MTTensor*)tens, (const MTChunk*)chunks);
+  CMHAR_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int cmhar_version(void) { return 1; }

@@ -1,0 +1,145 @@
+/*
+ * cmhar — C ABI of the MI355X (gfx950) HIP library behind the cross-modal IMU+video pretraining step.
+ *
+ * The reference (YOUNESELBOUKNIFY/CrossModal-IMU-Video-OOD-HAR) is pure Python: its hot path is the
+ * `CrossModalModel` / `SigmoidContrastiveLoss` forward+backward driven by `CrossModalTrainer.train_epoch`
+ * (src/train/trainer.py:130-144), executing through torch / transformers kernels.  There is no reference FFI;
+ * each entry point below replaces one op family of that path, cited as "replaces: file:line".  The Python
+ * host side (cmhar/_lib.py) binds these with ctypes; see INTEGRATION.md for the binding a maintainer would add.
+ *
+ * Conventions: all pointers are device pointers (HBM) unless stated; `stream` is a hipStream_t (the caller's
+ * current stream); functions never allocate or synchronise — workspaces are passed in; return 0 on success,
+ * a negative value for an unsupported argument combination, or a positive hipError_t from the launch.
+ * dtype codes: 0 = fp32, 1 = bf16.  Matrices are row-major with explicit leading dimensions (elements).
+ */
+#ifndef CMHAR_H
+#define CMHAR_H
+#include <hip/hip_runtime_api.h>   /* hipStream_t only: the header is plain C */
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Fused GEMM epilogue (see csrc/common.h for the element formula). */
+typedef struct CmharEpilogue {
+  const float* bias;      /* [N] fp32 or NULL */
+  const void* residual;   /* [M,N] output dtype, added last, or NULL */
+  long ldr;
+  const void* aux_in;     /* [M,N] pre-activation for act = 3 (dGELU) / 4 (dReLU) */
+  long lda;
+  void* aux_out;          /* [M,N] pre-activation written by act = 1 (GELU) */
+  long ldo;
+  const float* rowadd;    /* [rowadd_mod, rowadd_ld] fp32 table added at row m % rowadd_mod */
+  int rowadd_mod;
+  int rowadd_ld;
+  int act;                /* 0 none, 1 gelu(erf), 2 relu, 3 x*gelu'(aux_in), 4 x*(aux_in>0) */
+  float alpha;            /* out = alpha*acc ... */
+  float beta;             /* ... + beta*out_old (fp32 outputs; 0 = overwrite) */
+  float pdrop;            /* element dropout after the activation (mask = hash(seed, m, n) >= pdrop), 0 = off */
+  int pad_;
+  unsigned long long seed;
+} CmharEpilogue;
+
+int cmhar_version(void);
+
+/* bf16 MFMA GEMM (replaces: the nn.Linear forward/backward of the VideoMAE blocks, third-party
+ * transformers modeling_videomae.py:209-324, the tubelet Conv3d :159-168 as an im2col GEMM, and
+ * VideoEncoder.projection models.py:178,202).
+ * layout 0: C = A[M,K] · B[N,K]ᵀ   1: C = A[M,K] · B[K,N]   2: C = A[K,M]ᵀ · B[K,N].
+ * splits > 1: split-K with ws = splits*M*N fp32 floats. */
+int cmhar_gemm_bf16(int layout, int out_dtype, int M, int N, int K, const void* A, long lda, const void* B, long ldb,
+                    void* C, long ldc, const CmharEpilogue* epi, int splits, void* ws, hipStream_t stream);
+
+/* Exact-fp32 (or mixed) strided batched GEMM: C[z][m,n] = epi(Σ_k A[z][m*sam+k*sak] B[z][k*sbk+n*sbn])
+ * (replaces: the fp32 nn.Linear / IMU encoder / ProjectionHead matmuls, models.py:16-132, 221-234). */
+int cmhar_gemm_generic(int in_dtype, int out_dtype, int M, int N, int K, int batch, const void* A, long sam,
+                       long sak, long sAb, const void* B, long sbk, long sbn, long sBb, void* C, long ldc, long sCb,
+                       const CmharEpilogue* epi, hipStream_t stream);
+
+/* Attention softmax(scale·QKᵀ)V per (batch, head); Q/K/V/O rows [B*L, ld] with head h at cols h*D.
+ * bf16: D = 64 flash kernels (no dropout).  fp32: D in {8,16,32,64}, attention-prob dropout pdrop.
+ * lse: fp32 [B*H*Lq] (replaces: VideoMAESelfAttention modeling_videomae.py:209-258 and
+ * nn.MultiheadAttention inside nn.TransformerEncoderLayer, models.py:85-95). */
+int cmhar_attention_fwd(int dtype, int B, int H, int Lq, int Lk, int D, const void* Q, long ldq, const void* K,
+                        long ldk, const void* V, long ldv, void* O, long ldo, float* lse, float scale, float pdrop,
+                        unsigned long long seed, hipStream_t stream);
+int cmhar_attention_bwd(int dtype, int B, int H, int Lq, int Lk, int D, const void* Q, long ldq, const void* K,
+                        long ldk, const void* V, long ldv, const void* O, long ldo, const void* dO, long lddo,
+                        const float* lse, float* delta, void* dQ, long lddq, void* dK, long lddk, void* dV, long lddv,
+                        float scale, float pdrop, unsigned long long seed, hipStream_t stream);
+
+/* y = LayerNorm(a + dropout(b)) (b nullable); h_out (nullable) receives a + dropout(b)
+ * (replaces: VideoMAE layernorm_before/after modeling_videomae.py:337-350, IMU post-LN norm1/norm2 and
+ * final norm models.py:85-95,127). */
+int cmhar_layernorm_fwd(int dtype, int M, int N, const void* a, long lda, const void* b, long ldb, float pdrop,
+                        unsigned long long seed, void* h_out, long ldh, void* y, long ldy, const float* gamma,
+                        const float* beta, float* mean, float* rstd, float eps, hipStream_t stream);
+long cmhar_layernorm_bwd_ws(int M, int N);
+int cmhar_layernorm_bwd(int dtype, int M, int N, const void* dy, long lddy, const void* h, long ldh,
+                        const float* gamma, const float* mean, const float* rstd, const void* dres, long ldres,
+                        void* dh, long lddh, void* db_out, long lddb, float pdrop, unsigned long long seed,
+                        float* dgamma, float* dbeta, float beta_acc, float* ws, hipStream_t stream);
+
+/* out[n] = alpha Σ_m X[m,n] + beta out[n]  (bias gradients).  ws: cmhar_colsum_ws(M,N) floats. */
+long cmhar_colsum_ws(int M, int N);
+int cmhar_colsum(int dtype, int M, int N, const void* X, long ldx, float* out, float alpha, float beta, float* ws,
+                 long ws_floats, hipStream_t stream);
+
+/* BatchNorm1d (+ReLU) over [B,C] fp32 (replaces: ProjectionHead net.1/net.2 models.py:226-230,
+ * IMUClassifier classifier models.py:317-320). */
+int cmhar_batchnorm_fwd(int B, int C, const float* x, float* y, const float* w, const float* bias, float* rmean,
+                        float* rvar, float* smean, float* srstd, int training, float momentum, float eps, int relu,
+                        long long* num_batches_tracked, hipStream_t stream);
+int cmhar_batchnorm_bwd(int B, int C, const float* x, const float* y, const float* dy, const float* w,
+                        const float* smean, const float* srstd, float* dx, float* dw, float* db, int training,
+                        int relu, float beta_acc, hipStream_t stream);
+
+/* F.normalize(dim=1) (replaces: models.py:288-289). */
+int cmhar_l2normalize_fwd(int M, int N, const float* x, float* y, float* norm, float eps, hipStream_t stream);
+int cmhar_l2normalize_bwd(int M, int N, const float* y, const float* dy, const float* norm, float* dx, float eps,
+                          hipStream_t stream);
+
+/* SigmoidContrastiveLoss forward + gradients (replaces: src/models/losses.py:25-54). t, bias: device scalars.
+ * ws: cmhar_siglip_ws(Ba,Bb) floats. */
+long cmhar_siglip_ws(int Ba, int Bb);
+int cmhar_siglip_loss(int Ba, int Bb, int D, const float* a, const float* b, const float* t, const float* bias,
+                      float* loss, float* da, int a_off, int a_cnt, float* db, int b_off, int b_cnt, float* gt,
+                      float* gbias, float* ws, hipStream_t stream);
+
+/* VideoMAE tubelet patches (replaces: the Conv3d input side, modeling_videomae.py:159-168). */
+int cmhar_tubelet_im2col(int out_dtype, int B, int T, int C, int H, int W, int tub, int P, const float* video,
+                         void* out, hipStream_t stream);
+
+/* IMU PatchTST embedding + CLS + positional truncation (replaces: models.py:30-50, 108-123).
+ * w, bias, dw, db: HOST arrays of C device pointers. */
+int cmhar_imu_embed_fwd(int B, int C, int L, int N, int P, int S, int D, int T, const float* x,
+                        const float* const* w, const float* const* bias, const float* cls, const float* pos,
+                        float* out, hipStream_t stream);
+int cmhar_imu_embed_bwd(int B, int C, int L, int N, int P, int S, int D, int T, int Tpos, const float* x,
+                        const float* dout, float* dcls, float* dpos, float* const* dw, float* const* db,
+                        hipStream_t stream);
+
+/* dst[r, c] = alpha * src[r, c] * dropmask(seed, pdrop, r, c) + beta * dst[r, c], with dtype conversion
+ * (token-0 gather, casts, gradient adds, nn.Dropout forward/backward, models.py:85-95, 311-322). */
+int cmhar_copy2d(int in_dtype, int out_dtype, int rows, int cols, const void* src, long lds, void* dst, long ldd,
+                 float alpha, float beta, float pdrop, unsigned long long seed, hipStream_t stream);
+
+/* Multi-tensor optimizer (replaces: torch.nn.utils.clip_grad_norm_ and torch.optim.AdamW.step,
+ * trainer.py:74-78,140-141).  tens/chunks: DEVICE arrays of
+ *   struct { float* p; const float* g; float* m; float* v; bf16* p_bf16; float* p_copy; long n; float wd;
+ *            float lr_scale; }      (p_bf16 / p_copy: optional compute shadows refreshed in the same pass)
+ *   struct { int tensor; int pad; long start; long len; }
+ * grad_norm: out[0] = total L2 norm, out[1] = min(1, max_norm/(norm+1e-6)); apply_clip scales grads in place.
+ * adamw: step scalars precomputed by the host in double (torch semantics); gscale (nullable) = out of grad_norm. */
+int cmhar_mt_grad_norm(const void* tens, const void* chunks, int nchunks, float* part, float* out, float max_norm,
+                       int apply_clip, hipStream_t stream);
+int cmhar_mt_adamw(const void* tens, const void* chunks, int nchunks, float lr, float one_minus_beta1, float beta2,
+                   float one_minus_beta2, float eps, float step_size, float bias_correction2_sqrt,
+                   const float* gscale, hipStream_t stream);
+/* refresh the compute shadows (p_bf16 / p_copy) from p, e.g. after a foreign optimizer updated p. */
+int cmhar_mt_cast_bf16(const void* tens, const void* chunks, int nchunks, hipStream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CMHAR_H */

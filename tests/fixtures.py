@@ -34,6 +34,8 @@ def fixture_config(fx):
             for k, v in kv.items():
                 if isinstance(v, list) and k == 'video_resize':
                     v = tuple(v)
+                if k == 'video_backbone':
+                    v = '/nonexistent/videomae-fixture'     # the generator's temp dir; geometry comes from videomae_*
                 setattr(getattr(cfg, sect), k, v)
     return cfg
 

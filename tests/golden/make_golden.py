@@ -226,7 +226,12 @@ def g5_videomae_base(frames=16, image=224, B=1):
 
 
 if __name__ == '__main__':
+    import shutil
     which = sys.argv[1:] or ['g1', 'g2', 'g3', 'g4', 'g5']
-    for w in which:
-        {'g1': g1_imu_encoder, 'g2': g2_crossmodal_tiny, 'g3': g3_siglip, 'g4': g4_classifier,
-         'g5': lambda: g5_videomae_base(16, 224, 1)}[w]()
+    try:
+        for w in which:
+            {'g1': g1_imu_encoder, 'g2': g2_crossmodal_tiny, 'g3': g3_siglip, 'g4': g4_classifier,
+             'g5': lambda: g5_videomae_base(16, 224, 1)}[w]()
+    finally:
+        os.chdir('/')
+        shutil.rmtree(SCRATCH, ignore_errors=True)

@@ -1,0 +1,326 @@
+"""Kernel-level parity on the MI355X: every HIP kernel against a plain torch fp32 reference of the same op.
+
+Tolerances are written per test: exact-fp32 kernels ≤ 1e-5 relative; bf16-operand kernels are compared with the
+fp32 reference evaluated ON THE SAME bf16-ROUNDED INPUTS, so the only differences are accumulation order
+(fp32) and the final bf16 rounding of outputs (≤ 2^-8 relative)."""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+DEV = 'cuda'
+
+
+def K():
+    from cmhar import kernels
+    return kernels
+
+
+def L():
+    from cmhar import _lib
+    return _lib
+
+
+def rel(a, b):
+    a, b = a.float(), b.float()
+    return ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
+
+
+def _ints(shape, lo=-3, hi=4, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    return torch.randint(lo, hi, shape, generator=g).float()
+
+
+# ---------------------------------------------------------------------------------------------------------------
+# GEMM
+# ---------------------------------------------------------------------------------------------------------------
+def _ref_gemm(layout, a, b):
+    a, b = a.float(), b.float()
+    if layout == 0:
+        return a @ b.T
+    if layout == 1:
+        return a @ b
+    return a.T @ b
+
+
+def _operands(layout, M, N, Kd, maker, dt):
+    if layout == 0:
+        a, b = maker((M, Kd), 1), maker((N, Kd), 2)
+    elif layout == 1:
+        a, b = maker((M, Kd), 1), maker((Kd, N), 2)
+    else:
+        a, b = maker((Kd, M), 1), maker((Kd, N), 2)
+    return a.to(DEV, dt), b.to(DEV, dt)
+
+
+@pytest.mark.parametrize('layout', [0, 1, 2])
+@pytest.mark.parametrize('shape', [(128, 128, 64), (256, 384, 192), (200, 136, 72), (64, 8, 8), (1000, 768, 520)])
+def test_gemm_bf16_exact_integers(layout, shape):
+    """Small integers are exact in bf16 and their dot products exact in fp32: output must match bit-for-bit.
+    Asymmetric operands catch any row/column swap of the C/D layout."""
+    M, N, Kd = shape
+    a, b = _operands(layout, M, N, Kd, lambda s, sd: _ints(s, seed=sd), torch.bfloat16)
+    out = torch.empty(M, N, dtype=torch.float32, device=DEV)
+    K().gemm(layout, a, b, out, splits=1)
+    torch.cuda.synchronize()
+    assert torch.equal(out, _ref_gemm(layout, a, b))
+
+
+@pytest.mark.parametrize('layout', [0, 1, 2])
+def test_gemm_bf16_splitk_exact(layout):
+    M, N, Kd = 256, 256, 4096
+    a, b = _operands(layout, M, N, Kd, lambda s, sd: _ints(s, -2, 3, seed=sd), torch.bfloat16)
+    out = torch.empty(M, N, dtype=torch.float32, device=DEV)
+    K().gemm(layout, a, b, out, splits=7)
+    assert torch.equal(out, _ref_gemm(layout, a, b))
+
+
+def test_gemm_bf16_epilogues():
+    torch.manual_seed(0)
+    M, N, Kd = 384, 512, 256
+    a = torch.randn(M, Kd, device=DEV).bfloat16()
+    w = (torch.randn(N, Kd, device=DEV) / 16).bfloat16()
+    bias = torch.randn(N, device=DEV)
+    res = torch.randn(M, N, device=DEV).bfloat16()
+    ref_pre = a.float() @ w.float().T + bias
+    # GELU with pre-activation saved
+    pre = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+    y = K().linear(a, w, bias, act=L().ACT_GELU, aux_out=pre)
+    assert rel(pre, ref_pre) < 4e-3
+    assert rel(y, torch.nn.functional.gelu(ref_pre)) < 4e-3
+    # residual
+    y2 = K().linear(a, w, bias, residual=res)
+    assert rel(y2, ref_pre + res.float()) < 4e-3
+    # rowadd (position table) with modulus
+    tab = torch.randn(7, N, device=DEV)
+    y3 = K().linear(a, w, bias, rowadd=tab, rowadd_mod=7)
+    idx = torch.arange(M, device=DEV) % 7
+    assert rel(y3, ref_pre + tab[idx]) < 4e-3
+    # dgelu backward epilogue: (dy·W) * gelu'(pre)
+    dy = torch.randn(M, N, device=DEV).bfloat16()
+    w2 = (torch.randn(N, Kd, device=DEV) / 16).bfloat16()   # [N, K] weight; dgrad output [M, K]
+    g_in = torch.randn(M, Kd, device=DEV).bfloat16()
+    dx = K().linear_dgrad(dy, w2, act=L().ACT_DGELU, aux_in=g_in)
+    xg = g_in.float().requires_grad_(True)
+    gl = torch.autograd.grad(torch.nn.functional.gelu(xg), xg, torch.ones_like(xg))[0]
+    assert rel(dx, (dy.float() @ w2.float()) * gl) < 4e-3
+    # fp32 accumulate (beta = 1)
+    acc = torch.randn(N, Kd, device=DEV)
+    ref = acc + dy.float().T @ a.float()
+    K().linear_wgrad(dy, a, out=acc, beta=1.0)
+    assert rel(acc, ref) < 1e-5
+
+
+@pytest.mark.parametrize('layout', [0, 1, 2])
+def test_gemm_generic_fp32(layout):
+    torch.manual_seed(1)
+    M, N, Kd = 173, 91, 67
+    a, b = _operands(layout, M, N, Kd, lambda s, sd: torch.randn(s), torch.float32)
+    out = torch.empty(M, N, device=DEV)
+    K().gemm(layout, a, b, out)
+    assert rel(out, _ref_gemm(layout, a, b)) < 1e-6
+
+
+# ---------------------------------------------------------------------------------------------------------------
+# attention
+# ---------------------------------------------------------------------------------------------------------------
+def _attn_ref(q, k, v, B, H, Lq, Lk, D, scale):
+    q = q.float().view(B, Lq, H, D).transpose(1, 2)
+    k = k.float().view(B, Lk, H, D).transpose(1, 2)
+    v = v.float().view(B, Lk, H, D).transpose(1, 2)
+    p = torch.softmax(q @ k.transpose(-1, -2) * scale, -1)
+    return (p @ v).transpose(1, 2).reshape(B * Lq, H * D)
+
+
+@pytest.mark.parametrize('L_', [64, 200, 1568])
+def test_flash_attention_bf16_fwd_bwd(L_):
+    torch.manual_seed(2)
+    B, H, D = 2, 3, 64
+    scale = D ** -0.5
+    qkv = (torch.randn(B * L_, 3 * H * D, device=DEV) * 1.5).bfloat16()
+    q, k, v = qkv[:, :H * D], qkv[:, H * D:2 * H * D], qkv[:, 2 * H * D:]
+    o = torch.empty(B * L_, H * D, dtype=torch.bfloat16, device=DEV)
+    lse = torch.empty(B * H * L_, device=DEV)
+    K().attention_fwd(q, k, v, o, lse, B=B, H=H, Lq=L_, Lk=L_, D=D, scale=scale)
+    qr, kr, vr = (t.float().clone().requires_grad_(True) for t in (q, k, v))
+    ref = _attn_ref(qr, kr, vr, B, H, L_, L_, D, scale)
+    assert rel(o, ref) < 1e-2
+    do = torch.randn(B * L_, H * D, device=DEV).bfloat16()
+    gq, gk, gv = torch.autograd.grad(ref, (qr, kr, vr), do.float())
+    dqkv = torch.empty_like(qkv)
+    K().attention_bwd(q, k, v, o, do, lse, dqkv[:, :H * D], dqkv[:, H * D:2 * H * D], dqkv[:, 2 * H * D:],
+                      B=B, H=H, Lq=L_, Lk=L_, D=D, scale=scale)
+    assert rel(dqkv[:, :H * D], gq) < 2e-2
+    assert rel(dqkv[:, H * D:2 * H * D], gk) < 2e-2
+    assert rel(dqkv[:, 2 * H * D:], gv) < 2e-2
+
+
+@pytest.mark.parametrize('D', [16, 64])
+def test_attention_fp32_exact(D):
+    torch.manual_seed(3)
+    B, H, L_ = 3, 2, 13 if D == 16 else 130
+    scale = D ** -0.5
+    qkv = torch.randn(B * L_, 3 * H * D, device=DEV)
+    q, k, v = qkv[:, :H * D], qkv[:, H * D:2 * H * D], qkv[:, 2 * H * D:]
+    o = torch.empty(B * L_, H * D, device=DEV)
+    lse = torch.empty(B * H * L_, device=DEV)
+    K().attention_fwd(q, k, v, o, lse, B=B, H=H, Lq=L_, Lk=L_, D=D, scale=scale)
+    qr, kr, vr = (t.clone().requires_grad_(True) for t in (q, k, v))
+    ref = _attn_ref(qr, kr, vr, B, H, L_, L_, D, scale)
+    assert rel(o, ref) < 1e-5
+    do = torch.randn(B * L_, H * D, device=DEV)
+    gq, gk, gv = torch.autograd.grad(ref, (qr, kr, vr), do)
+    dq, dk, dv = (torch.empty(B * L_, H * D, device=DEV) for _ in range(3))
+    K().attention_bwd(q, k, v, o, do, lse, dq, dk, dv, B=B, H=H, Lq=L_, Lk=L_, D=D, scale=scale)
+    assert rel(dq, gq) < 1e-5 and rel(dk, gk) < 1e-5 and rel(dv, gv) < 1e-5
+
+
+def test_attention_fp32_dropout_consistent():
+    """With prob-dropout the kernel computes a fixed (seeded) masked function; its backward must be that
+    function's exact gradient: checked against a central finite difference along a random direction."""
+    torch.manual_seed(4)
+    B, H, L_, D = 2, 2, 13, 16
+    p = 0.3
+    scale = D ** -0.5
+    qkv = torch.randn(B * L_, 3 * H * D, device=DEV)
+    q, k, v = qkv[:, :H * D], qkv[:, H * D:2 * H * D], qkv[:, 2 * H * D:]
+    o = torch.empty(B * L_, H * D, device=DEV)
+    lse = torch.empty(B * H * L_, device=DEV)
+    K().attention_fwd(q, k, v, o, lse, B=B, H=H, Lq=L_, Lk=L_, D=D, scale=scale, pdrop=p, seed=1234)
+    # dropout changes the output; without it the kernel is the softmax average
+    o0 = torch.empty_like(o)
+    K().attention_fwd(q, k, v, o0, lse, B=B, H=H, Lq=L_, Lk=L_, D=D, scale=scale)
+    assert rel(o0, _attn_ref(q, k, v, B, H, L_, L_, D, scale)) < 1e-5
+    assert rel(o, o0) > 1e-3
+    # gradient check by directional finite difference of the (deterministic) masked function
+    K().attention_fwd(q, k, v, o, lse, B=B, H=H, Lq=L_, Lk=L_, D=D, scale=scale, pdrop=p, seed=1234)
+    do = torch.randn_like(o)
+    dq, dk, dv = (torch.empty_like(o) for _ in range(3))
+    K().attention_bwd(q, k, v, o, do, lse, dq, dk, dv, B=B, H=H, Lq=L_, Lk=L_, D=D, scale=scale, pdrop=p, seed=1234)
+    dirs = [torch.randn_like(o) * 1e-2 for _ in range(3)]
+    def f(qq, kk_, vv):
+        oo = torch.empty_like(o)
+        ll = torch.empty_like(lse)
+        K().attention_fwd(qq, kk_, vv, oo, ll, B=B, H=H, Lq=L_, Lk=L_, D=D, scale=scale, pdrop=p, seed=1234)
+        return (oo.double() * do.double()).sum().item()
+    fd = (f(q + dirs[0], k + dirs[1], v + dirs[2]) - f(q - dirs[0], k - dirs[1], v - dirs[2])) / 2
+    an = sum((g.double() * d.double()).sum().item() for g, d in zip((dq, dk, dv), dirs))
+    assert abs(fd - an) < 2e-3 * abs(an) + 1e-6
+
+
+# ---------------------------------------------------------------------------------------------------------------
+# norms / small ops
+# ---------------------------------------------------------------------------------------------------------------
+@pytest.mark.parametrize('dt', [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize('N', [768, 128])
+def test_layernorm_fwd_bwd(dt, N):
+    torch.manual_seed(5)
+    M = 333
+    x = torch.randn(M, N, device=DEV).to(dt)
+    g = 1 + 0.1 * torch.randn(N, device=DEV)
+    b = 0.1 * torch.randn(N, device=DEV)
+    eps = 1e-12 if N == 768 else 1e-5
+    y, mu, rs = K().layernorm_fwd(x, g, b, eps)
+    xr = x.float().clone().requires_grad_(True)
+    gr, br = g.clone().requires_grad_(True), b.clone().requires_grad_(True)
+    ref = torch.nn.functional.layer_norm(xr, (N,), gr, br, eps)
+    tol = 1e-5 if dt == torch.float32 else 8e-3
+    assert rel(y, ref) < tol
+    dy = torch.randn(M, N, device=DEV).to(dt)
+    dres = torch.randn(M, N, device=DEV).to(dt)
+    gx, gg, gb = torch.autograd.grad(ref, (xr, gr, br), dy.float())
+    dgam = torch.empty(N, device=DEV)
+    dbet = torch.empty(N, device=DEV)
+    dx = K().layernorm_bwd(dy, x, g, mu, rs, dgam, dbet, dres=dres)
+    assert rel(dx, gx + dres.float()) < (1e-5 if dt == torch.float32 else 1e-2)
+    assert rel(dgam, gg) < 1e-4 and rel(dbet, gb) < 1e-5
+
+
+def test_colsum_and_copy():
+    torch.manual_seed(6)
+    x = torch.randn(5000, 300, device=DEV).bfloat16()
+    out = torch.full((300,), 2.0, device=DEV)
+    K().colsum(x, out, beta=1.0)
+    assert rel(out, x.float().sum(0) + 2.0) < 1e-5
+    y = torch.empty(5000, 300, device=DEV)
+    K().copy2d(x, y, alpha=0.5)
+    assert torch.equal(y, x.float() * 0.5)
+
+
+def test_batchnorm_relu_l2norm():
+    torch.manual_seed(7)
+    B, Cc = 32, 512
+    x = torch.randn(B, Cc, device=DEV)
+    bn = torch.nn.BatchNorm1d(Cc).to(DEV)
+    with torch.no_grad():
+        bn.weight.normal_(1, 0.1)
+        bn.bias.normal_(0, 0.1)
+    rm, rv = bn.running_mean.clone(), bn.running_var.clone()
+    y, sm, sr = K().batchnorm_fwd(x, bn.weight, bn.bias, rm, rv, True, 0.1, 1e-5, True)
+    xr = x.clone().requires_grad_(True)
+    ref = torch.relu(bn(xr))
+    assert rel(y, ref) < 1e-5
+    assert rel(rm, bn.running_mean) < 1e-6 and rel(rv, bn.running_var) < 1e-6
+    dy = torch.randn_like(x)
+    gx, gw, gb = torch.autograd.grad(ref, (xr, bn.weight, bn.bias), dy)
+    dx, dw, db = K().batchnorm_bwd(x, y, dy, bn.weight, sm, sr, True, True)
+    assert rel(dx, gx) < 1e-5 and rel(dw, gw) < 1e-5 and rel(db, gb) < 1e-5
+    yn, nrm = K().l2normalize_fwd(x)
+    xr = x.clone().requires_grad_(True)
+    refn = torch.nn.functional.normalize(xr, dim=1)
+    assert rel(yn, refn) < 1e-6
+    (gn,) = torch.autograd.grad(refn, xr, dy)
+    assert rel(K().l2normalize_bwd(yn, dy, nrm), gn) < 1e-5
+
+
+def test_siglip_loss_matches_reference_formula():
+    from cmhar.losses import SigmoidContrastiveLoss
+    from fixtures import load
+    fx = load('g3_siglip')
+    a = torch.tensor(fx['a'], device=DEV, requires_grad=True)
+    b = torch.tensor(fx['b'], device=DEV, requires_grad=True)
+    lf = SigmoidContrastiveLoss().to(DEV)
+    loss = lf(a, b)
+    loss.backward()
+    assert abs(loss.item() - float(fx['loss'])) < 1e-6
+    assert rel(a.grad.cpu(), torch.tensor(fx['grad_a'])) < 1e-5
+    assert rel(b.grad.cpu(), torch.tensor(fx['grad_b'])) < 1e-5
+    assert abs(lf.temperature.grad.item() - float(fx['grad_temperature'])) < 1e-5 * max(1, abs(float(fx['grad_temperature'])))
+    assert abs(lf.bias.grad.item() - float(fx['grad_bias'])) < 1e-6
+
+
+def test_tubelet_im2col_gemm_equals_conv3d():
+    torch.manual_seed(8)
+    B, T, Cc, H, W, P, tub, Hd = 2, 4, 3, 32, 48, 16, 2, 64
+    video = torch.randn(B, T, Cc, H, W, device=DEV)
+    conv = torch.nn.Conv3d(Cc, Hd, (tub, P, P), stride=(tub, P, P)).to(DEV)
+    ref = conv(video.permute(0, 2, 1, 3, 4)).flatten(2).transpose(1, 2).reshape(-1, Hd)
+    patches = K().tubelet_im2col(video, tub, P, torch.float32)
+    out = K().linear(patches, conv.weight.detach().reshape(Hd, -1), conv.bias.detach())
+    assert rel(out, ref) < 1e-5
+
+
+def test_clip_and_fused_adamw_match_torch():
+    from cmhar.optim import FusedAdamW, clip_grad_norm_
+    torch.manual_seed(9)
+    shapes = [(300, 77), (1000,), (3, 5, 7), (65536 + 17,)]
+    ps = [torch.randn(s, device=DEV) for s in shapes]
+    ours = [torch.nn.Parameter(p.clone()) for p in ps]
+    theirs = [torch.nn.Parameter(p.clone()) for p in ps]
+    opt_a = FusedAdamW(ours, lr=1e-3, weight_decay=0.01)
+    opt_b = torch.optim.AdamW(theirs, lr=1e-3, weight_decay=0.01)
+    for step in range(3):
+        for a, b in zip(ours, theirs):
+            g = torch.randn_like(a) * (10 if step == 0 else 0.01)
+            a.grad, b.grad = g.clone(), g.clone()
+        na = clip_grad_norm_(ours, 1.0)
+        nb = torch.nn.utils.clip_grad_norm_(theirs, 1.0)
+        assert abs(na.item() - nb.item()) < 1e-5 * nb.item()
+        opt_a.step()
+        opt_b.step()
+    for a, b in zip(ours, theirs):
+        assert (a - b).abs().max().item() < 1e-6
+        assert rel(opt_a.state[a]['exp_avg_sq'], opt_b.state[b]['exp_avg_sq']) < 1e-6
