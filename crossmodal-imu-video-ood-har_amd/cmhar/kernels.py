@@ -217,12 +217,12 @@ def attention_fwd(q, k, v, out, lse, *, B, H, Lq, Lk, D, scale, pdrop=0.0, seed=
     if lse.numel() < B * H * Lq or lse.dtype != torch.float32:
         raise ValueError('lse workspace')
     dt = L.dtype_code(q.dtype)
-    if dt == L.BF16:
-        if D != 64 or pdrop != 0.0:
-            raise ValueError('bf16 flash attention supports head dim 64 without dropout')
+    if D not in (8, 16, 32, 64):
+        raise ValueError(f'head dim {D} not supported')
+    if dt == L.BF16 and D == 64 and pdrop == 0.0:     # flash (MFMA) path: 16-B aligned rows
         for t, n in ((q, 'q'), (k, 'k'), (v, 'v'), (out, 'o')):
             _check_bf16_operand(t, n)
-    ev = TRACE.begin() if dt == L.BF16 else None
+    ev = TRACE.begin() if (dt == L.BF16 and D == 64 and pdrop == 0.0) else None
     call('cmhar_attention_fwd', dt, B, H, Lq, Lk, D, ptr(q), q.stride(0), ptr(k), k.stride(0), ptr(v), v.stride(0),
          ptr(out), out.stride(0), ptr(lse), scale, pdrop, seed, L.stream(q.device))
     TRACE.end(ev, 'attn_fwd_bf16', 4 * B * H * Lq * Lk * D, 2 * (B * Lq + 2 * B * Lk + B * Lq) * H * D)
@@ -234,11 +234,14 @@ def attention_bwd(q, k, v, o, do, lse, dq, dk, dv, *, B, H, Lq, Lk, D, scale, pd
                      (dk, 'dk', Lk), (dv, 'dv', Lk)):
         _head_view_ok(t, B, Lx, H, D, n)
     dt = L.dtype_code(q.dtype)
-    if dt == L.BF16:
+    if D not in (8, 16, 32, 64):
+        raise ValueError(f'head dim {D} not supported')
+    flash = dt == L.BF16 and D == 64 and pdrop == 0.0
+    if flash:
         for t, n in ((q, 'q'), (k, 'k'), (v, 'v'), (o, 'o'), (do, 'do'), (dq, 'dq'), (dk, 'dk'), (dv, 'dv')):
             _check_bf16_operand(t, n)
     delta = workspace(B * H * Lq, q.device)
-    ev = TRACE.begin() if dt == L.BF16 else None
+    ev = TRACE.begin() if flash else None
     call('cmhar_attention_bwd', dt, B, H, Lq, Lk, D, ptr(q), q.stride(0), ptr(k), k.stride(0), ptr(v), v.stride(0),
          ptr(o), o.stride(0), ptr(do), do.stride(0), ptr(lse), ptr(delta), ptr(dq), dq.stride(0), ptr(dk),
          dk.stride(0), ptr(dv), dv.stride(0), scale, pdrop, seed, L.stream(q.device))

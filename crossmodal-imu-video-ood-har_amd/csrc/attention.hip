@@ -431,9 +431,9 @@ __device__ __forceinline__ float drop_scale(unsigned long long seed, float p, un
   return u >= p ? 1.f / (1.f - p) : 0.f;
 }
 
-template <int D>
-__global__ void attn_fwd_f32(int H, int Lq, int Lk, const float* __restrict__ Q, long ldq, const float* __restrict__ K,
-                             long ldk, const float* __restrict__ V, long ldv, float* __restrict__ O, long ldo,
+template <typename T, int D>
+__global__ void attn_fwd_f32(int H, int Lq, int Lk, const T* __restrict__ Q, long ldq, const T* __restrict__ K,
+                             long ldk, const T* __restrict__ V, long ldv, T* __restrict__ O, long ldo,
                              float* __restrict__ lse, float scale, float pdrop, unsigned long long seed) {
   const int hd = blockIdx.y, b = blockIdx.z;
   const int q = blockIdx.x * blockDim.x + threadIdx.x;
@@ -442,7 +442,7 @@ __global__ void attn_fwd_f32(int H, int Lq, int Lk, const float* __restrict__ Q,
   const bool active = q < Lq;
   const int qq = active ? q : 0;
 #pragma unroll
-  for (int d = 0; d < D; ++d) { qv[d] = Q[((long)b * Lq + qq) * ldq + hd * D + d] * scale; o[d] = 0.f; }
+  for (int d = 0; d < D; ++d) { qv[d] = to_f<T>(Q[((long)b * Lq + qq) * ldq + hd * D + d]) * scale; o[d] = 0.f; }
   float m = -INFINITY, l = 0.f;
   const unsigned bh = b * H + hd;
   for (int k0 = 0; k0 < Lk; k0 += 64) {
@@ -450,8 +450,8 @@ __global__ void attn_fwd_f32(int H, int Lq, int Lk, const float* __restrict__ Q,
     for (int i = threadIdx.x; i < 64 * D; i += blockDim.x) {
       const int kk = i / D, d = i % D;
       const bool ok = k0 + kk < Lk;
-      sK[kk][d] = ok ? K[((long)b * Lk + k0 + kk) * ldk + hd * D + d] : 0.f;
-      sV[kk][d] = ok ? V[((long)b * Lk + k0 + kk) * ldv + hd * D + d] : 0.f;
+      sK[kk][d] = ok ? to_f<T>(K[((long)b * Lk + k0 + kk) * ldk + hd * D + d]) : 0.f;
+      sV[kk][d] = ok ? to_f<T>(V[((long)b * Lk + k0 + kk) * ldv + hd * D + d]) : 0.f;
     }
     __syncthreads();
     const int kn = min(64, Lk - k0);
@@ -471,16 +471,16 @@ __global__ void attn_fwd_f32(int H, int Lq, int Lk, const float* __restrict__ Q,
   }
   if (active) {
 #pragma unroll
-    for (int d = 0; d < D; ++d) O[((long)b * Lq + q) * ldo + hd * D + d] = o[d] / l;
+    for (int d = 0; d < D; ++d) O[((long)b * Lq + q) * ldo + hd * D + d] = from_f<T>(o[d] / l);
     lse[((long)bh) * Lq + q] = m + __logf(l);     // natural-log LSE of scale*s
   }
 }
 
-template <int D>
-__global__ void attn_bwd_dq_f32(int H, int Lq, int Lk, const float* __restrict__ Q, long ldq, const float* __restrict__ K,
-                                long ldk, const float* __restrict__ V, long ldv, const float* __restrict__ O, long ldo,
-                                const float* __restrict__ dO, long lddo, const float* __restrict__ lse,
-                                float* __restrict__ delta_out, float* __restrict__ dQ, long lddq, float scale,
+template <typename T, int D>
+__global__ void attn_bwd_dq_f32(int H, int Lq, int Lk, const T* __restrict__ Q, long ldq, const T* __restrict__ K,
+                                long ldk, const T* __restrict__ V, long ldv, const T* __restrict__ O, long ldo,
+                                const T* __restrict__ dO, long lddo, const float* __restrict__ lse,
+                                float* __restrict__ delta_out, T* __restrict__ dQ, long lddq, float scale,
                                 float pdrop, unsigned long long seed) {
   const int hd = blockIdx.y, b = blockIdx.z;
   const int q = blockIdx.x * blockDim.x + threadIdx.x;
@@ -492,9 +492,9 @@ __global__ void attn_bwd_dq_f32(int H, int Lq, int Lk, const float* __restrict__
   float delta = 0.f;
 #pragma unroll
   for (int d = 0; d < D; ++d) {
-    qv[d] = Q[((long)b * Lq + qq) * ldq + hd * D + d] * scale;
-    g[d] = dO[((long)b * Lq + qq) * lddo + hd * D + d];
-    delta += g[d] * O[((long)b * Lq + qq) * ldo + hd * D + d];
+    qv[d] = to_f<T>(Q[((long)b * Lq + qq) * ldq + hd * D + d]) * scale;
+    g[d] = to_f<T>(dO[((long)b * Lq + qq) * lddo + hd * D + d]);
+    delta += g[d] * to_f<T>(O[((long)b * Lq + qq) * ldo + hd * D + d]);
     dq[d] = 0.f;
   }
   const float L = lse[(long)bh * Lq + qq];
@@ -503,8 +503,8 @@ __global__ void attn_bwd_dq_f32(int H, int Lq, int Lk, const float* __restrict__
     for (int i = threadIdx.x; i < 64 * D; i += blockDim.x) {
       const int kk = i / D, d = i % D;
       const bool ok = k0 + kk < Lk;
-      sK[kk][d] = ok ? K[((long)b * Lk + k0 + kk) * ldk + hd * D + d] : 0.f;
-      sV[kk][d] = ok ? V[((long)b * Lk + k0 + kk) * ldv + hd * D + d] : 0.f;
+      sK[kk][d] = ok ? to_f<T>(K[((long)b * Lk + k0 + kk) * ldk + hd * D + d]) : 0.f;
+      sV[kk][d] = ok ? to_f<T>(V[((long)b * Lk + k0 + kk) * ldv + hd * D + d]) : 0.f;
     }
     __syncthreads();
     const int kn = min(64, Lk - k0);
@@ -520,17 +520,17 @@ __global__ void attn_bwd_dq_f32(int H, int Lq, int Lk, const float* __restrict__
   }
   if (active) {
 #pragma unroll
-    for (int d = 0; d < D; ++d) dQ[((long)b * Lq + q) * lddq + hd * D + d] = dq[d] * scale;
+    for (int d = 0; d < D; ++d) dQ[((long)b * Lq + q) * lddq + hd * D + d] = from_f<T>(dq[d] * scale);
     delta_out[(long)bh * Lq + q] = delta;
   }
 }
 
-template <int D>
-__global__ void attn_bwd_dkdv_f32(int H, int Lq, int Lk, const float* __restrict__ Q, long ldq,
-                                  const float* __restrict__ K, long ldk, const float* __restrict__ V, long ldv,
-                                  const float* __restrict__ dO, long lddo, const float* __restrict__ lse,
-                                  const float* __restrict__ delta, float* __restrict__ dK, long lddk,
-                                  float* __restrict__ dV, long lddv, float scale, float pdrop,
+template <typename T, int D>
+__global__ void attn_bwd_dkdv_f32(int H, int Lq, int Lk, const T* __restrict__ Q, long ldq,
+                                  const T* __restrict__ K, long ldk, const T* __restrict__ V, long ldv,
+                                  const T* __restrict__ dO, long lddo, const float* __restrict__ lse,
+                                  const float* __restrict__ delta, T* __restrict__ dK, long lddk,
+                                  T* __restrict__ dV, long lddv, float scale, float pdrop,
                                   unsigned long long seed) {
   const int hd = blockIdx.y, b = blockIdx.z;
   const int k = blockIdx.x * blockDim.x + threadIdx.x;
@@ -541,8 +541,8 @@ __global__ void attn_bwd_dkdv_f32(int H, int Lq, int Lk, const float* __restrict
   float kv[D], vv[D], dk[D], dv[D];
 #pragma unroll
   for (int d = 0; d < D; ++d) {
-    kv[d] = K[((long)b * Lk + kk) * ldk + hd * D + d];
-    vv[d] = V[((long)b * Lk + kk) * ldv + hd * D + d];
+    kv[d] = to_f<T>(K[((long)b * Lk + kk) * ldk + hd * D + d]);
+    vv[d] = to_f<T>(V[((long)b * Lk + kk) * ldv + hd * D + d]);
     dk[d] = 0.f;
     dv[d] = 0.f;
   }
@@ -551,8 +551,8 @@ __global__ void attn_bwd_dkdv_f32(int H, int Lq, int Lk, const float* __restrict
     for (int i = threadIdx.x; i < 64 * D; i += blockDim.x) {
       const int qi = i / D, d = i % D;
       const bool ok = q0 + qi < Lq;
-      sQ[qi][d] = ok ? Q[((long)b * Lq + q0 + qi) * ldq + hd * D + d] * scale : 0.f;
-      sG[qi][d] = ok ? dO[((long)b * Lq + q0 + qi) * lddo + hd * D + d] : 0.f;
+      sQ[qi][d] = ok ? to_f<T>(Q[((long)b * Lq + q0 + qi) * ldq + hd * D + d]) * scale : 0.f;
+      sG[qi][d] = ok ? to_f<T>(dO[((long)b * Lq + q0 + qi) * lddo + hd * D + d]) : 0.f;
     }
     for (int i = threadIdx.x; i < 64; i += blockDim.x) {
       const bool ok = q0 + i < Lq;
@@ -578,8 +578,8 @@ __global__ void attn_bwd_dkdv_f32(int H, int Lq, int Lk, const float* __restrict
   if (active) {
 #pragma unroll
     for (int d = 0; d < D; ++d) {
-      dK[((long)b * Lk + k) * lddk + hd * D + d] = dk[d];
-      dV[((long)b * Lk + k) * lddv + hd * D + d] = dv[d];
+      dK[((long)b * Lk + k) * lddk + hd * D + d] = from_f<T>(dk[d]);
+      dV[((long)b * Lk + k) * lddv + hd * D + d] = from_f<T>(dv[d]);
     }
   }
 }
@@ -598,16 +598,21 @@ extern "C" int cmhar_attention_fwd(int dtype, int B, int H, int Lq, int Lk, int 
                                    const void* K, long ldk, const void* V, long ldv, void* O, long ldo, float* lse,
                                    float scale, float pdrop, unsigned long long seed, hipStream_t st) {
   if (B <= 0 || Lq <= 0) return 0;
-  if (dtype == CMHAR_BF16) {
-    if (D != 64 || pdrop != 0.f) return -1;
+  if (dtype == CMHAR_BF16 && D == 64 && pdrop == 0.f) {
     dim3 grid(cdiv(Lq, 128), H, B);
     attn_fwd_bf16<<<grid, 256, 0, st>>>(H, Lq, Lk, (const bf16*)Q, ldq, (const bf16*)K, ldk, (const bf16*)V, ldv,
                                         (bf16*)O, ldo, lse, scale);
   } else {
+    // exact-fp32 math path (fp32 storage, or bf16 storage with a head dim / dropout the flash kernel lacks);
+    // its LSE is in natural-log units and is only ever consumed by the matching backward below
     dim3 grid(cdiv(Lq, 64), H, B);
-#define F(DD) attn_fwd_f32<DD><<<grid, 64, 0, st>>>(H, Lq, Lk, (const float*)Q, ldq, (const float*)K, ldk, \
-                                                    (const float*)V, ldv, (float*)O, ldo, lse, scale, pdrop, seed)
-    switch (D) { case 16: F(16); break; case 32: F(32); break; case 64: F(64); break; case 8: F(8); break; default: return -1; }
+#define F(TT, DD)                                                                                         \
+  attn_fwd_f32<TT, DD><<<grid, 64, 0, st>>>(H, Lq, Lk, (const TT*)Q, ldq, (const TT*)K, ldk, (const TT*)V, ldv, \
+                                            (TT*)O, ldo, lse, scale, pdrop, seed)
+#define SW(TT) switch (D) { case 8: F(TT, 8); break; case 16: F(TT, 16); break; case 32: F(TT, 32); break;  \
+                            case 64: F(TT, 64); break; default: return -1; }
+    if (dtype == CMHAR_BF16) { SW(bf16) } else { SW(float) }
+#undef SW
 #undef F
   }
   CMHAR_CHECK_LAUNCH();
@@ -621,8 +626,7 @@ extern "C" int cmhar_attention_bwd(int dtype, int B, int H, int Lq, int Lk, int 
                                    void* dK, long lddk, void* dV, long lddv, float scale, float pdrop,
                                    unsigned long long seed, hipStream_t st) {
   if (B <= 0 || Lq <= 0) return 0;
-  if (dtype == CMHAR_BF16) {
-    if (D != 64 || pdrop != 0.f) return -1;
+  if (dtype == CMHAR_BF16 && D == 64 && pdrop == 0.f) {
     const long n = (long)B * H * Lq;
     attn_bwd_delta<<<cdiv(n, 256), 256, 0, st>>>(H, Lq, (const bf16*)O, ldo, (const bf16*)dO, lddo, delta, B);
     attn_bwd_dq_bf16<<<dim3(cdiv(Lq, 128), H, B), 256, 0, st>>>(H, Lq, Lk, (const bf16*)Q, ldq, (const bf16*)K, ldk,
@@ -632,16 +636,19 @@ extern "C" int cmhar_attention_bwd(int dtype, int B, int H, int Lq, int Lk, int 
                                                                   (const bf16*)V, ldv, (const bf16*)dO, lddo, lse,
                                                                   delta, (bf16*)dK, lddk, (bf16*)dV, lddv, scale);
   } else {
-#define F(DD)                                                                                                      \
-  attn_bwd_dq_f32<DD><<<dim3(cdiv(Lq, 64), H, B), 64, 0, st>>>(H, Lq, Lk, (const float*)Q, ldq, (const float*)K,     \
-                                                               ldk, (const float*)V, ldv, (const float*)O, ldo,     \
-                                                               (const float*)dO, lddo, lse, delta, (float*)dQ,      \
-                                                               lddq, scale, pdrop, seed);                           \
-  attn_bwd_dkdv_f32<DD><<<dim3(cdiv(Lk, 64), H, B), 64, 0, st>>>(H, Lq, Lk, (const float*)Q, ldq, (const float*)K,   \
-                                                                 ldk, (const float*)V, ldv, (const float*)dO, lddo, \
-                                                                 lse, delta, (float*)dK, lddk, (float*)dV, lddv,    \
-                                                                 scale, pdrop, seed)
-    switch (D) { case 16: F(16); break; case 32: F(32); break; case 64: F(64); break; case 8: F(8); break; default: return -1; }
+#define F(TT, DD)                                                                                               \
+  attn_bwd_dq_f32<TT, DD><<<dim3(cdiv(Lq, 64), H, B), 64, 0, st>>>(H, Lq, Lk, (const TT*)Q, ldq, (const TT*)K, ldk,   \
+                                                                   (const TT*)V, ldv, (const TT*)O, ldo,             \
+                                                                   (const TT*)dO, lddo, lse, delta, (TT*)dQ, lddq,   \
+                                                                   scale, pdrop, seed);                              \
+  attn_bwd_dkdv_f32<TT, DD><<<dim3(cdiv(Lk, 64), H, B), 64, 0, st>>>(H, Lq, Lk, (const TT*)Q, ldq, (const TT*)K,      \
+                                                                     ldk, (const TT*)V, ldv, (const TT*)dO, lddo,     \
+                                                                     lse, delta, (TT*)dK, lddk, (TT*)dV, lddv, scale, \
+                                                                     pdrop, seed)
+#define SW(TT) switch (D) { case 8: F(TT, 8); break; case 16: F(TT, 16); break; case 32: F(TT, 32); break;  \
+                            case 64: F(TT, 64); break; default: return -1; }
+    if (dtype == CMHAR_BF16) { SW(bf16) } else { SW(float) }
+#undef SW
 #undef F
   }
   CMHAR_CHECK_LAUNCH();

@@ -27,7 +27,9 @@ __device__ __forceinline__ int mc_off(int k, int chunk) { return k * 256 + ((chu
 template <bool KC>
 struct Stage {
   uint4_t r[4];
-  // Load this operand's tile (rows r0.., k0..) into registers; rows = M or N index.
+  // Load this operand's tile (rows r0.., k0..) into registers; rows = M or N index.  BOUNDS: rows / k past the
+  // matrix edge read a clamped (valid) address and are zeroed by a value select — never a branch around a load.
+  template <bool BOUNDS>
   __device__ __forceinline__ void load(const bf16* __restrict__ P, long ld, int rows_total, int r0, int k0,
                                        int kend, int tid) {
 #pragma unroll
@@ -36,10 +38,14 @@ struct Stage {
       int row, kk;
       if (KC) { row = c >> 3; kk = (c & 7) * 8; } else { kk = c >> 4; row = (c & 15) * 8; }
       const int gr = r0 + row, gk = k0 + kk;
-      bool ok = KC ? (gr < rows_total && gk < kend) : (gk < kend && gr < rows_total);
-      const bf16* src = KC ? (P + (long)gr * ld + gk) : (P + (long)gk * ld + gr);
-      if (ok) r[it] = *(const uint4_t*)src;
-      else r[it] = uint4_t{0u, 0u, 0u, 0u};
+      if (BOUNDS) {
+        const bool ok = gr < rows_total && gk < kend;
+        const bf16* src = ok ? (KC ? (P + (long)gr * ld + gk) : (P + (long)gk * ld + gr)) : P;
+        const uint4_t v = *(const uint4_t*)src;
+        r[it] = ok ? v : uint4_t{0u, 0u, 0u, 0u};
+      } else {
+        r[it] = *(const uint4_t*)(KC ? (P + (long)gr * ld + gk) : (P + (long)gk * ld + gr));
+      }
     }
   }
   __device__ __forceinline__ void store(char* lds, int tid) const {
@@ -82,12 +88,56 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8;
 }
 
-template <bool A_KC, bool B_KC, typename OutT>
+// Vectorised epilogue for 8 consecutive columns n0..n0+7 of row m (N % 8 == 0 on this path).
+template <typename OutT>
+__device__ __forceinline__ void epilogue_store8(const Epilogue& e, OutT* __restrict__ C, long ldc, int m, int n0,
+                                                float (&v)[8]) {
+  float aux[8], res[8];
+  if (e.aux_in) {
+    const OutT* p = (const OutT*)e.aux_in + (long)m * e.lda + n0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) aux[j] = to_f<OutT>(p[j]);
+  }
+  if (e.residual) {
+    const OutT* p = (const OutT*)e.residual + (long)m * e.ldr + n0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) res[j] = to_f<OutT>(p[j]);
+  }
+  OutT pre[8], outv[8];
+  OutT* dst = C + (long)m * ldc + n0;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int n = n0 + j;
+    float x = e.alpha * v[j];
+    if (e.bias) x += e.bias[n];
+    if (e.rowadd) x += e.rowadd[(long)(m % e.rowadd_mod) * e.rowadd_ld + n];
+    if (e.act == ACT_GELU) { pre[j] = from_f<OutT>(x); x = gelu_erf(x); }
+    else if (e.act == ACT_RELU) x = fmaxf(x, 0.f);
+    else if (e.act == ACT_DGELU) x *= gelu_erf_grad(aux[j]);
+    else if (e.act == ACT_DRELU) x = aux[j] > 0.f ? x : 0.f;
+    if (e.pdrop > 0.f) x *= drop_mask(e.seed, e.pdrop, m, n);
+    if (e.residual) x += res[j];
+    if (e.beta != 0.f) x += e.beta * to_f<OutT>(dst[j]);
+    outv[j] = from_f<OutT>(x);
+  }
+  if (e.act == ACT_GELU && e.aux_out) {
+    OutT* p = (OutT*)e.aux_out + (long)m * e.ldo + n0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) p[j] = pre[j];
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) dst[j] = outv[j];
+}
+
+constexpr int EPI_LD = BN + 4;                       // padded fp32 staging row: conflict-free acc writes
+constexpr int SMEM_BYTES = BM * EPI_LD * 4;          // 67584 B ≥ the 64 KiB of double-buffered A/B stages
+
+template <bool A_KC, bool B_KC, typename OutT, bool BOUNDS>
 __global__ __launch_bounds__(NT, 2) void gemm_bf16_kernel(int M, int N, int K, const bf16* __restrict__ A, long lda,
                                                           const bf16* __restrict__ B, long ldb,
                                                           OutT* __restrict__ C, long ldc, Epilogue e, int klen,
                                                           long split_stride, int raw_out) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
+  __shared__ __attribute__((aligned(16))) char smem[SMEM_BYTES];
   // stage buffers: A at smem + 16K*buf, B at smem + 32K + 16K*buf
 #define As(buf) (smem + 16384 * (buf))
 #define Bs(buf) (smem + 32768 + 16384 * (buf))
@@ -95,8 +145,9 @@ __global__ __launch_bounds__(NT, 2) void gemm_bf16_kernel(int M, int N, int K, c
   const int wr = wave >> 1, wc = wave & 1;
   const int tiles_n = (N + BN - 1) / BN, tiles_m = (M + BM - 1) / BM;
   const int bid = xcd_remap(blockIdx.x, tiles_m * tiles_n);
-  // column-major tile order within a split: consecutive blocks share the same B (weight) panel
-  const int tn = bid / tiles_m, tm = bid % tiles_m;
+  // row-major tile order: the blocks an XCD runs together share A row panels while the whole (small) weight
+  // matrix stays resident in that XCD's L2 — activations are streamed from HBM once
+  const int tm = bid / tiles_n, tn = bid % tiles_n;
   const int bm = tm * BM, bn = tn * BN;
   const int kbeg = blockIdx.z * klen;
   const int kend = min(K, kbeg + klen);
@@ -112,8 +163,8 @@ __global__ __launch_bounds__(NT, 2) void gemm_bf16_kernel(int M, int N, int K, c
   Stage<B_KC> sb;
   const int nk = (kend - kbeg + BK - 1) / BK;
   if (nk > 0) {
-    sa.load(A, lda, M, bm, kbeg, kend, tid);
-    sb.load(B, ldb, N, bn, kbeg, kend, tid);
+    sa.template load<BOUNDS>(A, lda, M, bm, kbeg, kend, tid);
+    sb.template load<BOUNDS>(B, ldb, N, bn, kbeg, kend, tid);
     sa.store(As(0), tid);
     sb.store(Bs(0), tid);
   }
@@ -122,8 +173,8 @@ __global__ __launch_bounds__(NT, 2) void gemm_bf16_kernel(int M, int N, int K, c
     const int cur = kt & 1;
     const bool more = kt + 1 < nk;
     if (more) {
-      sa.load(A, lda, M, bm, kbeg + (kt + 1) * BK, kend, tid);
-      sb.load(B, ldb, N, bn, kbeg + (kt + 1) * BK, kend, tid);
+      sa.template load<BOUNDS>(A, lda, M, bm, kbeg + (kt + 1) * BK, kend, tid);
+      sb.template load<BOUNDS>(B, ldb, N, bn, kbeg + (kt + 1) * BK, kend, tid);
     }
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
@@ -144,20 +195,40 @@ __global__ __launch_bounds__(NT, 2) void gemm_bf16_kernel(int M, int N, int K, c
     __syncthreads();
   }
 
-  // epilogue: lane holds rows 4*(lane>>4)+r, column lane&15 of each 16x16 block
+  // Epilogue: stage the fp32 tile through LDS (static accumulator indexing — the accumulators stay in
+  // registers through the main loop), then every thread emits 8 consecutive columns per row with 16-B stores.
+  float* T = (float*)smem;
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int m = bm + wr * 64 + i * 16 + 4 * (lane >> 4) + r;
-        const int n = bn + wc * 64 + j * 16 + (lane & 15);
-        if (m < M && n < N) {
-          if (raw_out) ((float*)C)[(long)m * ldc + n] = acc[i][j][r];
-          else epilogue_store<OutT>(e, C, ldc, m, n, acc[i][j][r]);
-        }
+      for (int r = 0; r < 4; ++r)
+        T[(wr * 64 + i * 16 + 4 * (lane >> 4) + r) * EPI_LD + wc * 64 + j * 16 + (lane & 15)] = acc[i][j][r];
+  __syncthreads();
+  const int cg = (tid & 15) * 8;        // 16 threads x 8 columns per row
+  const int n0 = bn + cg;
+  for (int rr = tid >> 4; rr < BM; rr += NT / 16) {
+    const int m = bm + rr;
+    if (m >= M) break;
+    float v[8];
+    const floatx4 lo = *(const floatx4*)&T[rr * EPI_LD + cg], hi = *(const floatx4*)&T[rr * EPI_LD + cg + 4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { v[j] = lo[j]; v[4 + j] = hi[j]; }
+    if (raw_out) {
+      float* dst = (float*)C + (long)m * ldc + n0;
+      if (!BOUNDS || n0 + 8 <= N) {
+        *(floatx4*)dst = lo;
+        *(floatx4*)(dst + 4) = hi;
+      } else {
+        for (int j = 0; j < 8 && n0 + j < N; ++j) dst[j] = v[j];
       }
+    } else if (!BOUNDS || n0 + 8 <= N) {
+      epilogue_store8<OutT>(e, C, ldc, m, n0, v);
+    } else {
+      for (int j = 0; j < 8 && n0 + j < N; ++j) epilogue_store<OutT>(e, C, ldc, m, n0 + j, v[j]);
+    }
+  }
 }
 
 #undef As
@@ -184,16 +255,19 @@ int launch(int M, int N, int K, const bf16* A, long lda, const bf16* B, long ldb
   if (splits > 1) klen = cdiv(cdiv(K, splits), BK) * BK;
   const int nsplit = cdiv(K, klen);
   dim3 grid(tiles, 1, nsplit);
-  const size_t lds = 65536;
-  if (nsplit == 1) {
-    gemm_bf16_kernel<AK, BKc, OutT><<<grid, NT, lds, st>>>(M, N, K, A, lda, B, ldb, C, ldc, e, klen, 0, 0);
-  } else {
-    if (!ws) return -2;
-    const long ss = (long)M * N;
-    gemm_bf16_kernel<AK, BKc, float><<<grid, NT, lds, st>>>(M, N, K, A, lda, B, ldb, ws, N, e, klen, ss, 1);
-    const long total = (long)M * N;
-    splitk_reduce_kernel<OutT><<<cdiv(total, 256), 256, 0, st>>>(M, N, nsplit, ws, ss, C, ldc, e);
-  }
+  const bool full = (M % BM == 0) && (N % BN == 0) && (K % BK == 0) && (klen % BK == 0);
+  const long ss = (long)M * N;
+  if (nsplit > 1 && !ws) return -2;
+#define GO(BND)                                                                                               \
+  do {                                                                                                        \
+    if (nsplit == 1)                                                                                          \
+      gemm_bf16_kernel<AK, BKc, OutT, BND><<<grid, NT, 0, st>>>(M, N, K, A, lda, B, ldb, C, ldc, e, klen, 0, 0); \
+    else                                                                                                      \
+      gemm_bf16_kernel<AK, BKc, float, BND><<<grid, NT, 0, st>>>(M, N, K, A, lda, B, ldb, ws, N, e, klen, ss, 1); \
+  } while (0)
+  if (full) GO(false); else GO(true);
+#undef GO
+  if (nsplit > 1) splitk_reduce_kernel<OutT><<<cdiv(ss, 256), 256, 0, st>>>(M, N, nsplit, ws, ss, C, ldc, e);
   CMHAR_CHECK_LAUNCH();
   return 0;
 }

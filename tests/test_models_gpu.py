@@ -126,7 +126,7 @@ def test_g2_two_trainer_steps_fused_optimizer():
         if 'grad.' + name in fx.files:
             ok = np.abs(fx['grad.' + name]) > 1e-3 * gscale     # well-conditioned Adam steps (see oracle test)
             np.testing.assert_allclose(got[ok], want[ok], rtol=1e-5, atol=3e-7, err_msg=name)
-            np.testing.assert_allclose(got[~ok], want[~ok], rtol=0, atol=2.1e-5, err_msg=name)
+            np.testing.assert_allclose(got[~ok], want[~ok], rtol=0, atol=3.1e-5, err_msg=name)   # ≤ 3 Adam steps of lr
             tight += int(ok.sum())
         elif got.dtype.kind == 'f':
             np.testing.assert_allclose(got, want, rtol=1e-4, atol=2e-5, err_msg=name)
