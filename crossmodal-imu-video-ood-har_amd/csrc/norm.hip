@@ -21,6 +21,11 @@ __device__ __forceinline__ float elem_drop(unsigned long long seed, float p, lon
 
 constexpr int MAXPER = 16;   // columns per lane: N <= 1024
 
+// the vectorised LayerNorm kernels need N a multiple of 256 and 4-element aligned leading dimensions
+static bool ln_vec_ok(int N, long a, long b, long c) {
+  return N % 256 == 0 && N <= 1024 && (a % 4) == 0 && (b % 4) == 0 && (c % 4) == 0;
+}
+
 // y = LN(a + drop(b)) with gamma/beta; h_out (optional) = a + drop(b); mean/rstd per row.
 template <typename T>
 __global__ __launch_bounds__(256) void ln_fwd_kernel(int M, int N, const T* __restrict__ a, long lda,
@@ -60,6 +65,46 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(int M, int N, const T* __re
       if (h_out) h_out[row * ldh + c] = from_f<T>(v[i]);
       y[row * ldy + c] = from_f<T>((v[i] - mu) * r * gamma[c] + beta[c]);
     }
+  }
+  if (lane == 0) { mean[row] = mu; rstd[row] = r; }
+}
+
+// Vectorised forward for N % 256 == 0 without the add/dropout input: one wave per row, 4 consecutive columns per
+// lane per 256-column group (8-B bf16 / 16-B fp32 accesses), two-pass statistics in registers.
+template <typename T, int G>
+__global__ __launch_bounds__(256) void ln_fwd_vec_kernel(int M, const T* __restrict__ a, long lda, T* __restrict__ y,
+                                                         long ldy, const float* __restrict__ gamma,
+                                                         const float* __restrict__ beta, float* __restrict__ mean,
+                                                         float* __restrict__ rstd, float eps) {
+  constexpr int N = 256 * G;
+  typedef __attribute__((ext_vector_type(4))) T vec4;
+  const int lane = threadIdx.x & 63;
+  const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= M) return;
+  float v[G][4];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < G; ++i) {
+    const vec4 x = *(const vec4*)(a + row * lda + 256 * i + 4 * lane);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { v[i][j] = to_f<T>(x[j]); s += v[i][j]; }
+  }
+  const float mu = wave_sum(s) * (1.f / N);
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < G; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { const float d = v[i][j] - mu; q += d * d; }
+  const float r = rsqrtf(wave_sum(q) * (1.f / N) + eps);
+#pragma unroll
+  for (int i = 0; i < G; ++i) {
+    vec4 o;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int c = 256 * i + 4 * lane + j;
+      o[j] = from_f<T>((v[i][j] - mu) * r * gamma[c] + beta[c]);
+    }
+    *(vec4*)(y + row * ldy + 256 * i + 4 * lane) = o;
   }
   if (lane == 0) { mean[row] = mu; rstd[row] = r; }
 }
@@ -126,30 +171,61 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(int M, int N, const T* __re
   }
 }
 
-// out[n] = alpha * Σ_m X[m*ldx + n] + beta * out[n]   (fp32 out); two-level: blocks of 64 columns x row chunks.
+// out[n] = alpha * Σ_m X[m*ldx + n] + beta * out[n]   (fp32 out).  Two levels, both parallel over rows:
+//   partial: block = 4 waves x (64 lanes x 4 consecutive columns) over a chunk of rows → part[chunk][N]
+//   final:   block = 4 row-groups x 64 columns over all chunks, LDS tree → out
+constexpr int CS_VEC = 4;
 template <typename T>
 __global__ __launch_bounds__(256) void colsum_partial_kernel(int M, int N, const T* __restrict__ X, long ldx,
                                                              int rows_per_chunk, float* __restrict__ part) {
-  __shared__ float red[4][64];
-  const int col = blockIdx.x * 64 + (threadIdx.x & 63);
-  const int sub = threadIdx.x >> 6;
+  __shared__ float red[4][64 * CS_VEC];
+  const int lane = threadIdx.x & 63, sub = threadIdx.x >> 6;
+  const int c0 = blockIdx.x * 64 * CS_VEC + lane * CS_VEC;
   const long r0 = (long)blockIdx.y * rows_per_chunk;
   const long r1 = min((long)M, r0 + rows_per_chunk);
-  float s = 0.f;
-  if (col < N)
-    for (long r = r0 + sub; r < r1; r += 4) s += to_f<T>(X[r * ldx + col]);
-  red[sub][threadIdx.x & 63] = s;
+  float s[CS_VEC] = {0.f, 0.f, 0.f, 0.f};
+  const bool vec = (c0 + CS_VEC <= N) && ((ldx & 3) == 0) && (((uintptr_t)X & 15) == 0);
+  if (vec) {
+    for (long r = r0 + sub; r < r1; r += 4) {
+      const T* p = X + r * ldx + c0;
+      if constexpr (sizeof(T) == 2) {
+        const bf16x4 v = *(const bf16x4*)p;
+#pragma unroll
+        for (int j = 0; j < CS_VEC; ++j) s[j] += (float)v[j];
+      } else {
+        const floatx4 v = *(const floatx4*)p;
+#pragma unroll
+        for (int j = 0; j < CS_VEC; ++j) s[j] += v[j];
+      }
+    }
+  } else {
+    for (long r = r0 + sub; r < r1; r += 4)
+#pragma unroll
+      for (int j = 0; j < CS_VEC; ++j)
+        if (c0 + j < N) s[j] += to_f<T>(X[r * ldx + c0 + j]);
+  }
+#pragma unroll
+  for (int j = 0; j < CS_VEC; ++j) red[sub][lane * CS_VEC + j] = s[j];
   __syncthreads();
-  if (sub == 0 && col < N) part[(long)blockIdx.y * N + col] = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
+  const int t = threadIdx.x;
+  const int col = blockIdx.x * 64 * CS_VEC + t;
+  if (col < N) part[(long)blockIdx.y * N + col] = red[0][t] + red[1][t] + red[2][t] + red[3][t];
 }
 
-__global__ void colsum_final_kernel(int chunks, int N, const float* __restrict__ part, float* __restrict__ out,
-                                    float alpha, float beta) {
-  const int col = blockIdx.x * blockDim.x + threadIdx.x;
-  if (col >= N) return;
+__global__ __launch_bounds__(256) void colsum_final_kernel(int chunks, int N, const float* __restrict__ part,
+                                                           float* __restrict__ out, float alpha, float beta) {
+  __shared__ float red[4][64];
+  const int lane = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const int col = blockIdx.x * 64 + lane;
   float s = 0.f;
-  for (int c = 0; c < chunks; ++c) s += part[(long)c * N + col];
-  out[col] = alpha * s + (beta != 0.f ? beta * out[col] : 0.f);
+  if (col < N)
+    for (int c = g; c < chunks; c += 4) s += part[(long)c * N + col];
+  red[g][lane] = s;
+  __syncthreads();
+  if (g == 0 && col < N) {
+    const float t = red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane];
+    out[col] = alpha * t + (beta != 0.f ? beta * out[col] : 0.f);
+  }
 }
 
 // BatchNorm1d (+ optional ReLU) over x [B][C] fp32: one thread per channel.
@@ -252,7 +328,16 @@ extern "C" int cmhar_layernorm_fwd(int dtype, int M, int N, const void* a, long 
   if (M <= 0) return 0;
   if (N > 64 * MAXPER) return -1;
   const int grid = cdiv(M, 4);
-  if (dtype == CMHAR_BF16)
+  if (!b && !h_out && ln_vec_ok(N, lda, ldy, ldy)) {
+#define LF(TT, G) ln_fwd_vec_kernel<TT, G><<<grid, 256, 0, st>>>(M, (const TT*)a, lda, (TT*)y, ldy, gamma, beta, mean, rstd, eps)
+    const int G = N / 256;
+    if (dtype == CMHAR_BF16) {
+      switch (G) { case 1: LF(bf16, 1); break; case 2: LF(bf16, 2); break; case 3: LF(bf16, 3); break; default: LF(bf16, 4); }
+    } else {
+      switch (G) { case 1: LF(float, 1); break; case 2: LF(float, 2); break; case 3: LF(float, 3); break; default: LF(float, 4); }
+    }
+#undef LF
+  } else if (dtype == CMHAR_BF16)
     ln_fwd_kernel<bf16><<<grid, 256, 0, st>>>(M, N, (const bf16*)a, lda, (const bf16*)b, ldb, pdrop, seed,
                                               (bf16*)h_out, ldh, (bf16*)y, ldy, gamma, beta, mean, rstd, eps);
   else
@@ -262,11 +347,111 @@ extern "C" int cmhar_layernorm_fwd(int dtype, int M, int N, const void* a, long 
   return 0;
 }
 
-// Number of fp32 floats the caller must provide in `ws` for cmhar_layernorm_bwd.
-extern "C" long cmhar_layernorm_bwd_ws(int M, int N) { return 2L * cdiv(M, 4 * LN_BWD_ROWS) * N; }
+// Sum `rows` fp32 partial rows [rows][N] into out (alpha/beta), via a second partial level when rows is large.
+constexpr int CS_ROWS = 128;
+static long reduce_rows_ws(int rows, int N) { return rows > 32 ? (long)cdiv(rows, CS_ROWS) * N : 0; }
+static void reduce_rows(const float* part, int rows, int N, float* out, float alpha, float beta, float* scratch,
+                        hipStream_t st) {
+  if (rows > 32) {
+    const int chunks = cdiv(rows, CS_ROWS);
+    colsum_partial_kernel<float><<<dim3(cdiv(N, 64 * CS_VEC), chunks), 256, 0, st>>>(rows, N, part, N, CS_ROWS,
+                                                                                     scratch);
+    colsum_final_kernel<<<cdiv(N, 64), 256, 0, st>>>(chunks, N, scratch, out, alpha, beta);
+  } else {
+    colsum_final_kernel<<<cdiv(N, 64), 256, 0, st>>>(rows, N, part, out, alpha, beta);
+  }
+}
 
-extern "C" int cmhar_colsum(int dtype, int M, int N, const void* X, long ldx, float* out, float alpha, float beta,
-                            float* ws, long ws_floats, hipStream_t st);
+// Vectorised LayerNorm backward for N % 256 == 0 (VideoMAE hidden 768): 8 waves x LNV_ROWS rows per block, each
+// lane owns N/256 groups of 4 consecutive columns (8-B bf16 / 16-B fp32 loads), next row prefetched into registers.
+constexpr int LNV_ROWS = 8, LNV_WAVES = 8;
+template <typename T, int G>
+__global__ __launch_bounds__(512) void ln_bwd_vec_kernel(int M, const T* __restrict__ dy, long lddy,
+                                                         const T* __restrict__ h, long ldh,
+                                                         const float* __restrict__ gamma,
+                                                         const float* __restrict__ mean, const float* __restrict__ rstd,
+                                                         const T* __restrict__ dres, long ldres, T* __restrict__ dh,
+                                                         long lddh, float* __restrict__ pgamma,
+                                                         float* __restrict__ pbeta) {
+  constexpr int N = 256 * G;
+  __shared__ float red[2][LNV_WAVES][N];
+  typedef __attribute__((ext_vector_type(4))) T vec4;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  float gam[G][4], ag[G][4], ab[G][4];
+#pragma unroll
+  for (int i = 0; i < G; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { gam[i][j] = gamma[256 * i + 4 * lane + j]; ag[i][j] = 0.f; ab[i][j] = 0.f; }
+  const long row0 = ((long)blockIdx.x * LNV_WAVES + wave) * LNV_ROWS;
+  vec4 vdy[G], vh[G];
+  auto load = [&](long row) {
+#pragma unroll
+    for (int i = 0; i < G; ++i) {
+      vdy[i] = *(const vec4*)(dy + row * lddy + 256 * i + 4 * lane);
+      vh[i] = *(const vec4*)(h + row * ldh + 256 * i + 4 * lane);
+    }
+  };
+  if (row0 < M) load(row0);
+  for (int rr = 0; rr < LNV_ROWS; ++rr) {
+    const long row = row0 + rr;
+    if (row >= M) break;
+    float d[G][4], xh[G][4];
+    const float mu = mean[row], r = rstd[row];
+#pragma unroll
+    for (int i = 0; i < G; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) { d[i][j] = to_f<T>(vdy[i][j]); xh[i][j] = (to_f<T>(vh[i][j]) - mu) * r; }
+    if (rr + 1 < LNV_ROWS && row + 1 < M) load(row + 1);     // prefetch the next row under this row's math
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < G; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float g = d[i][j] * gam[i][j];
+        ag[i][j] += d[i][j] * xh[i][j];
+        ab[i][j] += d[i][j];
+        s1 += g;
+        s2 += g * xh[i][j];
+      }
+    s1 = wave_sum(s1) * (1.f / N);
+    s2 = wave_sum(s2) * (1.f / N);
+#pragma unroll
+    for (int i = 0; i < G; ++i) {
+      vec4 res;
+      if (dres) res = *(const vec4*)(dres + row * ldres + 256 * i + 4 * lane);
+      vec4 o;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float v = r * (d[i][j] * gam[i][j] - s1 - xh[i][j] * s2);
+        if (dres) v += to_f<T>(res[j]);
+        o[j] = from_f<T>(v);
+      }
+      *(vec4*)(dh + row * lddh + 256 * i + 4 * lane) = o;
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < G; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { red[0][wave][256 * i + 4 * lane + j] = ag[i][j]; red[1][wave][256 * i + 4 * lane + j] = ab[i][j]; }
+  __syncthreads();
+  for (int c = threadIdx.x; c < N; c += 512) {
+    float sg = 0.f, sb = 0.f;
+#pragma unroll
+    for (int w = 0; w < LNV_WAVES; ++w) { sg += red[0][w][c]; sb += red[1][w][c]; }
+    pgamma[(long)blockIdx.x * N + c] = sg;
+    pbeta[(long)blockIdx.x * N + c] = sb;
+  }
+}
+
+static int ln_bwd_blocks(int M, int N, bool vec) {
+  return vec ? cdiv(M, LNV_WAVES * LNV_ROWS) : cdiv(M, 4 * LN_BWD_ROWS);
+}
+
+// Number of fp32 floats the caller must provide in `ws` for cmhar_layernorm_bwd (upper bound over both paths).
+extern "C" long cmhar_layernorm_bwd_ws(int M, int N) {
+  const int blocks = ln_bwd_blocks(M, N, false);
+  return 2L * blocks * N + 2 * reduce_rows_ws(blocks, N);
+}
 
 // dgamma/dbeta are written as out = Σ + beta_acc * out (beta_acc = 1 to accumulate into existing grads).
 extern "C" int cmhar_layernorm_bwd(int dtype, int M, int N, const void* dy, long lddy, const void* h, long ldh,
@@ -276,44 +461,57 @@ extern "C" int cmhar_layernorm_bwd(int dtype, int M, int N, const void* dy, long
                                    hipStream_t st) {
   if (M <= 0) return 0;
   if (N > 64 * MAXPER) return -1;
-  const int blocks = cdiv(M, 4 * LN_BWD_ROWS);
+  const bool vec = !db_out && ln_vec_ok(N, lddy, ldh, lddh) && (!dres || ldres % 4 == 0);
+  const int blocks = ln_bwd_blocks(M, N, vec);
   float* pg = ws;
   float* pb = ws + (long)blocks * N;
-  if (dtype == CMHAR_BF16)
+  float* scr = pb + (long)blocks * N;
+  if (vec) {
+#define LV(TT, G)                                                                                             \
+  ln_bwd_vec_kernel<TT, G><<<blocks, 512, 0, st>>>(M, (const TT*)dy, lddy, (const TT*)h, ldh, gamma, mean, rstd, \
+                                                   (const TT*)dres, ldres, (TT*)dh, lddh, pg, pb)
+    const int G = N / 256;
+    if (dtype == CMHAR_BF16) {
+      switch (G) { case 1: LV(bf16, 1); break; case 2: LV(bf16, 2); break; case 3: LV(bf16, 3); break; default: LV(bf16, 4); }
+    } else {
+      switch (G) { case 1: LV(float, 1); break; case 2: LV(float, 2); break; case 3: LV(float, 3); break; default: LV(float, 4); }
+    }
+#undef LV
+  } else if (dtype == CMHAR_BF16) {
     ln_bwd_kernel<bf16><<<blocks, 256, 0, st>>>(M, N, (const bf16*)dy, lddy, (const bf16*)h, ldh, gamma, mean, rstd,
                                                 (const bf16*)dres, ldres, (bf16*)dh, lddh, (bf16*)db_out, lddb, pdrop,
                                                 seed, pg, pb);
-  else
+  } else {
     ln_bwd_kernel<float><<<blocks, 256, 0, st>>>(M, N, (const float*)dy, lddy, (const float*)h, ldh, gamma, mean,
                                                  rstd, (const float*)dres, ldres, (float*)dh, lddh, (float*)db_out,
                                                  lddb, pdrop, seed, pg, pb);
+  }
   CMHAR_CHECK_LAUNCH();
-  const int g = cdiv(N, 256);
-  colsum_final_kernel<<<g, 256, 0, st>>>(blocks, N, pg, dgamma, 1.f, beta_acc);
-  colsum_final_kernel<<<g, 256, 0, st>>>(blocks, N, pb, dbeta, 1.f, beta_acc);
+  reduce_rows(pg, blocks, N, dgamma, 1.f, beta_acc, scr, st);
+  reduce_rows(pb, blocks, N, dbeta, 1.f, beta_acc, scr + reduce_rows_ws(blocks, N), st);
   CMHAR_CHECK_LAUNCH();
   return 0;
 }
 
+constexpr int CS_CHUNK = 256;
 extern "C" long cmhar_colsum_ws(int M, int N) {
-  const int rows_per_chunk = 256;
-  return (long)cdiv(M, rows_per_chunk) * N;
+  const int chunks = cdiv(M, CS_CHUNK);
+  return (long)chunks * N + reduce_rows_ws(chunks, N);
 }
 
 extern "C" int cmhar_colsum(int dtype, int M, int N, const void* X, long ldx, float* out, float alpha, float beta,
                             float* ws, long ws_floats, hipStream_t st) {
   if (N <= 0) return 0;
-  const int rows_per_chunk = 256;
-  const int chunks = cdiv(M, rows_per_chunk);
-  if ((long)chunks * N > ws_floats) return -2;
-  dim3 grid(cdiv(N, 64), chunks);
+  const int chunks = cdiv(M, CS_CHUNK);
+  if ((long)chunks * N + reduce_rows_ws(chunks, N) > ws_floats) return -2;
   if (M > 0) {
+    dim3 grid(cdiv(N, 64 * CS_VEC), chunks);
     if (dtype == CMHAR_BF16)
-      colsum_partial_kernel<bf16><<<grid, 256, 0, st>>>(M, N, (const bf16*)X, ldx, rows_per_chunk, ws);
+      colsum_partial_kernel<bf16><<<grid, 256, 0, st>>>(M, N, (const bf16*)X, ldx, CS_CHUNK, ws);
     else
-      colsum_partial_kernel<float><<<grid, 256, 0, st>>>(M, N, (const float*)X, ldx, rows_per_chunk, ws);
+      colsum_partial_kernel<float><<<grid, 256, 0, st>>>(M, N, (const float*)X, ldx, CS_CHUNK, ws);
   }
-  colsum_final_kernel<<<cdiv(N, 256), 256, 0, st>>>(M > 0 ? chunks : 0, N, ws, out, alpha, beta);
+  reduce_rows(ws, M > 0 ? chunks : 0, N, out, alpha, beta, ws + (long)chunks * N, st);
   CMHAR_CHECK_LAUNCH();
   return 0;
 }

@@ -239,13 +239,15 @@ def test_layernorm_fwd_bwd(dt, N):
     assert rel(dgam, gg) < 1e-4 and rel(dbet, gb) < 1e-5
 
 
-def test_colsum_and_copy():
+@pytest.mark.parametrize('shape', [(5000, 300), (20000, 768), (50176, 3072)])
+def test_colsum_and_copy(shape):
     torch.manual_seed(6)
-    x = torch.randn(5000, 300, device=DEV).bfloat16()
-    out = torch.full((300,), 2.0, device=DEV)
+    Mr, Nc = shape
+    x = torch.randn(Mr, Nc, device=DEV).bfloat16()
+    out = torch.full((Nc,), 2.0, device=DEV)
     K().colsum(x, out, beta=1.0)
     assert rel(out, x.float().sum(0) + 2.0) < 1e-5
-    y = torch.empty(5000, 300, device=DEV)
+    y = torch.empty(Mr, Nc, device=DEV)
     K().copy2d(x, y, alpha=0.5)
     assert torch.equal(y, x.float() * 0.5)
 

@@ -22,7 +22,7 @@ def rel(a, b):
     return ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
 
 
-def _grad_errors(model, fx, prefix=''):
+def _grad_errors(model, fx, prefix='', zero_tol=1e-4):
     errs = {}
     gscale = max(float(np.abs(fx[k]).max()) for k in fx.files if k.startswith('grad.'))
     for key in fx.files:
@@ -31,7 +31,7 @@ def _grad_errors(model, fx, prefix=''):
             p = dict(model.named_parameters())[name]
             ref = np.asarray(fx[key])
             if np.abs(ref).max() < 1e-5 * gscale:      # mathematically-zero gradient (noise in the reference)
-                assert p.grad is None or p.grad.abs().max().item() < 1e-4 * gscale, name
+                assert p.grad is None or p.grad.abs().max().item() < zero_tol * gscale, name
                 continue
             errs[name] = rel(p.grad, ref)
         elif key.startswith('gnorm.'):
@@ -88,7 +88,7 @@ def test_g2_crossmodal_forward_backward(dtype, tol_out, tol_grad):
     loss = lf(a, b)
     assert abs(loss.item() - float(fx['loss'])) < tol_out * abs(float(fx['loss']))
     loss.backward()
-    errs = _grad_errors(m, fx)
+    errs = _grad_errors(m, fx, zero_tol=1e-4 if dtype == 'fp32' else 2e-3)   # bf16 rounding noise on zero grads
     worst = sorted(errs.items(), key=lambda kv: -kv[1])[:5]
     assert max(errs.values()) < tol_grad, worst
     for key in fx.files:
