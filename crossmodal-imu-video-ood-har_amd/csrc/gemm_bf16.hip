@@ -247,17 +247,171 @@ __global__ void splitk_reduce_kernel(int M, int N, int splits, const float* __re
   epilogue_store<OutT>(e, C, ldc, m, n, s);
 }
 
+// ---------------------------------------------------------------------------------------------------------------
+// 256x256x64 tile, 512 threads = 8 waves (2 x 4, 128x64 outputs per wave = 8x4 mfma_f32_16x16x32_bf16 blocks),
+// operands staged by LDS-DMA (global_load_lds_dwordx4: 16 B per lane straight into LDS, no VGPR round trip, no
+// ds_write), two 64 KiB LDS buffers: tile k+1 streams in while tile k is consumed; one barrier per K-tile.
+// The XOR swizzles are applied on the per-lane GLOBAL source address (the DMA's LDS destination is lane-linear)
+// and the same swizzles on the fragment reads.  Used when M, N % 256 == 0 and K (per split) % 64 == 0 — every
+// VideoMAE-B GEMM at 16×224² and 16×112².
+// ---------------------------------------------------------------------------------------------------------------
+constexpr int TM2 = 256, TN2 = 256, TK2 = 64, NT2 = 512;
+constexpr int EPI2_LD = 68;                                  // per-wave 64x64 fp32 staging row (+4 pad)
+constexpr int SMEM2 = 8 * 64 * EPI2_LD * 4;                  // 139264 B ≥ 2 x 64 KiB operand buffers
+
+__device__ __forceinline__ int mc_off512(int k, int chunk) { return k * 512 + ((chunk ^ mc_swz(k)) << 4); }
+
+typedef __attribute__((address_space(3))) void* lds_void_ptr;
+
+// Issue this wave's 4 LDS-DMA instructions for one operand tile (256 rows/cols x 64 k).
+template <bool KC>
+__device__ __forceinline__ void dma_tile(const bf16* __restrict__ P, long ld, int r0, int k0, char* lds, int wave,
+                                         int lane) {
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const int i = wave * 4 + t;                            // 1 KiB piece index (32 per tile)
+    const bf16* src;
+    if (KC) {   // [256 rows][64 k]: piece = 8 rows of 128 B
+      const int row = 8 * i + (lane >> 3);
+      const int lc = (lane & 7) ^ ((row >> 1) & 7);
+      src = P + (long)(r0 + row) * ld + k0 + lc * 8;
+    } else {    // [64 k][256 cols]: piece = 2 k-rows of 512 B
+      const int k = 2 * i + (lane >> 5);
+      const int lc = (lane & 31) ^ mc_swz(k);
+      src = P + (long)(k0 + k) * ld + r0 + lc * 8;
+    }
+    __builtin_amdgcn_global_load_lds((const void*)src, (lds_void_ptr)(lds + i * 1024), 16, 0, 0);
+  }
+}
+
+template <bool KC>
+__device__ __forceinline__ bf16x8 frag256(const char* lds, int r0, int kk, int lane) {
+  if (KC) {
+    const int row = r0 + (lane & 15);
+    return *(const bf16x8*)(lds + kc_off(row, kk * 4 + (lane >> 4)));
+  } else {
+    const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+    const int chunk = (r0 >> 3) + (p >> 1);
+    const int k = kk * 32 + 8 * g + q;
+    const short4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(short4_t, lds + mc_off512(k, chunk) + (p & 1) * 8));
+    const short4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(short4_t, lds + mc_off512(k + 4, chunk) + (p & 1) * 8));
+    short8_t v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    return __builtin_bit_cast(bf16x8, v);
+  }
+}
+
+template <bool A_KC, bool B_KC, typename OutT>
+__global__ __launch_bounds__(NT2, 2) void gemm256_kernel(int M, int N, int K, const bf16* __restrict__ A, long lda,
+                                                         const bf16* __restrict__ B, long ldb, OutT* __restrict__ C,
+                                                         long ldc, Epilogue e, int klen, long split_stride,
+                                                         int raw_out) {
+  __shared__ __attribute__((aligned(16))) char smem[SMEM2];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave >> 2, wc = wave & 3;
+  const int tiles_n = N / TN2, tiles_m = M / TM2;
+  const int bid = xcd_remap(blockIdx.x, tiles_m * tiles_n);
+  const int tm = bid / tiles_n, tn = bid % tiles_n;
+  const int bm = tm * TM2, bn = tn * TN2;
+  const int kbeg = blockIdx.z * klen;
+  const int kend = min(K, kbeg + klen);
+  C += (long)blockIdx.z * split_stride;
+  const int nk = (kend - kbeg) / TK2;
+
+  floatx4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+  if (nk > 0) {
+    dma_tile<A_KC>(A, lda, bm, kbeg, smem, wave, lane);
+    dma_tile<B_KC>(B, ldb, bn, kbeg, smem + 32768, wave, lane);
+  }
+  for (int kt = 0; kt < nk; ++kt) {
+    __syncthreads();                                        // tile kt landed (vmcnt(0)) + buffer kt+1 free
+    const char* a_s = smem + (kt & 1) * 65536;
+    const char* b_s = a_s + 32768;
+    if (kt + 1 < nk) {
+      char* nxt = smem + ((kt + 1) & 1) * 65536;
+      dma_tile<A_KC>(A, lda, bm, kbeg + (kt + 1) * TK2, nxt, wave, lane);
+      dma_tile<B_KC>(B, ldb, bn, kbeg + (kt + 1) * TK2, nxt + 32768, wave, lane);
+    }
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      bf16x8 bfr[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bfr[j] = frag256<B_KC>(b_s, wc * 64 + j * 16, kk, lane);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const bf16x8 af = frag256<A_KC>(a_s, wr * 128 + i * 16, kk, lane);
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfr[j], acc[i][j], 0, 0, 0);
+        __builtin_amdgcn_s_setprio(0);
+      }
+    }
+  }
+  __syncthreads();
+
+  // epilogue: per wave, two passes of 64x64 through a private LDS slab, 16-B stores
+  float* T = (float*)(smem + wave * 64 * EPI2_LD * 4);
+#pragma unroll
+  for (int pass = 0; pass < 2; ++pass) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          T[(i * 16 + 4 * (lane >> 4) + r) * EPI2_LD + j * 16 + (lane & 15)] = acc[pass * 4 + i][j][r];
+    __syncthreads();
+    const int cg = (lane & 7) * 8;
+    const int n0 = bn + wc * 64 + cg;
+#pragma unroll 1
+    for (int rr = lane >> 3; rr < 64; rr += 8) {
+      const int m = bm + wr * 128 + pass * 64 + rr;
+      const floatx4 lo = *(const floatx4*)&T[rr * EPI2_LD + cg], hi = *(const floatx4*)&T[rr * EPI2_LD + cg + 4];
+      if (raw_out) {
+        float* dst = (float*)C + (long)m * ldc + n0;
+        *(floatx4*)dst = lo;
+        *(floatx4*)(dst + 4) = hi;
+      } else {
+        float v[8];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) { v[j] = lo[j]; v[4 + j] = hi[j]; }
+        epilogue_store8<OutT>(e, C, ldc, m, n0, v);
+      }
+    }
+    __syncthreads();
+  }
+}
+
 template <bool AK, bool BKc, typename OutT>
 int launch(int M, int N, int K, const bf16* A, long lda, const bf16* B, long ldb, OutT* C, long ldc,
            const Epilogue& e, int splits, float* ws, hipStream_t st) {
+  const long ss = (long)M * N;
+  if (splits > 1 && !ws) return -2;
+  if (M % TM2 == 0 && N % TN2 == 0 && K % TK2 == 0) {
+    int klen = K;
+    if (splits > 1) klen = cdiv(cdiv(K, splits), TK2) * TK2;
+    const int nsplit = cdiv(K, klen);
+    dim3 grid((M / TM2) * (N / TN2), 1, nsplit);
+    if (nsplit == 1)
+      gemm256_kernel<AK, BKc, OutT><<<grid, NT2, 0, st>>>(M, N, K, A, lda, B, ldb, C, ldc, e, klen, 0, 0);
+    else {
+      gemm256_kernel<AK, BKc, float><<<grid, NT2, 0, st>>>(M, N, K, A, lda, B, ldb, ws, N, e, klen, ss, 1);
+      splitk_reduce_kernel<OutT><<<cdiv(ss, 256), 256, 0, st>>>(M, N, nsplit, ws, ss, C, ldc, e);
+    }
+    CMHAR_CHECK_LAUNCH();
+    return 0;
+  }
   const int tiles = cdiv(M, BM) * cdiv(N, BN);
   int klen = K;
   if (splits > 1) klen = cdiv(cdiv(K, splits), BK) * BK;
   const int nsplit = cdiv(K, klen);
   dim3 grid(tiles, 1, nsplit);
   const bool full = (M % BM == 0) && (N % BN == 0) && (K % BK == 0) && (klen % BK == 0);
-  const long ss = (long)M * N;
-  if (nsplit > 1 && !ws) return -2;
 #define GO(BND)                                                                                               \
   do {                                                                                                        \
     if (nsplit == 1)                                                                                          \

@@ -57,7 +57,8 @@ def _operands(layout, M, N, Kd, maker, dt):
 
 
 @pytest.mark.parametrize('layout', [0, 1, 2])
-@pytest.mark.parametrize('shape', [(128, 128, 64), (256, 384, 192), (200, 136, 72), (64, 8, 8), (1000, 768, 520)])
+@pytest.mark.parametrize('shape', [(128, 128, 64), (256, 384, 192), (200, 136, 72), (64, 8, 8), (1000, 768, 520),
+                                   (256, 256, 64), (512, 768, 256), (1024, 512, 3072)])   # last 3: 256² DMA kernel
 def test_gemm_bf16_exact_integers(layout, shape):
     """Small integers are exact in bf16 and their dot products exact in fp32: output must match bit-for-bit.
     Asymmetric operands catch any row/column swap of the C/D layout."""
