@@ -300,7 +300,9 @@ __device__ __forceinline__ bf16x8 frag256(const char* lds, int r0, int kk, int l
   }
 }
 
-template <bool A_KC, bool B_KC, typename OutT>
+// MODE (ablation builds only, tools/debug): 0 = product; 1 = operand DMA only (no MFMA); 2 = MFMA only (no DMA
+// after the first tile); 3 = epilogue only (no K loop); 4 = K loop only (no epilogue).
+template <bool A_KC, bool B_KC, typename OutT, int MODE = 0>
 __global__ __launch_bounds__(NT2, 2) void gemm256_kernel(int M, int N, int K, const bf16* __restrict__ A, long lda,
                                                          const bf16* __restrict__ B, long ldb, OutT* __restrict__ C,
                                                          long ldc, Epilogue e, int klen, long split_stride,
@@ -316,7 +318,7 @@ __global__ __launch_bounds__(NT2, 2) void gemm256_kernel(int M, int N, int K, co
   const int kbeg = blockIdx.z * klen;
   const int kend = min(K, kbeg + klen);
   C += (long)blockIdx.z * split_stride;
-  const int nk = (kend - kbeg) / TK2;
+  const int nk = MODE == 3 ? 0 : (kend - kbeg) / TK2;
 
   floatx4 acc[8][4];
 #pragma unroll
@@ -332,27 +334,46 @@ __global__ __launch_bounds__(NT2, 2) void gemm256_kernel(int M, int N, int K, co
     __syncthreads();                                        // tile kt landed (vmcnt(0)) + buffer kt+1 free
     const char* a_s = smem + (kt & 1) * 65536;
     const char* b_s = a_s + 32768;
-    if (kt + 1 < nk) {
+    if (MODE != 2 && kt + 1 < nk) {
       char* nxt = smem + ((kt + 1) & 1) * 65536;
       dma_tile<A_KC>(A, lda, bm, kbeg + (kt + 1) * TK2, nxt, wave, lane);
       dma_tile<B_KC>(B, ldb, bn, kbeg + (kt + 1) * TK2, nxt + 32768, wave, lane);
     }
+    if (MODE == 1) continue;
+    // Rolling fragment prefetch: all of k-step 0's fragments plus k-step 1's B fragments are requested up
+    // front (16 ds_reads); each A slot is refilled with its k-step-1 fragment as soon as its 4 MFMAs have
+    // issued, so ~11 reads stay in flight under the MFMAs and every wait is a counted lgkmcnt.  The
+    // sched_barriers stop the scheduler from sinking the reads back next to their uses.
+    bf16x8 af[8], bf0[4], bf1[4];
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      bf16x8 bfr[4];
+    for (int j = 0; j < 4; ++j) bf0[j] = frag256<B_KC>(b_s, wc * 64 + j * 16, 0, lane);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) bfr[j] = frag256<B_KC>(b_s, wc * 64 + j * 16, kk, lane);
+    for (int i = 0; i < 8; ++i) af[i] = frag256<A_KC>(a_s, wr * 128 + i * 16, 0, lane);
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const bf16x8 af = frag256<A_KC>(a_s, wr * 128 + i * 16, kk, lane);
-        __builtin_amdgcn_s_setprio(1);
+    for (int j = 0; j < 4; ++j) bf1[j] = frag256<B_KC>(b_s, wc * 64 + j * 16, 1, lane);
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfr[j], acc[i][j], 0, 0, 0);
-        __builtin_amdgcn_s_setprio(0);
-      }
+    for (int i = 0; i < 8; ++i) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bf0[j], acc[i][j], 0, 0, 0);
+      af[i] = frag256<A_KC>(a_s, wr * 128 + i * 16, 1, lane);
+      __builtin_amdgcn_sched_barrier(0);
     }
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bf1[j], acc[i][j], 0, 0, 0);
   }
   __syncthreads();
+  if (MODE == 4) {   // keep every accumulator live, store nothing
+    float t = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) t += acc[i][j][0] + acc[i][j][1] + acc[i][j][2] + acc[i][j][3];
+    if (t == 1234.5f) ((float*)C)[tid] = t;
+    return;
+  }
 
   // epilogue: per wave, two passes of 64x64 through a private LDS slab, 16-B stores
   float* T = (float*)(smem + wave * 64 * EPI2_LD * 4);
