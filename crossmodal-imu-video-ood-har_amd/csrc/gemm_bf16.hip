@@ -88,45 +88,84 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8;
 }
 
-// Vectorised epilogue for 8 consecutive columns n0..n0+7 of row m (N % 8 == 0 on this path).
+// 8 consecutive elements of an OutT row as fp32 / back, with single 16-B (bf16) or 2 x 16-B (fp32) accesses.
+template <typename OutT>
+__device__ __forceinline__ void load8(const OutT* __restrict__ p, float (&x)[8]) {
+  if constexpr (sizeof(OutT) == 2) {
+    const bf16x8 v = *(const bf16x8*)p;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) x[j] = (float)v[j];
+  } else {
+    const floatx4 a = *(const floatx4*)p, b = *(const floatx4*)(p + 4);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { x[j] = a[j]; x[4 + j] = b[j]; }
+  }
+}
+template <typename OutT>
+__device__ __forceinline__ void store8(OutT* __restrict__ p, const float (&x)[8]) {
+  if constexpr (sizeof(OutT) == 2) {
+    bf16x8 v;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = (bf16)x[j];
+    *(bf16x8*)p = v;
+  } else {
+    *(floatx4*)p = floatx4{x[0], x[1], x[2], x[3]};
+    *(floatx4*)(p + 4) = floatx4{x[4], x[5], x[6], x[7]};
+  }
+}
+
+// Vectorised epilogue for 8 consecutive columns n0..n0+7 of row m: every operand is moved with 16-B accesses
+// (callers guarantee 16-B alignment: N % 8 == 0 on this path, leading dimensions % 8 == 0, checked on the host).
+// Each optional stage is a wave-uniform branch on a kernel argument.
 template <typename OutT>
 __device__ __forceinline__ void epilogue_store8(const Epilogue& e, OutT* __restrict__ C, long ldc, int m, int n0,
                                                 float (&v)[8]) {
-  float aux[8], res[8];
-  if (e.aux_in) {
-    const OutT* p = (const OutT*)e.aux_in + (long)m * e.lda + n0;
+  float x[8], t[8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) aux[j] = to_f<OutT>(p[j]);
+  for (int j = 0; j < 8; ++j) x[j] = e.alpha * v[j];
+  if (e.bias) {
+    const floatx4 b0 = *(const floatx4*)(e.bias + n0), b1 = *(const floatx4*)(e.bias + n0 + 4);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { x[j] += b0[j]; x[4 + j] += b1[j]; }
+  }
+  if (e.rowadd) {
+    const float* r = e.rowadd + (long)(m % e.rowadd_mod) * e.rowadd_ld + n0;
+    const floatx4 r0 = *(const floatx4*)r, r1 = *(const floatx4*)(r + 4);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { x[j] += r0[j]; x[4 + j] += r1[j]; }
+  }
+  if (e.act == ACT_GELU) {
+    if (e.aux_out) store8<OutT>((OutT*)e.aux_out + (long)m * e.ldo + n0, x);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) x[j] = gelu_erf(x[j]);
+  } else if (e.act == ACT_RELU) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) x[j] = fmaxf(x[j], 0.f);
+  } else if (e.act == ACT_DGELU) {
+    load8<OutT>((const OutT*)e.aux_in + (long)m * e.lda + n0, t);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) x[j] *= gelu_erf_grad(t[j]);
+  } else if (e.act == ACT_DRELU) {
+    load8<OutT>((const OutT*)e.aux_in + (long)m * e.lda + n0, t);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) x[j] = t[j] > 0.f ? x[j] : 0.f;
+  }
+  if (e.pdrop > 0.f) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) x[j] *= drop_mask(e.seed, e.pdrop, m, n0 + j);
   }
   if (e.residual) {
-    const OutT* p = (const OutT*)e.residual + (long)m * e.ldr + n0;
+    load8<OutT>((const OutT*)e.residual + (long)m * e.ldr + n0, t);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) res[j] = to_f<OutT>(p[j]);
+    for (int j = 0; j < 8; ++j) x[j] += t[j];
   }
-  OutT pre[8], outv[8];
   OutT* dst = C + (long)m * ldc + n0;
+  if (e.beta != 0.f) {
+    load8<OutT>(dst, t);
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const int n = n0 + j;
-    float x = e.alpha * v[j];
-    if (e.bias) x += e.bias[n];
-    if (e.rowadd) x += e.rowadd[(long)(m % e.rowadd_mod) * e.rowadd_ld + n];
-    if (e.act == ACT_GELU) { pre[j] = from_f<OutT>(x); x = gelu_erf(x); }
-    else if (e.act == ACT_RELU) x = fmaxf(x, 0.f);
-    else if (e.act == ACT_DGELU) x *= gelu_erf_grad(aux[j]);
-    else if (e.act == ACT_DRELU) x = aux[j] > 0.f ? x : 0.f;
-    if (e.pdrop > 0.f) x *= drop_mask(e.seed, e.pdrop, m, n);
-    if (e.residual) x += res[j];
-    if (e.beta != 0.f) x += e.beta * to_f<OutT>(dst[j]);
-    outv[j] = from_f<OutT>(x);
+    for (int j = 0; j < 8; ++j) x[j] += e.beta * t[j];
   }
-  if (e.act == ACT_GELU && e.aux_out) {
-    OutT* p = (OutT*)e.aux_out + (long)m * e.ldo + n0;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) p[j] = pre[j];
-  }
-#pragma unroll
-  for (int j = 0; j < 8; ++j) dst[j] = outv[j];
+  store8<OutT>(dst, x);
 }
 
 constexpr int EPI_LD = BN + 4;                       // padded fp32 staging row: conflict-free acc writes
@@ -301,7 +340,8 @@ __device__ __forceinline__ bf16x8 frag256(const char* lds, int r0, int kk, int l
 }
 
 // MODE (ablation builds only, tools/debug): 0 = product; 1 = operand DMA only (no MFMA); 2 = MFMA only (no DMA
-// after the first tile); 3 = epilogue only (no K loop); 4 = K loop only (no epilogue).
+// after the first tile); 3 = epilogue only (no K loop); 4 = K loop only (no epilogue); 5 = LDS staging only;
+// 6 = staging + plain bf16 stores.
 template <bool A_KC, bool B_KC, typename OutT, int MODE = 0>
 __global__ __launch_bounds__(NT2, 2) void gemm256_kernel(int M, int N, int K, const bf16* __restrict__ A, long lda,
                                                          const bf16* __restrict__ B, long ldb, OutT* __restrict__ C,
@@ -318,7 +358,7 @@ __global__ __launch_bounds__(NT2, 2) void gemm256_kernel(int M, int N, int K, co
   const int kbeg = blockIdx.z * klen;
   const int kend = min(K, kbeg + klen);
   C += (long)blockIdx.z * split_stride;
-  const int nk = MODE == 3 ? 0 : (kend - kbeg) / TK2;
+  const int nk = MODE >= 3 && MODE != 4 ? 0 : (kend - kbeg) / TK2;
 
   floatx4 acc[8][4];
 #pragma unroll
@@ -389,11 +429,19 @@ __global__ __launch_bounds__(NT2, 2) void gemm256_kernel(int M, int N, int K, co
     __syncthreads();
     const int cg = (lane & 7) * 8;
     const int n0 = bn + wc * 64 + cg;
-#pragma unroll 1
-    for (int rr = lane >> 3; rr < 64; rr += 8) {
+#pragma unroll 2
+    for (int it = 0; it < 8; ++it) {
+      const int rr = it * 8 + (lane >> 3);
       const int m = bm + wr * 128 + pass * 64 + rr;
       const floatx4 lo = *(const floatx4*)&T[rr * EPI2_LD + cg], hi = *(const floatx4*)&T[rr * EPI2_LD + cg + 4];
-      if (raw_out) {
+      if (MODE == 5) {
+        if (lo[0] + hi[3] == 1234.5f) ((float*)C)[tid] = lo[1];
+      } else if (MODE == 6) {
+        bf16x8 o;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) { o[j] = (bf16)lo[j]; o[4 + j] = (bf16)hi[j]; }
+        *(bf16x8*)((bf16*)C + (long)m * ldc + n0) = o;
+      } else if (raw_out) {
         float* dst = (float*)C + (long)m * ldc + n0;
         *(floatx4*)dst = lo;
         *(floatx4*)(dst + 4) = hi;
@@ -458,9 +506,12 @@ extern "C" int cmhar_gemm_bf16(int layout, int out_dtype, int M, int N, int K, c
   const bf16* a = (const bf16*)A;
   const bf16* b = (const bf16*)B;
   float* w = (float*)ws;
+  Epilogue plain{};
+  plain.alpha = 1.f;
+  const Epilogue& e = epi ? *epi : plain;             // NULL = the plain product
 #define DISPATCH(AK, BKc)                                                                                     \
-  return out_dtype == CMHAR_BF16 ? launch<AK, BKc, bf16>(M, N, K, a, lda, b, ldb, (bf16*)C, ldc, *epi, splits, w, stream) \
-                                 : launch<AK, BKc, float>(M, N, K, a, lda, b, ldb, (float*)C, ldc, *epi, splits, w, stream)
+  return out_dtype == CMHAR_BF16 ? launch<AK, BKc, bf16>(M, N, K, a, lda, b, ldb, (bf16*)C, ldc, e, splits, w, stream) \
+                                 : launch<AK, BKc, float>(M, N, K, a, lda, b, ldb, (float*)C, ldc, e, splits, w, stream)
   switch (layout) {
     case 0: DISPATCH(true, true);
     case 1: DISPATCH(true, false);

@@ -64,7 +64,9 @@ extern "C" int cmhar_gemm_generic(int in_dtype, int out_dtype, int M, int N, int
                                   long sam, long sak, long sAb, const void* B, long sbk, long sbn, long sBb, void* C,
                                   long ldc, long sCb, const Epilogue* epi, hipStream_t stream) {
   if (M <= 0 || N <= 0 || batch <= 0) return 0;
-  Epilogue e = *epi;
+  Epilogue e{};
+  e.alpha = 1.f;
+  if (epi) e = *epi;                                   // NULL = the plain product
   dim3 grid(cdiv(N, TN), cdiv(M, TM), batch);
 #define LAUNCH(TI, TO)                                                                                     \
   gemm_generic_kernel<TI, TO><<<grid, 256, 0, stream>>>(M, N, K, (const TI*)A, sam, sak, sAb, (const TI*)B, \

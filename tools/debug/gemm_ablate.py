@@ -40,7 +40,8 @@ def main():
         c = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
         fl = 2 * M * N * K
         res = {}
-        for mode, tag in ((0, 'full'), (1, 'dma_only'), (2, 'mfma_only'), (3, 'epi_only'), (4, 'no_epi')):
+        for mode, tag in ((0, 'full'), (1, 'dma_only'), (2, 'mfma_only'), (3, 'epi_only'), (4, 'no_epi'),
+                          (5, 'stage_only'), (6, 'plain_store')):
             ms = run(lambda: lib.ablate_gemm256(mode, layout, M, N, K, a.data_ptr(), a.stride(0), b.data_ptr(),
                                                 b.stride(0), c.data_ptr(), c.stride(0), st))
             res[tag] = (ms, fl / ms / 1e9)
@@ -49,6 +50,8 @@ def main():
         res['gemm128'] = (ms, fl / ms / 1e9)
         ms = run(lambda: torch.matmul(a.T if layout == 2 else a, b.T if layout == 0 else b, out=None))
         res['torch(hipblaslt)'] = (ms, fl / ms / 1e9)
+        ms = run(lambda: c.zero_())
+        res['zero_'] = (ms, c.numel() * 2 / ms / 1e6)   # GB/s in the TF slot
         print(name, M, N, K, ' '.join(f'{k}={v[0]:.3f}ms/{v[1]:.0f}TF' for k, v in res.items()), flush=True)
 
 
