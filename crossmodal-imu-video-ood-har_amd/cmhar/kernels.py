@@ -83,10 +83,17 @@ def _check_bf16_operand(t, name):
 
 
 def _splits_for(M, N, K):
-    tiles = math.ceil(M / 128) * math.ceil(N / 128)
-    if tiles >= 384 or K < 1024:
+    """Split-K factor so that small-output / long-K GEMMs (the weight gradients: K = B·L tokens) fill the 256 CUs.
+    Mirrors the library's kernel choice: 256² tiles (one 512-thread workgroup per CU) when M, N % 256 == 0 and
+    K % 64 == 0, else 128² tiles (two per CU)."""
+    big = M % 256 == 0 and N % 256 == 0 and K % 64 == 0
+    if big:
+        tiles, slots = (M // 256) * (N // 256), 256
+    else:
+        tiles, slots = math.ceil(M / 128) * math.ceil(N / 128), 512
+    if tiles * 3 >= slots * 2 or K < 1024:
         return 1
-    return max(1, min(32, round(512 / tiles), K // 256))
+    return max(1, min(32, round(slots / tiles), K // 512))
 
 
 # ------------------------------------------------------------------------------------------------------------
@@ -148,6 +155,8 @@ def gemm(layout: int, a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, *, bi
              ptr(out), out.stride(0), C.byref(epi), s, ptr(ws), st)
         if ev is not None:
             name = _GEMM_SYMBOL[layout].format(o='float' if (s > 1 or out.dtype == torch.float32) else 'bf16')
+            if M % 256 == 0 and N % 256 == 0 and K % 64 == 0:
+                name = name.replace('gemm_bf16_kernel', 'gemm256_kernel')
             if s > 1:
                 name += '+splitk_reduce'
             TRACE.end(ev, name, 2 * M * N * K, 2 * (M * K + N * K) + out.element_size() * M * N)

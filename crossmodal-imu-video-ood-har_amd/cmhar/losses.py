@@ -21,6 +21,23 @@ from . import _lib as L
 from . import kernels as K
 
 
+def gather_global(a_local, b_local, group):
+    """All-gather the two (B_local, D) fp32 embedding matrices of every rank in `group` (rank order) — the
+    global batch DataParallel's gather forms on device 0 (torch `data_parallel.py:173-198`).  Returns
+    (a_all, b_all, row offset of this rank's shard).  `group=None`: single process, no copy."""
+    if group is None:
+        return a_local, b_local, 0
+    import torch.distributed as dist
+    ws = dist.get_world_size(group)
+    rk = dist.get_rank(group)
+    Bl, D = a_local.shape
+    a_all = torch.empty(ws * Bl, D, dtype=a_local.dtype, device=a_local.device)
+    b_all = torch.empty(ws * Bl, D, dtype=b_local.dtype, device=b_local.device)
+    dist.all_gather_into_tensor(a_all, a_local, group=group)
+    dist.all_gather_into_tensor(b_all, b_local, group=group)
+    return a_all, b_all, rk * Bl
+
+
 class _SigLIPFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, a_local, b_local, t, bias, group):
@@ -28,17 +45,7 @@ class _SigLIPFn(torch.autograd.Function):
         a_local = a_local.contiguous().float()
         b_local = b_local.contiguous().float()
         Bl, D = a_local.shape
-        if group is not None:
-            import torch.distributed as dist
-            ws = dist.get_world_size(group)
-            rk = dist.get_rank(group)
-            a_all = torch.empty(ws * Bl, D, dtype=torch.float32, device=dev)
-            b_all = torch.empty(ws * Bl, D, dtype=torch.float32, device=dev)
-            dist.all_gather_into_tensor(a_all, a_local, group=group)
-            dist.all_gather_into_tensor(b_all, b_local, group=group)
-            off = rk * Bl
-        else:
-            a_all, b_all, off = a_local, b_local, 0
+        a_all, b_all, off = gather_global(a_local, b_local, group)
         Bg = a_all.shape[0]
         t_dev = t.detach().reshape(1).to(device=dev, dtype=torch.float32)
         b_dev = bias.detach().reshape(1).to(device=dev, dtype=torch.float32)

@@ -273,17 +273,35 @@ __global__ __launch_bounds__(NT, 2) void gemm_bf16_kernel(int M, int N, int K, c
 #undef As
 #undef Bs
 
-// Sum split-K fp32 partial slabs and apply the epilogue.
+// Sum split-K fp32 partial slabs and apply the epilogue; 8 consecutive columns per thread when N % 8 == 0.
 template <typename OutT>
 __global__ void splitk_reduce_kernel(int M, int N, int splits, const float* __restrict__ P, long split_stride,
                                      OutT* __restrict__ C, long ldc, Epilogue e) {
   const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if ((N & 7) == 0) {
+    const long e0 = idx * 8;
+    if (e0 >= (long)M * N) return;
+    const int m = (int)(e0 / N), n0 = (int)(e0 % N);
+    float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int z = 0; z < splits; ++z) {
+      const floatx4 a = *(const floatx4*)(P + z * split_stride + e0), b = *(const floatx4*)(P + z * split_stride + e0 + 4);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) { s[j] += a[j]; s[4 + j] += b[j]; }
+    }
+    epilogue_store8<OutT>(e, C, ldc, m, n0, s);
+    return;
+  }
   const long total = (long)M * N;
   if (idx >= total) return;
   const int m = (int)(idx / N), n = (int)(idx % N);
   float s = 0.f;
   for (int z = 0; z < splits; ++z) s += P[z * split_stride + idx];
   epilogue_store<OutT>(e, C, ldc, m, n, s);
+}
+
+static inline int reduce_blocks(int M, int N) {
+  const long total = (long)M * N;
+  return (N & 7) == 0 ? cdiv(cdiv(total, 8), 256) : cdiv(total, 256);
 }
 
 // ---------------------------------------------------------------------------------------------------------------
@@ -470,7 +488,7 @@ int launch(int M, int N, int K, const bf16* A, long lda, const bf16* B, long ldb
       gemm256_kernel<AK, BKc, OutT><<<grid, NT2, 0, st>>>(M, N, K, A, lda, B, ldb, C, ldc, e, klen, 0, 0);
     else {
       gemm256_kernel<AK, BKc, float><<<grid, NT2, 0, st>>>(M, N, K, A, lda, B, ldb, ws, N, e, klen, ss, 1);
-      splitk_reduce_kernel<OutT><<<cdiv(ss, 256), 256, 0, st>>>(M, N, nsplit, ws, ss, C, ldc, e);
+      splitk_reduce_kernel<OutT><<<reduce_blocks(M, N), 256, 0, st>>>(M, N, nsplit, ws, ss, C, ldc, e);
     }
     CMHAR_CHECK_LAUNCH();
     return 0;
@@ -490,7 +508,7 @@ int launch(int M, int N, int K, const bf16* A, long lda, const bf16* B, long ldb
   } while (0)
   if (full) GO(false); else GO(true);
 #undef GO
-  if (nsplit > 1) splitk_reduce_kernel<OutT><<<cdiv(ss, 256), 256, 0, st>>>(M, N, nsplit, ws, ss, C, ldc, e);
+  if (nsplit > 1) splitk_reduce_kernel<OutT><<<reduce_blocks(M, N), 256, 0, st>>>(M, N, nsplit, ws, ss, C, ldc, e);
   CMHAR_CHECK_LAUNCH();
   return 0;
 }

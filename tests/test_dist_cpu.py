@@ -1,0 +1,182 @@
+"""Data-parallel path on CPU: world_size-2 `gloo` process groups (the RCCL path on the GPU box uses the same
+code with backend "nccl").
+
+What is checked:
+* `losses.gather_global` forms the global batch in rank order (the gather `nn.DataParallel` does on device 0,
+  reference `main.py:89-93`);
+* DataParallel semantics end to end on a small two-tower stand-in model (Linear → BatchNorm1d(train) → ReLU →
+  Linear per modality, L2-normalised, oracle SigLIP loss over the GLOBAL batch, each rank back-propagating its
+  local rows): after `GradReducer.finish()` every rank holds exactly the gradient of the single-process
+  computation with per-replica BN — i.e. gradients are SUMMED, not averaged;
+* `GradReducer` with a VideoMAE backbone: the flat gradient buffer is cut into several buckets, each bucket's
+  all-reduce is launched as soon as its last parameter is produced (before `finish()`, so it overlaps the rest of
+  backward), and the reduced buffer equals the sum over ranks; the non-backbone parameters are reduced too.
+"""
+import os
+import socket
+import sys
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+import torch.nn as nn
+import torch.nn.functional as F
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(REPO, 'crossmodal-imu-video-ood-har_amd')
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(('127.0.0.1', 0))
+        return s.getsockname()[1]
+
+
+def _init(rank, world, port):
+    for p in (REPO, PKG):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    torch.set_num_threads(1)
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+
+
+def _spawn(fn, world=2):
+    port = _free_port()
+    mp.spawn(fn, args=(world, port), nprocs=world, join=True)
+
+
+# ---------------------------------------------------------------------------------------------------------------
+def _gather_worker(rank, world, port):
+    _init(rank, world, port)
+    from cmhar.losses import gather_global
+    a = torch.full((3, 4), float(rank)) + torch.arange(12.).view(3, 4)
+    b = -a
+    a_all, b_all, off = gather_global(a, b, dist.group.WORLD)
+    assert off == 3 * rank
+    want = torch.cat([torch.full((3, 4), float(r)) + torch.arange(12.).view(3, 4) for r in range(world)])
+    assert torch.equal(a_all, want) and torch.equal(b_all, -want)
+    a1, b1, off1 = gather_global(a, b, None)
+    assert a1 is a and b1 is b and off1 == 0
+    dist.destroy_process_group()
+
+
+def test_gather_global_rank_order():
+    _spawn(_gather_worker)
+
+
+# ---------------------------------------------------------------------------------------------------------------
+class _Tower(nn.Module):
+    def __init__(self, din):
+        super().__init__()
+        self.net = nn.Sequential(nn.Linear(din, 16), nn.BatchNorm1d(16), nn.ReLU(), nn.Linear(16, 8))
+
+    def forward(self, x):
+        return F.normalize(self.net(x), dim=1)
+
+
+class _TwoTower(nn.Module):
+    def __init__(self):
+        super().__init__()
+        self.imu = _Tower(6)
+        self.video = _Tower(10)
+
+    def forward(self, x, y):
+        return self.imu(x), self.video(y)
+
+
+def _data(world, bl=4):
+    g = torch.Generator().manual_seed(7)
+    return torch.randn(world * bl, 6, generator=g), torch.randn(world * bl, 10, generator=g)
+
+
+def _dp_worker(rank, world, port):
+    _init(rank, world, port)
+    from cmhar.dist import GradReducer, broadcast_parameters
+    from cmhar.losses import gather_global
+    from oracle.cpu_model import siglip_loss
+    torch.manual_seed(100 + rank)               # different init per rank: broadcast must fix it
+    model = _TwoTower().train()
+    broadcast_parameters(model)
+    reducer = GradReducer(model, backbone=None)
+    X, Y = _data(world)
+    bl = X.shape[0] // world
+    a, b = model(X[rank * bl:(rank + 1) * bl], Y[rank * bl:(rank + 1) * bl])
+    a_all, b_all, off = gather_global(a.detach().contiguous(), b.detach().contiguous(), dist.group.WORLD)
+    # this rank's rows carry the autograd graph, the others are constants (what the fused loss kernel does)
+    a_all = torch.cat([a_all[:off], a, a_all[off + bl:]])
+    b_all = torch.cat([b_all[:off], b, b_all[off + bl:]])
+    loss = siglip_loss(a_all, b_all, torch.tensor(10.0).log(), torch.tensor(-10.0))
+    reducer.start_step()
+    loss.backward()
+    reducer.finish()
+    # single-process DataParallel equivalent: per-replica BN (each shard through the model separately), one loss
+    torch.manual_seed(100)
+    ref = _TwoTower().train()
+    ref.load_state_dict({k: v for k, v in model.state_dict().items() if 'running' not in k and 'num_batches' not in k},
+                        strict=False)
+    outs = [ref(X[r * bl:(r + 1) * bl], Y[r * bl:(r + 1) * bl]) for r in range(world)]
+    ra = torch.cat([o[0] for o in outs])
+    rb = torch.cat([o[1] for o in outs])
+    rloss = siglip_loss(ra, rb, torch.tensor(10.0).log(), torch.tensor(-10.0))
+    rloss.backward()
+    assert abs(loss.item() - rloss.item()) < 1e-6
+    for (n, p), (_, q) in zip(model.named_parameters(), ref.named_parameters()):
+        torch.testing.assert_close(p.grad, q.grad, rtol=1e-5, atol=1e-7, msg=n)
+    dist.destroy_process_group()
+
+
+def test_dataparallel_semantics_global_loss_summed_grads():
+    _spawn(_dp_worker)
+
+
+# ---------------------------------------------------------------------------------------------------------------
+def _bucket_worker(rank, world, port):
+    _init(rank, world, port)
+    from cmhar.dist import GradReducer, backbone_param_order
+    from cmhar.videomae import VideoMAEBackbone, default_videomae_config
+    cfg = default_videomae_config(image_size=16, patch_size=8, num_frames=4, hidden_size=64, num_hidden_layers=3,
+                                  num_attention_heads=4, intermediate_size=128)
+    torch.manual_seed(0)
+
+    class Wrap(nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.backbone = VideoMAEBackbone(cfg, compute_dtype='fp32')
+            self.head = nn.Linear(64, 5)
+
+    model = Wrap()
+    reducer = GradReducer(model, backbone=model.backbone, bucket_mb=0.05)
+    sink = reducer.sink
+    assert len(reducer.buckets) >= 3
+    order = backbone_param_order(model.backbone)
+    assert [id(p) for p in sink.order] == [id(p) for p in order if p.requires_grad]
+    assert set(map(id, sink.order)) == set(map(id, model.backbone.parameters()))
+    # simulate backward: parameters are produced in sink order, one at a time (β = 0: fresh gradients)
+    reducer.start_step()
+    for i, p in enumerate(sink.order):
+        dst, beta = sink.dest([p], p.shape, 'cpu')
+        assert beta == 0.0 and p.grad is not None
+        dst.copy_(torch.full(p.shape, float(rank + 1)) * (i + 1))
+        sink.done([p])
+    assert all(reducer._launched), 'every bucket must be in flight before finish()'
+    model.head.weight.grad = torch.full_like(model.head.weight, float(rank + 1))
+    model.head.bias.grad = torch.full_like(model.head.bias, 2.0 * (rank + 1))
+    reducer.finish()
+    tot = sum(r + 1 for r in range(world))
+    for i, p in enumerate(sink.order):
+        assert torch.equal(p.grad, torch.full(p.shape, float(tot) * (i + 1))), i
+    assert torch.equal(model.head.weight.grad, torch.full_like(model.head.weight, float(tot)))
+    assert torch.equal(model.head.bias.grad, torch.full_like(model.head.bias, 2.0 * tot))
+    # second step reuses the same buffer: accumulation (β = 1) when .grad is kept
+    reducer.start_step()
+    p0 = sink.order[0]
+    dst, beta = sink.dest([p0], p0.shape, 'cpu')
+    assert beta == 1.0 and dst.data_ptr() == p0.grad.data_ptr()
+    dist.destroy_process_group()
+
+
+def test_grad_reducer_buckets_overlap_and_sum():
+    _spawn(_bucket_worker)
