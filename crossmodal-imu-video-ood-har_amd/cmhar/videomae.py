@@ -257,6 +257,16 @@ def _forward_impl(m: VideoMAEBackbone, video: torch.Tensor, save: bool):
     return x, st
 
 
+_AUX = {}
+
+
+def _aux_stream(dev):
+    s = _AUX.get(dev)
+    if s is None:
+        s = _AUX[dev] = torch.cuda.Stream(dev)
+    return s
+
+
 def _backward_impl(m: VideoMAEBackbone, st, dx, sink):
     """dx: [M, Hd] gradient of the backbone output (compute dtype).  Parameter gradients go to `sink`
     (cmhar.grads): fp32, written by the wgrad GEMM / colsum / LN-backward epilogues with β = 0 or 1."""
@@ -268,9 +278,20 @@ def _backward_impl(m: VideoMAEBackbone, st, dx, sink):
         out, beta = sink.dest(params, shape, dev)
         K.linear_wgrad(dy, x, out=out, beta=beta)
 
+    # Bias gradients (column sums of dy, HBM-bound) run on an auxiliary stream beside the MFMA-bound GEMMs that
+    # read the same dy; the main stream joins it before a layer's gradients are declared final.
+    cur = torch.cuda.current_stream(dev)
+    aux = _aux_stream(dev)
+
     def bgrad(params, dy):
         out, beta = sink.dest(params, (sum(q.numel() for q in params),), dev)
-        K.colsum(dy, out, beta=beta)
+        aux.wait_stream(cur)
+        with torch.cuda.stream(aux):
+            K.colsum(dy, out, beta=beta)
+        dy.record_stream(aux)
+
+    def join():
+        cur.wait_stream(aux)
 
     def ln_grads(wp, bp):
         gw, bw = sink.dest([wp], wp.shape, dev)
@@ -317,10 +338,12 @@ def _backward_impl(m: VideoMAEBackbone, st, dx, sink):
         gw1, gb1, beta = ln_grads(p['ln1w'], p['ln1b'])
         dx = K.layernorm_bwd(dh1, x, p['ln1w'], mu1, rs1, gw1, gb1, dres=dx1, beta_acc=beta)
         del dh1, dx1
+        join()
         sink.done([q for q in p.values() if q is not None])
     pe = m.embeddings.patch_embeddings.projection
     wgrad([pe.weight], dx, st.patches, (pe.weight.shape[0], pe.weight[0].numel()))
     bgrad([pe.bias], dx)
+    join()
     sink.done([pe.weight, pe.bias])
     st.patches = None
 

@@ -17,6 +17,10 @@ namespace {
 
 constexpr float LOG2E = 1.4426950408889634f;
 
+// Raw v_exp_f32: exp2f() wraps it in denormal range fix-ups (cmp/cndmask/ldexp per element) that the softmax
+// does not need — arguments are <= 0 and an underflow to 0 is the right answer.
+__device__ __forceinline__ float fexp2(float x) { return __builtin_amdgcn_exp2f(x); }
+
 // [64 rows][64 bf16] image, 128-B rows; 16-B chunk XOR-swizzle that is conflict-free for both the row reads
 // (ds_read_b128) and the transposed reads (ds_read_b64_tr_b16) of every kernel below (tools/lds_banks.py).
 __device__ __forceinline__ int att_off(int row, int chunk) {
@@ -79,8 +83,13 @@ __device__ __forceinline__ float xhalf(float v) { return __shfl_xor(v, 32); }
 // ---------------------------------------------------------------------------------------------------------------
 // forward
 // ---------------------------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256, 2) void attn_fwd_bf16(int H, int Lq, int Lk, const bf16* __restrict__ Q, long ldq,
-                                                        const bf16* __restrict__ K, long ldk,
+// QB q-blocks of 32 rows per wave (QB = 2: 64 rows): every K row fragment and V transposed fragment read from
+// LDS feeds QB MFMA chains, so LDS read traffic per MFMA is 1/QB of the one-block form (at QB = 1 the reads
+// alone saturate the CU's 128 B/clk LDS port at the MFMA rate).  A workgroup = 4 waves = 128·QB queries starting
+// at q_base; K/V tiles of 64 keys are register-staged into a double-buffered LDS pair (issue early, write late).
+template <int QB>
+__global__ __launch_bounds__(256, 2) void attn_fwd_bf16(int H, int Lq, int Lk, int q_base, const bf16* __restrict__ Q,
+                                                        long ldq, const bf16* __restrict__ K, long ldk,
                                                         const bf16* __restrict__ V, long ldv, bf16* __restrict__ O,
                                                         long ldo, float* __restrict__ lse, float scale) {
   __shared__ __attribute__((aligned(16))) char smem[4 * 8192];
@@ -88,23 +97,29 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_bf16(int H, int Lq, int Lk, c
 #define Vs(buf) (smem + 16384 + 8192 * (buf))
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5;
   const int hd = blockIdx.y, b = blockIdx.z;
-  const int q0 = blockIdx.x * 128 + wave * 32;
+  const int q0 = q_base + blockIdx.x * (128 * QB) + wave * (32 * QB);
   const bf16* Qb = Q + (long)b * Lq * ldq + hd * 64;
   const bf16* Kb = K + (long)b * Lk * ldk + hd * 64;
   const bf16* Vb = V + (long)b * Lk * ldv + hd * 64;
   const float c = scale * LOG2E;
 
-  const int myq = min(q0 + (lane & 31), Lq - 1);
-  bf16x8 qf[4];
+  bf16x8 qf[QB][4];
 #pragma unroll
-  for (int t = 0; t < 4; ++t) qf[t] = *(const bf16x8*)(Qb + (long)myq * ldq + 16 * t + 8 * h);
-
-  floatx16 o[2];
+  for (int j = 0; j < QB; ++j) {
+    const int myq = min(q0 + 32 * j + (lane & 31), Lq - 1);
 #pragma unroll
-  for (int d = 0; d < 2; ++d)
+    for (int t = 0; t < 4; ++t) qf[j][t] = *(const bf16x8*)(Qb + (long)myq * ldq + 16 * t + 8 * h);
+  }
+  floatx16 o[QB][2];
 #pragma unroll
-    for (int r = 0; r < 16; ++r) o[d][r] = 0.f;
-  float m = -INFINITY, l = 0.f;
+  for (int j = 0; j < QB; ++j)
+#pragma unroll
+    for (int d = 0; d < 2; ++d)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) o[j][d][r] = 0.f;
+  float m[QB], l[QB];
+#pragma unroll
+  for (int j = 0; j < QB; ++j) { m[j] = -INFINITY; l[j] = 0.f; }
 
   const int nt = (Lk + 63) / 64;
   Tile64 tk, tv;
@@ -116,78 +131,105 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_bf16(int H, int Lq, int Lk, c
   for (int kt = 0; kt < nt; ++kt) {
     const int cur = kt & 1;
     const bool more = kt + 1 < nt;
-    if (more) {
-      tk.load(Kb, ldk, (kt + 1) * 64, Lk, tid);
-      tv.load(Vb, ldv, (kt + 1) * 64, Lk, tid);
-    }
-    floatx16 s[2];
+    // Sᵀ = K·Qᵀ for every q-block; each K fragment is read once and used QB times
+    floatx16 s[QB][2];
 #pragma unroll
     for (int kb = 0; kb < 2; ++kb) {
 #pragma unroll
-      for (int r = 0; r < 16; ++r) s[kb][r] = 0.f;
+      for (int j = 0; j < QB; ++j)
 #pragma unroll
-      for (int t = 0; t < 4; ++t)
-        s[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag(Ks(cur), kb * 32, t, lane), qf[t], s[kb], 0, 0, 0);
+        for (int r = 0; r < 16; ++r) s[j][kb][r] = 0.f;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const bf16x8 kf = row_frag(Ks(cur), kb * 32, t, lane);
+#pragma unroll
+        for (int j = 0; j < QB; ++j)
+          s[j][kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[j][t], s[j][kb], 0, 0, 0);
+      }
     }
-    float mt = -INFINITY;
+    if (more) {   // next tile's global loads fly under the softmax and P·V (written to LDS after them)
+      tk.load(Kb, ldk, (kt + 1) * 64, Lk, tid);
+      tv.load(Vb, ldv, (kt + 1) * 64, Lk, tid);
+    }
     const int kbase = kt * 64;
-    const bool partial = kbase + 64 > Lk;
+    if (kbase + 64 > Lk) {   // ragged last tile only (wave-uniform branch)
+#pragma unroll
+      for (int j = 0; j < QB; ++j)
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+          for (int r = 0; r < 16; ++r)
+            if (kbase + kb * 32 + acc_row(r, h) >= Lk) s[j][kb][r] = -INFINITY;
+    }
+    bf16x8 pb[QB][2][2];
+#pragma unroll
+    for (int j = 0; j < QB; ++j) {
+      float mt = -INFINITY;
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float v = s[j][kb][r] * c;
+          s[j][kb][r] = v;
+          mt = fmaxf(mt, v);
+        }
+      mt = fmaxf(mt, xhalf(mt));
+      const float mn = fmaxf(m[j], mt);
+      const float alpha = fexp2(m[j] - mn);
+      m[j] = mn;
+      l[j] *= alpha;
+#pragma unroll
+      for (int d = 0; d < 2; ++d)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) o[j][d][r] *= alpha;
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float p = fexp2(s[j][kb][r] - mn);
+          s[j][kb][r] = p;
+          l[j] += p;
+        }
+#pragma unroll
+        for (int ss = 0; ss < 2; ++ss) pb[j][kb][ss] = pack8(s[j][kb], ss);   // P leaves fp32 registers here
+      }
+    }
+    // Oᵀ += Vᵀ·Pᵀ; each V transposed fragment is read once and used QB times
 #pragma unroll
     for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        float v = s[kb][r] * c;
-        if (partial && kbase + kb * 32 + acc_row(r, h) >= Lk) v = -INFINITY;
-        s[kb][r] = v;
-        mt = fmaxf(mt, v);
-      }
-    mt = fmaxf(mt, xhalf(mt));
-    const float mn = fmaxf(m, mt);
-    const float alpha = exp2f(m - mn);
-    m = mn;
-    l *= alpha;
+      for (int ss = 0; ss < 2; ++ss)
 #pragma unroll
-    for (int d = 0; d < 2; ++d)
+        for (int d = 0; d < 2; ++d) {
+          const bf16x8 vf = tr_frag(Vs(cur), kb * 32, ss, d * 32, lane);
 #pragma unroll
-      for (int r = 0; r < 16; ++r) o[d][r] *= alpha;
-#pragma unroll
-    for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const float p = exp2f(s[kb][r] - mn);
-        s[kb][r] = p;
-        l += p;
-      }
-#pragma unroll
-    for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-      for (int ss = 0; ss < 2; ++ss) {
-        const bf16x8 pb = pack8(s[kb], ss);
-#pragma unroll
-        for (int d = 0; d < 2; ++d)
-          o[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_frag(Vs(cur), kb * 32, ss, d * 32, lane), pb, o[d], 0, 0, 0);
-      }
+          for (int j = 0; j < QB; ++j)
+            o[j][d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pb[j][kb][ss], o[j][d], 0, 0, 0);
+        }
     if (more) {
       tk.store(Ks(cur ^ 1), tid);
       tv.store(Vs(cur ^ 1), tid);
     }
     __syncthreads();
   }
-  l += xhalf(l);
-  const float inv = 1.f / l;
-  const int q = q0 + (lane & 31);
-  if (q < Lq) {
-    bf16* orow = O + ((long)b * Lq + q) * ldo + hd * 64;
 #pragma unroll
-    for (int d = 0; d < 2; ++d)
+  for (int j = 0; j < QB; ++j) {
+    const float lj = l[j] + xhalf(l[j]);
+    const float inv = 1.f / lj;
+    const int q = q0 + 32 * j + (lane & 31);
+    if (q < Lq) {
+      bf16* orow = O + ((long)b * Lq + q) * ldo + hd * 64;
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        bf16x4 v;
+      for (int d = 0; d < 2; ++d)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) v[j] = (bf16)(o[d][4 * g + j] * inv);
-        *(bf16x4*)(orow + d * 32 + 8 * g + 4 * h) = v;
-      }
-    if (h == 0) lse[((long)b * H + hd) * Lq + q] = m + log2f(l);   // log2-domain LSE of (scale*log2e)*s
+        for (int g = 0; g < 4; ++g) {
+          bf16x4 v;
+#pragma unroll
+          for (int jj = 0; jj < 4; ++jj) v[jj] = (bf16)(o[j][d][4 * g + jj] * inv);
+          *(bf16x4*)(orow + d * 32 + 8 * g + 4 * h) = v;
+        }
+      if (h == 0) lse[((long)b * H + hd) * Lq + q] = m[j] + log2f(lj);   // log2-domain LSE of (scale*log2e)*s
+    }
   }
 }
 
@@ -233,6 +275,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_bf16(int H, int Lq, int 
   const float* lseb = lse + ((long)b * H + hd) * Lq;
   const float* delb = delta + ((long)b * H + hd) * Lq;
   const float c = scale * LOG2E;
+  const float inv_c = 1.f / c;
 
   const int myk = min(k0 + (lane & 31), Lk - 1);
   bf16x8 kf[4], vf[4];
@@ -253,10 +296,10 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_bf16(int H, int Lq, int 
   auto load_rows = [&](int qt) {
     tq.load(Qb, ldq, qt * 64, Lq, tid);
     tg.load(Gb, lddo, qt * 64, Lq, tid);
-    if (tid < 64) {
+    if (tid < 64) {   // row constants staged pre-negated (and -lse pre-divided by c): accumulator seeds
       const int q = qt * 64 + tid;
-      lv = q < Lq ? lseb[q] : INFINITY;
-      dv_ = q < Lq ? delb[q] : 0.f;
+      lv = q < Lq ? -lseb[q] * inv_c : -INFINITY;
+      dv_ = q < Lq ? -delb[q] : 0.f;
     }
   };
   auto store_rows = [&](int buf) {
@@ -280,8 +323,8 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_bf16(int H, int Lq, int 
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int q = qb * 32 + acc_row(r, h);
-        s[r] = -L_[q] / c;
-        dp[r] = -D_[q];
+        s[r] = L_[q];
+        dp[r] = D_[q];
       }
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
@@ -290,7 +333,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_bf16(int H, int Lq, int 
       }
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const float p = exp2f(s[r] * c);
+        const float p = fexp2(s[r] * c);
         s[r] = p;
         dp[r] = p * dp[r];   // dS = P ∘ (dP − δ)
       }
@@ -380,12 +423,13 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_bf16(int H, int Lq, int Lk
         s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag(Ks(cur), kb * 32, t, lane), qf[t], s, 0, 0, 0);
         dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag(Vs(cur), kb * 32, t, lane), gf[t], dp, 0, 0, 0);
       }
+      if (kbase + 64 > Lk) {   // ragged last tile only (wave-uniform branch)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        float p = exp2f(s[r] * c);
-        if (kbase + kb * 32 + acc_row(r, h) >= Lk) p = 0.f;
-        dp[r] = p * dp[r];
+        for (int r = 0; r < 16; ++r)
+          if (kbase + kb * 32 + acc_row(r, h) >= Lk) s[r] = -INFINITY;
       }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) dp[r] = fexp2(s[r] * c) * dp[r];
 #pragma unroll
       for (int ss = 0; ss < 2; ++ss) {
         const bf16x8 db = pack8(dp, ss);
@@ -599,9 +643,15 @@ extern "C" int cmhar_attention_fwd(int dtype, int B, int H, int Lq, int Lk, int 
                                    float scale, float pdrop, unsigned long long seed, hipStream_t st) {
   if (B <= 0 || Lq <= 0) return 0;
   if (dtype == CMHAR_BF16 && D == 64 && pdrop == 0.f) {
-    dim3 grid(cdiv(Lq, 128), H, B);
-    attn_fwd_bf16<<<grid, 256, 0, st>>>(H, Lq, Lk, (const bf16*)Q, ldq, (const bf16*)K, ldk, (const bf16*)V, ldv,
-                                        (bf16*)O, ldo, lse, scale);
+    // 256-query workgroups (64 rows per wave) over the bulk, 128-query workgroups (32 rows per wave) for the rest
+    const int bulk = (Lq / 256) * 256;
+    if (bulk > 0)
+      attn_fwd_bf16<2><<<dim3(bulk / 256, H, B), 256, 0, st>>>(H, Lq, Lk, 0, (const bf16*)Q, ldq, (const bf16*)K, ldk,
+                                                               (const bf16*)V, ldv, (bf16*)O, ldo, lse, scale);
+    if (Lq > bulk)
+      attn_fwd_bf16<1><<<dim3(cdiv(Lq - bulk, 128), H, B), 256, 0, st>>>(H, Lq, Lk, bulk, (const bf16*)Q, ldq,
+                                                                         (const bf16*)K, ldk, (const bf16*)V, ldv,
+                                                                         (bf16*)O, ldo, lse, scale);
   } else {
     // exact-fp32 math path (fp32 storage, or bf16 storage with a head dim / dropout the flash kernel lacks);
     // its LSE is in natural-log units and is only ever consumed by the matching backward below

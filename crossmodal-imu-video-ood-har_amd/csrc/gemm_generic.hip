@@ -7,14 +7,50 @@
 
 namespace {
 
-constexpr int TM = 64, TN = 64, TK = 16;
+constexpr int TM = 64, TN = 64, TK = 32, NTH = 256;
+constexpr int PER = TM * TK / NTH;        // 8 A and 8 B elements staged per thread per K-tile
+
+// The GEMMs this kernel serves are small (tens of blocks) with K up to a few thousand, so a K-step is bounded by
+// memory LATENCY, not bandwidth: tile k+1 is loaded into registers while tile k is consumed from LDS (double-
+// buffered LDS, one barrier per K-step), so each step pays compute + one overlapped fetch.
+template <typename TIn>
+struct GenStage {
+  float a[PER], b[PER];
+  __device__ __forceinline__ void load(const TIn* __restrict__ A, long sam, long sak, const TIn* __restrict__ B,
+                                       long sbk, long sbn, int M, int N, int K, int bm, int bn, int k0, int tid) {
+#pragma unroll
+    for (int it = 0; it < PER; ++it) {
+      const int i = it * NTH + tid;
+      int mm, kk;
+      if (sak == 1) { mm = i / TK; kk = i % TK; } else { kk = i / TM; mm = i % TM; }
+      const int gm = bm + mm, gk = k0 + kk;
+      a[it] = (gm < M && gk < K) ? to_f<TIn>(A[gm * sam + gk * sak]) : 0.f;
+      int nn, kb;
+      if (sbn == 1) { kb = i / TN; nn = i % TN; } else { nn = i / TK; kb = i % TK; }
+      const int gn = bn + nn, gkb = k0 + kb;
+      b[it] = (gn < N && gkb < K) ? to_f<TIn>(B[gkb * sbk + gn * sbn]) : 0.f;
+    }
+  }
+  __device__ __forceinline__ void store(float (*As)[TM + 4], float (*Bs)[TN + 4], long sak, long sbn, int tid) const {
+#pragma unroll
+    for (int it = 0; it < PER; ++it) {
+      const int i = it * NTH + tid;
+      int mm, kk;
+      if (sak == 1) { mm = i / TK; kk = i % TK; } else { kk = i / TM; mm = i % TM; }
+      As[kk][mm] = a[it];
+      int nn, kb;
+      if (sbn == 1) { kb = i / TN; nn = i % TN; } else { nn = i / TK; kb = i % TK; }
+      Bs[kb][nn] = b[it];
+    }
+  }
+};
 
 template <typename TIn, typename TOut>
-__global__ __launch_bounds__(256) void gemm_generic_kernel(
+__global__ __launch_bounds__(NTH) void gemm_generic_kernel(
     int M, int N, int K, const TIn* __restrict__ A, long sam, long sak, long sAb, const TIn* __restrict__ B,
     long sbk, long sbn, long sBb, TOut* __restrict__ C, long ldc, long sCb, Epilogue e) {
-  __shared__ float As[TK][TM + 4];
-  __shared__ float Bs[TK][TN + 4];
+  __shared__ float As[2][TK][TM + 4];
+  __shared__ float Bs[2][TK][TN + 4];
   const int tid = threadIdx.x;
   const int bm = blockIdx.y * TM, bn = blockIdx.x * TN;
   A += blockIdx.z * sAb;
@@ -22,31 +58,25 @@ __global__ __launch_bounds__(256) void gemm_generic_kernel(
   C += blockIdx.z * sCb;
   const int tr = tid / 16, tc = tid % 16;   // 16x16 threads, 4x4 outputs each
   float acc[4][4] = {};
-  for (int k0 = 0; k0 < K; k0 += TK) {
-    for (int i = tid; i < TM * TK; i += 256) {
-      // A tile: choose the faster-varying index along the contiguous dimension
-      int mm, kk;
-      if (sak == 1) { mm = i / TK; kk = i % TK; } else { kk = i / TM; mm = i % TM; }
-      const int gm = bm + mm, gk = k0 + kk;
-      As[kk][mm] = (gm < M && gk < K) ? to_f<TIn>(A[gm * sam + gk * sak]) : 0.f;
-    }
-    for (int i = tid; i < TN * TK; i += 256) {
-      int nn, kk;
-      if (sbn == 1) { kk = i / TN; nn = i % TN; } else { nn = i / TK; kk = i % TK; }
-      const int gn = bn + nn, gk = k0 + kk;
-      Bs[kk][nn] = (gn < N && gk < K) ? to_f<TIn>(B[gk * sbk + gn * sbn]) : 0.f;
-    }
-    __syncthreads();
-#pragma unroll
+  const int nk = (K + TK - 1) / TK;
+  GenStage<TIn> st;
+  st.load(A, sam, sak, B, sbk, sbn, M, N, K, bm, bn, 0, tid);
+  st.store(As[0], Bs[0], sak, sbn, tid);
+  __syncthreads();
+  for (int t = 0; t < nk; ++t) {
+    const int cur = t & 1;
+    if (t + 1 < nk) st.load(A, sam, sak, B, sbk, sbn, M, N, K, bm, bn, (t + 1) * TK, tid);
+#pragma unroll 8
     for (int kk = 0; kk < TK; ++kk) {
       float a[4], b[4];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) { a[i] = As[kk][tr + 16 * i]; b[i] = Bs[kk][tc + 16 * i]; }
+      for (int i = 0; i < 4; ++i) { a[i] = As[cur][kk][tr + 16 * i]; b[i] = Bs[cur][kk][tc + 16 * i]; }
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = fmaf(a[i], b[j], acc[i][j]);
     }
+    if (t + 1 < nk) st.store(As[cur ^ 1], Bs[cur ^ 1], sak, sbn, tid);
     __syncthreads();
   }
 #pragma unroll
