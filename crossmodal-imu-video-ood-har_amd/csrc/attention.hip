@@ -164,16 +164,13 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_bf16(int H, int Lq, int Lk, i
     bf16x8 pb[QB][2][2];
 #pragma unroll
     for (int j = 0; j < QB; ++j) {
+      // row max on the raw scores (c > 0), then p = exp2(c·s − m) as one fma + v_exp per element
       float mt = -INFINITY;
 #pragma unroll
       for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const float v = s[j][kb][r] * c;
-          s[j][kb][r] = v;
-          mt = fmaxf(mt, v);
-        }
-      mt = fmaxf(mt, xhalf(mt));
+        for (int r = 0; r < 16; ++r) mt = fmaxf(mt, s[j][kb][r]);
+      mt = fmaxf(mt, xhalf(mt)) * c;
       const float mn = fmaxf(m[j], mt);
       const float alpha = fexp2(m[j] - mn);
       m[j] = mn;
@@ -186,7 +183,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_bf16(int H, int Lq, int Lk, i
       for (int kb = 0; kb < 2; ++kb) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const float p = fexp2(s[j][kb][r] - mn);
+          const float p = fexp2(fmaf(s[j][kb][r], c, -mn));
           s[j][kb][r] = p;
           l[j] += p;
         }
