@@ -357,9 +357,8 @@ __device__ __forceinline__ bf16x8 frag256(const char* lds, int r0, int kk, int l
   }
 }
 
-// MODE (ablation builds only, tools/debug): 0 = product; 1 = operand DMA only (no MFMA); 2 = MFMA only (no DMA
-// after the first tile); 3 = epilogue only (no K loop); 4 = K loop only (no epilogue); 5 = LDS staging only;
-// 6 = staging + plain bf16 stores.
+// MODE (ablation builds only, tools/debug): 0 = product; 3 = epilogue only (no K loop); 4 = K loop only (no
+// epilogue); 5 = LDS staging only; 6 = staging + plain bf16 stores.
 template <bool A_KC, bool B_KC, typename OutT, int MODE = 0>
 __global__ __launch_bounds__(NT2, 2) void gemm256_kernel(int M, int N, int K, const bf16* __restrict__ A, long lda,
                                                          const bf16* __restrict__ B, long ldb, OutT* __restrict__ C,
@@ -384,31 +383,41 @@ __global__ __launch_bounds__(NT2, 2) void gemm256_kernel(int M, int N, int K, co
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
 
+  // Software-pipelined K loop.  Per K-tile of 64 (two 32-deep MFMA steps kk = 0, 1):
+  //   issue the LDS-DMA of tile kt+1 into the other buffer;
+  //   kk = 0: 32 MFMAs, each A slot refilled with its kk = 1 fragment once its 4 MFMAs have issued;
+  //   kk = 1, A rows 0-3: 16 MFMAs;
+  //   sync point: vmcnt(0) (own DMA of kt+1 landed) + lgkmcnt(0) (own reads of tile kt done) + barrier;
+  //     then tile kt+1's kk = 0 fragments are read into the freed slots WHILE
+  //   kk = 1, A rows 4-7: the last 16 MFMAs of tile kt still run.
+  // So the post-barrier LDS read latency hides under MFMAs instead of stalling all 8 waves at every barrier.
+  bf16x8 af[8], bf0[4], bf1[4];
+  auto load_k0 = [&](const char* a_s, const char* b_s, int i_lo, int i_hi, bool with_b) {
+    if (with_b) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bf0[j] = frag256<B_KC>(b_s, wc * 64 + j * 16, 0, lane);
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+      if (i >= i_lo && i < i_hi) af[i] = frag256<A_KC>(a_s, wr * 128 + i * 16, 0, lane);
+  };
   if (nk > 0) {
     dma_tile<A_KC>(A, lda, bm, kbeg, smem, wave, lane);
     dma_tile<B_KC>(B, ldb, bn, kbeg, smem + 32768, wave, lane);
+    __syncthreads();                                        // tile 0 landed
+    load_k0(smem, smem + 32768, 0, 8, true);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) bf1[j] = frag256<B_KC>(smem + 32768, wc * 64 + j * 16, 1, lane);
   }
   for (int kt = 0; kt < nk; ++kt) {
-    __syncthreads();                                        // tile kt landed (vmcnt(0)) + buffer kt+1 free
     const char* a_s = smem + (kt & 1) * 65536;
     const char* b_s = a_s + 32768;
-    if (MODE != 2 && kt + 1 < nk) {
-      char* nxt = smem + ((kt + 1) & 1) * 65536;
+    const bool more = kt + 1 < nk;
+    char* nxt = smem + ((kt + 1) & 1) * 65536;
+    if (more) {
       dma_tile<A_KC>(A, lda, bm, kbeg + (kt + 1) * TK2, nxt, wave, lane);
       dma_tile<B_KC>(B, ldb, bn, kbeg + (kt + 1) * TK2, nxt + 32768, wave, lane);
     }
-    if (MODE == 1) continue;
-    // Rolling fragment prefetch: all of k-step 0's fragments plus k-step 1's B fragments are requested up
-    // front (16 ds_reads); each A slot is refilled with its k-step-1 fragment as soon as its 4 MFMAs have
-    // issued, so ~11 reads stay in flight under the MFMAs and every wait is a counted lgkmcnt.  The
-    // sched_barriers stop the scheduler from sinking the reads back next to their uses.
-    bf16x8 af[8], bf0[4], bf1[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) bf0[j] = frag256<B_KC>(b_s, wc * 64 + j * 16, 0, lane);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) af[i] = frag256<A_KC>(a_s, wr * 128 + i * 16, 0, lane);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) bf1[j] = frag256<B_KC>(b_s, wc * 64 + j * 16, 1, lane);
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
@@ -418,9 +427,27 @@ __global__ __launch_bounds__(NT2, 2) void gemm256_kernel(int M, int N, int K, co
       __builtin_amdgcn_sched_barrier(0);
     }
 #pragma unroll
-    for (int i = 0; i < 8; ++i)
+    for (int i = 0; i < 4; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bf1[j], acc[i][j], 0, 0, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    if (more) {
+      // own DMA of tile kt+1 landed, own reads of tile kt returned; then everyone's
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      load_k0(nxt, nxt + 32768, 0, 4, true);               // slots 0-3 and bf0 are free now
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int i = 4; i < 8; ++i) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bf1[j], acc[i][j], 0, 0, 0);
+      if (more) af[i] = frag256<A_KC>(nxt, wr * 128 + i * 16, 0, lane);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if (more) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bf1[j] = frag256<B_KC>(nxt + 32768, wc * 64 + j * 16, 1, lane);
+    }
   }
   __syncthreads();
   if (MODE == 4) {   // keep every accumulator live, store nothing

@@ -10,6 +10,7 @@ lib = C.CDLL(os.path.join(HERE, 'libablate.so'))
 vp, i32, i64 = C.c_void_p, C.c_int, C.c_long
 lib.ablate_gemm256.argtypes = [i32, i32, i32, i32, i32, vp, i64, vp, i64, vp, i64, vp]
 lib.ablate_gemm128.argtypes = [i32, i32, i32, i32, vp, i64, vp, i64, vp, i64, vp]
+lib.ablate_gemm256p.argtypes = [i32, i32, i32, i32, vp, i64, vp, i64, vp, i64, vp]
 
 
 def run(fn, reps=20):
@@ -30,7 +31,12 @@ def main():
     st = torch.cuda.current_stream().cuda_stream
     shapes = [('qkv', 0, 50176, 2304, 768), ('fc1', 0, 50176, 3072, 768), ('fc2', 0, 50176, 768, 3072),
               ('dgrad_fc1', 1, 50176, 768, 3072), ('wgrad_fc1', 2, 3072, 768, 50176)]
+    only = sys.argv[1].split(',') if len(sys.argv) > 1 else None
+    modes = [int(x) for x in sys.argv[2].split(',')] if len(sys.argv) > 2 else [0, 3, 4, 5, 6]
+    tags = {0: 'full', 1: 'dma_only', 2: 'mfma_only', 3: 'epi_only', 4: 'no_epi', 5: 'stage_only', 6: 'plain_store'}
     for name, layout, M, N, K in shapes:
+        if only and name not in only:
+            continue
         if layout == 0:
             a = torch.randn(M, K, device=dev).bfloat16(); b = torch.randn(N, K, device=dev).bfloat16()
         elif layout == 1:
@@ -40,11 +46,13 @@ def main():
         c = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
         fl = 2 * M * N * K
         res = {}
-        for mode, tag in ((0, 'full'), (1, 'dma_only'), (2, 'mfma_only'), (3, 'epi_only'), (4, 'no_epi'),
-                          (5, 'stage_only'), (6, 'plain_store')):
+        for mode, tag in ((m, tags[m]) for m in modes):
             ms = run(lambda: lib.ablate_gemm256(mode, layout, M, N, K, a.data_ptr(), a.stride(0), b.data_ptr(),
                                                 b.stride(0), c.data_ptr(), c.stride(0), st))
             res[tag] = (ms, fl / ms / 1e9)
+        ms = run(lambda: lib.ablate_gemm256p(layout, M, N, K, a.data_ptr(), a.stride(0), b.data_ptr(), b.stride(0),
+                                             c.data_ptr(), c.stride(0), st))
+        res['gemm256p'] = (ms, fl / ms / 1e9)
         ms = run(lambda: lib.ablate_gemm128(layout, M, N, K, a.data_ptr(), a.stride(0), b.data_ptr(), b.stride(0),
                                             c.data_ptr(), c.stride(0), st))
         res['gemm128'] = (ms, fl / ms / 1e9)
