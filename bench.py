@@ -28,6 +28,27 @@ PEAK_BF16_TFLOPS = 2500.0      # MI355X dense bf16 MFMA (MI355X_MICROARCH.md; sp
 PEAK_HBM_GBS = 8000.0
 
 
+TRAFFIC_JSON = os.path.join(REPO, 'profiles', 'r01_pmc_traffic.json')
+
+
+def pmc_traffic(label):
+    """HBM bytes per launch of the traced kernel `label` (e.g. 'gemm256_kernel<true,false,bf16>') from the committed
+    PMC summary of this same bench command (tools/pmc_traffic.py), or None when it has no entry."""
+    if not os.path.exists(TRAFFIC_JSON) or '<' not in label:
+        return None
+    base, args = label.split('<', 1)
+    code = {'true': 'Lb1E', 'false': 'Lb0E', 'bf16': 'DF16b', 'float': 'f'}
+    mangled = base + 'I' + ''.join(code[a.strip()] for a in args.rstrip('>').split(','))
+    with open(TRAFFIC_JSON) as f:
+        ks = json.load(f)['kernels']
+    demangled = base + '<' + ', '.join(a.strip() for a in args.rstrip('>').split(','))   # rocprof demangles some
+    hits = [v for k, v in ks.items() if mangled in k or demangled in k]
+    if not hits:
+        return None
+    n = sum(v['dispatches'] for v in hits)
+    return int(sum(v['hbm_bytes_per_launch'] * v['dispatches'] for v in hits) / n)
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
@@ -173,15 +194,18 @@ def main():
     value = clips / elapsed
     ms = 1000 * elapsed / args.steps
 
-    # dominant kernel (largest total time among traced HIP kernels), FLOP-weighted over its launches
+    # dominant kernel: the single HIP kernel (not a multi-kernel entry such as attention backward or split-K +
+    # reduce) with the largest traced time; achieved = its algorithmic FLOPs / its HIP-event-measured time
     roof = None
     summ = K.TRACE.summary() if not args.no_trace else {}
-    if summ:
-        name, (n, tot_ms, fl, nb) = max(summ.items(), key=lambda kv: kv[1][1])
+    single = {k: v for k, v in summ.items() if '+' not in k and '(' not in k}
+    if single:
+        name, (n, tot_ms, fl, nb) = max(single.items(), key=lambda kv: kv[1][1])
         achieved = fl / (tot_ms / 1e3) / 1e12
         roof = {'bound': 'mfma', 'achieved': round(achieved, 1), 'peak': PEAK_BF16_TFLOPS, 'unit': 'TFLOP/s',
-                'frac': round(achieved / PEAK_BF16_TFLOPS, 4), 'traffic': None, 'kernel': name,
-                'launches': n, 'avg_launch_ms': round(tot_ms / n, 4)}
+                'frac': round(achieved / PEAK_BF16_TFLOPS, 4), 'traffic': pmc_traffic(name), 'kernel': name,
+                'launches': n, 'avg_launch_ms': round(tot_ms / n, 4),
+                'algorithmic_bytes_per_launch': int(nb / n)}
     embed_f, fwd_f = videomae_flops_per_clip(args.frames, args.image, args.image)
     step_flops_clip = 3 * fwd_f - embed_f           # fwd + 2x bwd, no pixel gradient for the tubelet conv
     whole_tflops = step_flops_clip * clips / elapsed / 1e12

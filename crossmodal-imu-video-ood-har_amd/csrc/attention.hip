@@ -80,6 +80,17 @@ __device__ __forceinline__ int acc_row(int r, int h) { return (r & 3) + 8 * (r >
 
 __device__ __forceinline__ float xhalf(float v) { return __shfl_xor(v, 32); }
 
+// (block, head, batch) of a flash workgroup with every block of one (batch, head) on the same XCD (K/V, or Q/dO,
+// of that head is then fetched into one L2 and re-read from it by the head's other blocks).
+struct BlkIdx { int blk, hd, b; };
+__device__ __forceinline__ BlkIdx flash_block(int H) {
+  const int nb = gridDim.x;
+  const int lin = blockIdx.x + nb * (blockIdx.y + gridDim.y * blockIdx.z);
+  const int r = xcd_remap(lin, nb * gridDim.y * gridDim.z);
+  const int bh = r / nb;
+  return {r % nb, bh % H, bh / H};
+}
+
 // ---------------------------------------------------------------------------------------------------------------
 // forward
 // ---------------------------------------------------------------------------------------------------------------
@@ -96,8 +107,9 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_bf16(int H, int Lq, int Lk, i
 #define Ks(buf) (smem + 8192 * (buf))
 #define Vs(buf) (smem + 16384 + 8192 * (buf))
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5;
-  const int hd = blockIdx.y, b = blockIdx.z;
-  const int q0 = q_base + blockIdx.x * (128 * QB) + wave * (32 * QB);
+  const BlkIdx bi = flash_block(H);
+  const int hd = bi.hd, b = bi.b;
+  const int q0 = q_base + bi.blk * (128 * QB) + wave * (32 * QB);
   const bf16* Qb = Q + (long)b * Lq * ldq + hd * 64;
   const bf16* Kb = K + (long)b * Lk * ldk + hd * 64;
   const bf16* Vb = V + (long)b * Lk * ldv + hd * 64;
@@ -265,8 +277,9 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_bf16(int H, int Lq, int 
   float* Ls = (float*)(smem + 32768);          // [2][64] lse
   float* Ds = Ls + 128;                         // [2][64] delta
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5;
-  const int hd = blockIdx.y, b = blockIdx.z;
-  const int k0 = blockIdx.x * 128 + wave * 32;
+  const BlkIdx bi = flash_block(H);
+  const int hd = bi.hd, b = bi.b;
+  const int k0 = bi.blk * 128 + wave * 32;
   const bf16* Qb = Q + (long)b * Lq * ldq + hd * 64;
   const bf16* Gb = dO + (long)b * Lq * lddo + hd * 64;
   const float* lseb = lse + ((long)b * H + hd) * Lq;
@@ -376,8 +389,9 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_bf16(int H, int Lq, int Lk
 #define Ks(buf) (smem + 8192 * (buf))
 #define Vs(buf) (smem + 16384 + 8192 * (buf))
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5;
-  const int hd = blockIdx.y, b = blockIdx.z;
-  const int q0 = blockIdx.x * 128 + wave * 32;
+  const BlkIdx bi = flash_block(H);
+  const int hd = bi.hd, b = bi.b;
+  const int q0 = bi.blk * 128 + wave * 32;
   const bf16* Kb = K + (long)b * Lk * ldk + hd * 64;
   const bf16* Vb = V + (long)b * Lk * ldv + hd * 64;
   const float c = scale * LOG2E;

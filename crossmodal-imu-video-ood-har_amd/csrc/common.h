@@ -86,6 +86,14 @@ __device__ __forceinline__ void epilogue_store(const Epilogue& e, OutT* __restri
   *p = from_f<OutT>(v);
 }
 
+// XCD-aware bijective block remap: workgroups are dispatched round-robin over the 8 XCDs by linear block id, so
+// id → (id % 8)'s contiguous chunk of the logical index space; logically adjacent blocks (sharing operand panels,
+// or the K/V of one attention head) then run on one XCD and share its L2.
+__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
+  const int q = nwg / 8, r = nwg % 8, xcd = bid % 8;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8;
+}
+
 #define CMHAR_CHECK_LAUNCH() do { hipError_t _e = hipGetLastError(); if (_e != hipSuccess) return (int)_e; } while (0)
 
 static inline int cdiv(long a, long b) { return (int)((a + b - 1) / b); }

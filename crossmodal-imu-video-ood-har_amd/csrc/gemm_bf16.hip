@@ -83,10 +83,6 @@ __device__ __forceinline__ bf16x8 frag(const char* lds, int r0, int kk, int lane
   }
 }
 
-__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
-  const int q = nwg / 8, r = nwg % 8, xcd = bid % 8;
-  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8;
-}
 
 // 8 consecutive elements of an OutT row as fp32 / back, with single 16-B (bf16) or 2 x 16-B (fp32) accesses.
 template <typename OutT>
@@ -183,14 +179,17 @@ __global__ __launch_bounds__(NT, 2) void gemm_bf16_kernel(int M, int N, int K, c
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wr = wave >> 1, wc = wave & 1;
   const int tiles_n = (N + BN - 1) / BN, tiles_m = (M + BM - 1) / BM;
-  const int bid = xcd_remap(blockIdx.x, tiles_m * tiles_n);
+  // split index folded into the XCD remap: one XCD runs whole splits, whose CUs then share each K-slice in L2
+  const int ntile = tiles_m * tiles_n;
+  const int rlin = xcd_remap(blockIdx.x + ntile * blockIdx.z, ntile * gridDim.z);
+  const int bid = rlin % ntile, split = rlin / ntile;
   // row-major tile order: the blocks an XCD runs together share A row panels while the whole (small) weight
   // matrix stays resident in that XCD's L2 — activations are streamed from HBM once
   const int tm = bid / tiles_n, tn = bid % tiles_n;
   const int bm = tm * BM, bn = tn * BN;
-  const int kbeg = blockIdx.z * klen;
+  const int kbeg = split * klen;
   const int kend = min(K, kbeg + klen);
-  C += (long)blockIdx.z * split_stride;
+  C += (long)split * split_stride;
 
   floatx4 acc[4][4];
 #pragma unroll
@@ -369,12 +368,15 @@ __global__ __launch_bounds__(NT2, 2) void gemm256_kernel(int M, int N, int K, co
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = wave >> 2, wc = wave & 3;
   const int tiles_n = N / TN2, tiles_m = M / TM2;
-  const int bid = xcd_remap(blockIdx.x, tiles_m * tiles_n);
+  // split index folded into the XCD remap: one XCD runs whole splits, whose CUs then share each K-slice in L2
+  const int ntile = tiles_m * tiles_n;
+  const int rlin = xcd_remap(blockIdx.x + ntile * blockIdx.z, ntile * gridDim.z);
+  const int bid = rlin % ntile, split = rlin / ntile;
   const int tm = bid / tiles_n, tn = bid % tiles_n;
   const int bm = tm * TM2, bn = tn * TN2;
-  const int kbeg = blockIdx.z * klen;
+  const int kbeg = split * klen;
   const int kend = min(K, kbeg + klen);
-  C += (long)blockIdx.z * split_stride;
+  C += (long)split * split_stride;
   const int nk = MODE >= 3 && MODE != 4 ? 0 : (kend - kbeg) / TK2;
 
   floatx4 acc[8][4];
