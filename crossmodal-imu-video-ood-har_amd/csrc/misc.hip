@@ -2,6 +2,7 @@
 // PatchTST embedding, strided copies with dtype conversion, and the multi-tensor optimizer step
 // (clip_grad_norm_ + AdamW, trainer.py:138-141) with fused bf16 shadow-weight refresh.
 #include "common.h"
+#include <algorithm>
 
 namespace {
 
@@ -59,39 +60,41 @@ __global__ void imu_embed_fwd_kernel(int B, int C, int L, int N, int P, int S, i
 }
 
 // Gradients: dcls, dpos[0:T] (rest of the table untouched → zero), dW_c, db_c (channels without live tokens → 0).
-__global__ void imu_embed_bwd_kernel(int B, int C, int L, int N, int P, int S, int D, int T, int Tpos,
-                                     const float* __restrict__ x, const float* __restrict__ dout,
-                                     float* __restrict__ dcls, float* __restrict__ dpos, MutPtrTable8 dw,
-                                     MutPtrTable8 db) {
-  const int d = blockIdx.x * blockDim.x + threadIdx.x;
-  if (d >= D) return;
-  const int which = blockIdx.y;   // 0: cls/pos, 1..C: channel which-1
-  if (which == 0) {
-    for (int tok = 0; tok < Tpos; ++tok) {
-      float s = 0.f;
-      if (tok < T)
-        for (int b = 0; b < B; ++b) s += dout[((long)b * T + tok) * D + d];
-      dpos[(long)tok * D + d] = s;
-      if (tok == 0) dcls[d] = s;
-    }
+// blockIdx.y = 0: dpos[tok, d] = Σ_b dout[b, tok, d] (tok < T; rows past the used length get 0) and dcls = dpos[0];
+// blockIdx.y = 1 + c: one thread per (d, p) of channel c's Linear(P → D): dW[d, p] = Σ_{n, b} dout[b, tok, d]·x[b, c,
+// nS + p] over the channel's tokens that survive the pos-table truncation (models.py:122-123: channels 1.. get
+// exact zeros), and the p == 0 threads also form the bias gradient.
+__global__ __launch_bounds__(256) void imu_embed_bwd_kernel(int B, int C, int L, int N, int P, int S, int D, int T,
+                                                            int Tpos, const float* __restrict__ x,
+                                                            const float* __restrict__ dout, float* __restrict__ dcls,
+                                                            float* __restrict__ dpos, MutPtrTable8 dw,
+                                                            MutPtrTable8 db) {
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (blockIdx.y == 0) {
+    if (idx >= Tpos * D) return;
+    const int tok = idx / D, d = idx % D;
+    float s = 0.f;
+    if (tok < T)
+      for (int b = 0; b < B; ++b) s += dout[((long)b * T + tok) * D + d];
+    dpos[(long)tok * D + d] = s;
+    if (tok == 0) dcls[d] = s;
     return;
   }
-  const int c = which - 1;
-  float gb = 0.f;
-  float gw[32];
-  for (int p = 0; p < P && p < 32; ++p) gw[p] = 0.f;
+  if (idx >= D * P) return;
+  const int c = blockIdx.y - 1, d = idx / P, p = idx % P;
+  float gw = 0.f, gb = 0.f;
   for (int n = 0; n < N; ++n) {
     const int tok = 1 + c * N + n;
     if (tok >= T) break;
+#pragma unroll 4
     for (int b = 0; b < B; ++b) {
       const float g = dout[((long)b * T + tok) * D + d];
       gb += g;
-      const float* xs = x + ((long)b * C + c) * L + (long)n * S;
-      for (int p = 0; p < P && p < 32; ++p) gw[p] = fmaf(g, xs[p], gw[p]);
+      gw = fmaf(g, x[((long)b * C + c) * L + (long)n * S + p], gw);
     }
   }
-  db.p[c][d] = gb;
-  for (int p = 0; p < P && p < 32; ++p) dw.p[c][(long)d * P + p] = gw[p];
+  dw.p[c][(long)d * P + p] = gw;
+  if (p == 0) db.p[c][d] = gb;
 }
 
 // dst = alpha * src * dropmask(seed, p, r, c) + beta * dst   (dropout forward/backward, casts, adds, gathers)
@@ -253,11 +256,11 @@ extern "C" int cmhar_imu_embed_fwd(int B, int C, int L, int N, int P, int S, int
 extern "C" int cmhar_imu_embed_bwd(int B, int C, int L, int N, int P, int S, int D, int T, int Tpos, const float* x,
                                    const float* dout, float* dcls, float* dpos, float* const* dw, float* const* db,
                                    hipStream_t st) {
-  if (C > 8 || P > 32) return -1;
+  if (C > 8) return -1;
   MutPtrTable8 tw{}, tb{};
   for (int c = 0; c < C; ++c) { tw.p[c] = dw[c]; tb.p[c] = db[c]; }
-  imu_embed_bwd_kernel<<<dim3(cdiv(D, 64), C + 1), 64, 0, st>>>(B, C, L, N, P, S, D, T, Tpos, x, dout, dcls, dpos,
-                                                                 tw, tb);
+  const int nblk = cdiv(std::max(D * P, Tpos * D), 256);
+  imu_embed_bwd_kernel<<<dim3(nblk, C + 1), 256, 0, st>>>(B, C, L, N, P, S, D, T, Tpos, x, dout, dcls, dpos, tw, tb);
   CMHAR_CHECK_LAUNCH();
   return 0;
 }

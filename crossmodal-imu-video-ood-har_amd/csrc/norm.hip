@@ -6,6 +6,7 @@
 //   L2 normalise       — F.normalize(dim=1, eps=1e-12) (models.py:288-289).
 //   column sums        — bias gradients and slab reductions.
 #include "common.h"
+#include <algorithm>
 
 namespace {
 
@@ -13,6 +14,16 @@ __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
   return v;
+}
+
+// Two independent wave sums with their shuffle chains interleaved (half the dependent latency of two calls).
+__device__ __forceinline__ void wave_sum2(float& a, float& b) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+    const float ta = __shfl_xor(a, o), tb = __shfl_xor(b, o);
+    a += ta;
+    b += tb;
+  }
 }
 
 __device__ __forceinline__ float elem_drop(unsigned long long seed, float p, long row, int col) {
@@ -362,9 +373,10 @@ static void reduce_rows(const float* part, int rows, int N, float* out, float al
   }
 }
 
-// Vectorised LayerNorm backward for N % 256 == 0 (VideoMAE hidden 768): 8 waves x LNV_ROWS rows per block, each
-// lane owns N/256 groups of 4 consecutive columns (8-B bf16 / 16-B fp32 loads), next row prefetched into registers.
-constexpr int LNV_ROWS = 8, LNV_WAVES = 8;
+// Vectorised LayerNorm backward for N % 256 == 0 (VideoMAE hidden 768): 8 waves per block, rows grid-strided over
+// all waves; each lane owns N/256 groups of 4 consecutive columns (8-B bf16 / 16-B fp32 loads), the next row's dy,
+// h and residual gradient prefetched into registers under the current row's math.
+constexpr int LNV_WAVES = 8;
 template <typename T, int G>
 __global__ __launch_bounds__(512) void ln_bwd_vec_kernel(int M, const T* __restrict__ dy, long lddy,
                                                          const T* __restrict__ h, long ldh,
@@ -382,26 +394,31 @@ __global__ __launch_bounds__(512) void ln_bwd_vec_kernel(int M, const T* __restr
   for (int i = 0; i < G; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) { gam[i][j] = gamma[256 * i + 4 * lane + j]; ag[i][j] = 0.f; ab[i][j] = 0.f; }
-  const long row0 = ((long)blockIdx.x * LNV_WAVES + wave) * LNV_ROWS;
-  vec4 vdy[G], vh[G];
-  auto load = [&](long row) {
+  // grid-stride over rows: every wave of the (two-per-CU) grid takes rows w, w + W, w + 2W, ...  (W = all waves)
+  const long wstride = (long)gridDim.x * LNV_WAVES;
+  const long row0 = (long)blockIdx.x * LNV_WAVES + wave;
+  vec4 vdy[G], vh[G], vr[G];
+  auto load = [&](long row) {   // dy, h and the residual gradient of one row, all issued before any is used
 #pragma unroll
     for (int i = 0; i < G; ++i) {
       vdy[i] = *(const vec4*)(dy + row * lddy + 256 * i + 4 * lane);
       vh[i] = *(const vec4*)(h + row * ldh + 256 * i + 4 * lane);
+      if (dres) vr[i] = *(const vec4*)(dres + row * ldres + 256 * i + 4 * lane);
     }
   };
   if (row0 < M) load(row0);
-  for (int rr = 0; rr < LNV_ROWS; ++rr) {
-    const long row = row0 + rr;
-    if (row >= M) break;
-    float d[G][4], xh[G][4];
+  for (long row = row0; row < M; row += wstride) {
+    float d[G][4], xh[G][4], rs[G][4];
     const float mu = mean[row], r = rstd[row];
 #pragma unroll
     for (int i = 0; i < G; ++i)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) { d[i][j] = to_f<T>(vdy[i][j]); xh[i][j] = (to_f<T>(vh[i][j]) - mu) * r; }
-    if (rr + 1 < LNV_ROWS && row + 1 < M) load(row + 1);     // prefetch the next row under this row's math
+      for (int j = 0; j < 4; ++j) {
+        d[i][j] = to_f<T>(vdy[i][j]);
+        xh[i][j] = (to_f<T>(vh[i][j]) - mu) * r;
+        rs[i][j] = dres ? to_f<T>(vr[i][j]) : 0.f;
+      }
+    if (row + wstride < M) load(row + wstride);     // prefetch the next row under this row's math
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
     for (int i = 0; i < G; ++i)
@@ -413,19 +430,14 @@ __global__ __launch_bounds__(512) void ln_bwd_vec_kernel(int M, const T* __restr
         s1 += g;
         s2 += g * xh[i][j];
       }
-    s1 = wave_sum(s1) * (1.f / N);
-    s2 = wave_sum(s2) * (1.f / N);
+    wave_sum2(s1, s2);
+    s1 *= 1.f / N;
+    s2 *= 1.f / N;
 #pragma unroll
     for (int i = 0; i < G; ++i) {
-      vec4 res;
-      if (dres) res = *(const vec4*)(dres + row * ldres + 256 * i + 4 * lane);
       vec4 o;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        float v = r * (d[i][j] * gam[i][j] - s1 - xh[i][j] * s2);
-        if (dres) v += to_f<T>(res[j]);
-        o[j] = from_f<T>(v);
-      }
+      for (int j = 0; j < 4; ++j) o[j] = from_f<T>(r * (d[i][j] * gam[i][j] - s1 - xh[i][j] * s2) + rs[i][j]);
       *(vec4*)(dh + row * lddh + 256 * i + 4 * lane) = o;
     }
   }
@@ -444,12 +456,13 @@ __global__ __launch_bounds__(512) void ln_bwd_vec_kernel(int M, const T* __restr
 }
 
 static int ln_bwd_blocks(int M, int N, bool vec) {
-  return vec ? cdiv(M, LNV_WAVES * LNV_ROWS) : cdiv(M, 4 * LN_BWD_ROWS);
+  // vector path: a balanced grid of at most two 512-thread blocks per CU (256 CUs), rows grid-strided
+  return vec ? std::min(512, cdiv(M, LNV_WAVES)) : cdiv(M, 4 * LN_BWD_ROWS);
 }
 
 // Number of fp32 floats the caller must provide in `ws` for cmhar_layernorm_bwd (upper bound over both paths).
 extern "C" long cmhar_layernorm_bwd_ws(int M, int N) {
-  const int blocks = ln_bwd_blocks(M, N, false);
+  const int blocks = std::max(ln_bwd_blocks(M, N, false), ln_bwd_blocks(M, N, true));
   return 2L * blocks * N + 2 * reduce_rows_ws(blocks, N);
 }
 
