@@ -15,7 +15,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get('CMHAR_LIB', os.path.join(_HERE, 'libcmhar.so'))
 
 F32, BF16 = 0, 1
-ACT_NONE, ACT_GELU, ACT_RELU, ACT_DGELU, ACT_DRELU = 0, 1, 2, 3, 4
+ACT_NONE, ACT_GELU, ACT_RELU, ACT_DGELU, ACT_DRELU, ACT_GELU_SAVEGRAD, ACT_MULAUX = 0, 1, 2, 3, 4, 5, 6
 
 vp, i32, i64, f32, u64 = C.c_void_p, C.c_int, C.c_long, C.c_float, C.c_ulonglong
 
@@ -23,7 +23,8 @@ vp, i32, i64, f32, u64 = C.c_void_p, C.c_int, C.c_long, C.c_float, C.c_ulonglong
 class Epilogue(C.Structure):
     _fields_ = [('bias', vp), ('residual', vp), ('ldr', i64), ('aux_in', vp), ('lda', i64), ('aux_out', vp),
                 ('ldo', i64), ('rowadd', vp), ('rowadd_mod', i32), ('rowadd_ld', i32), ('act', i32),
-                ('alpha', f32), ('beta', f32), ('pdrop', f32), ('pad_', i32), ('seed', u64)]
+                ('alpha', f32), ('beta', f32), ('pdrop', f32), ('pad_', i32), ('seed', u64), ('rowsum', vp),
+                ('rowsum_beta', f32), ('pad2_', i32)]
 
 
 _SIGS = {
@@ -104,8 +105,10 @@ def dtype_code(dt):
 
 
 def epilogue(bias=None, residual=None, aux_in=None, aux_out=None, rowadd=None, rowadd_mod=1, act=ACT_NONE,
-             alpha=1.0, beta=0.0, pdrop=0.0, seed=0):
+             alpha=1.0, beta=0.0, pdrop=0.0, seed=0, rowsum=None, rowsum_beta=0.0):
     e = Epilogue()
+    e.rowsum = ptr(rowsum)
+    e.rowsum_beta = rowsum_beta
     e.bias = ptr(bias)
     e.residual = ptr(residual)
     e.ldr = residual.stride(0) if residual is not None else 0

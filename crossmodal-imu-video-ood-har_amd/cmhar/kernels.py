@@ -101,8 +101,9 @@ def _splits_for(M, N, K):
 # ------------------------------------------------------------------------------------------------------------
 def gemm(layout: int, a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, *, bias=None, residual=None,
          aux_in=None, aux_out=None, rowadd=None, rowadd_mod=1, act=L.ACT_NONE, alpha=1.0, beta=0.0, splits=None,
-         pdrop=0.0, seed=0):
-    """layout 0: out[M,N] = a[M,K]·b[N,K]ᵀ;  1: a[M,K]·b[K,N];  2: a[K,M]ᵀ·b[K,N]."""
+         pdrop=0.0, seed=0, rowsum=None, rowsum_beta=0.0):
+    """layout 0: out[M,N] = a[M,K]·b[N,K]ᵀ;  1: a[M,K]·b[K,N];  2: a[K,M]ᵀ·b[K,N].
+    rowsum (layout 2, bf16, 256-tile shapes): rowsum[m] = Σ_k a[k,m] + rowsum_beta·rowsum[m] (bias gradient)."""
     for t, n in ((a, 'A'), (b, 'B'), (out, 'C')):
         _check_2d(t, n)
     if layout == 0:
@@ -137,7 +138,13 @@ def gemm(layout: int, a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, *, bi
         raise ValueError('rowadd must be [mod, N]')
     if beta != 0.0 and out.dtype != torch.float32:
         raise ValueError('beta accumulation only for fp32 outputs')
-    epi = L.epilogue(bias, residual, aux_in, aux_out, rowadd, rowadd_mod, act, alpha, beta, pdrop, seed)
+    if rowsum is not None:
+        if not rowsum_supported(layout, a.dtype, M, N, K):
+            raise ValueError('rowsum needs the bf16 256-tile weight-gradient path')
+        if rowsum.dtype != torch.float32 or rowsum.numel() != M or not rowsum.is_contiguous():
+            raise ValueError(f'rowsum must be a contiguous fp32 [{M}] tensor')
+    epi = L.epilogue(bias, residual, aux_in, aux_out, rowadd, rowadd_mod, act, alpha, beta, pdrop, seed, rowsum,
+                     rowsum_beta)
     st = L.stream(out.device)
     if a.dtype == torch.bfloat16:
         _check_bf16_operand(a, 'A')
@@ -149,7 +156,7 @@ def gemm(layout: int, a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, *, bi
         s = _splits_for(M, N, K) if splits is None else splits
         ws = None
         if s > 1:
-            ws = workspace(s * M * N, out.device)
+            ws = workspace(s * M * N + (s * M if rowsum is not None else 0), out.device)
         ev = TRACE.begin()
         call('cmhar_gemm_bf16', layout, L.dtype_code(out.dtype), M, N, K, ptr(a), a.stride(0), ptr(b), b.stride(0),
              ptr(out), out.stride(0), C.byref(epi), s, ptr(ws), st)
@@ -190,12 +197,21 @@ def linear_dgrad(dy, w, *, act=L.ACT_NONE, aux_in=None, residual=None, out=None,
     return gemm(1, dy, w, out, act=act, aux_in=aux_in, residual=residual, beta=beta, pdrop=pdrop, seed=seed)
 
 
-def linear_wgrad(dy, x, *, out=None, beta=0.0):
-    """dW[N,K] (fp32) = dyᵀ·x."""
+def rowsum_supported(layout, dtype, M, N, K):
+    return layout == 2 and dtype == torch.bfloat16 and M % 256 == 0 and N % 256 == 0 and K % 64 == 0
+
+
+def linear_wgrad(dy, x, *, out=None, beta=0.0, bias_out=None, bias_beta=0.0):
+    """dW[N,K] (fp32) = dyᵀ·x;  bias_out[N] (fp32, optional) = Σ_m dy[m, :] (+ bias_beta·bias_out).
+    The bias gradient rides on the wgrad GEMM's own MFMA operand tiles when the shape allows it, else it is a
+    separate column-sum launch."""
     N, K = dy.shape[1], x.shape[1]
     if out is None:
         out = torch.empty(N, K, dtype=torch.float32, device=dy.device)
-    return gemm(2, dy, x, out, beta=beta)
+    if bias_out is not None and not rowsum_supported(2, dy.dtype, N, K, dy.shape[0]):
+        colsum(dy, bias_out, beta=bias_beta)
+        bias_out = None
+    return gemm(2, dy, x, out, beta=beta, rowsum=bias_out, rowsum_beta=bias_beta)
 
 
 def colsum(x, out=None, *, alpha=1.0, beta=0.0):

@@ -10,8 +10,8 @@ autograd node whose body is a sequence of HIP launches:
   im2col(tubelet) → GEMM(+bias +sin-cos pos) → 12 × [LN → QKV GEMM(+bias) → flash attention
   → out-proj GEMM(+bias +residual) → LN → FC1 GEMM(+bias, GELU, pre-act saved) → FC2 GEMM(+bias +residual)]
 
-and the mirrored backward (dgrad GEMMs with fused GELU'/residual epilogues, split-K fp32 wgrad GEMMs, flash
-attention backward, fused LN backward with the residual gradient).  Compute dtype: bf16 (MFMA, fp32 accumulate)
+and the mirrored backward (dgrad GEMMs with fused GELU'/residual epilogues, split-K fp32 wgrad GEMMs that also
+emit the bias gradients, flash attention backward, fused LN backward with the residual gradient).  Compute dtype: bf16 (MFMA, fp32 accumulate)
 or fp32 (exact parity mode); master weights and their gradients stay fp32.
 """
 from __future__ import annotations
@@ -244,8 +244,10 @@ def _forward_impl(m: VideoMAEBackbone, video: torch.Tensor, save: bool):
                         scale=scale)
         x1 = K.linear(o, W[f'o{len(st.layers)}'], p['ob'], residual=x)
         h2, mu2, rs2 = K.layernorm_fwd(x1, p['ln2w'], p['ln2b'], layer.layernorm_after.eps)
-        pre = torch.empty(M, cfg.intermediate_size, dtype=dt, device=x.device)
-        g = K.linear(h2, W[f'fc1_{len(st.layers)}'], p['f1b'], act=L.ACT_GELU, aux_out=pre)
+        # the FC1 epilogue writes gelu(a) and gelu'(a) (shared transcendentals); the backward only multiplies
+        pre = torch.empty(M, cfg.intermediate_size, dtype=dt, device=x.device) if save else None
+        g = K.linear(h2, W[f'fc1_{len(st.layers)}'], p['f1b'], act=L.ACT_GELU_SAVEGRAD if save else L.ACT_GELU,
+                     aux_out=pre)
         x2 = K.linear(g, W[f'fc2_{len(st.layers)}'], p['f2b'], residual=x1)
         st.layers.append((x, h1, mu1, rs1, qkv, o, lse, x1, h2, mu2, rs2, pre, g) if save else None)
         x = x2
@@ -257,16 +259,6 @@ def _forward_impl(m: VideoMAEBackbone, video: torch.Tensor, save: bool):
     return x, st
 
 
-_AUX = {}
-
-
-def _aux_stream(dev):
-    s = _AUX.get(dev)
-    if s is None:
-        s = _AUX[dev] = torch.cuda.Stream(dev)
-    return s
-
-
 def _backward_impl(m: VideoMAEBackbone, st, dx, sink):
     """dx: [M, Hd] gradient of the backbone output (compute dtype).  Parameter gradients go to `sink`
     (cmhar.grads): fp32, written by the wgrad GEMM / colsum / LN-backward epilogues with β = 0 or 1."""
@@ -274,24 +266,13 @@ def _backward_impl(m: VideoMAEBackbone, st, dx, sink):
     B, Lt, M, Hd, nh, D, scale = st.geom
     dev = dx.device
 
-    def wgrad(params, dy, x, shape):
+    def wgrad(params, dy, x, shape, bias=None):
+        """Weight gradient GEMM; the bias gradient (Σ_tokens dy) rides on the same GEMM's MFMA operand tiles."""
         out, beta = sink.dest(params, shape, dev)
-        K.linear_wgrad(dy, x, out=out, beta=beta)
-
-    # Bias gradients (column sums of dy, HBM-bound) run on an auxiliary stream beside the MFMA-bound GEMMs that
-    # read the same dy; the main stream joins it before a layer's gradients are declared final.
-    cur = torch.cuda.current_stream(dev)
-    aux = _aux_stream(dev)
-
-    def bgrad(params, dy):
-        out, beta = sink.dest(params, (sum(q.numel() for q in params),), dev)
-        aux.wait_stream(cur)
-        with torch.cuda.stream(aux):
-            K.colsum(dy, out, beta=beta)
-        dy.record_stream(aux)
-
-    def join():
-        cur.wait_stream(aux)
+        bout, bbeta = (None, 0.0)
+        if bias:
+            bout, bbeta = sink.dest(bias, (sum(q.numel() for q in bias),), dev)
+        K.linear_wgrad(dy, x, out=out, beta=beta, bias_out=bout, bias_beta=bbeta)
 
     def ln_grads(wp, bp):
         gw, bw = sink.dest([wp], wp.shape, dev)
@@ -311,39 +292,32 @@ def _backward_impl(m: VideoMAEBackbone, st, dx, sink):
         x, h1, mu1, rs1, qkv, o, lse, x1, h2, mu2, rs2, pre, g = st.layers[li]
         st.layers[li] = None
         # x2 = x1 + FC2(gelu(FC1(LN2(x1))))
-        dpre = K.linear_dgrad(dx, W[f'fc2_{li}'], act=L.ACT_DGELU, aux_in=pre)
-        wgrad([p['f2w']], dx, g, p['f2w'].shape)
-        bgrad([p['f2b']], dx)
+        dpre = K.linear_dgrad(dx, W[f'fc2_{li}'], act=L.ACT_MULAUX, aux_in=pre)     # pre holds gelu'(a)
+        wgrad([p['f2w']], dx, g, p['f2w'].shape, [p['f2b']])
         del g
         dh2 = K.linear_dgrad(dpre, W[f'fc1_{li}'])
-        wgrad([p['f1w']], dpre, h2, p['f1w'].shape)
-        bgrad([p['f1b']], dpre)
+        wgrad([p['f1w']], dpre, h2, p['f1w'].shape, [p['f1b']])
         del dpre, pre
         gw2, gb2, beta = ln_grads(p['ln2w'], p['ln2b'])
         dx1 = K.layernorm_bwd(dh2, x1, p['ln2w'], mu2, rs2, gw2, gb2, dres=dx, beta_acc=beta)
         del dh2, dx
         # x1 = x + O·Woᵀ + bo
         do = K.linear_dgrad(dx1, W[f'o{li}'])
-        wgrad([p['ow']], dx1, o, p['ow'].shape)
-        bgrad([p['ob']], dx1)
+        wgrad([p['ow']], dx1, o, p['ow'].shape, [p['ob']])
         dqkv = torch.empty(M, 3 * Hd, dtype=dx1.dtype, device=dev)
         K.attention_bwd(qkv[:, :Hd], qkv[:, Hd:2 * Hd], qkv[:, 2 * Hd:], o, do, lse, dqkv[:, :Hd],
                         dqkv[:, Hd:2 * Hd], dqkv[:, 2 * Hd:], B=B, H=nh, Lq=Lt, Lk=Lt, D=D, scale=scale)
         del do, o, qkv
         dh1 = K.linear_dgrad(dqkv, W[f'qkv{li}'])
-        wgrad([p['qw'], p['kw'], p['vw']], dqkv, h1, (3 * Hd, Hd))
-        if p['qb'] is not None:
-            bgrad([p['qb'], p['kb'], p['vb']], dqkv)
+        wgrad([p['qw'], p['kw'], p['vw']], dqkv, h1, (3 * Hd, Hd),
+              [p['qb'], p['kb'], p['vb']] if p['qb'] is not None else None)
         del dqkv
         gw1, gb1, beta = ln_grads(p['ln1w'], p['ln1b'])
         dx = K.layernorm_bwd(dh1, x, p['ln1w'], mu1, rs1, gw1, gb1, dres=dx1, beta_acc=beta)
         del dh1, dx1
-        join()
         sink.done([q for q in p.values() if q is not None])
     pe = m.embeddings.patch_embeddings.projection
-    wgrad([pe.weight], dx, st.patches, (pe.weight.shape[0], pe.weight[0].numel()))
-    bgrad([pe.bias], dx)
-    join()
+    wgrad([pe.weight], dx, st.patches, (pe.weight.shape[0], pe.weight[0].numel()), [pe.bias])
     sink.done([pe.weight, pe.bias])
     st.patches = None
 

@@ -25,6 +25,8 @@ enum {
   ACT_RELU = 2,        // out = relu(acc + bias)
   ACT_DGELU = 3,       // out = acc * gelu_erf'(aux_in)
   ACT_DRELU = 4,       // out = acc * (aux_in > 0)
+  ACT_GELU_SAVEGRAD = 5,  // out = gelu_erf(acc + bias); aux_out = gelu_erf'(acc + bias)
+  ACT_MULAUX = 6,      // out = acc * aux_in   (the GELU backward against a saved derivative)
 };
 
 // The epilogue struct is part of the C ABI (include/cmhar.h); every extern "C" definition in csrc/ is checked
@@ -42,12 +44,32 @@ template <typename T> __device__ __forceinline__ T from_f(float x);
 template <> __device__ __forceinline__ float from_f<float>(float x) { return x; }
 template <> __device__ __forceinline__ bf16 from_f<bf16>(float x) { return (bf16)x; }
 
-__device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
-__device__ __forceinline__ float gelu_erf_grad(float x) {
-  const float cdf = 0.5f * (1.0f + erff(x * 0.70710678118654752f));
-  const float pdf = 0.39894228040143268f * __expf(-0.5f * x * x);
-  return cdf + x * pdf;
+// GELU(erf) and its derivative from ONE shared set of transcendentals.  Φ(x) = ½·erfc(−x/√2) with erfc(z), z ≥ 0,
+// from the Chebyshev-fitted form erfc(z) = t·exp(−z² + R(t)), t = 1/(1 + z/2) (Numerical Recipes `erfcc`,
+// relative error < 1.2e-7 for every z, so the x < 0 tail keeps full relative precision — no 1 − erf cancellation).
+// exp(−z²) = exp(−x²/2) is also the Gaussian density factor of Φ'(x), so gelu and gelu' cost 2 v_exp + 1 v_rcp
+// + ~14 FMA-class ops together (ocml erff alone is a branchy ~25-op polynomial).
+__device__ __forceinline__ void gelu_pair(float x, float& g, float& gp) {
+  const float z = fabsf(x) * 0.70710678118654752f;
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.5f, z, 1.0f));
+  float r = 0.17087277f;
+  r = fmaf(r, t, -0.82215223f);
+  r = fmaf(r, t, 1.48851587f);
+  r = fmaf(r, t, -1.13520398f);
+  r = fmaf(r, t, 0.27886807f);
+  r = fmaf(r, t, -0.18628806f);
+  r = fmaf(r, t, 0.09678418f);
+  r = fmaf(r, t, 0.37409196f);
+  r = fmaf(r, t, 1.00002368f);
+  r = fmaf(r, t, -1.26551223f);
+  const float e1 = __expf(-0.5f * x * x);          // exp(−z²)
+  const float half_erfc = 0.5f * t * e1 * __expf(r);  // Φ(−|x|)
+  const float cdf = x < 0.f ? half_erfc : 1.0f - half_erfc;
+  g = x * cdf;
+  gp = fmaf(x, 0.39894228040143268f * e1, cdf);
 }
+__device__ __forceinline__ float gelu_erf(float x) { float g, gp; gelu_pair(x, g, gp); return g; }
+__device__ __forceinline__ float gelu_erf_grad(float x) { float g, gp; gelu_pair(x, g, gp); return gp; }
 
 // Counter-hash dropout mask shared by every kernel that applies or regenerates an element dropout:
 // keep (m, n) iff hash(seed, m, n) / 2^32 >= p; kept values are scaled by 1/(1-p) (nn.Dropout semantics).
@@ -77,6 +99,14 @@ __device__ __forceinline__ void epilogue_store(const Epilogue& e, OutT* __restri
     case ACT_RELU: v = v > 0.f ? v : 0.f; break;
     case ACT_DGELU: v *= gelu_erf_grad(to_f<OutT>(((const OutT*)e.aux_in)[(long)m * e.lda + n])); break;
     case ACT_DRELU: v = to_f<OutT>(((const OutT*)e.aux_in)[(long)m * e.lda + n]) > 0.f ? v : 0.f; break;
+    case ACT_GELU_SAVEGRAD: {
+      float g, gp;
+      gelu_pair(v, g, gp);
+      if (e.aux_out) ((OutT*)e.aux_out)[(long)m * e.ldo + n] = from_f<OutT>(gp);
+      v = g;
+      break;
+    }
+    case ACT_MULAUX: v *= to_f<OutT>(((const OutT*)e.aux_in)[(long)m * e.lda + n]); break;
     default: break;
   }
   if (e.pdrop > 0.f) v *= drop_mask(e.seed, e.pdrop, m, n);

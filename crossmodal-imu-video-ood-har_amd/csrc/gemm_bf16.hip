@@ -145,6 +145,14 @@ __device__ __forceinline__ void epilogue_store8(const Epilogue& e, OutT* __restr
     load8<OutT>((const OutT*)e.aux_in + (long)m * e.lda + n0, t);
 #pragma unroll
     for (int j = 0; j < 8; ++j) x[j] = t[j] > 0.f ? x[j] : 0.f;
+  } else if (e.act == ACT_GELU_SAVEGRAD) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) gelu_pair(x[j], x[j], t[j]);
+    if (e.aux_out) store8<OutT>((OutT*)e.aux_out + (long)m * e.ldo + n0, t);
+  } else if (e.act == ACT_MULAUX) {
+    load8<OutT>((const OutT*)e.aux_in + (long)m * e.lda + n0, t);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) x[j] *= t[j];
   }
   if (e.pdrop > 0.f) {
 #pragma unroll
@@ -287,6 +295,11 @@ __global__ void splitk_reduce_kernel(int M, int N, int splits, const float* __re
 #pragma unroll
       for (int j = 0; j < 4; ++j) { s[j] += a[j]; s[4 + j] += b[j]; }
     }
+    if (e.rowsum && idx < M) {                       // bias-gradient slabs follow the C slabs
+      float r = 0.f;
+      for (int z = 0; z < splits; ++z) r += P[splits * split_stride + (long)z * M + idx];
+      e.rowsum[idx] = e.rowsum_beta != 0.f ? r + e.rowsum_beta * e.rowsum[idx] : r;
+    }
     epilogue_store8<OutT>(e, C, ldc, m, n0, s);
     return;
   }
@@ -376,8 +389,15 @@ __global__ __launch_bounds__(NT2, 2) void gemm256_kernel(int M, int N, int K, co
   const int bm = tm * TM2, bn = tn * TN2;
   const int kbeg = split * klen;
   const int kend = min(K, kbeg + klen);
+  float* const rs_slab = raw_out ? (float*)C + (long)gridDim.z * split_stride + (long)split * M : nullptr;
   C += (long)split * split_stride;
   const int nk = MODE >= 3 && MODE != 4 ? 0 : (kend - kbeg) / TK2;
+  // Weight-gradient GEMMs (A = dYᵀ, M-contiguous) can also emit the bias gradient Σ_k A(m,k): one extra MFMA of an
+  // A fragment against an all-ones B fragment.  One block per row panel (tn == tm % tiles_n, spreading the panels
+  // over the column tiles) does it, each of its waves for 2 of its 8 A fragments: +2 MFMAs per 32 on those blocks.
+  const bool rs = !A_KC && e.rowsum != nullptr && tn == tm % tiles_n;
+  const bf16x8 ones = {(bf16)1.f, (bf16)1.f, (bf16)1.f, (bf16)1.f, (bf16)1.f, (bf16)1.f, (bf16)1.f, (bf16)1.f};
+  floatx4 accb[2] = {floatx4{0.f, 0.f, 0.f, 0.f}, floatx4{0.f, 0.f, 0.f, 0.f}};
 
   floatx4 acc[8][4];
 #pragma unroll
@@ -425,13 +445,18 @@ __global__ __launch_bounds__(NT2, 2) void gemm256_kernel(int M, int N, int K, co
     for (int i = 0; i < 8; ++i) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bf0[j], acc[i][j], 0, 0, 0);
+      if (!A_KC && rs && wc == (i >> 1))
+        accb[i & 1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], ones, accb[i & 1], 0, 0, 0);
       af[i] = frag256<A_KC>(a_s, wr * 128 + i * 16, 1, lane);
       __builtin_amdgcn_sched_barrier(0);
     }
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < 4; ++i) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bf1[j], acc[i][j], 0, 0, 0);
+      if (!A_KC && rs && wc == (i >> 1))
+        accb[i & 1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], ones, accb[i & 1], 0, 0, 0);
+    }
     __builtin_amdgcn_sched_barrier(0);
     if (more) {
       // own DMA of tile kt+1 landed, own reads of tile kt returned; then everyone's
@@ -443,6 +468,8 @@ __global__ __launch_bounds__(NT2, 2) void gemm256_kernel(int M, int N, int K, co
     for (int i = 4; i < 8; ++i) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bf1[j], acc[i][j], 0, 0, 0);
+      if (!A_KC && rs && wc == (i >> 1))
+        accb[i & 1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], ones, accb[i & 1], 0, 0, 0);
       if (more) af[i] = frag256<A_KC>(nxt, wr * 128 + i * 16, 0, lane);
       __builtin_amdgcn_sched_barrier(0);
     }
@@ -450,6 +477,16 @@ __global__ __launch_bounds__(NT2, 2) void gemm256_kernel(int M, int N, int K, co
 #pragma unroll
       for (int j = 0; j < 4; ++j) bf1[j] = frag256<B_KC>(nxt + 32768, wc * 64 + j * 16, 1, lane);
     }
+  }
+  if (!A_KC && rs && (lane & 15) == 0) {       // every column of a ones-product holds the row sum: lanes 0,16,32,48
+#pragma unroll
+    for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = bm + wr * 128 + (2 * wc + ii) * 16 + 4 * (lane >> 4) + r;
+        if (rs_slab) rs_slab[m] = accb[ii][r];
+        else e.rowsum[m] = e.rowsum_beta != 0.f ? accb[ii][r] + e.rowsum_beta * e.rowsum[m] : accb[ii][r];
+      }
   }
   __syncthreads();
   if (MODE == 4) {   // keep every accumulator live, store nothing
@@ -508,7 +545,9 @@ int launch(int M, int N, int K, const bf16* A, long lda, const bf16* B, long ldb
            const Epilogue& e, int splits, float* ws, hipStream_t st) {
   const long ss = (long)M * N;
   if (splits > 1 && !ws) return -2;
-  if (M % TM2 == 0 && N % TN2 == 0 && K % TK2 == 0) {
+  const bool big = M % TM2 == 0 && N % TN2 == 0 && K % TK2 == 0;
+  if (e.rowsum && (AK || !big)) return -3;            // row sums only on the 256-tile weight-gradient path
+  if (big) {
     int klen = K;
     if (splits > 1) klen = cdiv(cdiv(K, splits), TK2) * TK2;
     const int nsplit = cdiv(K, klen);

@@ -97,6 +97,7 @@ extern "C" int cmhar_gemm_generic(int in_dtype, int out_dtype, int M, int N, int
   Epilogue e{};
   e.alpha = 1.f;
   if (epi) e = *epi;                                   // NULL = the plain product
+  if (e.rowsum) return -3;                             // row sums: 256-tile bf16 weight-gradient path only
   dim3 grid(cdiv(N, TN), cdiv(M, TM), batch);
 #define LAUNCH(TI, TO)                                                                                     \
   gemm_generic_kernel<TI, TO><<<grid, 256, 0, stream>>>(M, N, K, (const TI*)A, sam, sak, sAb, (const TI*)B, \

@@ -25,19 +25,25 @@ typedef struct CmharEpilogue {
   const float* bias;      /* [N] fp32 or NULL */
   const void* residual;   /* [M,N] output dtype, added last, or NULL */
   long ldr;
-  const void* aux_in;     /* [M,N] pre-activation for act = 3 (dGELU) / 4 (dReLU) */
+  const void* aux_in;     /* [M,N] pre-activation for act = 3 (dGELU) / 4 (dReLU); multiplier for act = 6 */
   long lda;
-  void* aux_out;          /* [M,N] pre-activation written by act = 1 (GELU) */
+  void* aux_out;          /* [M,N] written by act = 1 (pre-activation) / act = 5 (GELU derivative) */
   long ldo;
   const float* rowadd;    /* [rowadd_mod, rowadd_ld] fp32 table added at row m % rowadd_mod */
   int rowadd_mod;
   int rowadd_ld;
-  int act;                /* 0 none, 1 gelu(erf), 2 relu, 3 x*gelu'(aux_in), 4 x*(aux_in>0) */
+  int act;                /* 0 none, 1 gelu(erf), 2 relu, 3 x*gelu'(aux_in), 4 x*(aux_in>0),
+                             5 gelu(erf) with aux_out = gelu'(x) (the backward then needs only act 6),
+                             6 x*aux_in */
   float alpha;            /* out = alpha*acc ... */
   float beta;             /* ... + beta*out_old (fp32 outputs; 0 = overwrite) */
   float pdrop;            /* element dropout after the activation (mask = hash(seed, m, n) >= pdrop), 0 = off */
   int pad_;
   unsigned long long seed;
+  float* rowsum;          /* layout 2 (weight gradient) only: rowsum[m] = Σ_k A(m,k) + rowsum_beta·rowsum[m] —
+                             the bias gradient Σ_tokens dY, taken from the same MFMA operand tiles; or NULL */
+  float rowsum_beta;
+  int pad2_;
 } CmharEpilogue;
 
 int cmhar_version(void);
@@ -46,7 +52,8 @@ int cmhar_version(void);
  * transformers modeling_videomae.py:209-324, the tubelet Conv3d :159-168 as an im2col GEMM, and
  * VideoEncoder.projection models.py:178,202).
  * layout 0: C = A[M,K] · B[N,K]ᵀ   1: C = A[M,K] · B[K,N]   2: C = A[K,M]ᵀ · B[K,N].
- * splits > 1: split-K with ws = splits*M*N fp32 floats. */
+ * splits > 1: split-K with ws = splits*M*N (+ splits*M when epi->rowsum) fp32 floats.
+ * epi->rowsum is supported on the 256-tile path (M, N % 256 == 0, K % 64 == 0) of layout 2; else returns -3. */
 int cmhar_gemm_bf16(int layout, int out_dtype, int M, int N, int K, const void* A, long lda, const void* B, long ldb,
                     void* C, long ldc, const CmharEpilogue* epi, int splits, void* ws, hipStream_t stream);
 

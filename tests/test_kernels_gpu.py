@@ -115,6 +115,71 @@ def test_gemm_bf16_epilogues():
     assert rel(acc, ref) < 1e-5
 
 
+def _gelu_ref(x):
+    x64 = x.double()
+    g = torch.nn.functional.gelu(x64)
+    gp = 0.5 * (1 + torch.erf(x64 / math.sqrt(2))) + x64 * torch.exp(-0.5 * x64 * x64) / math.sqrt(2 * math.pi)
+    return g, gp
+
+
+@pytest.mark.parametrize('shape', [(512, 512, 256), (384, 520, 136)])     # 256-tile DMA kernel and the 128² kernel
+def test_gemm_gelu_savegrad_and_mulaux(shape):
+    """act 5: out = gelu(a), aux = gelu'(a) from shared transcendentals; act 6: out = acc · aux (the backward).
+    Compared against float64 erf-GELU on the same bf16 operands: only bf16 output rounding may differ."""
+    torch.manual_seed(3)
+    M, N, Kd = shape
+    a = torch.randn(M, Kd, device=DEV).bfloat16()
+    w = (torch.randn(N, Kd, device=DEV) / 8).bfloat16()
+    bias = torch.randn(N, device=DEV)
+    pre = a.double() @ w.double().T + bias.double()
+    gp = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+    y = K().linear(a, w, bias, act=L().ACT_GELU_SAVEGRAD, aux_out=gp)
+    g_ref, gp_ref = _gelu_ref(pre)
+    assert rel(y, g_ref) < 4e-3 and rel(gp, gp_ref) < 4e-3
+    # fp32 output: the formula itself (relative error of erfc < 1.2e-7) — tight
+    y32 = torch.empty(M, N, device=DEV)
+    gp32 = torch.empty(M, N, device=DEV)
+    K().gemm(0, a, w, y32, bias=bias, act=L().ACT_GELU_SAVEGRAD, aux_out=gp32)
+    assert rel(y32, g_ref) < 2e-6 and rel(gp32, gp_ref) < 2e-6
+    neg = pre < -3
+    # tail precision: the erfc form keeps ~1e-6 relative accuracy where 1 + erf(x/√2) (torch's fp32 GELU) cancels to
+    # percent-level error at x ≈ -5; 5e-5 covers the fp32 GEMM's own rounding of the pre-activation × |d ln g/dx|
+    assert ((y32[neg].double() - g_ref[neg]).abs() <= 5e-5 * g_ref[neg].abs() + 1e-30).all()
+    # backward against the saved derivative
+    dy = torch.randn(M, N, device=DEV).bfloat16()
+    w2 = (torch.randn(N, Kd, device=DEV) / 8).bfloat16()
+    aux = torch.randn(M, Kd, device=DEV).bfloat16()
+    dx = K().linear_dgrad(dy, w2, act=L().ACT_MULAUX, aux_in=aux)
+    assert rel(dx, (dy.float() @ w2.float()) * aux.float()) < 4e-3
+
+
+@pytest.mark.parametrize('splits', [1, 5])
+@pytest.mark.parametrize('beta', [0.0, 1.0])
+def test_wgrad_fused_bias_rowsum_exact(splits, beta):
+    """The wgrad GEMM's all-ones MFMA row sum (bias gradient) on integer operands: bit-exact, with and without
+    split-K, overwrite and accumulate."""
+    T, N, Kin = 2048, 768, 512           # dy [T, N], x [T, Kin] → dW [N, Kin], db [N]
+    dy = _ints((T, N), seed=4).to(DEV, torch.bfloat16)
+    x = _ints((T, Kin), seed=5).to(DEV, torch.bfloat16)
+    dw = torch.full((N, Kin), 3.0, device=DEV)
+    db = torch.full((N,), 2.0, device=DEV)
+    K().gemm(2, dy, x, dw, beta=beta, splits=splits, rowsum=db, rowsum_beta=beta)
+    torch.cuda.synchronize()
+    assert torch.equal(dw, dy.float().T @ x.float() + 3.0 * beta)
+    assert torch.equal(db, dy.float().sum(0) + 2.0 * beta)
+
+
+def test_wgrad_bias_fallback_shapes():
+    """Shapes off the 256-tile path get the bias gradient from the column-sum kernel instead."""
+    torch.manual_seed(5)
+    dy = torch.randn(304, 200, device=DEV).bfloat16()
+    x = torch.randn(304, 72, device=DEV).bfloat16()
+    db = torch.empty(200, device=DEV)
+    dw = K().linear_wgrad(dy, x, bias_out=db)
+    assert rel(dw, dy.float().T @ x.float()) < 1e-5
+    assert rel(db, dy.float().sum(0)) < 1e-5
+
+
 @pytest.mark.parametrize('layout', [0, 1, 2])
 def test_gemm_generic_fp32(layout):
     torch.manual_seed(1)

@@ -47,6 +47,20 @@ def main():
     ref = torch.softmax(qf @ kf.transpose(1, 2) * sc, -1) @ vf
     got = o[:L].float().view(L, H, D)[:, :2].transpose(0, 1)
     print('fwd rel err', ((got - ref).norm() / ref.norm()).item())
+    # torch SDPA (ROCm flash backend) at the same shape, for a ceiling reference
+    import torch.nn.functional as F
+    qt = q.reshape(B, L, H, D).transpose(1, 2).contiguous().requires_grad_(True)
+    kt = k.reshape(B, L, H, D).transpose(1, 2).contiguous().requires_grad_(True)
+    vt = v.reshape(B, L, H, D).transpose(1, 2).contiguous().requires_grad_(True)
+    got = do.reshape(B, L, H, D).transpose(1, 2).contiguous()
+    try:
+        tf = run(lambda: F.scaled_dot_product_attention(qt, kt, vt))
+        out = F.scaled_dot_product_attention(qt, kt, vt)
+        tb = run(lambda: torch.autograd.grad(out, (qt, kt, vt), got, retain_graph=True))
+        print(f'torch sdpa fwd {tf * 1e3:.1f} us {fl / tf / 1e9:.0f} TF | bwd {tb * 1e3:.1f} us '
+              f'{2.5 * fl / tb / 1e9:.0f} TF', flush=True)
+    except Exception as ex:  # noqa: BLE001
+        print('torch sdpa unavailable:', ex)
 
 
 if __name__ == '__main__':
