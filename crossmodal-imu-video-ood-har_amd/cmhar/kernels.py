@@ -96,6 +96,17 @@ def _splits_for(M, N, K):
     return max(1, min(32, round(slots / tiles), K // 512))
 
 
+_TAIL_WS = {}
+
+
+def _tail_ws(M, N, K):
+    key = (M, N, K)
+    v = _TAIL_WS.get(key)
+    if v is None:
+        v = _TAIL_WS[key] = int(L.lib().cmhar_gemm_bf16_ws(M, N, K))
+    return v
+
+
 # ------------------------------------------------------------------------------------------------------------
 # GEMM: C = A·B in one of three layouts (see include/cmhar.h)
 # ------------------------------------------------------------------------------------------------------------
@@ -157,6 +168,10 @@ def gemm(layout: int, a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, *, bi
         ws = None
         if s > 1:
             ws = workspace(s * M * N + (s * M if rowsum is not None else 0), out.device)
+        elif splits is None and rowsum is None:
+            n = _tail_ws(M, N, K)
+            if n:
+                ws = workspace(n, out.device)
         ev = TRACE.begin()
         call('cmhar_gemm_bf16', layout, L.dtype_code(out.dtype), M, N, K, ptr(a), a.stride(0), ptr(b), b.stride(0),
              ptr(out), out.stride(0), C.byref(epi), s, ptr(ws), st)

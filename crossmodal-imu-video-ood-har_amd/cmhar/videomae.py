@@ -259,12 +259,30 @@ def _forward_impl(m: VideoMAEBackbone, video: torch.Tensor, save: bool):
     return x, st
 
 
-def _backward_impl(m: VideoMAEBackbone, st, dx, sink):
+_WGRAD_STREAMS = {}
+
+
+def _wgrad_stream(dev):
+    s = _WGRAD_STREAMS.get(dev)
+    if s is None:
+        s = _WGRAD_STREAMS[dev] = torch.cuda.Stream(dev)
+    return s
+
+
+def _backward_impl(m: VideoMAEBackbone, st, dx, sink, overlap_wgrad=True):
     """dx: [M, Hd] gradient of the backbone output (compute dtype).  Parameter gradients go to `sink`
     (cmhar.grads): fp32, written by the wgrad GEMM / colsum / LN-backward epilogues with β = 0 or 1."""
     W = m._weights()
     B, Lt, M, Hd, nh, D, scale = st.geom
     dev = dx.device
+
+    # Optionally (module attribute `overlap_wgrad`) the weight gradients (dW = dYᵀX, split-K), which do not feed the
+    # rest of the backward, run on their own stream so their workgroups can fill CUs the critical-path kernels leave
+    # idle; parameter groups are then declared final (gradient bucket all-reduce) from that stream, after it has
+    # caught up with the main stream's LayerNorm gradients.  Measured on MI355X at B=32: no gain (the two GEMMs
+    # slow each other through shared L2), so it is off by default.
+    cur = torch.cuda.current_stream(dev)
+    side = _wgrad_stream(dev) if overlap_wgrad else cur
 
     def wgrad(params, dy, x, shape, bias=None):
         """Weight gradient GEMM; the bias gradient (Σ_tokens dy) rides on the same GEMM's MFMA operand tiles."""
@@ -272,7 +290,22 @@ def _backward_impl(m: VideoMAEBackbone, st, dx, sink):
         bout, bbeta = (None, 0.0)
         if bias:
             bout, bbeta = sink.dest(bias, (sum(q.numel() for q in bias),), dev)
-        K.linear_wgrad(dy, x, out=out, beta=beta, bias_out=bout, bias_beta=bbeta)
+        if side is cur:
+            K.linear_wgrad(dy, x, out=out, beta=beta, bias_out=bout, bias_beta=bbeta)
+            return
+        side.wait_stream(cur)
+        with torch.cuda.stream(side):
+            K.linear_wgrad(dy, x, out=out, beta=beta, bias_out=bout, bias_beta=bbeta)
+        dy.record_stream(side)
+        x.record_stream(side)
+
+    def done(params):
+        if side is cur:
+            sink.done(params)
+            return
+        side.wait_stream(cur)
+        with torch.cuda.stream(side):
+            sink.done(params)
 
     def ln_grads(wp, bp):
         gw, bw = sink.dest([wp], wp.shape, dev)
@@ -315,10 +348,12 @@ def _backward_impl(m: VideoMAEBackbone, st, dx, sink):
         gw1, gb1, beta = ln_grads(p['ln1w'], p['ln1b'])
         dx = K.layernorm_bwd(dh1, x, p['ln1w'], mu1, rs1, gw1, gb1, dres=dx1, beta_acc=beta)
         del dh1, dx1
-        sink.done([q for q in p.values() if q is not None])
+        done([q for q in p.values() if q is not None])
     pe = m.embeddings.patch_embeddings.projection
     wgrad([pe.weight], dx, st.patches, (pe.weight.shape[0], pe.weight[0].numel()), [pe.bias])
-    sink.done([pe.weight, pe.bias])
+    done([pe.weight, pe.bias])
+    if side is not cur:
+        cur.wait_stream(side)
     st.patches = None
 
 
@@ -351,7 +386,7 @@ class _BackboneFn(torch.autograd.Function):
             dx = torch.empty(M, Hd, dtype=dt, device=gout.device)
             K.copy2d(gout.view(M, Hd), dx)
         sink = getattr(m, '_grad_sink', None) or AutogradSink()
-        _backward_impl(m, st, dx, sink)
+        _backward_impl(m, st, dx, sink, overlap_wgrad=getattr(m, "overlap_wgrad", False))
         ctx.st = None
         out = [None, None, None]
         for p in ctx.params:

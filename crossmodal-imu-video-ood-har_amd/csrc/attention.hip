@@ -140,11 +140,15 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_bf16(int H, int Lq, int Lk, i
   tk.store(Ks(0), tid);
   tv.store(Vs(0), tid);
   __syncthreads();
+  // A wave whose queries all lie past Lq (the ragged last workgroup of a head) still helps stage K/V tiles and
+  // joins every barrier, but issues no MFMA / softmax work: its SIMD's matrix pipe goes to the co-resident waves.
+  const bool active = q0 < Lq;
   for (int kt = 0; kt < nt; ++kt) {
     const int cur = kt & 1;
     const bool more = kt + 1 < nt;
     // Sᵀ = K·Qᵀ for every q-block; each K fragment is read once and used QB times
     floatx16 s[QB][2];
+    if (active) {
 #pragma unroll
     for (int kb = 0; kb < 2; ++kb) {
 #pragma unroll
@@ -159,10 +163,12 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_bf16(int H, int Lq, int Lk, i
           s[j][kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[j][t], s[j][kb], 0, 0, 0);
       }
     }
+    }
     if (more) {   // next tile's global loads fly under the softmax and P·V (written to LDS after them)
       tk.load(Kb, ldk, (kt + 1) * 64, Lk, tid);
       tv.load(Vb, ldv, (kt + 1) * 64, Lk, tid);
     }
+    if (active) {
     const int kbase = kt * 64;
     if (kbase + 64 > Lk) {   // ragged last tile only (wave-uniform branch)
 #pragma unroll
@@ -215,6 +221,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_bf16(int H, int Lq, int Lk, i
           for (int j = 0; j < QB; ++j)
             o[j][d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pb[j][kb][ss], o[j][d], 0, 0, 0);
         }
+    }
     if (more) {
       tk.store(Ks(cur ^ 1), tid);
       tv.store(Vs(cur ^ 1), tid);
@@ -320,6 +327,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_bf16(int H, int Lq, int 
   load_rows(0);
   store_rows(0);
   __syncthreads();
+  const bool active = k0 < Lk;      // waves past the last key only stage tiles and join barriers (see forward)
   for (int qt = 0; qt < nt; ++qt) {
     const int cur = qt & 1;
     const bool more = qt + 1 < nt;
@@ -328,6 +336,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_bf16(int H, int Lq, int 
     const float* D_ = Ds + cur * 64;
 #pragma unroll
     for (int qb = 0; qb < 2; ++qb) {
+      if (!active) break;
       // S = Q·Kᵀ (key on lane), pre-loaded with -lse/c so that p = exp2(c*acc)
       floatx16 s, dp;
 #pragma unroll
@@ -416,6 +425,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_bf16(int H, int Lq, int Lk
   tk.store(Ks(0), tid);
   tv.store(Vs(0), tid);
   __syncthreads();
+  const bool active = q0 < Lq;      // waves past the last query only stage tiles and join barriers (see forward)
   for (int kt = 0; kt < nt; ++kt) {
     const int cur = kt & 1;
     const bool more = kt + 1 < nt;
@@ -426,6 +436,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_bf16(int H, int Lq, int Lk
     const int kbase = kt * 64;
 #pragma unroll
     for (int kb = 0; kb < 2; ++kb) {
+      if (!active) break;
       floatx16 s, dp;
 #pragma unroll
       for (int r = 0; r < 16; ++r) { s[r] = -L2 / c; dp[r] = -Dl; }
@@ -654,7 +665,8 @@ extern "C" int cmhar_attention_fwd(int dtype, int B, int H, int Lq, int Lk, int 
                                    float scale, float pdrop, unsigned long long seed, hipStream_t st) {
   if (B <= 0 || Lq <= 0) return 0;
   if (dtype == CMHAR_BF16 && D == 64 && pdrop == 0.f) {
-    // 256-query workgroups (64 rows per wave) over the bulk, 128-query workgroups (32 rows per wave) for the rest
+    // 256-query workgroups (64 rows per wave) over the bulk, 128-query workgroups (32 rows per wave, waves past Lq
+    // skip the math) for the rest
     const int bulk = (Lq / 256) * 256;
     if (bulk > 0)
       attn_fwd_bf16<2><<<dim3(bulk / 256, H, B), 256, 0, st>>>(H, Lq, Lk, 0, (const bf16*)Q, ldq, (const bf16*)K, ldk,

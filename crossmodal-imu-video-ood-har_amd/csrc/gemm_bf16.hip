@@ -281,14 +281,15 @@ __global__ __launch_bounds__(NT, 2) void gemm_bf16_kernel(int M, int N, int K, c
 #undef Bs
 
 // Sum split-K fp32 partial slabs and apply the epilogue; 8 consecutive columns per thread when N % 8 == 0.
+// m_base: the slabs hold rows m_base .. m_base+M-1 of C (tail-split hybrid); 0 for a plain split-K GEMM.
 template <typename OutT>
 __global__ void splitk_reduce_kernel(int M, int N, int splits, const float* __restrict__ P, long split_stride,
-                                     OutT* __restrict__ C, long ldc, Epilogue e) {
+                                     OutT* __restrict__ C, long ldc, Epilogue e, int m_base = 0) {
   const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if ((N & 7) == 0) {
     const long e0 = idx * 8;
     if (e0 >= (long)M * N) return;
-    const int m = (int)(e0 / N), n0 = (int)(e0 % N);
+    const int m = (int)(e0 / N) + m_base, n0 = (int)(e0 % N);
     float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     for (int z = 0; z < splits; ++z) {
       const floatx4 a = *(const floatx4*)(P + z * split_stride + e0), b = *(const floatx4*)(P + z * split_stride + e0 + 4);
@@ -332,25 +333,30 @@ __device__ __forceinline__ int mc_off512(int k, int chunk) { return k * 512 + ((
 
 typedef __attribute__((address_space(3))) void* lds_void_ptr;
 
-// Issue this wave's 4 LDS-DMA instructions for one operand tile (256 rows/cols x 64 k).
+// Issue one of this wave's 4 LDS-DMA pieces (t = 0..3) of an operand tile (256 rows/cols x 64 k).
+template <bool KC>
+__device__ __forceinline__ void dma_piece(const bf16* __restrict__ P, long ld, int r0, int k0, char* lds, int wave,
+                                          int lane, int t) {
+  const int i = wave * 4 + t;                              // 1 KiB piece index (32 per tile)
+  const bf16* src;
+  if (KC) {   // [256 rows][64 k]: piece = 8 rows of 128 B
+    const int row = 8 * i + (lane >> 3);
+    const int lc = (lane & 7) ^ ((row >> 1) & 7);
+    src = P + (long)(r0 + row) * ld + k0 + lc * 8;
+  } else {    // [64 k][256 cols]: piece = 2 k-rows of 512 B
+    const int k = 2 * i + (lane >> 5);
+    const int lc = (lane & 31) ^ mc_swz(k);
+    src = P + (long)(k0 + k) * ld + r0 + lc * 8;
+  }
+  __builtin_amdgcn_global_load_lds((const void*)src, (lds_void_ptr)(lds + i * 1024), 16, 0, 0);
+}
+
+// Issue this wave's 4 LDS-DMA instructions for one operand tile.
 template <bool KC>
 __device__ __forceinline__ void dma_tile(const bf16* __restrict__ P, long ld, int r0, int k0, char* lds, int wave,
                                          int lane) {
 #pragma unroll
-  for (int t = 0; t < 4; ++t) {
-    const int i = wave * 4 + t;                            // 1 KiB piece index (32 per tile)
-    const bf16* src;
-    if (KC) {   // [256 rows][64 k]: piece = 8 rows of 128 B
-      const int row = 8 * i + (lane >> 3);
-      const int lc = (lane & 7) ^ ((row >> 1) & 7);
-      src = P + (long)(r0 + row) * ld + k0 + lc * 8;
-    } else {    // [64 k][256 cols]: piece = 2 k-rows of 512 B
-      const int k = 2 * i + (lane >> 5);
-      const int lc = (lane & 31) ^ mc_swz(k);
-      src = P + (long)(k0 + k) * ld + r0 + lc * 8;
-    }
-    __builtin_amdgcn_global_load_lds((const void*)src, (lds_void_ptr)(lds + i * 1024), 16, 0, 0);
-  }
+  for (int t = 0; t < 4; ++t) dma_piece<KC>(P, ld, r0, k0, lds, wave, lane, t);
 }
 
 template <bool KC>
@@ -370,28 +376,55 @@ __device__ __forceinline__ bf16x8 frag256(const char* lds, int r0, int kk, int l
 }
 
 // MODE (ablation builds only, tools/debug): 0 = product; 3 = epilogue only (no K loop); 4 = K loop only (no
-// epilogue); 5 = LDS staging only; 6 = staging + plain bf16 stores.
+// epilogue); 5 = LDS staging only; 6 = staging + plain bf16 stores; 7 = K loop without the LDS-DMA (stale
+// operands), no epilogue; 8 = K loop with the DMA pieces spread between the MFMAs, no epilogue.
 template <bool A_KC, bool B_KC, typename OutT, int MODE = 0>
 __global__ __launch_bounds__(NT2, 2) void gemm256_kernel(int M, int N, int K, const bf16* __restrict__ A, long lda,
                                                          const bf16* __restrict__ B, long ldb, OutT* __restrict__ C,
                                                          long ldc, Epilogue e, int klen, long split_stride,
-                                                         int raw_out) {
+                                                         int raw_out, float* __restrict__ sk_ws, int n_dp,
+                                                         int sk_klen) {
   __shared__ __attribute__((aligned(16))) char smem[SMEM2];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = wave >> 2, wc = wave & 3;
   const int tiles_n = N / TN2, tiles_m = M / TM2;
-  // split index folded into the XCD remap: one XCD runs whole splits, whose CUs then share each K-slice in L2
   const int ntile = tiles_m * tiles_n;
-  const int rlin = xcd_remap(blockIdx.x + ntile * blockIdx.z, ntile * gridDim.z);
-  const int bid = rlin % ntile, split = rlin / ntile;
+  int bid, split, kbeg, kend;
+  bool sk = false;
+  if (n_dp > 0) {
+    // Tail split (data-parallel + split-K hybrid): blocks [0, n_dp) are whole tiles (full rounds of the chip); the
+    // remaining tail tiles — whole tile rows, n_dp is row-aligned — are split along K over the rest of the grid so
+    // the last round fills the CUs; their fp32 partials go to sk_ws and splitk_reduce applies the epilogue.
+    if ((int)blockIdx.x < n_dp) {
+      bid = xcd_remap(blockIdx.x, n_dp);
+      split = 0;
+      kbeg = 0;
+      kend = K;
+    } else {
+      const int n_tail = ntile - n_dp;
+      const int u = xcd_remap(blockIdx.x - n_dp, gridDim.x - n_dp);
+      bid = n_dp + u % n_tail;
+      split = u / n_tail;
+      kbeg = split * sk_klen;
+      kend = min(K, kbeg + sk_klen);
+      sk = true;
+    }
+  } else {
+    // split index folded into the XCD remap: one XCD runs whole splits, whose CUs then share each K-slice in L2
+    const int rlin = xcd_remap(blockIdx.x + ntile * blockIdx.z, ntile * gridDim.z);
+    bid = rlin % ntile;
+    split = rlin / ntile;
+    kbeg = split * klen;
+    kend = min(K, kbeg + klen);
+  }
   const int tm = bid / tiles_n, tn = bid % tiles_n;
   const int bm = tm * TM2, bn = tn * TN2;
-  const int kbeg = split * klen;
-  const int kend = min(K, kbeg + klen);
+  const int tail_m0 = (n_dp / max(tiles_n, 1)) * TM2;
+  const long sk_stride = (long)(M - tail_m0) * N;
   float* const rs_slab = raw_out ? (float*)C + (long)gridDim.z * split_stride + (long)split * M : nullptr;
   C += (long)split * split_stride;
-  const int nk = MODE >= 3 && MODE != 4 ? 0 : (kend - kbeg) / TK2;
+  const int nk = MODE >= 3 && MODE != 4 && MODE != 7 && MODE != 8 ? 0 : (kend - kbeg) / TK2;
   // Weight-gradient GEMMs (A = dYᵀ, M-contiguous) can also emit the bias gradient Σ_k A(m,k): one extra MFMA of an
   // A fragment against an all-ones B fragment.  One block per row panel (tn == tm % tiles_n, spreading the panels
   // over the column tiles) does it, each of its waves for 2 of its 8 A fragments: +2 MFMAs per 32 on those blocks.
@@ -424,8 +457,10 @@ __global__ __launch_bounds__(NT2, 2) void gemm256_kernel(int M, int N, int K, co
       if (i >= i_lo && i < i_hi) af[i] = frag256<A_KC>(a_s, wr * 128 + i * 16, 0, lane);
   };
   if (nk > 0) {
-    dma_tile<A_KC>(A, lda, bm, kbeg, smem, wave, lane);
-    dma_tile<B_KC>(B, ldb, bn, kbeg, smem + 32768, wave, lane);
+    if (MODE != 7) {
+      dma_tile<A_KC>(A, lda, bm, kbeg, smem, wave, lane);
+      dma_tile<B_KC>(B, ldb, bn, kbeg, smem + 32768, wave, lane);
+    }
     __syncthreads();                                        // tile 0 landed
     load_k0(smem, smem + 32768, 0, 8, true);
 #pragma unroll
@@ -436,7 +471,7 @@ __global__ __launch_bounds__(NT2, 2) void gemm256_kernel(int M, int N, int K, co
     const char* b_s = a_s + 32768;
     const bool more = kt + 1 < nk;
     char* nxt = smem + ((kt + 1) & 1) * 65536;
-    if (more) {
+    if (more && MODE != 7 && MODE != 8) {
       dma_tile<A_KC>(A, lda, bm, kbeg + (kt + 1) * TK2, nxt, wave, lane);
       dma_tile<B_KC>(B, ldb, bn, kbeg + (kt + 1) * TK2, nxt + 32768, wave, lane);
     }
@@ -445,6 +480,10 @@ __global__ __launch_bounds__(NT2, 2) void gemm256_kernel(int M, int N, int K, co
     for (int i = 0; i < 8; ++i) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bf0[j], acc[i][j], 0, 0, 0);
+      if (MODE == 8 && more) {   // one DMA piece per 4 MFMAs: the issue cost interleaves with the matrix pipe
+        if (i < 4) dma_piece<A_KC>(A, lda, bm, kbeg + (kt + 1) * TK2, nxt, wave, lane, i);
+        else dma_piece<B_KC>(B, ldb, bn, kbeg + (kt + 1) * TK2, nxt + 32768, wave, lane, i - 4);
+      }
       if (!A_KC && rs && wc == (i >> 1))
         accb[i & 1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], ones, accb[i & 1], 0, 0, 0);
       af[i] = frag256<A_KC>(a_s, wr * 128 + i * 16, 1, lane);
@@ -489,7 +528,7 @@ __global__ __launch_bounds__(NT2, 2) void gemm256_kernel(int M, int N, int K, co
       }
   }
   __syncthreads();
-  if (MODE == 4) {   // keep every accumulator live, store nothing
+  if (MODE == 4 || MODE == 7 || MODE == 8) {   // keep every accumulator live, store nothing
     float t = 0.f;
 #pragma unroll
     for (int i = 0; i < 8; ++i)
@@ -529,6 +568,10 @@ __global__ __launch_bounds__(NT2, 2) void gemm256_kernel(int M, int N, int K, co
         float* dst = (float*)C + (long)m * ldc + n0;
         *(floatx4*)dst = lo;
         *(floatx4*)(dst + 4) = hi;
+      } else if (sk) {
+        float* dst = sk_ws + split * sk_stride + (long)(m - tail_m0) * N + n0;
+        *(floatx4*)dst = lo;
+        *(floatx4*)(dst + 4) = hi;
       } else {
         float v[8];
 #pragma unroll
@@ -538,6 +581,36 @@ __global__ __launch_bounds__(NT2, 2) void gemm256_kernel(int M, int N, int K, co
     }
     __syncthreads();
   }
+}
+
+// Tail split for a whole-K 256² GEMM whose tile count leaves the last round of the chip mostly empty: keep full
+// rounds data-parallel and split the remaining tile rows along K to fill the last round.
+constexpr int kCUs = 256;
+struct TailSplit {
+  int n_dp, n_sk, nsplit, sk_klen, tail_m0;
+};
+static TailSplit tail_split(int M, int N, int K) {
+  TailSplit t{0, 0, 0, 0, 0};
+  if (M % TM2 || N % TN2 || K % TK2) return t;
+  const int tiles_n = N / TN2, ntile = (M / TM2) * tiles_n;
+  if (ntile <= kCUs) return t;
+  const int rem = ntile % kCUs;
+  if (rem == 0 || rem * 2 > kCUs) return t;                 // last round already more than half full
+  const int n_dp = (ntile / kCUs) * kCUs / tiles_n * tiles_n; // row-aligned
+  const int n_tail = ntile - n_dp;
+  // the split partials cost a write + read of n_tail tiles of fp32 per split: only worth it when the tail tiles'
+  // K loop is long (measured on MI355X: N = 768 at K = 3072 / 2304 gains ~30 us, at K = 768 it loses ~30 us)
+  if (K < 2048) return t;
+  int s = kCUs / n_tail;
+  s = min(s, K / TK2 / 4);                                    // ≥ 4 K-tiles per split
+  if (s < 2) return t;
+  const int klen = cdiv(cdiv(K, s), TK2) * TK2;
+  t.nsplit = cdiv(K, klen);
+  t.sk_klen = klen;
+  t.n_dp = n_dp;
+  t.n_sk = n_tail * t.nsplit;
+  t.tail_m0 = n_dp / tiles_n * TM2;
+  return t;
 }
 
 template <bool AK, bool BKc, typename OutT>
@@ -552,10 +625,18 @@ int launch(int M, int N, int K, const bf16* A, long lda, const bf16* B, long ldb
     if (splits > 1) klen = cdiv(cdiv(K, splits), TK2) * TK2;
     const int nsplit = cdiv(K, klen);
     dim3 grid((M / TM2) * (N / TN2), 1, nsplit);
-    if (nsplit == 1)
-      gemm256_kernel<AK, BKc, OutT><<<grid, NT2, 0, st>>>(M, N, K, A, lda, B, ldb, C, ldc, e, klen, 0, 0);
-    else {
-      gemm256_kernel<AK, BKc, float><<<grid, NT2, 0, st>>>(M, N, K, A, lda, B, ldb, ws, N, e, klen, ss, 1);
+    const TailSplit ts = tail_split(M, N, K);
+    if (nsplit == 1 && ws && ts.n_dp > 0 && !e.rowsum) {
+      gemm256_kernel<AK, BKc, OutT><<<ts.n_dp + ts.n_sk, NT2, 0, st>>>(M, N, K, A, lda, B, ldb, C, ldc, e, K, 0, 0, ws,
+                                                                      ts.n_dp, ts.sk_klen);
+      const int tail_rows = M - ts.tail_m0;
+      splitk_reduce_kernel<OutT><<<reduce_blocks(tail_rows, N), 256, 0, st>>>(
+          tail_rows, N, ts.nsplit, ws, (long)tail_rows * N, C, ldc, e, ts.tail_m0);
+    } else if (nsplit == 1) {
+      gemm256_kernel<AK, BKc, OutT><<<grid, NT2, 0, st>>>(M, N, K, A, lda, B, ldb, C, ldc, e, klen, 0, 0, nullptr, 0, 0);
+    } else {
+      gemm256_kernel<AK, BKc, float><<<grid, NT2, 0, st>>>(M, N, K, A, lda, B, ldb, ws, N, e, klen, ss, 1, nullptr, 0,
+                                                           0);
       splitk_reduce_kernel<OutT><<<reduce_blocks(M, N), 256, 0, st>>>(M, N, nsplit, ws, ss, C, ldc, e);
     }
     CMHAR_CHECK_LAUNCH();
@@ -582,6 +663,12 @@ int launch(int M, int N, int K, const bf16* A, long lda, const bf16* B, long ldb
 }
 
 }  // namespace
+
+// fp32 workspace floats cmhar_gemm_bf16 can use for a whole-K (splits == 1) call: the tail-split partials, or 0.
+extern "C" long cmhar_gemm_bf16_ws(int M, int N, int K) {
+  const TailSplit t = tail_split(M, N, K);
+  return t.n_dp > 0 ? (long)t.nsplit * (M - t.tail_m0) * N : 0;
+}
 
 // layout: 0 = NT (A K-contig, B K-contig: Y = X Wᵀ), 1 = NN (A K-contig, B N-contig: dX = dY W),
 //         2 = TN (A M-contig, B N-contig: dW = dYᵀ X).  ws: fp32 workspace of splits*M*N floats when splits > 1.

@@ -1,0 +1,465 @@
+// Persistent "ping-pong" bf16 MFMA GEMM for gfx950: the VideoMAE Linear hot path with the epilogue hidden under MFMA.
+//
+// Why: the 256x256 one-workgroup-per-CU kernel (gemm_bf16.hip) runs its K loop at ~1250 TFLOP/s, but every
+// workgroup on the chip reaches its epilogue (bias / GELU / residual / bf16 stores) at the same moment, so the
+// matrix pipes idle through each epilogue and the 256-wide output tiles quantise badly on N = 768 (2.3 rounds of
+// 256 tiles → 3).  Here TWO 4-wave workgroups share each CU, each computing its own 256x128 tile sequence with its
+// own LDS ring and its own s_barrier; the second workgroup of a CU starts half a tile late, so one workgroup's
+// epilogue (VALU + HBM stores) runs while the other's K loop keeps the CU's matrix pipes busy.  The epilogue works
+// straight from the accumulator registers (no LDS staging): the MFMA operands are swapped (C tiles are produced
+// transposed), so each lane holds 4 consecutive output columns of one row → 8-B bf16 / 16-B fp32 vector stores.
+//
+// Tile 256(M) x 128(N) x 32(K), 256 threads = 4 waves (2 x 2, 128x64 outputs per wave = 8x4 mfma_f32_16x16x32_bf16),
+// 3-stage LDS ring of 24 KiB filled by LDS-DMA (global_load_lds_dwordx4; XOR swizzles applied on the per-lane
+// global source address, the same swizzles on the fragment reads: conflict-free, tools/lds_banks.py), one barrier
+// per K step, two K steps in flight.  72 KiB LDS per workgroup → two workgroups per CU.
+//
+// Layouts as gemm_bf16.hip: A_KC = A is K-contiguous ([M][K]) else M-contiguous ([K][M]); B_KC likewise for B.
+// Split-K: units = splits x tiles; raw fp32 partial slabs (+ bias row-sum slabs) reduced by splitk_reduce.
+#include "common.h"
+
+namespace {
+
+constexpr int PM = 256, PN = 128, PK = 32, PT = 256, PSTAGES = 3;
+constexpr int P_ASZ = PM * PK * 2;            // 16 KiB
+constexpr int P_BSZ = PN * PK * 2;            // 8 KiB
+constexpr int P_STAGE = P_ASZ + P_BSZ;        // 24 KiB
+constexpr int P_LDS = PSTAGES * P_STAGE;      // 72 KiB
+
+typedef __attribute__((address_space(3))) void* lds_void_ptr_t;
+
+// K-contiguous image [rows][32 k]: 64-B rows of 4 x 16-B chunks; chunk ^= (r & 1) | ((r >> 1) & 2).
+__device__ __forceinline__ int kc32_off(int r, int c) { return r * 64 + ((c ^ ((r & 1) | ((r >> 1) & 2))) << 4); }
+// Row-contraction images [32 k][W cols]: W*2-B rows, chunk ^= 2*((k&3) | ((k>>3)&1)<<2)  (gemm_bf16.hip's swizzle).
+__device__ __forceinline__ int pmc_swz(int k) { return ((k & 3) | (((k >> 3) & 1) << 2)) << 1; }
+template <int W>
+__device__ __forceinline__ int mcw_off(int k, int chunk) { return k * (W * 2) + ((chunk ^ pmc_swz(k)) << 4); }
+
+// LDS-DMA of one operand tile (ROWS x 32 k) into `lds`; this wave issues pieces wave, wave+4, ... (1 KiB each).
+template <bool KC, int ROWS>
+__device__ __forceinline__ void pp_dma(const bf16* __restrict__ P, long ld, int r0, int k0, char* lds, int wave,
+                                       int lane) {
+  constexpr int PIECES = ROWS * PK * 2 / 1024;
+#pragma unroll
+  for (int t = 0; t < PIECES / 4; ++t) {
+    const int i = t * 4 + wave;
+    const bf16* src;
+    if (KC) {          // piece = 16 rows x 64 B; lane → (row, swizzled chunk)
+      const int row = 16 * i + (lane >> 2);
+      const int c = (lane & 3) ^ ((row & 1) | ((row >> 1) & 2));
+      src = P + (long)(r0 + row) * ld + k0 + c * 8;
+    } else {           // [32 k][ROWS]: piece = 1024 / (2*ROWS) k-rows
+      constexpr int CH = ROWS / 8;                 // 16-B chunks per k-row
+      constexpr int KPP = 64 / CH;                 // k-rows per piece
+      const int k = KPP * i + lane / CH;
+      const int c = (lane % CH) ^ pmc_swz(k);
+      src = P + (long)(k0 + k) * ld + r0 + c * 8;
+    }
+    __builtin_amdgcn_global_load_lds((const void*)src, (lds_void_ptr_t)(lds + i * 1024), 16, 0, 0);
+  }
+}
+
+// 16 rows (r0 + lane&15) x 32 k (8*(lane>>4) + j) fragment of an operand image.
+template <bool KC, int ROWS>
+__device__ __forceinline__ bf16x8 pp_frag(const char* lds, int r0, int lane) {
+  if (KC) {
+    return *(const bf16x8*)(lds + kc32_off(r0 + (lane & 15), lane >> 4));
+  } else {
+    const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+    const int chunk = (r0 >> 3) + (p >> 1);
+    const int k = 8 * g + q;
+    const short4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        LDS_PTR(short4_t, lds + mcw_off<ROWS>(k, chunk) + (p & 1) * 8));
+    const short4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        LDS_PTR(short4_t, lds + mcw_off<ROWS>(k + 4, chunk) + (p & 1) * 8));
+    short8_t v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    return __builtin_bit_cast(bf16x8, v);
+  }
+}
+
+template <typename OutT>
+__device__ __forceinline__ void load4(const OutT* __restrict__ p, float (&x)[4]) {
+  if constexpr (sizeof(OutT) == 2) {
+    const bf16x4 v = *(const bf16x4*)p;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) x[j] = (float)v[j];
+  } else {
+    const floatx4 v = *(const floatx4*)p;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) x[j] = v[j];
+  }
+}
+template <typename OutT>
+__device__ __forceinline__ void store4(OutT* __restrict__ p, const float (&x)[4]) {
+  if constexpr (sizeof(OutT) == 2) {
+    bf16x4 v;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = (bf16)x[j];
+    *(bf16x4*)p = v;
+  } else {
+    *(floatx4*)p = floatx4{x[0], x[1], x[2], x[3]};
+  }
+}
+
+// Epilogue on 4 consecutive columns n0..n0+3 of row m (16-B aligned fp32 operands, 8-B aligned bf16 operands:
+// N % 8 == 0 and every leading dimension % 8 == 0, checked on the host).  The activation is a template parameter
+// so the 32 fully unrolled copies per wave stay small enough for the accumulators to remain in registers.
+template <typename OutT, int ACT>
+__device__ __forceinline__ void epi4(const Epilogue& e, OutT* __restrict__ C, long ldc, int m, int n0,
+                                     const floatx4& acc, const floatx4& bias) {
+  float x[4], t[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) x[j] = fmaf(e.alpha, acc[j], bias[j]);
+  if (e.rowadd) {
+    const floatx4 r = *(const floatx4*)(e.rowadd + (long)(m % e.rowadd_mod) * e.rowadd_ld + n0);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) x[j] += r[j];
+  }
+  if constexpr (ACT == ACT_GELU) {
+    if (e.aux_out) store4<OutT>((OutT*)e.aux_out + (long)m * e.ldo + n0, x);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) x[j] = gelu_erf(x[j]);
+  } else if constexpr (ACT == ACT_GELU_SAVEGRAD) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) gelu_pair(x[j], x[j], t[j]);
+    store4<OutT>((OutT*)e.aux_out + (long)m * e.ldo + n0, t);
+  } else if constexpr (ACT == ACT_MULAUX) {
+    load4<OutT>((const OutT*)e.aux_in + (long)m * e.lda + n0, t);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) x[j] *= t[j];
+  }
+  if (e.residual) {
+    load4<OutT>((const OutT*)e.residual + (long)m * e.ldr + n0, t);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) x[j] += t[j];
+  }
+  OutT* dst = C + (long)m * ldc + n0;
+  if (e.beta != 0.f) {
+    load4<OutT>(dst, t);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) x[j] += e.beta * t[j];
+  }
+  store4<OutT>(dst, x);
+}
+
+// Generic-act 4-column epilogue for the split-K reduce (any act code, dropout).
+template <typename OutT>
+__device__ __forceinline__ void epilogue_store4(const Epilogue& e, OutT* __restrict__ C, long ldc, int m, int n0,
+                                                const floatx4& acc) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) epilogue_store<OutT>(e, C, ldc, m, n0 + j, acc[j]);
+}
+
+struct PPUnit {
+  int bm, bn, kbeg, nk, split, tm, tn;
+  bool valid;
+};
+
+// Work assignment.  XCD x owns a fixed block of the (split, tile) space and its workgroups walk that block in
+// row-major tile order, so the tiles an XCD runs together share A row panels AND a B panel set small enough to stay
+// in its 4 MiB L2:
+//   nsplit % 8 == 0 (weight gradients): XCD x takes splits x, x+8, ... (their dY / X K-slices stay in its L2);
+//   otherwise the tile grid is cut into gm x gn blocks (gm * gn = 8, gn from the host: B panels per XCD ≤ ~2 MiB).
+// q = the workgroup's running index inside its XCD's block (slot, slot + G/8, ...).
+struct PPMap {
+  int tiles_m, tiles_n, nsplit, klen, K, gn;
+};
+
+__device__ __forceinline__ PPUnit pp_unit(const PPMap& mp, int xcd, int q) {
+  PPUnit p;
+  int split, tm, tn;
+  if (mp.nsplit % 8 == 0) {
+    const int ntile = mp.tiles_m * mp.tiles_n;
+    const int per = ntile * (mp.nsplit / 8);
+    p.valid = q < per;
+    const int qq = p.valid ? q : 0;
+    split = xcd + 8 * (qq / ntile);
+    const int t = qq % ntile;
+    tm = t / mp.tiles_n;
+    tn = t % mp.tiles_n;
+  } else {
+    const int gn = mp.gn, gm = 8 / gn;
+    const int xm = xcd / gn, xn = xcd % gn;
+    const int m_lo = xm * mp.tiles_m / gm, m_hi = (xm + 1) * mp.tiles_m / gm;
+    const int n_lo = xn * mp.tiles_n / gn, n_hi = (xn + 1) * mp.tiles_n / gn;
+    const int nw = n_hi - n_lo;
+    const int local = (m_hi - m_lo) * nw;
+    p.valid = q < local * mp.nsplit;
+    const int qq = p.valid ? q : 0;
+    split = qq / local;
+    const int t = qq % local;
+    tm = m_lo + t / nw;
+    tn = n_lo + t % nw;
+  }
+  p.split = split;
+  p.tm = tm;
+  p.tn = tn;
+  p.bm = tm * PM;
+  p.bn = tn * PN;
+  p.kbeg = split * mp.klen;
+  p.nk = (min(mp.K, p.kbeg + mp.klen) - p.kbeg) / PK;
+  return p;
+}
+
+// Persistent workgroup (xcd, slot) walks its XCD's block of units (pp_unit).  The K pipeline runs across unit
+// boundaries: global step g lives in ring stage g % 3; at the top of step g the workgroup waits for step g+1's
+// LDS-DMA and issues step g+3's (possibly the next unit's first steps, so the next tile's operands stream in under
+// this tile's last MFMAs and its epilogue); the fragments of step g+1 are read into the registers that step g's
+// MFMAs release (rolling refill), so LDS latency hides under the matrix pipe.
+// MODE (ablation builds only, tools/debug/gemm_pp_ablate.hip): 0 = product, 1 = no epilogue, 3 = no DMA,
+// 4 = product + per-unit s_memtime stamps.
+template <bool A_KC, bool B_KC, typename OutT, int ACT, int MODE = 0>
+__global__ __launch_bounds__(PT, 2) void gemm_pp_kernel(int M, int N, int K, const bf16* __restrict__ A, long lda,
+                                                        const bf16* __restrict__ B, long ldb, OutT* __restrict__ C,
+                                                        long ldc, Epilogue e, int klen, int nsplit, int raw_out,
+                                                        int delay_cycles, int gn) {
+  __shared__ __attribute__((aligned(16))) char smem[P_LDS];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave >> 1, wc = wave & 1;
+  const int tiles_n = N / PN, tiles_m = M / PM;
+  const int ntile = tiles_m * tiles_n;
+  const int units = ntile * nsplit;
+  const int G = gridDim.x;
+  const int per_xcd = G / 8;                              // host launches G % 8 == 0
+  const int xcd = blockIdx.x % 8, slot = blockIdx.x / 8;
+  const long split_stride = (long)M * N;
+  OutT* const C0 = C;
+  const PPMap mp{tiles_m, tiles_n, nsplit, klen, K, gn};
+  (void)units;
+
+  // Second workgroup of each CU (slots in the upper half of each XCD's range) starts half a tile late: the pair
+  // then alternates K loop and epilogue instead of idling the matrix pipes together.
+  if (slot >= per_xcd / 2 && delay_cycles > 0) {
+    const long t0 = __builtin_readcyclecounter();
+    while (__builtin_readcyclecounter() - t0 < delay_cycles) __builtin_amdgcn_s_sleep(32);
+  }
+
+  const bf16x8 ones = {(bf16)1.f, (bf16)1.f, (bf16)1.f, (bf16)1.f, (bf16)1.f, (bf16)1.f, (bf16)1.f, (bf16)1.f};
+  auto issue = [&](const PPUnit& p, int step, int stage) {
+    if (MODE == 3) return;
+    char* st = smem + stage * P_STAGE;
+    pp_dma<A_KC, PM>(A, lda, p.bm, p.kbeg + step * PK, st, wave, lane);
+    pp_dma<B_KC, PN>(B, ldb, p.bn, p.kbeg + step * PK, st + P_ASZ, wave, lane);
+  };
+
+  int q = slot;
+  PPUnit cu = pp_unit(mp, xcd, q);
+  if (!cu.valid) return;
+  PPUnit nu = pp_unit(mp, xcd, q + per_xcd);
+  // prologue: steps 0..2 of the first unit (host guarantees nk >= 3), fragments of step 0
+  issue(cu, 0, 0);
+  issue(cu, 1, 1);
+  issue(cu, 2, 2);
+  asm volatile("s_waitcnt vmcnt(12)\n\ts_barrier" ::: "memory");
+  bf16x8 af[8], bc[4], bnx[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) bc[j] = pp_frag<B_KC, PN>(smem + P_ASZ, wc * 64 + j * 16, lane);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) af[i] = pp_frag<A_KC, PM>(smem, wr * 128 + i * 16, lane);
+
+  int stage = 0;            // ring stage of the current global step
+  bool after_epi = false;   // first step after an epilogue: its stores are younger than the DMA waited for
+  int unit_no = 0;
+  for (;;) {
+    // MODE 4 (ablation): per-unit timestamps {start, end of K loop, end of epilogue} in e.rowsum (layout 0 only)
+    long long* stamps = MODE == 4 ? (long long*)e.rowsum + ((long)blockIdx.x * 64 + unit_no) * 3 : nullptr;
+    if (MODE == 4 && tid == 0 && unit_no < 64) stamps[0] = __builtin_readcyclecounter();
+    floatx4 acc[8][4];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+    floatx4 accb[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) accb[i] = floatx4{0.f, 0.f, 0.f, 0.f};
+    const bool rs = MODE != 4 && !A_KC && e.rowsum != nullptr && cu.tn == cu.tm % tiles_n;
+
+    for (int kt = 0; kt < cu.nk; ++kt) {
+      const bool ex1 = kt + 1 < cu.nk || nu.valid;          // step g+1 exists
+      const bool ex2 = kt + 2 < cu.nk || nu.valid;
+      const bool ex3 = kt + 3 < cu.nk || nu.valid;
+      if (ex2) {
+        if (after_epi) asm volatile("s_waitcnt vmcnt(38) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(6) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      } else if (ex1) {
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      }
+      after_epi = false;
+      const int s1 = stage == 2 ? 0 : stage + 1;
+      if (ex3) {
+        if (kt + 3 < cu.nk) issue(cu, kt + 3, stage);
+        else issue(nu, kt + 3 - cu.nk, stage);
+      }
+      const char* a_n = smem + s1 * P_STAGE;
+      const char* b_n = a_n + P_ASZ;
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j)   // swapped operands: the accumulator holds Cᵀ blocks (row m on the lane)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bc[j], af[i], acc[i][j], 0, 0, 0);
+        if (!A_KC && rs && wc == (i >> 2))
+          accb[i & 3] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], ones, accb[i & 3], 0, 0, 0);
+        if (ex1) {
+          af[i] = pp_frag<A_KC, PM>(a_n, wr * 128 + i * 16, lane);
+          if (i < 4) bnx[i] = pp_frag<B_KC, PN>(b_n, wc * 64 + i * 16, lane);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bc[j] = bnx[j];
+      stage = s1;
+    }
+
+    if (MODE == 4 && tid == 0 && unit_no < 64) stamps[1] = __builtin_readcyclecounter();
+    // epilogue straight from the accumulators: lane → row m = .. + (lane&15), columns n0 .. n0+3
+    if (MODE == 1) {   // no epilogue: keep the accumulators live
+      float t = 0.f;
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) t += acc[i][j][0] + acc[i][j][3];
+      if (t == 1234.5f) ((float*)C0)[tid] = t;
+    } else if (raw_out) {
+      float* Cs = (float*)C0 + (long)cu.split * split_stride;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int m = cu.bm + wr * 128 + i * 16 + (lane & 15);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int n0 = cu.bn + wc * 64 + j * 16 + 4 * (lane >> 4);
+          *(floatx4*)(Cs + (long)m * N + n0) = acc[i][j];
+        }
+      }
+    } else {
+      floatx4 bj[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int n0 = cu.bn + wc * 64 + j * 16 + 4 * (lane >> 4);
+        bj[j] = e.bias ? *(const floatx4*)(e.bias + n0) : floatx4{0.f, 0.f, 0.f, 0.f};
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int m = cu.bm + wr * 128 + i * 16 + (lane & 15);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int n0 = cu.bn + wc * 64 + j * 16 + 4 * (lane >> 4);
+          epi4<OutT, ACT>(e, C0, ldc, m, n0, acc[i][j], bj[j]);
+        }
+      }
+    }
+    if (!A_KC && rs && (lane & 15) == 0) {    // ones-product: every column holds the row sum; lanes 0,16,32,48
+      float* rs_slab = raw_out ? (float*)C0 + (long)nsplit * split_stride + (long)cu.split * M : nullptr;
+#pragma unroll
+      for (int ii = 0; ii < 4; ++ii)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int m = cu.bm + wr * 128 + (4 * wc + ii) * 16 + 4 * (lane >> 4) + r;
+          if (rs_slab) rs_slab[m] = accb[ii][r];
+          else e.rowsum[m] = e.rowsum_beta != 0.f ? accb[ii][r] + e.rowsum_beta * e.rowsum[m] : accb[ii][r];
+        }
+    }
+    if (MODE == 4 && tid == 0 && unit_no < 64) stamps[2] = __builtin_readcyclecounter();
+    ++unit_no;
+    if (!nu.valid) break;
+    q += per_xcd;
+    cu = nu;
+    nu = pp_unit(mp, xcd, q + per_xcd);
+    after_epi = true;
+  }
+}
+
+// Sum split-K fp32 partial slabs (+ bias row-sum slabs) and apply the epilogue; 8 consecutive columns per thread.
+template <typename OutT>
+__global__ void pp_splitk_reduce(int M, int N, int splits, const float* __restrict__ P, OutT* __restrict__ C, long ldc,
+                                 Epilogue e) {
+  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long ss = (long)M * N;
+  if (e.rowsum && idx < M) {
+    float r = 0.f;
+    for (int z = 0; z < splits; ++z) r += P[splits * ss + (long)z * M + idx];
+    e.rowsum[idx] = e.rowsum_beta != 0.f ? r + e.rowsum_beta * e.rowsum[idx] : r;
+  }
+  const long e0 = idx * 4;
+  if (e0 >= ss) return;
+  const int m = (int)(e0 / N), n0 = (int)(e0 % N);
+  floatx4 s = {0.f, 0.f, 0.f, 0.f};
+  for (int z = 0; z < splits; ++z) s += *(const floatx4*)(P + z * ss + e0);
+  epilogue_store4<OutT>(e, C, ldc, m, n0, s);
+}
+
+int g_num_cus = 0;
+
+}  // namespace
+
+// Returns 1 when the ping-pong kernel handles this problem (M % 256, N % 128, K/split % 32), 0 otherwise (caller
+// falls back), negative on error.  ws: splits*M*N (+ splits*M with rowsum) fp32 floats when splits > 1.
+extern "C" int cmhar_gemm_pp(int layout, int out_dtype, int M, int N, int K, const void* A, long lda, const void* B,
+                             long ldb, void* C, long ldc, const Epilogue* epi, int splits, void* ws, int delay_cycles,
+                             hipStream_t st) {
+  if (M % PM || N % PN || K % PK || layout < 0 || layout > 2) return 0;
+  Epilogue plain{};
+  plain.alpha = 1.f;
+  const Epilogue& e = epi ? *epi : plain;
+  if (e.rowsum && layout != 2) return -3;
+  // fused epilogues this kernel specialises (others — ReLU, dGELU from the pre-activation, dropout — stay on
+  // cmhar_gemm_bf16)
+  if (e.pdrop > 0.f || (e.act != ACT_NONE && e.act != ACT_GELU && e.act != ACT_GELU_SAVEGRAD && e.act != ACT_MULAUX))
+    return 0;
+  if (e.act == ACT_GELU_SAVEGRAD && !e.aux_out) return -4;
+  // activations per layout that the product uses: forward (0) GELU variants, dgrad (1) ×aux, wgrad (2) none
+  if ((layout == 1 && e.act != ACT_NONE && e.act != ACT_MULAUX) || (layout == 2 && e.act != ACT_NONE) ||
+      (layout == 0 && e.act == ACT_MULAUX))
+    return 0;
+  if (g_num_cus == 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&g_num_cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      g_num_cus = 0;
+    if (g_num_cus <= 0) g_num_cus = 256;
+  }
+  int klen = K;
+  if (splits > 1) klen = cdiv(cdiv(K, splits), PK) * PK;
+  const int nsplit = cdiv(K, klen);
+  if (klen < 3 * PK || (K - (nsplit - 1) * klen) < 3 * PK) return 0;   // the pipeline keeps 3 K steps in flight
+  if (nsplit > 1 && !ws) return -2;
+  const int units = (M / PM) * (N / PN) * nsplit;
+  int G = 2 * g_num_cus;
+  if (units < G) G = ((units + 7) / 8) * 8;
+  // N groups: B panels one XCD keeps in L2 ≲ 2 MiB (B bytes = N*K*2 for the whole matrix)
+  int gn = 1;
+  while (gn < 8 && (long)N / gn * K * 2 > (2l << 20) && (N / PN) % (gn * 2) == 0) gn *= 2;
+  const bool raw = nsplit > 1;
+  if (units <= G) delay_cycles = 0;                    // a single round: nothing to stagger against
+  const int act = raw ? ACT_NONE : e.act;             // split-K: the reduce applies the whole epilogue
+#define GO(AK, BK, OT, ACTV)                                                                                        \
+  gemm_pp_kernel<AK, BK, OT, ACTV><<<G, PT, 0, st>>>(M, N, K, (const bf16*)A, lda, (const bf16*)B, ldb,             \
+                                                     raw ? (OT*)ws : (OT*)C, ldc, e, klen, nsplit, raw ? 1 : 0,     \
+                                                     delay_cycles, gn)
+#define LAYOUT(OT)                                                                                                  \
+  do {                                                                                                              \
+    if (layout == 0) {                                                                                              \
+      if (act == ACT_NONE) GO(true, true, OT, ACT_NONE);                                                            \
+      else if (act == ACT_GELU) GO(true, true, OT, ACT_GELU);                                                       \
+      else GO(true, true, OT, ACT_GELU_SAVEGRAD);                                                                   \
+    } else if (layout == 1) {                                                                                       \
+      if (act == ACT_MULAUX) GO(true, false, OT, ACT_MULAUX); else GO(true, false, OT, ACT_NONE);                   \
+    } else {                                                                                                        \
+      GO(false, false, OT, ACT_NONE);                                                                               \
+    }                                                                                                               \
+  } while (0)
+  if (raw || out_dtype == CMHAR_F32) LAYOUT(float); else LAYOUT(bf16);
+#undef LAYOUT
+#undef GO
+  if (raw) {
+    const long n4 = (long)M * N / 4;
+    const int blocks = cdiv(n4 > M ? n4 : M, 256);
+    if (out_dtype == CMHAR_BF16)
+      pp_splitk_reduce<bf16><<<blocks, 256, 0, st>>>(M, N, nsplit, (const float*)ws, (bf16*)C, ldc, e);
+    else
+      pp_splitk_reduce<float><<<blocks, 256, 0, st>>>(M, N, nsplit, (const float*)ws, (float*)C, ldc, e);
+  }
+  CMHAR_CHECK_LAUNCH();
+  return 1;
+}

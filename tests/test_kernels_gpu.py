@@ -79,6 +79,22 @@ def test_gemm_bf16_splitk_exact(layout):
     assert torch.equal(out, _ref_gemm(layout, a, b))
 
 
+@pytest.mark.parametrize('layout', [0, 1])
+def test_gemm_bf16_tail_split_exact(layout):
+    """260 output tiles of 256²: two full chip rounds run whole-K, the last tile rows are split along K and reduced
+    with the epilogue (bias + residual at the right rows).  Integer operands: bit-exact."""
+    from cmhar import _lib
+    M, N, Kd = 256 * 130, 512, 2048
+    assert _lib.lib().cmhar_gemm_bf16_ws(M, N, Kd) > 0
+    a, b = _operands(layout, M, N, Kd, lambda s, sd: _ints(s, -2, 3, seed=sd), torch.bfloat16)
+    bias = _ints((N,), seed=7).to(DEV)
+    res = _ints((M, N), seed=8).to(DEV)
+    out = torch.empty(M, N, dtype=torch.float32, device=DEV)
+    K().gemm(layout, a, b, out, bias=bias, residual=res)
+    torch.cuda.synchronize()
+    assert torch.equal(out, _ref_gemm(layout, a, b) + bias + res)
+
+
 def test_gemm_bf16_epilogues():
     torch.manual_seed(0)
     M, N, Kd = 384, 512, 256
@@ -116,10 +132,11 @@ def test_gemm_bf16_epilogues():
 
 
 def _gelu_ref(x):
+    """float64 GELU(erf) and its derivative through erfc (1 + erf(x/√2) cancels to 0 below x ≈ -8.3 even in
+    float64, erfc keeps full relative precision)."""
     x64 = x.double()
-    g = torch.nn.functional.gelu(x64)
-    gp = 0.5 * (1 + torch.erf(x64 / math.sqrt(2))) + x64 * torch.exp(-0.5 * x64 * x64) / math.sqrt(2 * math.pi)
-    return g, gp
+    cdf = 0.5 * torch.erfc(-x64 / math.sqrt(2))
+    return x64 * cdf, cdf + x64 * torch.exp(-0.5 * x64 * x64) / math.sqrt(2 * math.pi)
 
 
 @pytest.mark.parametrize('shape', [(512, 512, 256), (384, 520, 136)])     # 256-tile DMA kernel and the 128² kernel
@@ -141,10 +158,19 @@ def test_gemm_gelu_savegrad_and_mulaux(shape):
     gp32 = torch.empty(M, N, device=DEV)
     K().gemm(0, a, w, y32, bias=bias, act=L().ACT_GELU_SAVEGRAD, aux_out=gp32)
     assert rel(y32, g_ref) < 2e-6 and rel(gp32, gp_ref) < 2e-6
-    neg = pre < -3
-    # tail precision: the erfc form keeps ~1e-6 relative accuracy where 1 + erf(x/√2) (torch's fp32 GELU) cancels to
-    # percent-level error at x ≈ -5; 5e-5 covers the fp32 GEMM's own rounding of the pre-activation × |d ln g/dx|
-    assert ((y32[neg].double() - g_ref[neg]).abs() <= 5e-5 * g_ref[neg].abs() + 1e-30).all()
+    # tail precision on EXACT pre-activations (one-hot rows pick bf16 weights, so the GEMM adds no rounding):
+    # the erfc form keeps ~2e-6 relative accuracy down to x = -9, where 1 + erf(x/√2) (torch's fp32 GELU) has
+    # already cancelled to percent-level error at x ≈ -5
+    Kx = 64
+    onehot = torch.zeros(Kx, Kx, device=DEV)
+    onehot[torch.arange(Kx), torch.arange(Kx)] = 1.0
+    xs = torch.linspace(-9.0, 3.0, 256 * Kx, device=DEV).bfloat16().view(256, Kx)
+    yt = torch.empty(Kx, 256, device=DEV)
+    gt = torch.empty(Kx, 256, device=DEV)
+    K().gemm(0, onehot.bfloat16(), xs, yt, act=L().ACT_GELU_SAVEGRAD, aux_out=gt)
+    gx, gpx = _gelu_ref(xs.double().T)
+    assert ((yt.double() - gx).abs() <= 2e-5 * gx.abs() + 1e-30).all()
+    assert ((gt.double() - gpx).abs() <= 2e-5 * gpx.abs() + 1e-6).all()
     # backward against the saved derivative
     dy = torch.randn(M, N, device=DEV).bfloat16()
     w2 = (torch.randn(N, Kd, device=DEV) / 8).bfloat16()

@@ -33,7 +33,8 @@ def main():
               ('dgrad_fc1', 1, 50176, 768, 3072), ('wgrad_fc1', 2, 3072, 768, 50176)]
     only = sys.argv[1].split(',') if len(sys.argv) > 1 else None
     modes = [int(x) for x in sys.argv[2].split(',')] if len(sys.argv) > 2 else [0, 3, 4, 5, 6]
-    tags = {0: 'full', 1: 'dma_only', 2: 'mfma_only', 3: 'epi_only', 4: 'no_epi', 5: 'stage_only', 6: 'plain_store'}
+    tags = {0: 'full', 1: 'dma_only', 2: 'mfma_only', 3: 'epi_only', 4: 'no_epi', 5: 'stage_only', 6: 'plain_store',
+            7: 'no_dma', 8: 'spread_no_epi'}
     for name, layout, M, N, K in shapes:
         if only and name not in only:
             continue
