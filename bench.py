@@ -63,6 +63,8 @@ def parse():
     ap.add_argument('--cpu-batch', type=int, default=2)
     ap.add_argument('--cpu-steps', type=int, default=2)
     ap.add_argument('--no-trace', action='store_true')
+    ap.add_argument('--imu-stream', choices=['side', 'main'], default='side',
+                    help='run the IMU branch on its own HIP stream (overlapping the video branch) or on the main one')
     return ap.parse_args()
 
 
@@ -146,6 +148,7 @@ def main():
         warnings.simplefilter('ignore')          # hub checkpoint not fetchable offline → random init
         model = CrossModalModel(make_cfg())
     model = model.to(dev).train()
+    model.overlap_imu = args.imu_stream == 'side'
     backbone = model.video_encoder.backbone
     cdist.broadcast_parameters(model)
     reducer = cdist.GradReducer(model, backbone=backbone)

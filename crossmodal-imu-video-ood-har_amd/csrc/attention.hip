@@ -189,14 +189,20 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_bf16(int H, int Lq, int Lk, i
 #pragma unroll
         for (int r = 0; r < 16; ++r) mt = fmaxf(mt, s[j][kb][r]);
       mt = fmaxf(mt, xhalf(mt)) * c;
-      const float mn = fmaxf(m[j], mt);
-      const float alpha = fexp2(m[j] - mn);
-      m[j] = mn;
-      l[j] *= alpha;
+      // Lazy rescale: the running max m only moves (and O, l are rescaled) when some row's tile max exceeds it by
+      // more than 8 (log2 units), so p = exp2(c·s − m) ≤ 2^8 stays well inside fp32/bf16 range; with the row
+      // maxima settling after the first key tiles this skips ~all rescales (64 v_mul per tile per wave).
+      if (__builtin_amdgcn_ballot_w64(mt > m[j] + 8.f) != 0) {
+        const float mn = fmaxf(m[j], mt);
+        const float alpha = fexp2(m[j] - mn);
+        m[j] = mn;
+        l[j] *= alpha;
 #pragma unroll
-      for (int d = 0; d < 2; ++d)
+        for (int d = 0; d < 2; ++d)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) o[j][d][r] *= alpha;
+          for (int r = 0; r < 16; ++r) o[j][d][r] *= alpha;
+      }
+      const float mn = m[j];
 #pragma unroll
       for (int kb = 0; kb < 2; ++kb) {
 #pragma unroll

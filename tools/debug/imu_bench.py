@@ -1,0 +1,44 @@
+"""IMU branch alone (encoder + projection head + normalize, fwd+bwd) at the bench shape B=32, 6x200.
+python tools/debug/imu_bench.py  (run under rocprofv3 --kernel-trace --stats for the per-kernel split)"""
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), '..', '..',
+                                'crossmodal-imu-video-ood-har_amd'))
+from cmhar.config import Config  # noqa: E402
+from cmhar.models import CrossModalModel  # noqa: E402
+
+
+def main():
+    cfg = Config()
+    cfg.data.video_frames_per_window = 4
+    cfg.data.video_resize = (32, 32)
+    cfg.model.video_backbone = '/nonexistent'
+    cfg.model.videomae_hidden_size, cfg.model.videomae_num_layers = 64, 1
+    cfg.model.videomae_num_heads, cfg.model.videomae_intermediate_size = 1, 64
+    import warnings
+    with warnings.catch_warnings():
+        warnings.simplefilter('ignore')
+        model = CrossModalModel(cfg).cuda().train()
+    imu = torch.randn(32, 6, 200, device='cuda')
+
+    def step():
+        a = model._imu_branch(imu)
+        a.sum().backward()
+
+    for _ in range(3):
+        step()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(10):
+        step()
+    e1.record()
+    torch.cuda.synchronize()
+    print(f'IMU branch fwd+bwd: {e0.elapsed_time(e1) / 10 * 1e3:.1f} us', flush=True)
+
+
+if __name__ == '__main__':
+    main()
