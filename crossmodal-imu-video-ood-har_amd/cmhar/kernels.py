@@ -285,7 +285,7 @@ def attention_bwd(q, k, v, o, do, lse, dq, dk, dv, *, B, H, Lq, Lk, D, scale, pd
     call('cmhar_attention_bwd', dt, B, H, Lq, Lk, D, ptr(q), q.stride(0), ptr(k), k.stride(0), ptr(v), v.stride(0),
          ptr(o), o.stride(0), ptr(do), do.stride(0), ptr(lse), ptr(delta), ptr(dq), dq.stride(0), ptr(dk),
          dk.stride(0), ptr(dv), dv.stride(0), scale, pdrop, seed, L.stream(q.device))
-    TRACE.end(ev, 'attn_bwd_bf16(delta+dq+dkdv)', 14 * B * H * Lq * Lk * D, 2 * (6 * B * Lq + 4 * B * Lk) * H * D)
+    TRACE.end(ev, 'attn_bwd_bf16(dq+delta,dkdv)', 14 * B * H * Lq * Lk * D, 2 * (6 * B * Lq + 4 * B * Lk) * H * D)
 
 
 # ------------------------------------------------------------------------------------------------------------

@@ -255,27 +255,6 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_bf16(int H, int Lq, int Lk, i
   }
 }
 
-// δ[q] = Σ_d dO[q,d]·O[q,d] per (b, h, q); one wave per 64 queries x 1 head... simple: one thread per (q, head).
-__global__ void attn_bwd_delta(int H, int Lq, const bf16* __restrict__ O, long ldo, const bf16* __restrict__ dO,
-                               long lddo, float* __restrict__ delta, int B) {
-  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  const long total = (long)B * H * Lq;
-  if (idx >= total) return;
-  const int q = idx % Lq;
-  const int hd = (idx / Lq) % H;
-  const int b = idx / ((long)Lq * H);
-  const bf16* o = O + ((long)b * Lq + q) * ldo + hd * 64;
-  const bf16* g = dO + ((long)b * Lq + q) * lddo + hd * 64;
-  float s = 0.f;
-#pragma unroll
-  for (int c = 0; c < 8; ++c) {
-    const bf16x8 a = *(const bf16x8*)(o + 8 * c), d = *(const bf16x8*)(g + 8 * c);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) s += (float)a[j] * (float)d[j];
-  }
-  delta[idx] = s;   // layout [(b*H + h)*Lq + q]
-}
-
 // dK, dV: one wave = 32 keys (K, V fragments in registers as B operands), q tiles of 64 staged in LDS.
 __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_bf16(int H, int Lq, int Lk, const bf16* __restrict__ Q,
                                                              long ldq, const bf16* __restrict__ K, long ldk,
@@ -393,12 +372,15 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_bf16(int H, int Lq, int 
 }
 
 // dQ: one wave = 32 queries (Q, dO fragments in registers), K/V tiles of 64 keys in LDS.
+// δ = rowsum(dO ∘ O) is computed here from the query rows this wave owns anyway (no separate pass over O and dO)
+// and written for the dK/dV kernel, which runs after this one on the same stream.
 __global__ __launch_bounds__(256, 2) void attn_bwd_dq_bf16(int H, int Lq, int Lk, const bf16* __restrict__ Q, long ldq,
                                                            const bf16* __restrict__ K, long ldk,
                                                            const bf16* __restrict__ V, long ldv,
+                                                           const bf16* __restrict__ O, long ldo,
                                                            const bf16* __restrict__ dO, long lddo,
                                                            const float* __restrict__ lse,
-                                                           const float* __restrict__ delta, bf16* __restrict__ dQ,
+                                                           float* __restrict__ delta, bf16* __restrict__ dQ,
                                                            long lddq, float scale) {
   __shared__ __attribute__((aligned(16))) char smem[4 * 8192];
 #define Ks(buf) (smem + 8192 * (buf))
@@ -418,7 +400,15 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_bf16(int H, int Lq, int Lk
     gf[t] = *(const bf16x8*)(dO + ((long)b * Lq + myq) * lddo + hd * 64 + 16 * t + 8 * h);
   }
   const float L2 = lse[((long)b * H + hd) * Lq + myq];
-  const float Dl = delta[((long)b * H + hd) * Lq + myq];
+  float Dl = 0.f;
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const bf16x8 ov = *(const bf16x8*)(O + ((long)b * Lq + myq) * ldo + hd * 64 + 16 * t + 8 * h);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) Dl = fmaf((float)gf[t][j], (float)ov[j], Dl);
+  }
+  Dl += xhalf(Dl);
+  if (h == 0 && q0 + (lane & 31) < Lq) delta[((long)b * H + hd) * Lq + myq] = Dl;
   floatx16 dq[2];
 #pragma unroll
   for (int d = 0; d < 2; ++d)
@@ -706,11 +696,10 @@ extern "C" int cmhar_attention_bwd(int dtype, int B, int H, int Lq, int Lk, int 
                                    unsigned long long seed, hipStream_t st) {
   if (B <= 0 || Lq <= 0) return 0;
   if (dtype == CMHAR_BF16 && D == 64 && pdrop == 0.f) {
-    const long n = (long)B * H * Lq;
-    attn_bwd_delta<<<cdiv(n, 256), 256, 0, st>>>(H, Lq, (const bf16*)O, ldo, (const bf16*)dO, lddo, delta, B);
     attn_bwd_dq_bf16<<<dim3(cdiv(Lq, 128), H, B), 256, 0, st>>>(H, Lq, Lk, (const bf16*)Q, ldq, (const bf16*)K, ldk,
-                                                                (const bf16*)V, ldv, (const bf16*)dO, lddo, lse, delta,
-                                                                (bf16*)dQ, lddq, scale);
+                                                                (const bf16*)V, ldv, (const bf16*)O, ldo,
+                                                                (const bf16*)dO, lddo, lse, delta, (bf16*)dQ, lddq,
+                                                                scale);
     attn_bwd_dkdv_bf16<<<dim3(cdiv(Lk, 128), H, B), 256, 0, st>>>(H, Lq, Lk, (const bf16*)Q, ldq, (const bf16*)K, ldk,
                                                                   (const bf16*)V, ldv, (const bf16*)dO, lddo, lse,
                                                                   delta, (bf16*)dK, lddk, (bf16*)dV, lddv, scale);

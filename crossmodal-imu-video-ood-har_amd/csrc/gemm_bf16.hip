@@ -179,14 +179,15 @@ template <bool A_KC, bool B_KC, typename OutT, bool BOUNDS>
 __global__ __launch_bounds__(NT, 2) void gemm_bf16_kernel(int M, int N, int K, const bf16* __restrict__ A, long lda,
                                                           const bf16* __restrict__ B, long ldb,
                                                           OutT* __restrict__ C, long ldc, Epilogue e, int klen,
-                                                          long split_stride, int raw_out) {
+                                                          long split_stride, int raw_out, int row0 = 0) {
   __shared__ __attribute__((aligned(16))) char smem[SMEM_BYTES];
   // stage buffers: A at smem + 16K*buf, B at smem + 32K + 16K*buf
 #define As(buf) (smem + 16384 * (buf))
 #define Bs(buf) (smem + 32768 + 16384 * (buf))
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wr = wave >> 1, wc = wave & 1;
-  const int tiles_n = (N + BN - 1) / BN, tiles_m = (M + BM - 1) / BM;
+  // row0: this launch covers output rows row0 .. M-1 only (the tail rows after a 256² launch over the full rounds)
+  const int tiles_n = (N + BN - 1) / BN, tiles_m = (M - row0 + BM - 1) / BM;
   // split index folded into the XCD remap: one XCD runs whole splits, whose CUs then share each K-slice in L2
   const int ntile = tiles_m * tiles_n;
   const int rlin = xcd_remap(blockIdx.x + ntile * blockIdx.z, ntile * gridDim.z);
@@ -194,7 +195,7 @@ __global__ __launch_bounds__(NT, 2) void gemm_bf16_kernel(int M, int N, int K, c
   // row-major tile order: the blocks an XCD runs together share A row panels while the whole (small) weight
   // matrix stays resident in that XCD's L2 — activations are streamed from HBM once
   const int tm = bid / tiles_n, tn = bid % tiles_n;
-  const int bm = tm * BM, bn = tn * BN;
+  const int bm = row0 + tm * BM, bn = tn * BN;
   const int kbeg = split * klen;
   const int kend = min(K, kbeg + klen);
   C += (long)split * split_stride;
@@ -599,7 +600,8 @@ static TailSplit tail_split(int M, int N, int K) {
   const int n_dp = (ntile / kCUs) * kCUs / tiles_n * tiles_n; // row-aligned
   const int n_tail = ntile - n_dp;
   // the split partials cost a write + read of n_tail tiles of fp32 per split: only worth it when the tail tiles'
-  // K loop is long (measured on MI355X: N = 768 at K = 3072 / 2304 gains ~30 us, at K = 768 it loses ~30 us)
+  // K loop is long (measured on MI355X: N = 768 at K = 3072 / 2304 gains ~30 us, at K = 768 it loses ~30 us; running
+  // the K = 768 tail rows as 128² tiles in a second launch instead measured neutral)
   if (K < 2048) return t;
   int s = kCUs / n_tail;
   s = min(s, K / TK2 / 4);                                    // ≥ 4 K-tiles per split

@@ -80,12 +80,14 @@ def test_gemm_bf16_splitk_exact(layout):
 
 
 @pytest.mark.parametrize('layout', [0, 1])
-def test_gemm_bf16_tail_split_exact(layout):
-    """260 output tiles of 256²: two full chip rounds run whole-K, the last tile rows are split along K and reduced
-    with the epilogue (bias + residual at the right rows).  Integer operands: bit-exact."""
+@pytest.mark.parametrize('Kd', [1024, 2048])
+def test_gemm_bf16_tail_split_exact(layout, Kd):
+    """260 output tiles of 256²: two full chip rounds run whole-K; the last tile rows are split along K and reduced
+    with the epilogue (K = 2048; K = 1024 stays one whole-K launch) — bias + residual must land on
+    the right rows.  Integer operands: bit-exact."""
     from cmhar import _lib
-    M, N, Kd = 256 * 130, 512, 2048
-    assert _lib.lib().cmhar_gemm_bf16_ws(M, N, Kd) > 0
+    M, N = 256 * 130, 512
+    assert (_lib.lib().cmhar_gemm_bf16_ws(M, N, Kd) > 0) == (Kd >= 2048)   # K = 1024: plain whole-K launch
     a, b = _operands(layout, M, N, Kd, lambda s, sd: _ints(s, -2, 3, seed=sd), torch.bfloat16)
     bias = _ints((N,), seed=7).to(DEV)
     res = _ints((M, N), seed=8).to(DEV)
