@@ -130,7 +130,10 @@ def main():
     from cmhar.models import CrossModalModel
     from cmhar.optim import FusedAdamW, clip_grad_norm_
 
-    rank, world, local = cdist.init_from_env()
+    # CMHAR_BENCH_BACKEND / CMHAR_BENCH_DEVICE: rehearsal knobs only (e.g. two gloo ranks sharing the one GPU of a
+    # test box); the measured configuration is one RCCL rank per GPU
+    rank, world, local = cdist.init_from_env(os.environ.get('CMHAR_BENCH_BACKEND') or None)
+    local = int(os.environ.get('CMHAR_BENCH_DEVICE', local))
     torch.cuda.set_device(local)
     dev = torch.device('cuda', local)
 
