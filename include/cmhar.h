@@ -61,14 +61,6 @@ int cmhar_gemm_bf16(int layout, int out_dtype, int M, int N, int K, const void* 
  * with the epilogue).  0 = no workspace needed; a call with ws == NULL always runs whole-K. */
 long cmhar_gemm_bf16_ws(int M, int N, int K);
 
-/* Persistent two-workgroups-per-CU variant of cmhar_gemm_bf16 (same layouts, epilogue, split-K workspace) whose
- * epilogues overlap the K loop of the CU's other workgroup.  Handles M % 256 == 0, N % 128 == 0, K (per split)
- * % 32 == 0 and returns 1; returns 0 (nothing launched) for other shapes, negative on error.  delay_cycles:
- * start offset of each CU's second workgroup (0 = none). */
-int cmhar_gemm_pp(int layout, int out_dtype, int M, int N, int K, const void* A, long lda, const void* B, long ldb,
-                  void* C, long ldc, const CmharEpilogue* epi, int splits, void* ws, int delay_cycles,
-                  hipStream_t stream);
-
 /* Exact-fp32 (or mixed) strided batched GEMM: C[z][m,n] = epi(Σ_k A[z][m*sam+k*sak] B[z][k*sbk+n*sbn])
  * (replaces: the fp32 nn.Linear / IMU encoder / ProjectionHead matmuls, models.py:16-132, 221-234). */
 int cmhar_gemm_generic(int in_dtype, int out_dtype, int M, int N, int K, int batch, const void* A, long sam,

@@ -1,3 +1,8 @@
+// EXPERIMENT (not part of the product library; built into tools/debug/libablate_pp.so by gemm_pp_ablate.hip).
+// Outcome on MI355X: at parity with the 256² kernel on forward shapes, slower on dgrad / wgrad — the 256x128 tile
+// needs 1.5x the L2→LDS bytes per FLOP and the K loop of both kernels is bound by that LDS-DMA stream (no-DMA
+// ablations run at 1.4-1.8 PFLOP/s), so the overlapped epilogue buys nothing.  Kept for the record and the tools.
+//
 // Persistent "ping-pong" bf16 MFMA GEMM for gfx950: the VideoMAE Linear hot path with the epilogue hidden under MFMA.
 //
 // Why: the 256x256 one-workgroup-per-CU kernel (gemm_bf16.hip) runs its K loop at ~1250 TFLOP/s, but every
@@ -16,7 +21,7 @@
 //
 // Layouts as gemm_bf16.hip: A_KC = A is K-contiguous ([M][K]) else M-contiguous ([K][M]); B_KC likewise for B.
 // Split-K: units = splits x tiles; raw fp32 partial slabs (+ bias row-sum slabs) reduced by splitk_reduce.
-#include "common.h"
+#include "../../crossmodal-imu-video-ood-har_amd/csrc/common.h"
 
 namespace {
 

@@ -1,6 +1,6 @@
 // Ablation build of the ping-pong GEMM (NOT part of the product library).
 //   hipcc --offload-arch=gfx950 -O3 -shared -fPIC -I include tools/debug/gemm_pp_ablate.hip -o tools/debug/libablate_pp.so
-#include "../../crossmodal-imu-video-ood-har_amd/csrc/gemm_pp.hip"
+#include "gemm_pp.hip"
 
 extern "C" int ablate_pp(int mode, int act, int M, int N, int K, const void* A, long lda, const void* B, long ldb,
                          void* C, long ldc, void* aux, void* stamps, int delay, hipStream_t st) {

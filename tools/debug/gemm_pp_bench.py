@@ -11,6 +11,10 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), '..'
 from cmhar import _lib as L  # noqa: E402
 from cmhar import kernels as K  # noqa: E402
 
+_PP = C.CDLL(os.path.join(os.path.dirname(os.path.abspath(__file__)), 'libablate_pp.so'))
+_PP.cmhar_gemm_pp.argtypes = [C.c_int] * 5 + [C.c_void_p, C.c_long, C.c_void_p, C.c_long, C.c_void_p, C.c_long,
+                                             C.POINTER(L.Epilogue), C.c_int, C.c_void_p, C.c_int, C.c_void_p]
+
 
 def run(fn, reps=20):
     for _ in range(3):
@@ -35,7 +39,7 @@ def pp(layout, a, b, out, delay, splits=1, **kw):
     epi = L.epilogue(kw.get('bias'), kw.get('residual'), kw.get('aux_in'), kw.get('aux_out'), None, 1,
                      kw.get('act', 0), 1.0, kw.get('beta', 0.0), 0.0, 0, kw.get('rowsum'), kw.get('rowsum_beta', 0.0))
     ws = K.workspace(splits * M * N + splits * M, out.device) if splits > 1 else None
-    rc = L.lib().cmhar_gemm_pp(layout, L.dtype_code(out.dtype), M, N, Kd, a.data_ptr(), a.stride(0), b.data_ptr(),
+    rc = _PP.cmhar_gemm_pp(layout, L.dtype_code(out.dtype), M, N, Kd, a.data_ptr(), a.stride(0), b.data_ptr(),
                                b.stride(0), out.data_ptr(), out.stride(0), C.byref(epi), splits, L.ptr(ws), delay,
                                L.stream(out.device))
     assert rc == 1, rc
