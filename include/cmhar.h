@@ -135,6 +135,12 @@ int cmhar_imu_embed_bwd(int B, int C, int L, int N, int P, int S, int D, int T, 
 int cmhar_copy2d(int in_dtype, int out_dtype, int rows, int cols, const void* src, long lds, void* dst, long ldd,
                  float alpha, float beta, float pdrop, unsigned long long seed, hipStream_t stream);
 
+/* Energy-score OOD head over classifier logits [N, C] (row stride ld): pred[i] = first argmax, maxlogit[i],
+ * energy[i] = -T * logsumexp(logits[i] / T)  (no reference counterpart — SURVEY §8(f) rank 1; the logits are those
+ * of Evaluator.predict, src/eval/evaluator.py:28-53).  Outputs are nullable. */
+int cmhar_logits_energy(int dtype, int N, int C, const void* logits, long ld, float temperature, int* pred,
+                        float* energy, float* maxlogit, hipStream_t stream);
+
 /* Multi-tensor optimizer (replaces: torch.nn.utils.clip_grad_norm_ and torch.optim.AdamW.step,
  * trainer.py:74-78,140-141).  tens/chunks: DEVICE arrays of
  *   struct { float* p; const float* g; float* m; float* v; bf16* p_bf16; float* p_copy; long n; float wd;

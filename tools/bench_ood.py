@@ -1,0 +1,77 @@
+"""BASELINE config 5: OOD evaluation stream — energy score over the cross-modal ("fused") logits of a 10k-clip
+synthetic stream, inference only (no autograd), bf16 MFMA compute (the fp16 of the config: same MFMA rate and
+width on gfx950; the model's trained weights are bf16-packed).
+
+Per batch of 32 clips: CrossModalModel.forward(imu, video) in eval mode → imu_proj, video_proj (unit rows) →
+logits S = exp(t)·imu_proj·video_projᵀ + bias (the SigLIP logits of src/models/losses.py:37-41, one row per IMU
+clip over the batch's video clips) → per-row prediction + energy E = −logsumexp(S) (cmhar_logits_energy).
+Prints one JSON line: clips/s and the energy-score kernel's share.   python tools/bench_ood.py [--clips 10000]
+"""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+import warnings
+
+import torch
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, 'crossmodal-imu-video-ood-har_amd'))
+from cmhar import kernels as K  # noqa: E402
+from cmhar.config import Config  # noqa: E402
+from cmhar.models import CrossModalModel  # noqa: E402
+from cmhar.ood import logits_energy  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--clips', type=int, default=10000)
+    ap.add_argument('--batch', type=int, default=32)
+    args = ap.parse_args()
+    dev = torch.device('cuda')
+    cfg = Config()
+    cfg.model.compute_dtype = 'bf16'
+    torch.manual_seed(0)
+    with warnings.catch_warnings():
+        warnings.simplefilter('ignore')
+        model = CrossModalModel(cfg).to(dev).eval()
+    B = args.batch
+    g = torch.Generator(device=dev).manual_seed(5)
+    video = torch.randn(B, 16, 3, 224, 224, device=dev, generator=g)
+    imu = torch.randn(B, 6, 200, device=dev, generator=g)
+    scale = math.exp(math.log(10.0))
+    bias = torch.full((B,), -10.0, device=dev)
+    S = torch.empty(B, B, device=dev)
+    nb = math.ceil(args.clips / B)
+
+    def batch():
+        a, b = model(imu, video)
+        K.gemm(0, a, b, S, bias=bias, alpha=scale)
+        return logits_energy(S)
+
+    with torch.no_grad():
+        for _ in range(3):
+            batch()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(nb):
+            pred, energy, _ = batch()
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(100):
+            logits_energy(S)
+        e1.record()
+        torch.cuda.synchronize()
+    print(json.dumps({'metric': 'clips/sec OOD energy-score eval stream (16x224^2 video + 6x200 IMU)',
+                      'value': round(nb * B / dt, 1), 'unit': 'clips/sec', 'clips': nb * B, 'batch': B,
+                      'dtype': 'bf16', 'ms_per_batch': round(1e3 * dt / nb, 3),
+                      'energy_kernel_us': round(e0.elapsed_time(e1) * 10, 2),
+                      'energy_mean': float(energy.mean()), 'pred_sample': pred[:8].tolist()}))
+
+
+if __name__ == '__main__':
+    main()
