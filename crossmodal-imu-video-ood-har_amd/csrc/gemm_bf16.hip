@@ -379,13 +379,16 @@ __device__ __forceinline__ bf16x8 frag256(const char* lds, int r0, int kk, int l
 // MODE (ablation builds only, tools/debug): 0 = product; 3 = epilogue only (no K loop); 4 = K loop only (no
 // epilogue); 5 = LDS staging only; 6 = staging + plain bf16 stores; 7 = K loop without the LDS-DMA (stale
 // operands), no epilogue; 8 = K loop with the DMA pieces spread between the MFMAs, no epilogue.
-template <bool A_KC, bool B_KC, typename OutT, int MODE = 0>
+// NA: A-operand LDS buffers.  2 = tile k+1 streams in while tile k is consumed (A and B double-buffered, 128 KiB);
+// 3 = the A tile (the HBM-streamed activation panel) is fetched TWO tiles ahead — three 32 KiB A buffers + two
+// 32 KiB B buffers = the whole 160 KiB LDS — so its longer HBM/MALL latency has two K-tiles of MFMAs to hide under.
+template <bool A_KC, bool B_KC, typename OutT, int MODE = 0, int NA = 2>
 __global__ __launch_bounds__(NT2, 2) void gemm256_kernel(int M, int N, int K, const bf16* __restrict__ A, long lda,
                                                          const bf16* __restrict__ B, long ldb, OutT* __restrict__ C,
                                                          long ldc, Epilogue e, int klen, long split_stride,
                                                          int raw_out, float* __restrict__ sk_ws, int n_dp,
                                                          int sk_klen) {
-  __shared__ __attribute__((aligned(16))) char smem[SMEM2];
+  __shared__ __attribute__((aligned(16))) char smem[NA == 3 ? 163840 : SMEM2];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = wave >> 2, wc = wave & 3;
@@ -457,33 +460,43 @@ __global__ __launch_bounds__(NT2, 2) void gemm256_kernel(int M, int N, int K, co
     for (int i = 0; i < 8; ++i)
       if (i >= i_lo && i < i_hi) af[i] = frag256<A_KC>(a_s, wr * 128 + i * 16, 0, lane);
   };
+  auto a_buf = [&](int t) -> char* { return NA == 3 ? smem + (t % 3) * 32768 : smem + (t & 1) * 65536; };
+  auto b_buf = [&](int t) -> char* { return NA == 3 ? smem + 98304 + (t & 1) * 32768 : smem + (t & 1) * 65536 + 32768; };
   if (nk > 0) {
     if (MODE != 7) {
-      dma_tile<A_KC>(A, lda, bm, kbeg, smem, wave, lane);
-      dma_tile<B_KC>(B, ldb, bn, kbeg, smem + 32768, wave, lane);
+      dma_tile<A_KC>(A, lda, bm, kbeg, a_buf(0), wave, lane);
+      dma_tile<B_KC>(B, ldb, bn, kbeg, b_buf(0), wave, lane);
+      if (NA == 3 && nk > 1) dma_tile<A_KC>(A, lda, bm, kbeg + TK2, a_buf(1), wave, lane);
     }
-    __syncthreads();                                        // tile 0 landed
-    load_k0(smem, smem + 32768, 0, 8, true);
+    if (NA == 3 && nk > 1) asm volatile("s_waitcnt vmcnt(4)\n\ts_barrier" ::: "memory");   // tile 0 landed
+    else __syncthreads();
+    load_k0(a_buf(0), b_buf(0), 0, 8, true);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) bf1[j] = frag256<B_KC>(smem + 32768, wc * 64 + j * 16, 1, lane);
+    for (int j = 0; j < 4; ++j) bf1[j] = frag256<B_KC>(b_buf(0), wc * 64 + j * 16, 1, lane);
   }
   for (int kt = 0; kt < nk; ++kt) {
-    const char* a_s = smem + (kt & 1) * 65536;
-    const char* b_s = a_s + 32768;
+    const char* a_s = a_buf(kt);
     const bool more = kt + 1 < nk;
-    char* nxt = smem + ((kt + 1) & 1) * 65536;
-    if (more && MODE != 7 && MODE != 8) {
+    const bool more2 = NA == 3 && kt + 2 < nk;
+    char* nxt = a_buf(kt + 1);
+    char* nxt_b = b_buf(kt + 1);
+    if (NA == 3 && MODE != 7) {
+      // B(kt+1) first, A(kt+2) second: vmcnt counts in issue order, so waiting for B(kt+1) (and the A(kt+1) issued
+      // a tile earlier) can leave A(kt+2)'s 4 pieces in flight
+      if (more) dma_tile<B_KC>(B, ldb, bn, kbeg + (kt + 1) * TK2, nxt_b, wave, lane);
+      if (more2) dma_tile<A_KC>(A, lda, bm, kbeg + (kt + 2) * TK2, a_buf(kt + 2), wave, lane);
+    } else if (more && MODE != 7 && MODE != 8) {
       dma_tile<A_KC>(A, lda, bm, kbeg + (kt + 1) * TK2, nxt, wave, lane);
-      dma_tile<B_KC>(B, ldb, bn, kbeg + (kt + 1) * TK2, nxt + 32768, wave, lane);
+      dma_tile<B_KC>(B, ldb, bn, kbeg + (kt + 1) * TK2, nxt_b, wave, lane);
     }
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bf0[j], acc[i][j], 0, 0, 0);
-      if (MODE == 8 && more) {   // one DMA piece per 4 MFMAs: the issue cost interleaves with the matrix pipe
+      if (MODE == 8 && NA == 2 && more) {   // one DMA piece per 4 MFMAs: the issue cost interleaves with the MFMAs
         if (i < 4) dma_piece<A_KC>(A, lda, bm, kbeg + (kt + 1) * TK2, nxt, wave, lane, i);
-        else dma_piece<B_KC>(B, ldb, bn, kbeg + (kt + 1) * TK2, nxt + 32768, wave, lane, i - 4);
+        else dma_piece<B_KC>(B, ldb, bn, kbeg + (kt + 1) * TK2, nxt_b, wave, lane, i - 4);
       }
       if (!A_KC && rs && wc == (i >> 1))
         accb[i & 1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], ones, accb[i & 1], 0, 0, 0);
@@ -500,8 +513,9 @@ __global__ __launch_bounds__(NT2, 2) void gemm256_kernel(int M, int N, int K, co
     __builtin_amdgcn_sched_barrier(0);
     if (more) {
       // own DMA of tile kt+1 landed, own reads of tile kt returned; then everyone's
-      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-      load_k0(nxt, nxt + 32768, 0, 4, true);               // slots 0-3 and bf0 are free now
+      if (more2) asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      load_k0(nxt, nxt_b, 0, 4, true);                     // slots 0-3 and bf0 are free now
     }
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -515,7 +529,7 @@ __global__ __launch_bounds__(NT2, 2) void gemm256_kernel(int M, int N, int K, co
     }
     if (more) {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) bf1[j] = frag256<B_KC>(nxt + 32768, wc * 64 + j * 16, 1, lane);
+      for (int j = 0; j < 4; ++j) bf1[j] = frag256<B_KC>(nxt_b, wc * 64 + j * 16, 1, lane);
     }
   }
   if (!A_KC && rs && (lane & 15) == 0) {       // every column of a ones-product holds the row sum: lanes 0,16,32,48
@@ -618,6 +632,9 @@ static TailSplit tail_split(int M, int N, int K) {
 template <bool AK, bool BKc, typename OutT>
 int launch(int M, int N, int K, const bf16* A, long lda, const bf16* B, long ldb, OutT* C, long ldc,
            const Epilogue& e, int splits, float* ws, hipStream_t st) {
+  // triple-buffered A for the forward / dgrad layouts (7-14 % faster, tools/debug/gemm_ablate.py mode 9); the
+  // weight-gradient layout (both operands row-contraction) runs out of registers with it and keeps two buffers
+  constexpr int kNA = AK ? 3 : 2;
   const long ss = (long)M * N;
   if (splits > 1 && !ws) return -2;
   const bool big = M % TM2 == 0 && N % TN2 == 0 && K % TK2 == 0;
@@ -629,15 +646,15 @@ int launch(int M, int N, int K, const bf16* A, long lda, const bf16* B, long ldb
     dim3 grid((M / TM2) * (N / TN2), 1, nsplit);
     const TailSplit ts = tail_split(M, N, K);
     if (nsplit == 1 && ws && ts.n_dp > 0 && !e.rowsum) {
-      gemm256_kernel<AK, BKc, OutT><<<ts.n_dp + ts.n_sk, NT2, 0, st>>>(M, N, K, A, lda, B, ldb, C, ldc, e, K, 0, 0, ws,
+      gemm256_kernel<AK, BKc, OutT, 0, kNA><<<ts.n_dp + ts.n_sk, NT2, 0, st>>>(M, N, K, A, lda, B, ldb, C, ldc, e, K, 0, 0, ws,
                                                                       ts.n_dp, ts.sk_klen);
       const int tail_rows = M - ts.tail_m0;
       splitk_reduce_kernel<OutT><<<reduce_blocks(tail_rows, N), 256, 0, st>>>(
           tail_rows, N, ts.nsplit, ws, (long)tail_rows * N, C, ldc, e, ts.tail_m0);
     } else if (nsplit == 1) {
-      gemm256_kernel<AK, BKc, OutT><<<grid, NT2, 0, st>>>(M, N, K, A, lda, B, ldb, C, ldc, e, klen, 0, 0, nullptr, 0, 0);
+      gemm256_kernel<AK, BKc, OutT, 0, kNA><<<grid, NT2, 0, st>>>(M, N, K, A, lda, B, ldb, C, ldc, e, klen, 0, 0, nullptr, 0, 0);
     } else {
-      gemm256_kernel<AK, BKc, float><<<grid, NT2, 0, st>>>(M, N, K, A, lda, B, ldb, ws, N, e, klen, ss, 1, nullptr, 0,
+      gemm256_kernel<AK, BKc, float, 0, kNA><<<grid, NT2, 0, st>>>(M, N, K, A, lda, B, ldb, ws, N, e, klen, ss, 1, nullptr, 0,
                                                            0);
       splitk_reduce_kernel<OutT><<<reduce_blocks(M, N), 256, 0, st>>>(M, N, nsplit, ws, ss, C, ldc, e);
     }

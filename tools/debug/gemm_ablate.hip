@@ -16,7 +16,12 @@ extern "C" int ablate_gemm256(int mode, int layout, int M, int N, int K, const v
 #define G(AK, BK, MD) gemm256_kernel<AK, BK, bf16, MD><<<grid, NT2, 0, st>>>(M, N, K, a, lda, b, ldb, c, ldc, e, K, 0, 0, nullptr, 0, 0)
 #define L3(AK, BK) if (mode == 0) G(AK, BK, 0); \
   else if (mode == 3) G(AK, BK, 3); else if (mode == 4) G(AK, BK, 4); \
-  else if (mode == 5) G(AK, BK, 5); else if (mode == 7) G(AK, BK, 7); else if (mode == 8) G(AK, BK, 8); else G(AK, BK, 6);
+  else if (mode == 5) G(AK, BK, 5); else if (mode == 7) G(AK, BK, 7); else if (mode == 8) G(AK, BK, 8); \
+  else if (mode == 9) gemm256_kernel<AK, BK, bf16, 0, 3><<<grid, NT2, 0, st>>>(M, N, K, a, lda, b, ldb, c, ldc, e, K, 0, \
+                                                                           0, nullptr, 0, 0); \
+  else if (mode == 10) gemm256_kernel<AK, BK, bf16, 4, 3><<<grid, NT2, 0, st>>>(M, N, K, a, lda, b, ldb, c, ldc, e, K, \
+                                                                            0, 0, nullptr, 0, 0); \
+  else G(AK, BK, 6);
   if (layout == 0) { L3(true, true) } else if (layout == 1) { L3(true, false) } else { L3(false, false) }
   return (int)hipGetLastError();
 }

@@ -34,7 +34,7 @@ def main():
     only = sys.argv[1].split(',') if len(sys.argv) > 1 else None
     modes = [int(x) for x in sys.argv[2].split(',')] if len(sys.argv) > 2 else [0, 3, 4, 5, 6]
     tags = {0: 'full', 1: 'dma_only', 2: 'mfma_only', 3: 'epi_only', 4: 'no_epi', 5: 'stage_only', 6: 'plain_store',
-            7: 'no_dma', 8: 'spread_no_epi'}
+            7: 'no_dma', 8: 'spread_no_epi', 9: 'A3_full', 10: 'A3_no_epi'}
     for name, layout, M, N, K in shapes:
         if only and name not in only:
             continue
