@@ -57,6 +57,9 @@ _SIGS = {
                                   C.POINTER(vp), vp]),
     'cmhar_copy2d': (i32, [i32, i32, i32, i32, vp, i64, vp, i64, f32, f32, f32, u64, vp]),
     'cmhar_logits_energy': (i32, [i32, i32, i32, vp, i64, f32, vp, vp, vp, vp]),
+    'cmhar_cross_entropy_ws': (i64, [i32]),
+    'cmhar_cross_entropy': (i32, [i32, i32, vp, i64, i64, vp, i64, f32, f32, f32, i32, vp, vp, vp, vp, vp, vp, i64,
+                                  i64, f32, f32, vp, vp, vp]),
     'cmhar_mt_grad_norm': (i32, [vp, vp, i32, vp, vp, f32, i32, vp]),
     'cmhar_mt_adamw': (i32, [vp, vp, i32, f32, f32, f32, f32, f32, f32, f32, vp, vp]),
     'cmhar_mt_cast_bf16': (i32, [vp, vp, i32, vp]),

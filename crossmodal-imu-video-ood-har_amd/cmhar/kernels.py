@@ -370,6 +370,36 @@ def copy2d(src, dst, alpha=1.0, beta=0.0, pdrop=0.0, seed=0):
     return dst
 
 
+_REDUCTIONS = {'none': 0, 'mean': 1, 'sum': 2}
+
+
+def cross_entropy(logits, labels=None, *, ignore_index=-100, label_smoothing=0.0, gamma=0.0, alpha=1.0,
+                  reduction='mean', loss=None, row_loss=None, pred=None, correct=None, status=None, dlogits=None,
+                  grad_scale=1.0, grad_beta=0.0, g_up=None):
+    """Row-softmax cross-entropy family on a (possibly transposed) fp32 logit view [N, C] — see include/cmhar.h.
+    labels: int64 device [N] or None (= arange, InfoNCE).  dlogits may have its own strides (e.g. a transposed
+    view accumulated with grad_beta = 1)."""
+    if logits.dim() != 2 or logits.dtype != torch.float32 or not logits.is_cuda:
+        raise ValueError('logits: fp32 device matrix expected')
+    N, Cc = logits.shape
+    if labels is not None and (labels.dtype != torch.int64 or labels.shape != (N,) or not labels.is_contiguous()):
+        raise ValueError(f'labels: contiguous int64 [{N}] expected')
+    for t, n in ((row_loss, 'row_loss'), (pred, 'pred')):
+        if t is not None and (t.numel() != N or not t.is_contiguous()):
+            raise ValueError(f'{n}: [{N}] expected')
+    if dlogits is not None and (tuple(dlogits.shape) != (N, Cc) or dlogits.dtype != torch.float32):
+        raise ValueError('dlogits shape')
+    red = _REDUCTIONS[reduction]
+    if dlogits is not None and red == 0 and (g_up is None or g_up.numel() != N):
+        raise ValueError("reduction='none' needs per-row upstream gradients")
+    ws = workspace(L.lib().cmhar_cross_entropy_ws(N), logits.device)
+    call('cmhar_cross_entropy', N, Cc, ptr(logits), logits.stride(0), logits.stride(1), ptr(labels), ignore_index,
+         label_smoothing, gamma, alpha, red, ptr(loss), ptr(row_loss), ptr(pred), ptr(correct), ptr(status),
+         ptr(dlogits), dlogits.stride(0) if dlogits is not None else 0,
+         dlogits.stride(1) if dlogits is not None else 0, grad_scale, grad_beta, ptr(g_up), ptr(ws),
+         L.stream(logits.device))
+
+
 def tubelet_im2col(video, tub, P, out_dtype):
     if video.dtype != torch.float32 or video.dim() != 5 or not video.is_contiguous():
         raise ValueError('video must be a contiguous fp32 (B,T,C,H,W) tensor')

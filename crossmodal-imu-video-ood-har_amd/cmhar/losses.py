@@ -103,3 +103,160 @@ class SigmoidContrastiveLoss(nn.Module):
             from . import dist as _d
             group = _d.loss_group()
         return _SigLIPFn.apply(imu_embeds, video_embeds, self.temperature, self.bias, group)
+
+
+# ------------------------------------------------------------------------------------------------------------------
+# Cross-entropy family (reference src/models/losses.py:57-167 and the nn.CrossEntropyLoss of ClassificationTrainer,
+# src/train/trainer.py:249) on the fused row-softmax kernel `cmhar_cross_entropy`: forward = loss (+ argmax) in two
+# launches; backward = one more pass writing dlogits scaled by the incoming (device) gradient — no host sync.
+# ------------------------------------------------------------------------------------------------------------------
+def _labels_on(labels, device, C, ignore_index):
+    if labels.dtype not in (torch.int64, torch.int32, torch.int16, torch.uint8):
+        raise TypeError(f'expected integer class labels, got {labels.dtype}')
+    if not labels.is_cuda:                       # host labels (the DataLoader case): validate without a device sync
+        bad = (labels != ignore_index) & ((labels < 0) | (labels >= C))
+        if bool(bad.any()):
+            raise IndexError(f'Target {int(labels[bad][0])} is out of bounds.')
+    return labels.to(device=device, dtype=torch.int64, non_blocking=True).contiguous()
+
+
+class _CrossEntropyFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, logits, labels, ignore_index, eps, gamma, alpha, reduction):
+        z = logits.float() if logits.dtype != torch.float32 else logits
+        N = z.shape[0]
+        out = torch.empty((N,) if reduction == 'none' else (), dtype=torch.float32, device=z.device)
+        K.cross_entropy(z, labels, ignore_index=ignore_index, label_smoothing=eps, gamma=gamma, alpha=alpha,
+                        reduction=reduction, loss=None if reduction == 'none' else out,
+                        row_loss=out if reduction == 'none' else None)
+        ctx.save_for_backward(z, labels)
+        ctx.args = (ignore_index, eps, gamma, alpha, reduction, logits.dtype)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        z, labels = ctx.saved_tensors
+        ignore_index, eps, gamma, alpha, reduction, dt = ctx.args
+        dz = torch.empty_like(z)
+        K.cross_entropy(z, labels, ignore_index=ignore_index, label_smoothing=eps, gamma=gamma, alpha=alpha,
+                        reduction=reduction, dlogits=dz, g_up=g.contiguous().float())
+        return dz.to(dt), None, None, None, None, None, None
+
+
+def cross_entropy(logits, target, ignore_index=-100, reduction='mean', label_smoothing=0.0, *, gamma=0.0,
+                  alpha=1.0):
+    """F.cross_entropy for (N, C) logits and class-index targets (+ the focal weighting of FocalLoss)."""
+    if logits.dim() != 2:
+        raise ValueError(f'expected (N, C) logits, got {tuple(logits.shape)}')
+    if reduction not in ('none', 'mean', 'sum'):
+        raise ValueError(f'{reduction} is not a valid value for reduction')
+    labels = _labels_on(target, logits.device, logits.shape[1], ignore_index)
+    return _CrossEntropyFn.apply(logits, labels, int(ignore_index), float(label_smoothing), float(gamma),
+                                 float(alpha), reduction)
+
+
+class CrossEntropyLoss(nn.Module):
+    """nn.CrossEntropyLoss (class-index targets, no class weights) — ClassificationTrainer's loss (trainer.py:249)."""
+
+    def __init__(self, weight=None, ignore_index=-100, reduction='mean', label_smoothing=0.0):
+        super().__init__()
+        if weight is not None:
+            raise NotImplementedError('class weights are not used by the reference')
+        self.ignore_index = ignore_index
+        self.reduction = reduction
+        self.label_smoothing = label_smoothing
+
+    def forward(self, inputs, targets):
+        return cross_entropy(inputs, targets, self.ignore_index, self.reduction, self.label_smoothing)
+
+
+class FocalLoss(nn.Module):
+    """Reference losses.py:90-116: alpha·(1-pt)^gamma·CE, reduction mean / sum / none."""
+
+    def __init__(self, alpha=1.0, gamma=2.0, reduction='mean'):
+        super().__init__()
+        self.alpha = alpha
+        self.gamma = gamma
+        self.reduction = reduction
+
+    def forward(self, inputs, targets):
+        return cross_entropy(inputs, targets, reduction=self.reduction, gamma=self.gamma, alpha=self.alpha)
+
+
+class LabelSmoothingCrossEntropy(nn.Module):
+    """Reference losses.py:119-150: targets (1-eps)·onehot + eps/C against log_softmax."""
+
+    def __init__(self, epsilon=0.1, reduction='mean'):
+        super().__init__()
+        self.epsilon = epsilon
+        self.reduction = reduction
+
+    def forward(self, inputs, targets):
+        return cross_entropy(inputs, targets, reduction=self.reduction, label_smoothing=self.epsilon)
+
+
+class _InfoNCEFn(torch.autograd.Function):
+    """S = a·bᵀ/τ (fp32 GEMM), loss = (CE(S, arange) + CE(Sᵀ, arange))/2; the transposed CE reads S through a
+    (1, B) stride view and accumulates its gradient into the same dS buffer."""
+
+    @staticmethod
+    def forward(ctx, a, b, inv_t):
+        a = a.contiguous().float()
+        b = b.contiguous().float()
+        B = a.shape[0]
+        S = torch.empty(B, B, dtype=torch.float32, device=a.device)
+        K.gemm(0, a, b, S, alpha=inv_t)
+        l1 = torch.empty((), dtype=torch.float32, device=a.device)
+        l2 = torch.empty((), dtype=torch.float32, device=a.device)
+        K.cross_entropy(S, None, loss=l1)
+        K.cross_entropy(S.t(), None, loss=l2)
+        ctx.save_for_backward(a, b, S)
+        ctx.inv_t = inv_t
+        loss = torch.empty((), dtype=torch.float32, device=a.device)
+        K.copy2d(l1.view(1, 1), loss.view(1, 1), alpha=0.5)
+        K.copy2d(l2.view(1, 1), loss.view(1, 1), alpha=0.5, beta=1.0)
+        return loss
+
+    @staticmethod
+    def backward(ctx, g):
+        a, b, S = ctx.saved_tensors
+        g = g.reshape(1).contiguous().float()
+        dS = torch.empty_like(S)
+        K.cross_entropy(S, None, dlogits=dS, grad_scale=0.5, g_up=g)
+        K.cross_entropy(S.t(), None, dlogits=dS.t(), grad_scale=0.5, grad_beta=1.0, g_up=g)
+        da = db = None
+        if ctx.needs_input_grad[0]:
+            da = torch.empty_like(a)
+            K.gemm(1, dS, b, da, alpha=ctx.inv_t)
+        if ctx.needs_input_grad[1]:
+            db = torch.empty_like(b)
+            K.gemm(2, dS, a, db, alpha=ctx.inv_t)
+        return da, db, None
+
+
+class InfoNCELoss(nn.Module):
+    """Reference losses.py:57-87 (symmetric NT-Xent over the batch similarity matrix)."""
+
+    def __init__(self, temperature=0.07):
+        super().__init__()
+        self.temperature = temperature
+
+    def forward(self, imu_embeds, video_embeds):
+        if imu_embeds.shape != video_embeds.shape or imu_embeds.dim() != 2:
+            raise ValueError('expected two (batch, dim) embedding matrices of equal shape')
+        return _InfoNCEFn.apply(imu_embeds, video_embeds, 1.0 / self.temperature)
+
+
+def get_loss_function(loss_name, **kwargs):
+    """Reference losses.py:153-167."""
+    if loss_name == 'sigmoid_contrastive':
+        return SigmoidContrastiveLoss(**kwargs)
+    if loss_name == 'infonce':
+        return InfoNCELoss(**kwargs)
+    if loss_name == 'cross_entropy':
+        return CrossEntropyLoss(**kwargs)
+    if loss_name == 'focal':
+        return FocalLoss(**kwargs)
+    if loss_name == 'label_smoothing':
+        return LabelSmoothingCrossEntropy(**kwargs)
+    raise ValueError(f'Loss function inconnue: {loss_name}')

@@ -141,6 +141,21 @@ int cmhar_copy2d(int in_dtype, int out_dtype, int rows, int cols, const void* sr
 int cmhar_logits_energy(int dtype, int N, int C, const void* logits, long ld, float temperature, int* pred,
                         float* energy, float* maxlogit, hipStream_t stream);
 
+/* Row-softmax cross-entropy family over the strided logit view z[r][c] = logits[r*s_row + c*s_col], r < N, c < C
+ * (replaces: nn.CrossEntropyLoss, ClassificationTrainer trainer.py:249,300; FocalLoss losses.py:90-116;
+ * LabelSmoothingCrossEntropy losses.py:119-150; both F.cross_entropy of InfoNCELoss losses.py:76-85).
+ * labels: device int64 [N] or NULL (= row index); rows whose label == ignore_index are skipped.  gamma/alpha: focal
+ * weighting (gamma = 0, alpha = 1: plain CE; label_smoothing and gamma are exclusive).  reduction 0 none / 1 mean /
+ * 2 sum.  Outputs (all nullable): loss scalar, row_loss [N], pred (first argmax) [N], correct = #(pred == label),
+ * status = 1 when a label is out of range (the host raises).  dlogits (nullable, strides d_row/d_col):
+ * dlogits = grad_beta*dlogits + grad_scale*g*dloss/dz, g = g_up[r] ('none', required) or (*g_up or 1) x (1/count
+ * for 'mean').  ws: cmhar_cross_entropy_ws(N) floats. */
+long cmhar_cross_entropy_ws(int N);
+int cmhar_cross_entropy(int N, int C, const float* logits, long s_row, long s_col, const long* labels,
+                        long ignore_index, float label_smoothing, float gamma, float alpha, int reduction, float* loss,
+                        float* row_loss, long* pred, int* correct, int* status, float* dlogits, long d_row, long d_col,
+                        float grad_scale, float grad_beta, const float* g_up, float* ws, hipStream_t stream);
+
 /* Multi-tensor optimizer (replaces: torch.nn.utils.clip_grad_norm_ and torch.optim.AdamW.step,
  * trainer.py:74-78,140-141).  tens/chunks: DEVICE arrays of
  *   struct { float* p; const float* g; float* m; float* v; bf16* p_bf16; float* p_copy; long n; float wd;

@@ -237,3 +237,43 @@ def adamw_step(params, grads, exp_avg, exp_avg_sq, step: int, lr: float, betas=(
         bc2 = 1 - b2 ** step
         denom = (v.sqrt() / math.sqrt(bc2)).add_(eps)
         p.addcdiv_(m, denom, value=-lr / bc1)
+
+
+# ----------------------------------------------------------------------------------------------------------
+# Cross-entropy family (losses.py:57-150; nn.CrossEntropyLoss of ClassificationTrainer, trainer.py:249,300)
+# ----------------------------------------------------------------------------------------------------------
+def _log_softmax(z: Tensor) -> Tensor:
+    m = z.max(dim=1, keepdim=True).values
+    return z - (m + (z - m).exp().sum(dim=1, keepdim=True).log())
+
+
+def _reduce(v: Tensor, reduction: str) -> Tensor:
+    return v.mean() if reduction == 'mean' else v.sum() if reduction == 'sum' else v
+
+
+def cross_entropy(z: Tensor, y: Tensor, reduction: str = 'mean', label_smoothing: float = 0.0) -> Tensor:
+    """F.cross_entropy with class-index targets (mean over rows) and optional label smoothing
+    (q = (1-eps)·onehot + eps/C), restated from log-softmax."""
+    lp = _log_softmax(z)
+    C = z.shape[1]
+    nll = -lp.gather(1, y.view(-1, 1)).squeeze(1)
+    v = (1 - label_smoothing) * nll + label_smoothing * (-lp.sum(dim=1) / C)
+    return _reduce(v, reduction)
+
+
+def focal_loss(z: Tensor, y: Tensor, alpha: float = 1.0, gamma: float = 2.0, reduction: str = 'mean') -> Tensor:
+    """losses.py:101-116: alpha·(1 - exp(-ce))^gamma·ce."""
+    ce = cross_entropy(z, y, 'none')
+    return _reduce(alpha * (1 - torch.exp(-ce)) ** gamma * ce, reduction)
+
+
+def label_smoothing_ce(z: Tensor, y: Tensor, epsilon: float = 0.1, reduction: str = 'mean') -> Tensor:
+    """losses.py:129-150."""
+    return cross_entropy(z, y, reduction, label_smoothing=epsilon)
+
+
+def info_nce(a: Tensor, b: Tensor, temperature: float = 0.07) -> Tensor:
+    """losses.py:67-87: symmetric CE over a·bᵀ/τ with diagonal targets."""
+    s = a @ b.T / temperature
+    y = torch.arange(a.shape[0])
+    return (cross_entropy(s, y) + cross_entropy(s.T, y)) / 2

@@ -225,13 +225,84 @@ def g5_videomae_base(frames=16, image=224, B=1):
          **sd_meta(sd))
 
 
+def g6_classification_trainer():
+    """ClassificationTrainer (trainer.py:236-413): 2 train_epoch steps in each mode + validate metrics, dropout 0."""
+    from src.train.trainer import ClassificationTrainer
+    vdir = local_videomae(64, 2, 4, 128, 16, 4, patch=8)
+    ov = tiny_overrides(vdir)
+    ov['model']['classifier_dropout'] = 0.0
+    ov['training'].update({'train_lr_head': 1e-3, 'train_lr_encoder': 1e-4, 'train_epochs': 4})
+    cfg = make_cfg(ov)
+    out = {'config': json.dumps({k: {kk: (list(vv) if isinstance(vv, tuple) else vv) for kk, vv in d.items()}
+                                 for k, d in ov.items()})}
+    B = 8
+    batches = []
+    for i in range(2):
+        lab = torch.tensor([(3 * j + i) % 7 for j in range(B)], dtype=torch.int64)
+        batches.append({'imu': seeded_input(61 + i, (B, 6, 64)), 'label': lab})
+        out[f'imu{i}'] = batches[i]['imu'].numpy()
+        out[f'label{i}'] = lab.numpy()
+    val = [{'imu': seeded_input(65, (12, 6, 64)), 'label': torch.tensor([j % 7 for j in range(12)])}]
+    out['val_imu'] = val[0]['imu'].numpy()
+    out['val_label'] = val[0]['label'].numpy()
+    sd = None
+    for mode in ('linear_probe', 'finetune'):
+        torch.manual_seed(0)
+        clf = IMUClassifier(IMUEncoder(cfg), cfg, freeze_encoder=False)
+        if sd is None:
+            sd = seeded_state_dict(clf.state_dict(), seed=6)
+            out.update(sd_meta(sd))
+        clf.load_state_dict(sd, strict=True)
+        tr = ClassificationTrainer(clf, cfg, device='cpu', mode=mode)
+        m = tr.train_epoch(batches)
+        v = tr.validate(val)
+        out[f'{mode}.train_loss'] = np.array(m['loss'])
+        out[f'{mode}.train_acc'] = np.array(m['accuracy'])
+        for k in ('loss', 'accuracy', 'balanced_accuracy', 'f1_macro'):
+            out[f'{mode}.val_{k}'] = np.array(v[k])
+        for k, t in clf.state_dict().items():
+            out[f'{mode}.after.{k}'] = t.detach().numpy().copy()
+    save('g6_classification_trainer', seed=6, **out)
+
+
+def g7_losses():
+    """The alternative losses of losses.py:57-167 (InfoNCE, Focal, LabelSmoothing, CE via the factory): values +
+    input gradients."""
+    from src.models.losses import get_loss_function
+    out = {}
+    a = torch.nn.functional.normalize(seeded_input(71, (24, 32)), dim=1)
+    b = torch.nn.functional.normalize(seeded_input(72, (24, 32)), dim=1)
+    a.requires_grad_(True)
+    b.requires_grad_(True)
+    l = get_loss_function('infonce', temperature=0.07)(a, b)
+    l.backward()
+    out.update(nce_a=a.detach().numpy(), nce_b=b.detach().numpy(), nce_loss=np.array(l.item()),
+               nce_grad_a=a.grad.numpy(), nce_grad_b=b.grad.numpy())
+    z = (3.0 * seeded_input(73, (40, 11))).requires_grad_(True)
+    y = torch.tensor([(7 * i) % 11 for i in range(40)], dtype=torch.int64)
+    out.update(cls_logits=z.detach().numpy(), cls_labels=y.numpy())
+    for name, kw in (('focal', {'alpha': 0.5, 'gamma': 2.0}), ('label_smoothing', {'epsilon': 0.1}),
+                     ('cross_entropy', {})):
+        for red in ('mean', 'sum', 'none'):
+            z.grad = None
+            kw2 = dict(kw, reduction=red)
+            lv = get_loss_function(name, **kw2)(z, y)
+            w = seeded_input(74, tuple(lv.shape)) if red == 'none' else torch.tensor(1.0)
+            (lv * w).sum().backward()
+            out[f'{name}.{red}.loss'] = lv.detach().numpy()
+            out[f'{name}.{red}.grad'] = z.grad.numpy().copy()
+            if red == 'none':
+                out[f'{name}.{red}.w'] = w.numpy()
+    save('g7_losses', **out)
+
+
 if __name__ == '__main__':
     import shutil
-    which = sys.argv[1:] or ['g1', 'g2', 'g3', 'g4', 'g5']
+    which = sys.argv[1:] or ['g1', 'g2', 'g3', 'g4', 'g5', 'g6', 'g7']
     try:
         for w in which:
             {'g1': g1_imu_encoder, 'g2': g2_crossmodal_tiny, 'g3': g3_siglip, 'g4': g4_classifier,
-             'g5': lambda: g5_videomae_base(16, 224, 1)}[w]()
+             'g5': lambda: g5_videomae_base(16, 224, 1), 'g6': g6_classification_trainer, 'g7': g7_losses}[w]()
     finally:
         os.chdir('/')
         shutil.rmtree(SCRATCH, ignore_errors=True)

@@ -9,9 +9,9 @@ from oracle import cpu_model as O
 torch.set_num_threads(8)
 
 
-def _close(a, b, rtol=1e-4, atol=1e-5):
+def _close(a, b, rtol=1e-4, atol=1e-5, msg=''):
     a = a.detach().numpy() if isinstance(a, torch.Tensor) else np.asarray(a)
-    np.testing.assert_allclose(a, np.asarray(b), rtol=rtol, atol=atol)
+    np.testing.assert_allclose(a, np.asarray(b), rtol=rtol, atol=atol, err_msg=msg)
 
 
 def _params(sd):
@@ -164,3 +164,94 @@ def test_g5_videomae_base_full_geometry():
     _close(h[:, 0], fx['token0'], 1e-4, 1e-4)
     _close(h[:, -1], fx['last_row'], 1e-4, 1e-4)
     _close(feat, fx['feat'], 1e-4, 1e-4)
+
+
+def _cls_names(sd):
+    enc = [k for k, v in sd.items() if k.startswith('imu_encoder.') and v.is_floating_point()]
+    head = [k for k, v in sd.items() if k.startswith('classifier.') and v.is_floating_point() and 'running' not in k]
+    return enc, head
+
+
+@pytest.mark.parametrize('mode', ['linear_probe', 'finetune'])
+def test_g6_classification_trainer(mode):
+    """ClassificationTrainer.train_epoch (trainer.py:287-314) over two batches + validate (:316-353): CE loss, clip
+    1.0, AdamW (head lr 1e-3; finetune: encoder group lr 1e-4), BN batch stats, metrics via sklearn."""
+    from sklearn.metrics import balanced_accuracy_score, f1_score
+    fx = load('g6_classification_trainer')
+    cfg = fixture_config(fx)
+    sd = _params(fixture_state_dict(fx))
+    mc = oracle_mcfg(cfg)
+    enc, head = _cls_names(sd)
+    groups = [(head, 1e-3)] + ([(enc, 1e-4)] if mode == 'finetune' else [])
+    state = {k: (torch.zeros_like(sd[k]), torch.zeros_like(sd[k])) for g, _ in groups for k in g}
+    losses, correct, total = [], 0, 0
+    for step in (1, 2):
+        for g, _ in groups:
+            for k in g:
+                sd[k].grad = None
+        x, y = t(fx[f'imu{step - 1}']), t(fx[f'label{step - 1}'])
+        logits = O.imu_classifier(sd, x, mc, training=True)
+        loss = O.cross_entropy(logits, y)
+        loss.backward()
+        losses.append(loss.item())
+        correct += int((logits.argmax(1) == y).sum())
+        total += len(y)
+        with torch.no_grad():
+            every = [sd[k].grad for g, _ in groups for k in g]
+            O.clip_grad_norm(every, 1.0)
+            for g, lr in groups:
+                O.adamw_step([sd[k] for k in g], [sd[k].grad for k in g], [state[k][0] for k in g],
+                             [state[k][1] for k in g], step, lr=lr)
+    assert np.mean(losses) == pytest.approx(float(fx[f'{mode}.train_loss']), rel=1e-5)
+    assert 100.0 * correct / total == pytest.approx(float(fx[f'{mode}.train_acc']))
+    with torch.no_grad():
+        le = O.imu_classifier(sd, t(fx['val_imu']), mc, training=False)
+        yv = t(fx['val_label'])
+        pred = le.argmax(1)
+        # rel 5e-4: eval BN uses running means fed by the noise-driven biases (below)
+        assert O.cross_entropy(le, yv).item() == pytest.approx(float(fx[f'{mode}.val_loss']), rel=5e-4)
+        assert 100.0 * balanced_accuracy_score(yv.numpy(), pred.numpy()) == pytest.approx(
+            float(fx[f'{mode}.val_balanced_accuracy']))
+        assert 100.0 * f1_score(yv.numpy(), pred.numpy(), average='macro') == pytest.approx(
+            float(fx[f'{mode}.val_f1_macro']))
+    # A Linear feeding a train-mode BatchNorm has a mathematically zero bias gradient (BN removes the batch mean):
+    # the reference's Adam step on it is driven by rounding noise (|step| ≤ ~lr each), and so is ours, possibly in
+    # the other direction: they agree within 2 x steps x lr; the BN running mean it feeds inherits 0.1x that.
+    # Everything else is compared tightly.
+    noisy = {f'classifier.{4 * i}.bias': 4.2e-3 for i in range(len(mc['classifier_hidden_dims']))}
+    noisy.update({f'classifier.{4 * i + 1}.running_mean': 4.2e-4 for i in range(len(mc['classifier_hidden_dims']))})
+    noisy['imu_encoder.norm.bias'] = 4.2e-4      # a per-feature constant the first BN removes as well
+    # Likewise the attention key biases (softmax is shift-invariant per query): within 2 encoder-lr steps.
+    for key in fx.files:
+        if key.startswith(f'{mode}.after.'):
+            name = key[len(mode) + 7:]
+            got, want = sd[name].detach(), fx[key]
+            if name.endswith('in_proj_bias'):
+                d = got.shape[0] // 3
+                _close(got[d:2 * d], want[d:2 * d], 0.0, 4.2e-4, name)
+                got, want = torch.cat([got[:d], got[2 * d:]]), np.concatenate([want[:d], want[2 * d:]])
+            _close(got, want, 1e-5 if name not in noisy else 0.0, noisy.get(name, 2e-6), name)
+
+
+def test_g7_alternative_losses():
+    """InfoNCE / Focal / LabelSmoothing / CE restatements vs the reference's losses.py (values + input grads)."""
+    fx = load('g7_losses')
+    a = t(fx['nce_a']).requires_grad_(True)
+    b = t(fx['nce_b']).requires_grad_(True)
+    loss = O.info_nce(a, b, 0.07)
+    loss.backward()
+    _close(loss, fx['nce_loss'], 1e-6, 1e-6)
+    _close(a.grad, fx['nce_grad_a'], 1e-5, 1e-7)
+    _close(b.grad, fx['nce_grad_b'], 1e-5, 1e-7)
+    y = t(fx['cls_labels'])
+    fns = {'focal': lambda z, r: O.focal_loss(z, y, alpha=0.5, gamma=2.0, reduction=r),
+           'label_smoothing': lambda z, r: O.label_smoothing_ce(z, y, 0.1, r),
+           'cross_entropy': lambda z, r: O.cross_entropy(z, y, r)}
+    for name, fn in fns.items():
+        for red in ('mean', 'sum', 'none'):
+            z = t(fx['cls_logits']).requires_grad_(True)
+            lv = fn(z, red)
+            w = t(fx[f'{name}.{red}.w']) if red == 'none' else torch.tensor(1.0)
+            (lv * w).sum().backward()
+            _close(lv, fx[f'{name}.{red}.loss'], 1e-5, 1e-6)
+            _close(z.grad, fx[f'{name}.{red}.grad'], 1e-5, 1e-7)
