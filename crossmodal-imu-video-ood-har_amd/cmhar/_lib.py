@@ -58,6 +58,11 @@ _SIGS = {
     'cmhar_copy2d': (i32, [i32, i32, i32, i32, vp, i64, vp, i64, f32, f32, f32, u64, vp]),
     'cmhar_logits_energy': (i32, [i32, i32, i32, vp, i64, f32, vp, vp, vp, vp]),
     'cmhar_cross_entropy_ws': (i64, [i32]),
+    'cmhar_resize_ksize': (i32, [i32, i32]),
+    'cmhar_video_ingest_ws': (i64, [i32, i32, i32, i32, i32]),
+    'cmhar_video_ingest': (i32, [i32, i32, vp, i64, i32, i32, vp, i32, i32, vp, vp, i32, vp, vp, i64, vp]),
+    'cmhar_imu_preprocess_ws': (i64, [i64, i32, i32]),
+    'cmhar_imu_preprocess': (i32, [i32, i32, vp, vp, i64, vp, i32, i32, i64, vp, vp, i32, vp, vp, vp]),
     'cmhar_cross_entropy': (i32, [i32, i32, vp, i64, i64, vp, i64, f32, f32, f32, i32, vp, vp, vp, vp, vp, vp, i64,
                                   i64, f32, f32, vp, vp, vp]),
     'cmhar_mt_grad_norm': (i32, [vp, vp, i32, vp, vp, f32, i32, vp]),

@@ -156,6 +156,28 @@ int cmhar_cross_entropy(int N, int C, const float* logits, long s_row, long s_co
                         float* row_loss, long* pred, int* correct, int* status, float* dlogits, long d_row, long d_col,
                         float grad_scale, float grad_beta, const float* g_up, float* ws, hipStream_t stream);
 
+/* Video clip ingestion (replaces: CrossModalDataset.load_video_clip + its transform, src/data/datasets.py:49-58,
+ * 155-235): decoded RGB uint8 frames [*][H0][W0][3] (frame f at frames + f*frame_stride bytes), frame_idx: device
+ * int32 [B*T] source frame per output frame → out fp32 (B,T,3,H,W) (channel_first = 0) or (B,3,T,H,W), each
+ * frame resized with Pillow's BILINEAR resample bit-exactly (22-bit fixed point, uint8 between the passes), then
+ * /255 and (x - mean)/std.  mean3/std3: HOST arrays of 3 floats.  ws: cmhar_video_ingest_ws(B*T, H0, W0, H, W) bytes. */
+int cmhar_resize_ksize(int in_size, int out_size);
+long cmhar_video_ingest_ws(int nframes, int H0, int W0, int H, int W);
+int cmhar_video_ingest(int B, int T, const unsigned char* frames, long frame_stride, int H0, int W0,
+                       const int* frame_idx, int H, int W, const float* mean3, const float* std3, int channel_first,
+                       float* out, void* ws, long ws_bytes, hipStream_t stream);
+
+/* IMU preprocessing (replaces: MMEAPreprocessor.load_imu_data unit conversion, preprocess_imu, create_imu_windows,
+ * src/data/preprocessing.py:176-183, 204-243).  raw: [total][C] fp32, recording r = rows offsets[r]..offsets[r+1]
+ * (device int64 [nrec+1]); div_r: device [C] unit divisors (raw / R) or NULL; median_k odd (1 = off; zero-padded
+ * edges like scipy.signal.medfilt); normalize: per-recording per-channel z-score, population std + 1e-8.
+ * Windows w < nwin: recording win_rec[w] (device int32), first sample win_start[w] (device int64), win samples,
+ * zero past the recording's end → out [nwin][C][win] fp32.  ws: cmhar_imu_preprocess_ws(total, nrec, C) floats. */
+long cmhar_imu_preprocess_ws(long total, int nrec, int C);
+int cmhar_imu_preprocess(int nrec, int C, const float* raw, const long* offsets, long total, const float* div_r,
+                         int median_k, int normalize, long nwin, const int* win_rec, const long* win_start, int win,
+                         float* out, float* ws, hipStream_t stream);
+
 /* Multi-tensor optimizer (replaces: torch.nn.utils.clip_grad_norm_ and torch.optim.AdamW.step,
  * trainer.py:74-78,140-141).  tens/chunks: DEVICE arrays of
  *   struct { float* p; const float* g; float* m; float* v; bf16* p_bf16; float* p_copy; long n; float wd;

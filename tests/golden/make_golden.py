@@ -296,13 +296,40 @@ def g7_losses():
     save('g7_losses', **out)
 
 
+def g8_imu_preprocessing():
+    """MMEAPreprocessor IMU path (preprocessing.py:176-243): unit conversion, median filter k=5, z-score, 250/125
+    windows incl. a short (padded) recording and a recording with repeated values (median ties)."""
+    from src.data.preprocessing import MMEAPreprocessor
+    cfg = Config()
+    pre = MMEAPreprocessor(cfg)
+    rng = np.random.default_rng(8)
+    lengths = [100, 250, 731, 1000]
+    out = {'lengths': np.array(lengths)}
+    for i, n in enumerate(lengths):
+        raw = rng.normal(0, 1, (n, 6)).astype(np.float32) * np.array([9000, 9000, 9000, 500, 500, 500], np.float32)
+        raw = np.round(raw)                              # integer raw counts, as the sensor CSVs hold
+        if i == 2:
+            raw[100:140] = raw[100]                      # flat segment: median ties
+        conv = np.concatenate([raw[:, :3] / float(getattr(cfg.data, 'Racc', 16384.0)),
+                               raw[:, 3:6] / float(getattr(cfg.data, 'Rgyro', 16.4))],
+                              axis=1).astype(np.float32)  # load_imu_data :176-183
+        proc = pre.preprocess_imu(conv)
+        wins = pre.create_imu_windows(proc)
+        out[f'raw{i}'] = raw
+        out[f'conv{i}'] = conv
+        out[f'proc{i}'] = proc
+        out[f'windows{i}'] = np.stack(wins)
+    save('g8_imu_preprocessing', **out)
+
+
 if __name__ == '__main__':
     import shutil
-    which = sys.argv[1:] or ['g1', 'g2', 'g3', 'g4', 'g5', 'g6', 'g7']
+    which = sys.argv[1:] or ['g1', 'g2', 'g3', 'g4', 'g5', 'g6', 'g7', 'g8']
     try:
         for w in which:
             {'g1': g1_imu_encoder, 'g2': g2_crossmodal_tiny, 'g3': g3_siglip, 'g4': g4_classifier,
-             'g5': lambda: g5_videomae_base(16, 224, 1), 'g6': g6_classification_trainer, 'g7': g7_losses}[w]()
+             'g5': lambda: g5_videomae_base(16, 224, 1), 'g6': g6_classification_trainer, 'g7': g7_losses,
+             'g8': g8_imu_preprocessing}[w]()
     finally:
         os.chdir('/')
         shutil.rmtree(SCRATCH, ignore_errors=True)
