@@ -322,14 +322,57 @@ def g8_imu_preprocessing():
     save('g8_imu_preprocessing', **out)
 
 
+def g9_checkpoint_resume():
+    """Checkpoint wire format (trainer.py:38-48,188-196; main.py:110-124,150-163): the reference trains 2 steps and
+    writes `last.pt` (model + optimizer + scheduler state, torch.save) and a DataParallel-style `module.`-prefixed
+    state_dict; then it continues one more step — the build must load those files and reproduce that step."""
+    import shutil as _sh
+    vdir = local_videomae(32, 1, 2, 64, 16, 4, patch=8)
+    ov = tiny_overrides(vdir)
+    ov['model'].update({'imu_d_model': 16, 'imu_nhead': 2, 'imu_num_layers': 1, 'video_d_model': 24,
+                        'projection_hidden_dim': 32, 'projection_dim': 16, 'videomae_hidden_size': 32,
+                        'videomae_num_layers': 1, 'videomae_num_heads': 2, 'videomae_intermediate_size': 64})
+    cfg = make_cfg(ov)
+    torch.manual_seed(0)
+    model = CrossModalModel(cfg)
+    sd = seeded_state_dict(model.state_dict(), seed=9)
+    model.load_state_dict(sd, strict=True)
+    B = 6
+    batches = [{'imu': seeded_input(91 + i, (B, 6, 64)), 'video': seeded_input(94 + i, (B, 4, 3, 16, 16))}
+               for i in range(3)]
+    trainer = CrossModalTrainer(model, SigmoidContrastiveLoss(learnable=True), cfg, device='cpu')
+    trainer.train_epoch(batches[:2])
+    trainer.scheduler.step()                                  # end of epoch 0 (fit, trainer.py:184)
+    trainer.save_checkpoint(__import__('pathlib').Path(SCRATCH) / 'last.pt',
+                            extra={'best_val_loss': 1.0, 'optimizer_state_dict': trainer.optimizer.state_dict(),
+                                   'scheduler_state_dict': trainer.scheduler.state_dict()})
+    _sh.copy(os.path.join(SCRATCH, 'last.pt'), os.path.join(HERE, 'g9_last.pt'))
+    dp_sd = {'module.' + k: v for k, v in model.state_dict().items()}   # what a DataParallel-wrapped model saves
+    torch.save({'epoch': 0, 'model_state_dict': dp_sd, 'history': {'train': [], 'val': []}},
+               os.path.join(HERE, 'g9_module_prefixed.pt'))
+    lr_epoch1 = trainer.optimizer.param_groups[0]['lr']
+    loss3 = trainer.train_epoch(batches[2:])
+    out = {'config': json.dumps({k: {kk: (list(vv) if isinstance(vv, tuple) else vv) for kk, vv in d.items()}
+                                 for k, d in ov.items()}),
+           'seed': 9, 'imu3': batches[2]['imu'].numpy(), 'video3': batches[2]['video'].numpy(),
+           'loss3': np.array(loss3), 'lr_epoch1': np.array(lr_epoch1), **sd_meta(sd)}
+    for k, v in model.state_dict().items():
+        out[f'after.{k}'] = v.detach().numpy().copy()
+    for i, p in enumerate(model.parameters()):
+        st = trainer.optimizer.state.get(p)
+        if st:
+            out[f'exp_avg.{i}'] = st['exp_avg'].numpy().copy()
+    save('g9_checkpoint_resume', **out)
+
+
 if __name__ == '__main__':
     import shutil
-    which = sys.argv[1:] or ['g1', 'g2', 'g3', 'g4', 'g5', 'g6', 'g7', 'g8']
+    which = sys.argv[1:] or ['g1', 'g2', 'g3', 'g4', 'g5', 'g6', 'g7', 'g8', 'g9']
     try:
         for w in which:
             {'g1': g1_imu_encoder, 'g2': g2_crossmodal_tiny, 'g3': g3_siglip, 'g4': g4_classifier,
              'g5': lambda: g5_videomae_base(16, 224, 1), 'g6': g6_classification_trainer, 'g7': g7_losses,
-             'g8': g8_imu_preprocessing}[w]()
+             'g8': g8_imu_preprocessing, 'g9': g9_checkpoint_resume}[w]()
     finally:
         os.chdir('/')
         shutil.rmtree(SCRATCH, ignore_errors=True)

@@ -178,3 +178,47 @@ def test_g6_classification_trainer(mode):
             _close(got[d:2 * d], want[d:2 * d], 0.0, 4.2e-4, name)
             got, want = torch.cat([got[:d], got[2 * d:]]), np.concatenate([want[:d], want[2 * d:]])
         _close(got, want, 1e-5 if name not in noisy else 0.0, noisy.get(name, 3e-6), name)
+
+
+def test_g9_resume_reference_checkpoint_and_step():
+    """A `last.pt` written by the REFERENCE's CrossModalTrainer after 2 steps + one scheduler step: model, AdamW
+    moments/step count and the LinearLR→Cosine schedule restored into the drop-ins; the next training step must
+    land where the reference's third step did."""
+    import os
+    from cmhar import models
+    from cmhar.checkpoint import resume
+    from cmhar.losses import SigmoidContrastiveLoss
+    from cmhar.trainer import CrossModalTrainer
+    fx = load('g9_checkpoint_resume')
+    cfg = fixture_config(fx)
+    cfg.model.compute_dtype = 'fp32'
+    torch.manual_seed(0)
+    m = models.CrossModalModel(cfg)
+    tr = CrossModalTrainer(m, SigmoidContrastiveLoss().to(DEV), cfg, device=DEV)
+    resume(tr, os.path.join(os.path.dirname(__file__), 'golden', 'g9_last.pt'))
+    assert tr.optimizer.param_groups[0]['lr'] == pytest.approx(float(fx['lr_epoch1']), rel=1e-12)
+    loss = tr.train_epoch([{'imu': torch.tensor(fx['imu3']), 'video': torch.tensor(fx['video3'])}])
+    assert loss == pytest.approx(float(fx['loss3']), rel=1e-5)
+    lr = float(fx['lr_epoch1'])
+    sd = m.state_dict()
+    params = list(m.parameters())
+    pidx = {id(p): i for i, p in enumerate(params)}
+    named = dict(m.named_parameters())
+    tight = 0
+    emax = max(float(np.abs(fx[k]).max()) for k in fx.files if k.startswith('exp_avg.'))
+    for key in fx.files:
+        if not key.startswith('after.'):
+            continue
+        name = key[6:]
+        got, want = sd[name].detach().cpu().numpy(), fx[key]
+        if name in named and f'exp_avg.{pidx[id(named[name])]}' in fx.files:
+            ea = np.abs(fx[f'exp_avg.{pidx[id(named[name])]}'])
+            ok = ea > 1e-3 * emax                          # steps driven by real gradients, not rounding noise
+            np.testing.assert_allclose(got[ok], want[ok], rtol=1e-5, atol=3e-7, err_msg=name)
+            np.testing.assert_allclose(got[~ok], want[~ok], rtol=0, atol=2.1 * lr, err_msg=name)
+            tight += int(ok.sum())
+        elif got.dtype.kind == 'f':
+            np.testing.assert_allclose(got, want, rtol=1e-4, atol=2e-5, err_msg=name)
+        else:
+            assert (got == want).all(), name
+    assert tight > 5_000
