@@ -33,6 +33,8 @@ _SIGS = {
     'cmhar_gemm_bf16_ws': (i64, [i32, i32, i32]),
     'cmhar_gemm_generic': (i32, [i32, i32, i32, i32, i32, i32, vp, i64, i64, i64, vp, i64, i64, i64, vp, i64, i64,
                                  C.POINTER(Epilogue), vp]),
+    'cmhar_gemm_generic_splitk': (i32, [i32, i32, i32, i32, i32, i32, vp, i64, i64, vp, i64, i64, vp, i64,
+                                        C.POINTER(Epilogue), vp, vp]),
     'cmhar_attention_fwd': (i32, [i32, i32, i32, i32, i32, i32, vp, i64, vp, i64, vp, i64, vp, i64, vp, f32, f32, u64,
                                   vp]),
     'cmhar_attention_bwd': (i32, [i32, i32, i32, i32, i32, i32, vp, i64, vp, i64, vp, i64, vp, i64, vp, i64, vp, vp,

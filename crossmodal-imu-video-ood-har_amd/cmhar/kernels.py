@@ -8,6 +8,7 @@ from __future__ import annotations
 
 import ctypes as C
 import math
+import os
 
 import torch
 
@@ -97,6 +98,21 @@ def _splits_for(M, N, K):
 
 
 _TAIL_WS = {}
+
+
+_NO_GENERIC_SPLIT = os.environ.get('CMHAR_GENERIC_SPLIT', '1') == '0'    # A/B knob (debug)
+
+
+def _generic_splits(M, N, K):
+    """Split-K factor for the fp32 LDS-tiled GEMM: one row of 64² tiles (M <= 64: the video projection and the
+    projection heads at M = batch rows) over K >= 512 leaves most CUs idle and the K loop latency-bound; aim at ~128
+    workgroups with >= 64 k per slice.  The IMU encoder's token GEMMs (M = 13·batch) keep the single-pass order:
+    their backward through post-LN layers amplifies summation-order differences (measured: split-K moved g1's
+    bias gradients by up to 9e-4 relative, deterministically, vs 1e-6 single-pass)."""
+    tiles = math.ceil(M / 64) * math.ceil(N / 64)
+    if M > 64 or N < 256 or tiles >= 64 or K < 512 or _NO_GENERIC_SPLIT:
+        return 1
+    return max(1, min(32, math.ceil(128 / tiles), K // 64))
 
 
 def _tail_ws(M, N, K):
@@ -189,8 +205,14 @@ def gemm(layout: int, a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, *, bi
             sam, sak, sbk, sbn = a.stride(0), 1, b.stride(0), 1
         else:
             sam, sak, sbk, sbn = 1, a.stride(0), b.stride(0), 1
-        call('cmhar_gemm_generic', L.dtype_code(a.dtype), L.dtype_code(out.dtype), M, N, K, 1, ptr(a), sam, sak, 0,
-             ptr(b), sbk, sbn, 0, ptr(out), out.stride(0), 0, C.byref(epi), st)
+        s = _generic_splits(M, N, K) if splits is None else splits
+        if s > 1:
+            ws = workspace(s * M * N, out.device)
+            call('cmhar_gemm_generic_splitk', L.dtype_code(a.dtype), L.dtype_code(out.dtype), M, N, K, s, ptr(a), sam,
+                 sak, ptr(b), sbk, sbn, ptr(out), out.stride(0), C.byref(epi), ptr(ws), st)
+        else:
+            call('cmhar_gemm_generic', L.dtype_code(a.dtype), L.dtype_code(out.dtype), M, N, K, 1, ptr(a), sam, sak,
+                 0, ptr(b), sbk, sbn, 0, ptr(out), out.stride(0), 0, C.byref(epi), st)
     return out
 
 

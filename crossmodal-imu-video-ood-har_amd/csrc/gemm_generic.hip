@@ -88,7 +88,62 @@ __global__ __launch_bounds__(NTH) void gemm_generic_kernel(
     }
 }
 
+// Split-K combine: C = epilogue(Σ_s P[s]) in a fixed split order (deterministic).
+template <typename TOut>
+__global__ __launch_bounds__(256) void generic_splitk_reduce(int M, int N, int S, const float* __restrict__ P,
+                                                             TOut* __restrict__ C, long ldc, Epilogue e) {
+  const long MN = (long)M * N;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < MN; i += (long)gridDim.x * blockDim.x) {
+    float acc = 0.f;
+    for (int s = 0; s < S; ++s) acc += P[s * MN + i];
+    epilogue_store<TOut>(e, C, ldc, (int)(i / N), (int)(i % N), acc);
+  }
+}
+
 }  // namespace
+
+// Skinny GEMMs (a handful of 64x64 output tiles over a long K: the video projection / projection heads at M = batch
+// rows, K = 768) are bound by the latency of their K loop on a few CUs.  Split K over `splits` batched slices into
+// fp32 partials (ws: splits*M*N floats), then combine with the epilogue.
+extern "C" int cmhar_gemm_generic_splitk(int in_dtype, int out_dtype, int M, int N, int K, int splits, const void* A,
+                                         long sam, long sak, const void* B, long sbk, long sbn, void* C, long ldc,
+                                         const Epilogue* epi, float* ws, hipStream_t stream) {
+  if (M <= 0 || N <= 0) return 0;
+  if (splits < 1 || !ws || in_dtype != out_dtype && !(in_dtype == CMHAR_BF16 && out_dtype == CMHAR_F32)) return -1;
+  Epilogue e{};
+  e.alpha = 1.f;
+  if (epi) e = *epi;
+  if (e.rowsum) return -3;
+  const int klen = cdiv(cdiv(K, splits), TK) * TK;
+  const int S = cdiv(K, klen);
+  Epilogue plain{};
+  plain.alpha = 1.f;
+  const int esz = in_dtype == CMHAR_BF16 ? 2 : 4;
+  // slice s: A advanced by s*klen along k, B likewise; the last slice's K is clamped by running it separately
+  const int full = K / klen;                           // slices of exactly klen
+  dim3 grid(cdiv(N, TN), cdiv(M, TM), full);
+#define LAUNCH(TI, GRID, KK, AOFF, BOFF, POFF)                                                                  \
+  gemm_generic_kernel<TI, float><<<GRID, 256, 0, stream>>>(M, N, KK, (const TI*)A + (AOFF), sam, sak,           \
+                                                           (long)klen * sak, (const TI*)B + (BOFF), sbk, sbn,   \
+                                                           (long)klen * sbk, ws + (POFF), N, (long)M * N, plain)
+  if (full > 0) {
+    if (in_dtype == CMHAR_F32) LAUNCH(float, grid, klen, 0, 0, 0);
+    else LAUNCH(bf16, grid, klen, 0, 0, 0);
+  }
+  if (full < S) {
+    const long k0 = (long)full * klen;
+    dim3 g1(cdiv(N, TN), cdiv(M, TM), 1);
+    if (in_dtype == CMHAR_F32) LAUNCH(float, g1, (int)(K - k0), k0 * sak, k0 * sbk, (long)full * M * N);
+    else LAUNCH(bf16, g1, (int)(K - k0), k0 * sak, k0 * sbk, (long)full * M * N);
+  }
+#undef LAUNCH
+  (void)esz;
+  const int blocks = min(1024, cdiv((long)M * N, 256));
+  if (out_dtype == CMHAR_F32) generic_splitk_reduce<float><<<blocks, 256, 0, stream>>>(M, N, S, ws, (float*)C, ldc, e);
+  else generic_splitk_reduce<bf16><<<blocks, 256, 0, stream>>>(M, N, S, ws, (bf16*)C, ldc, e);
+  CMHAR_CHECK_LAUNCH();
+  return 0;
+}
 
 extern "C" int cmhar_gemm_generic(int in_dtype, int out_dtype, int M, int N, int K, int batch, const void* A,
                                   long sam, long sak, long sAb, const void* B, long sbk, long sbn, long sBb, void* C,

@@ -66,6 +66,11 @@ long cmhar_gemm_bf16_ws(int M, int N, int K);
 int cmhar_gemm_generic(int in_dtype, int out_dtype, int M, int N, int K, int batch, const void* A, long sam,
                        long sak, long sAb, const void* B, long sbk, long sbn, long sBb, void* C, long ldc, long sCb,
                        const CmharEpilogue* epi, hipStream_t stream);
+/* Split-K form of the above (batch 1) for skinny GEMMs with a long K (the video projection and projection heads at
+ * M = batch rows): ws = splits*M*N fp32 partials, combined in a fixed order with the epilogue. */
+int cmhar_gemm_generic_splitk(int in_dtype, int out_dtype, int M, int N, int K, int splits, const void* A, long sam,
+                              long sak, const void* B, long sbk, long sbn, void* C, long ldc,
+                              const CmharEpilogue* epi, float* ws, hipStream_t stream);
 
 /* Attention softmax(scale·QKᵀ)V per (batch, head); Q/K/V/O rows [B*L, ld] with head h at cols h*D.
  * bf16: D = 64 flash kernels (no dropout).  fp32: D in {8,16,32,64}, attention-prob dropout pdrop.

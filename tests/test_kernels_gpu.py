@@ -218,6 +218,27 @@ def test_gemm_generic_fp32(layout):
     assert rel(out, _ref_gemm(layout, a, b)) < 1e-6
 
 
+@pytest.mark.parametrize('layout', [0, 1, 2])
+@pytest.mark.parametrize('M,N,Kd', [(32, 768, 768), (32, 512, 768), (7, 300, 1000), (64, 256, 4096)])
+def test_gemm_generic_splitk_fp32(layout, M, N, Kd):
+    """Skinny fp32 GEMMs take the split-K path (partials + ordered combine with the epilogue): bias, ReLU,
+    residual and beta accumulation must land as in the single-pass kernel."""
+    from cmhar.kernels import _generic_splits
+    assert _generic_splits(M, N, Kd) > 1
+    torch.manual_seed(2)
+    a, b = _operands(layout, M, N, Kd, lambda s, sd: torch.randn(s), torch.float32)
+    bias = torch.randn(N, device=DEV)
+    res = torch.randn(M, N, device=DEV)
+    out = torch.randn(M, N, device=DEV)
+    old = out.clone()
+    K().gemm(layout, a, b, out, bias=bias, residual=res, act=L().ACT_RELU, beta=0.5)
+    want = torch.relu(_ref_gemm(layout, a, b) + bias) + res + 0.5 * old
+    assert rel(out, want) < 3e-6
+    out1 = torch.empty(M, N, device=DEV)
+    K().gemm(layout, a, b, out1, splits=1)
+    assert rel(out1, _ref_gemm(layout, a, b)) < 3e-6
+
+
 # ---------------------------------------------------------------------------------------------------------------
 # attention
 # ---------------------------------------------------------------------------------------------------------------
