@@ -22,10 +22,11 @@ from ._lib import call, ptr
 class Tracer:
     def __init__(self):
         self.active = False
+        self.only = None       # optional set of kernel symbols to time (None = all)
         self.records = []      # (kernel symbol, flops, bytes, start_event, end_event)
 
-    def begin(self):
-        if not self.active:
+    def begin(self, name=None):
+        if not self.active or (self.only is not None and name not in self.only):
             return None
         ev = torch.cuda.Event(enable_timing=True)
         ev.record()
@@ -188,15 +189,17 @@ def gemm(layout: int, a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, *, bi
             n = _tail_ws(M, N, K)
             if n:
                 ws = workspace(n, out.device)
-        ev = TRACE.begin()
-        call('cmhar_gemm_bf16', layout, L.dtype_code(out.dtype), M, N, K, ptr(a), a.stride(0), ptr(b), b.stride(0),
-             ptr(out), out.stride(0), C.byref(epi), s, ptr(ws), st)
-        if ev is not None:
+        ev = name = None
+        if TRACE.active:
             name = _GEMM_SYMBOL[layout].format(o='float' if (s > 1 or out.dtype == torch.float32) else 'bf16')
             if M % 256 == 0 and N % 256 == 0 and K % 64 == 0:
                 name = name.replace('gemm_bf16_kernel', 'gemm256_kernel')
             if s > 1:
                 name += '+splitk_reduce'
+            ev = TRACE.begin(name)
+        call('cmhar_gemm_bf16', layout, L.dtype_code(out.dtype), M, N, K, ptr(a), a.stride(0), ptr(b), b.stride(0),
+             ptr(out), out.stride(0), C.byref(epi), s, ptr(ws), st)
+        if ev is not None:
             TRACE.end(ev, name, 2 * M * N * K, 2 * (M * K + N * K) + out.element_size() * M * N)
     else:
         if layout == 0:
@@ -284,7 +287,7 @@ def attention_fwd(q, k, v, out, lse, *, B, H, Lq, Lk, D, scale, pdrop=0.0, seed=
     if dt == L.BF16 and D == 64 and pdrop == 0.0:     # flash (MFMA) path: 16-B aligned rows
         for t, n in ((q, 'q'), (k, 'k'), (v, 'v'), (out, 'o')):
             _check_bf16_operand(t, n)
-    ev = TRACE.begin() if (dt == L.BF16 and D == 64 and pdrop == 0.0) else None
+    ev = TRACE.begin('attn_fwd_bf16') if (dt == L.BF16 and D == 64 and pdrop == 0.0) else None
     call('cmhar_attention_fwd', dt, B, H, Lq, Lk, D, ptr(q), q.stride(0), ptr(k), k.stride(0), ptr(v), v.stride(0),
          ptr(out), out.stride(0), ptr(lse), scale, pdrop, seed, L.stream(q.device))
     TRACE.end(ev, 'attn_fwd_bf16', 4 * B * H * Lq * Lk * D, 2 * (B * Lq + 2 * B * Lk + B * Lq) * H * D)
@@ -303,7 +306,7 @@ def attention_bwd(q, k, v, o, do, lse, dq, dk, dv, *, B, H, Lq, Lk, D, scale, pd
         for t, n in ((q, 'q'), (k, 'k'), (v, 'v'), (o, 'o'), (do, 'do'), (dq, 'dq'), (dk, 'dk'), (dv, 'dv')):
             _check_bf16_operand(t, n)
     delta = workspace(B * H * Lq, q.device)
-    ev = TRACE.begin() if flash else None
+    ev = TRACE.begin('attn_bwd_bf16(dq+delta,dkdv)') if flash else None
     call('cmhar_attention_bwd', dt, B, H, Lq, Lk, D, ptr(q), q.stride(0), ptr(k), k.stride(0), ptr(v), v.stride(0),
          ptr(o), o.stride(0), ptr(do), do.stride(0), ptr(lse), ptr(delta), ptr(dq), dq.stride(0), ptr(dk),
          dk.stride(0), ptr(dv), dv.stride(0), scale, pdrop, seed, L.stream(q.device))
