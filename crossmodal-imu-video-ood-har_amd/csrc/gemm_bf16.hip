@@ -564,7 +564,8 @@ __global__ __launch_bounds__(NT2, 2) void gemm256_kernel(int M, int N, int K, co
 #pragma unroll
         for (int r = 0; r < 4; ++r)
           T[(i * 16 + 4 * (lane >> 4) + r) * EPI2_LD + j * 16 + (lane & 15)] = acc[pass * 4 + i][j][r];
-    __syncthreads();
+    // the slab is private to this wave and a wave's LDS operations complete in order: no workgroup barrier
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     const int cg = (lane & 7) * 8;
     const int n0 = bn + wc * 64 + cg;
 #pragma unroll 2
@@ -594,7 +595,7 @@ __global__ __launch_bounds__(NT2, 2) void gemm256_kernel(int M, int N, int K, co
         epilogue_store8<OutT>(e, C, ldc, m, n0, v);
       }
     }
-    __syncthreads();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this pass' slab reads done before the next overwrite
   }
 }
 
