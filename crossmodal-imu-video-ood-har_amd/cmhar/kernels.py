@@ -200,7 +200,9 @@ def gemm(layout: int, a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, *, bi
         call('cmhar_gemm_bf16', layout, L.dtype_code(out.dtype), M, N, K, ptr(a), a.stride(0), ptr(b), b.stride(0),
              ptr(out), out.stride(0), C.byref(epi), s, ptr(ws), st)
         if ev is not None:
-            TRACE.end(ev, name, 2 * M * N * K, 2 * (M * K + N * K) + out.element_size() * M * N)
+            # algorithmic bytes: operands once + output once + every epilogue tensor (residual / aux in / aux out)
+            extra = sum(t.element_size() * M * N for t in (residual, aux_in, aux_out) if t is not None)
+            TRACE.end(ev, name, 2 * M * N * K, 2 * (M * K + N * K) + out.element_size() * M * N + extra)
     else:
         if layout == 0:
             sam, sak, sbk, sbn = a.stride(0), 1, 1, b.stride(0)
