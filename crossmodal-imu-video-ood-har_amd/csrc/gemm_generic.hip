@@ -7,14 +7,14 @@
 
 namespace {
 
-constexpr int TM = 64, TN = 64, TK = 32, NTH = 256;
-constexpr int PER = TM * TK / NTH;        // 8 A and 8 B elements staged per thread per K-tile
+constexpr int TM = 64, TN = 64, TK = 32, NTH = 256;   // default tile; T = 32 for grids of few 64² tiles
 
 // The GEMMs this kernel serves are small (tens of blocks) with K up to a few thousand, so a K-step is bounded by
 // memory LATENCY, not bandwidth: tile k+1 is loaded into registers while tile k is consumed from LDS (double-
 // buffered LDS, one barrier per K-step), so each step pays compute + one overlapped fetch.
-template <typename TIn>
+template <typename TIn, int T>
 struct GenStage {
+  static constexpr int PER = T * TK / NTH;      // A and B elements staged per thread per K-tile
   float a[PER], b[PER];
   __device__ __forceinline__ void load(const TIn* __restrict__ A, long sam, long sak, const TIn* __restrict__ B,
                                        long sbk, long sbn, int M, int N, int K, int bm, int bn, int k0, int tid) {
@@ -22,44 +22,48 @@ struct GenStage {
     for (int it = 0; it < PER; ++it) {
       const int i = it * NTH + tid;
       int mm, kk;
-      if (sak == 1) { mm = i / TK; kk = i % TK; } else { kk = i / TM; mm = i % TM; }
+      if (sak == 1) { mm = i / TK; kk = i % TK; } else { kk = i / T; mm = i % T; }
       const int gm = bm + mm, gk = k0 + kk;
       a[it] = (gm < M && gk < K) ? to_f<TIn>(A[gm * sam + gk * sak]) : 0.f;
       int nn, kb;
-      if (sbn == 1) { kb = i / TN; nn = i % TN; } else { nn = i / TK; kb = i % TK; }
+      if (sbn == 1) { kb = i / T; nn = i % T; } else { nn = i / TK; kb = i % TK; }
       const int gn = bn + nn, gkb = k0 + kb;
       b[it] = (gn < N && gkb < K) ? to_f<TIn>(B[gkb * sbk + gn * sbn]) : 0.f;
     }
   }
-  __device__ __forceinline__ void store(float (*As)[TM + 4], float (*Bs)[TN + 4], long sak, long sbn, int tid) const {
+  __device__ __forceinline__ void store(float (*As)[T + 4], float (*Bs)[T + 4], long sak, long sbn, int tid) const {
 #pragma unroll
     for (int it = 0; it < PER; ++it) {
       const int i = it * NTH + tid;
       int mm, kk;
-      if (sak == 1) { mm = i / TK; kk = i % TK; } else { kk = i / TM; mm = i % TM; }
+      if (sak == 1) { mm = i / TK; kk = i % TK; } else { kk = i / T; mm = i % T; }
       As[kk][mm] = a[it];
       int nn, kb;
-      if (sbn == 1) { kb = i / TN; nn = i % TN; } else { nn = i / TK; kb = i % TK; }
+      if (sbn == 1) { kb = i / T; nn = i % T; } else { nn = i / TK; kb = i % TK; }
       Bs[kb][nn] = b[it];
     }
   }
 };
 
-template <typename TIn, typename TOut>
+// T x T output tile, 16 x 16 threads with (T/16)² outputs each.  Every output is one fmaf chain over k = 0..K-1 in
+// order whatever T is, so the two tile sizes give bit-identical results (T = 32 quadruples the workgroups of the
+// IMU encoder's few-tile GEMMs and quarters each one's K-loop FMA count).
+template <typename TIn, typename TOut, int T = TM>
 __global__ __launch_bounds__(NTH) void gemm_generic_kernel(
     int M, int N, int K, const TIn* __restrict__ A, long sam, long sak, long sAb, const TIn* __restrict__ B,
     long sbk, long sbn, long sBb, TOut* __restrict__ C, long ldc, long sCb, Epilogue e) {
-  __shared__ float As[2][TK][TM + 4];
-  __shared__ float Bs[2][TK][TN + 4];
+  constexpr int R = T / 16;
+  __shared__ float As[2][TK][T + 4];
+  __shared__ float Bs[2][TK][T + 4];
   const int tid = threadIdx.x;
-  const int bm = blockIdx.y * TM, bn = blockIdx.x * TN;
+  const int bm = blockIdx.y * T, bn = blockIdx.x * T;
   A += blockIdx.z * sAb;
   B += blockIdx.z * sBb;
   C += blockIdx.z * sCb;
-  const int tr = tid / 16, tc = tid % 16;   // 16x16 threads, 4x4 outputs each
-  float acc[4][4] = {};
+  const int tr = tid / 16, tc = tid % 16;   // 16x16 threads, R x R outputs each
+  float acc[R][R] = {};
   const int nk = (K + TK - 1) / TK;
-  GenStage<TIn> st;
+  GenStage<TIn, T> st;
   st.load(A, sam, sak, B, sbk, sbn, M, N, K, bm, bn, 0, tid);
   st.store(As[0], Bs[0], sak, sbn, tid);
   __syncthreads();
@@ -68,21 +72,21 @@ __global__ __launch_bounds__(NTH) void gemm_generic_kernel(
     if (t + 1 < nk) st.load(A, sam, sak, B, sbk, sbn, M, N, K, bm, bn, (t + 1) * TK, tid);
 #pragma unroll 8
     for (int kk = 0; kk < TK; ++kk) {
-      float a[4], b[4];
+      float a[R], b[R];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) { a[i] = As[cur][kk][tr + 16 * i]; b[i] = Bs[cur][kk][tc + 16 * i]; }
+      for (int i = 0; i < R; ++i) { a[i] = As[cur][kk][tr + 16 * i]; b[i] = Bs[cur][kk][tc + 16 * i]; }
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < R; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = fmaf(a[i], b[j], acc[i][j]);
+        for (int j = 0; j < R; ++j) acc[i][j] = fmaf(a[i], b[j], acc[i][j]);
     }
     if (t + 1 < nk) st.store(As[cur ^ 1], Bs[cur ^ 1], sak, sbn, tid);
     __syncthreads();
   }
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < R; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
+    for (int j = 0; j < R; ++j) {
       const int m = bm + tr + 16 * i, n = bn + tc + 16 * j;
       if (m < M && n < N) epilogue_store<TOut>(e, C, ldc, m, n, acc[i][j]);
     }
@@ -153,10 +157,18 @@ extern "C" int cmhar_gemm_generic(int in_dtype, int out_dtype, int M, int N, int
   e.alpha = 1.f;
   if (epi) e = *epi;                                   // NULL = the plain product
   if (e.rowsum) return -3;                             // row sums: 256-tile bf16 weight-gradient path only
-  dim3 grid(cdiv(N, TN), cdiv(M, TM), batch);
-#define LAUNCH(TI, TO)                                                                                     \
-  gemm_generic_kernel<TI, TO><<<grid, 256, 0, stream>>>(M, N, K, (const TI*)A, sam, sak, sAb, (const TI*)B, \
-                                                        sbk, sbn, sBb, (TO*)C, ldc, sCb, e)
+  // few 64² tiles (the IMU encoder's token GEMMs: M = 13·batch): 32² tiles for 4x the workgroups
+  const bool small = (long)cdiv(N, TN) * cdiv(M, TM) * batch < 128;
+  dim3 grid(cdiv(N, TN), cdiv(M, TM), batch), grid32(cdiv(N, 32), cdiv(M, 32), batch);
+#define LAUNCH(TI, TO)                                                                                          \
+  do {                                                                                                          \
+    if (small)                                                                                                  \
+      gemm_generic_kernel<TI, TO, 32><<<grid32, 256, 0, stream>>>(M, N, K, (const TI*)A, sam, sak, sAb,        \
+                                                                  (const TI*)B, sbk, sbn, sBb, (TO*)C, ldc, sCb, e); \
+    else                                                                                                        \
+      gemm_generic_kernel<TI, TO><<<grid, 256, 0, stream>>>(M, N, K, (const TI*)A, sam, sak, sAb, (const TI*)B, \
+                                                            sbk, sbn, sBb, (TO*)C, ldc, sCb, e);                \
+  } while (0)
   if (in_dtype == CMHAR_F32 && out_dtype == CMHAR_F32) LAUNCH(float, float);
   else if (in_dtype == CMHAR_BF16 && out_dtype == CMHAR_BF16) LAUNCH(bf16, bf16);
   else if (in_dtype == CMHAR_BF16 && out_dtype == CMHAR_F32) LAUNCH(bf16, float);
