@@ -177,8 +177,8 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(int M, int N, const T* __re
   }
   __syncthreads();
   for (int c = threadIdx.x; c < N; c += 256) {
-    pgamma[(long)blockIdx.x * N + c] = red[0][0][c] + red[0][1][c] + red[0][2][c] + red[0][3][c];
-    pbeta[(long)blockIdx.x * N + c] = red[1][0][c] + red[1][1][c] + red[1][2][c] + red[1][3][c];
+    pgamma[(long)blockIdx.x * 2 * N + c] = red[0][0][c] + red[0][1][c] + red[0][2][c] + red[0][3][c];
+    pbeta[(long)blockIdx.x * 2 * N + c] = red[1][0][c] + red[1][1][c] + red[1][2][c] + red[1][3][c];
   }
 }
 
@@ -236,6 +236,27 @@ __global__ __launch_bounds__(256) void colsum_final_kernel(int chunks, int N, co
   if (g == 0 && col < N) {
     const float t = red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane];
     out[col] = alpha * t + (beta != 0.f ? beta * out[col] : 0.f);
+  }
+}
+
+// As colsum_final_kernel over [chunks][2*N2] partials whose columns [0, N2) go to out0 and [N2, 2*N2) to out1
+// (the interleaved dγ | dβ partial rows of the LayerNorm backward: one launch reduces both).
+__global__ __launch_bounds__(256) void colsum_final2_kernel(int chunks, int N2, const float* __restrict__ part,
+                                                            float* __restrict__ out0, float* __restrict__ out1,
+                                                            float beta) {
+  __shared__ float red[4][64];
+  const int lane = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const int N = 2 * N2;
+  const int col = blockIdx.x * 64 + lane;
+  float s = 0.f;
+  if (col < N)
+    for (int c = g; c < chunks; c += 4) s += part[(long)c * N + col];
+  red[g][lane] = s;
+  __syncthreads();
+  if (g == 0 && col < N) {
+    const float t = red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane];
+    float* o = col < N2 ? out0 + col : out1 + (col - N2);
+    *o = t + (beta != 0.f ? beta * *o : 0.f);
   }
 }
 
@@ -373,6 +394,19 @@ static void reduce_rows(const float* part, int rows, int N, float* out, float al
   }
 }
 
+// dγ and dβ from interleaved partial rows [rows][dγ(N) | dβ(N)] in one (or two, for many rows) launches.
+static void reduce_rows_gb(const float* part, int rows, int N, float* dgamma, float* dbeta, float beta,
+                           float* scratch, hipStream_t st) {
+  if (rows > 32) {
+    const int chunks = cdiv(rows, CS_ROWS);
+    colsum_partial_kernel<float><<<dim3(cdiv(2 * N, 64 * CS_VEC), chunks), 256, 0, st>>>(rows, 2 * N, part, 2 * N,
+                                                                                         CS_ROWS, scratch);
+    colsum_final2_kernel<<<cdiv(2 * N, 64), 256, 0, st>>>(chunks, N, scratch, dgamma, dbeta, beta);
+  } else {
+    colsum_final2_kernel<<<cdiv(2 * N, 64), 256, 0, st>>>(rows, N, part, dgamma, dbeta, beta);
+  }
+}
+
 // Vectorised LayerNorm backward for N % 256 == 0 (VideoMAE hidden 768): 8 waves per block, rows grid-strided over
 // all waves; each lane owns N/256 groups of 4 consecutive columns (8-B bf16 / 16-B fp32 loads), the next row's dy,
 // h and residual gradient prefetched into registers under the current row's math.
@@ -450,8 +484,8 @@ __global__ __launch_bounds__(512) void ln_bwd_vec_kernel(int M, const T* __restr
     float sg = 0.f, sb = 0.f;
 #pragma unroll
     for (int w = 0; w < LNV_WAVES; ++w) { sg += red[0][w][c]; sb += red[1][w][c]; }
-    pgamma[(long)blockIdx.x * N + c] = sg;
-    pbeta[(long)blockIdx.x * N + c] = sb;
+    pgamma[(long)blockIdx.x * 2 * N + c] = sg;
+    pbeta[(long)blockIdx.x * 2 * N + c] = sb;
   }
 }
 
@@ -463,7 +497,7 @@ static int ln_bwd_blocks(int M, int N, bool vec) {
 // Number of fp32 floats the caller must provide in `ws` for cmhar_layernorm_bwd (upper bound over both paths).
 extern "C" long cmhar_layernorm_bwd_ws(int M, int N) {
   const int blocks = std::max(ln_bwd_blocks(M, N, false), ln_bwd_blocks(M, N, true));
-  return 2L * blocks * N + 2 * reduce_rows_ws(blocks, N);
+  return 2L * blocks * N + reduce_rows_ws(blocks, 2 * N);
 }
 
 // dgamma/dbeta are written as out = Σ + beta_acc * out (beta_acc = 1 to accumulate into existing grads).
@@ -476,9 +510,9 @@ extern "C" int cmhar_layernorm_bwd(int dtype, int M, int N, const void* dy, long
   if (N > 64 * MAXPER) return -1;
   const bool vec = !db_out && ln_vec_ok(N, lddy, ldh, lddh) && (!dres || ldres % 4 == 0);
   const int blocks = ln_bwd_blocks(M, N, vec);
-  float* pg = ws;
-  float* pb = ws + (long)blocks * N;
-  float* scr = pb + (long)blocks * N;
+  float* pg = ws;                                       // partial rows [blocks][dγ | dβ], row stride 2N
+  float* pb = ws + N;
+  float* scr = ws + 2L * blocks * N;
   if (vec) {
 #define LV(TT, G)                                                                                             \
   ln_bwd_vec_kernel<TT, G><<<blocks, 512, 0, st>>>(M, (const TT*)dy, lddy, (const TT*)h, ldh, gamma, mean, rstd, \
@@ -500,8 +534,7 @@ extern "C" int cmhar_layernorm_bwd(int dtype, int M, int N, const void* dy, long
                                                  lddb, pdrop, seed, pg, pb);
   }
   CMHAR_CHECK_LAUNCH();
-  reduce_rows(pg, blocks, N, dgamma, 1.f, beta_acc, scr, st);
-  reduce_rows(pb, blocks, N, dbeta, 1.f, beta_acc, scr + reduce_rows_ws(blocks, N), st);
+  reduce_rows_gb(pg, blocks, N, dgamma, dbeta, beta_acc, scr, st);
   CMHAR_CHECK_LAUNCH();
   return 0;
 }
