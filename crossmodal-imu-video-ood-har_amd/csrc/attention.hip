@@ -494,7 +494,7 @@ __device__ __forceinline__ float drop_scale(unsigned long long seed, float p, un
 }
 
 template <typename T, int D>
-__global__ void attn_fwd_f32(int H, int Lq, int Lk, const T* __restrict__ Q, long ldq, const T* __restrict__ K,
+__global__ __launch_bounds__(64) void attn_fwd_f32(int H, int Lq, int Lk, const T* __restrict__ Q, long ldq, const T* __restrict__ K,
                              long ldk, const T* __restrict__ V, long ldv, T* __restrict__ O, long ldo,
                              float* __restrict__ lse, float scale, float pdrop, unsigned long long seed) {
   const int hd = blockIdx.y, b = blockIdx.z;
@@ -539,7 +539,7 @@ __global__ void attn_fwd_f32(int H, int Lq, int Lk, const T* __restrict__ Q, lon
 }
 
 template <typename T, int D>
-__global__ void attn_bwd_dq_f32(int H, int Lq, int Lk, const T* __restrict__ Q, long ldq, const T* __restrict__ K,
+__global__ __launch_bounds__(64) void attn_bwd_dq_f32(int H, int Lq, int Lk, const T* __restrict__ Q, long ldq, const T* __restrict__ K,
                                 long ldk, const T* __restrict__ V, long ldv, const T* __restrict__ O, long ldo,
                                 const T* __restrict__ dO, long lddo, const float* __restrict__ lse,
                                 float* __restrict__ delta_out, T* __restrict__ dQ, long lddq, float scale,
@@ -588,7 +588,7 @@ __global__ void attn_bwd_dq_f32(int H, int Lq, int Lk, const T* __restrict__ Q, 
 }
 
 template <typename T, int D>
-__global__ void attn_bwd_dkdv_f32(int H, int Lq, int Lk, const T* __restrict__ Q, long ldq,
+__global__ __launch_bounds__(64) void attn_bwd_dkdv_f32(int H, int Lq, int Lk, const T* __restrict__ Q, long ldq,
                                   const T* __restrict__ K, long ldk, const T* __restrict__ V, long ldv,
                                   const T* __restrict__ dO, long lddo, const float* __restrict__ lse,
                                   const float* __restrict__ delta, T* __restrict__ dK, long lddk,
