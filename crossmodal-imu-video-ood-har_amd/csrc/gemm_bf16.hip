@@ -334,31 +334,46 @@ __device__ __forceinline__ int mc_off512(int k, int chunk) { return k * 512 + ((
 
 typedef __attribute__((address_space(3))) void* lds_void_ptr;
 
-// Issue one of this wave's 4 LDS-DMA pieces (t = 0..3) of an operand tile (256 rows/cols x 64 k).
+// LDS-DMA source of one operand (256 rows/cols x 64 k per tile) as a BUFFER load: the scalar resource holds the
+// tile's K-slice origin (advanced per K-tile with two SALU ops), the per-lane byte offsets of this wave's 4 pieces
+// (swizzle included) are computed once, so issuing a piece costs no VALU at all (`buffer_load_dwordx4 … lds`).
+// (The `global_load_lds` form needs a 64-bit per-lane address per piece: 2 `v_lshl_add_u64` + a move each, 8 pieces
+// per wave per K-tile.)
 template <bool KC>
-__device__ __forceinline__ void dma_piece(const bf16* __restrict__ P, long ld, int r0, int k0, char* lds, int wave,
-                                          int lane, int t) {
-  const int i = wave * 4 + t;                              // 1 KiB piece index (32 per tile)
-  const bf16* src;
-  if (KC) {   // [256 rows][64 k]: piece = 8 rows of 128 B
-    const int row = 8 * i + (lane >> 3);
-    const int lc = (lane & 7) ^ ((row >> 1) & 7);
-    src = P + (long)(r0 + row) * ld + k0 + lc * 8;
-  } else {    // [64 k][256 cols]: piece = 2 k-rows of 512 B
-    const int k = 2 * i + (lane >> 5);
-    const int lc = (lane & 31) ^ mc_swz(k);
-    src = P + (long)(k0 + k) * ld + r0 + lc * 8;
-  }
-  __builtin_amdgcn_global_load_lds((const void*)src, (lds_void_ptr)(lds + i * 1024), 16, 0, 0);
-}
-
-// Issue this wave's 4 LDS-DMA instructions for one operand tile.
-template <bool KC>
-__device__ __forceinline__ void dma_tile(const bf16* __restrict__ P, long ld, int r0, int k0, char* lds, int wave,
-                                         int lane) {
+struct DmaSrc {
+  const char* base;   // operand + tile origin (bytes)
+  long kstride;       // bytes per k step
+  int voff[4];
+  __device__ __forceinline__ void init(const bf16* __restrict__ P, long ld, int r0, int wave, int lane) {
 #pragma unroll
-  for (int t = 0; t < 4; ++t) dma_piece<KC>(P, ld, r0, k0, lds, wave, lane, t);
-}
+    for (int t = 0; t < 4; ++t) {
+      const int i = wave * 4 + t;                          // 1 KiB piece index (32 per tile)
+      if (KC) {   // [256 rows][64 k]: piece = 8 rows of 128 B
+        const int row = 8 * i + (lane >> 3);
+        const int lc = (lane & 7) ^ ((row >> 1) & 7);
+        voff[t] = (int)(((long)row * ld + lc * 8) * 2);
+      } else {    // [64 k][256 cols]: piece = 2 k-rows of 512 B
+        const int k = 2 * i + (lane >> 5);
+        const int lc = (lane & 31) ^ mc_swz(k);
+        voff[t] = (int)(((long)k * ld + lc * 8) * 2);
+      }
+    }
+    base = (const char*)(KC ? P + (long)r0 * ld : P + r0);
+    kstride = KC ? 2 : ld * 2;
+  }
+  __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(int k0) const {
+    return __builtin_amdgcn_make_buffer_rsrc((void*)(base + (long)k0 * kstride), (short)0, 0x7fffffff, 0x00020000);
+  }
+  // Issue one of this wave's 4 pieces (t = 0..3).
+  __device__ __forceinline__ void piece(__amdgpu_buffer_rsrc_t r, char* lds, int wave, int t) const {
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void_ptr)(lds + (wave * 4 + t) * 1024), 16, voff[t], 0, 0, 0);
+  }
+  __device__ __forceinline__ void tile(int k0, char* lds, int wave) const {
+    const __amdgpu_buffer_rsrc_t r = rsrc(k0);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) piece(r, lds, wave, t);
+  }
+};
 
 template <bool KC>
 __device__ __forceinline__ bf16x8 frag256(const char* lds, int r0, int kk, int lane) {
@@ -378,7 +393,7 @@ __device__ __forceinline__ bf16x8 frag256(const char* lds, int r0, int kk, int l
 
 // MODE (ablation builds only, tools/debug): 0 = product; 3 = epilogue only (no K loop); 4 = K loop only (no
 // epilogue); 5 = LDS staging only; 6 = staging + plain bf16 stores; 7 = K loop without the LDS-DMA (stale
-// operands), no epilogue; 8 = K loop with the DMA pieces spread between the MFMAs, no epilogue.
+// operands), no epilogue; 8 = as 4 (the spread-DMA ablation it named is recorded in DESIGN.md).
 // NA: A-operand LDS buffers.  2 = tile k+1 streams in while tile k is consumed (A and B double-buffered, 128 KiB);
 // 3 = the A tile (the HBM-streamed activation panel) is fetched TWO tiles ahead — three 32 KiB A buffers + two
 // 32 KiB B buffers = the whole 160 KiB LDS — so its longer HBM/MALL latency has two K-tiles of MFMAs to hide under.
@@ -462,11 +477,15 @@ __global__ __launch_bounds__(NT2, 2) void gemm256_kernel(int M, int N, int K, co
   };
   auto a_buf = [&](int t) -> char* { return NA == 3 ? smem + (t % 3) * 32768 : smem + (t & 1) * 65536; };
   auto b_buf = [&](int t) -> char* { return NA == 3 ? smem + 98304 + (t & 1) * 32768 : smem + (t & 1) * 65536 + 32768; };
+  DmaSrc<A_KC> da;
+  DmaSrc<B_KC> db;
+  da.init(A, lda, bm, wave, lane);
+  db.init(B, ldb, bn, wave, lane);
   if (nk > 0) {
     if (MODE != 7) {
-      dma_tile<A_KC>(A, lda, bm, kbeg, a_buf(0), wave, lane);
-      dma_tile<B_KC>(B, ldb, bn, kbeg, b_buf(0), wave, lane);
-      if (NA == 3 && nk > 1) dma_tile<A_KC>(A, lda, bm, kbeg + TK2, a_buf(1), wave, lane);
+      da.tile(kbeg, a_buf(0), wave);
+      db.tile(kbeg, b_buf(0), wave);
+      if (NA == 3 && nk > 1) da.tile(kbeg + TK2, a_buf(1), wave);
     }
     if (NA == 3 && nk > 1) asm volatile("s_waitcnt vmcnt(4)\n\ts_barrier" ::: "memory");   // tile 0 landed
     else __syncthreads();
@@ -480,24 +499,24 @@ __global__ __launch_bounds__(NT2, 2) void gemm256_kernel(int M, int N, int K, co
     const bool more2 = NA == 3 && kt + 2 < nk;
     char* nxt = a_buf(kt + 1);
     char* nxt_b = b_buf(kt + 1);
-    if (NA == 3 && MODE != 7) {
-      // B(kt+1) first, A(kt+2) second: vmcnt counts in issue order, so waiting for B(kt+1) (and the A(kt+1) issued
-      // a tile earlier) can leave A(kt+2)'s 4 pieces in flight
-      if (more) dma_tile<B_KC>(B, ldb, bn, kbeg + (kt + 1) * TK2, nxt_b, wave, lane);
-      if (more2) dma_tile<A_KC>(A, lda, bm, kbeg + (kt + 2) * TK2, a_buf(kt + 2), wave, lane);
-    } else if (more && MODE != 7 && MODE != 8) {
-      dma_tile<A_KC>(A, lda, bm, kbeg + (kt + 1) * TK2, nxt, wave, lane);
-      dma_tile<B_KC>(B, ldb, bn, kbeg + (kt + 1) * TK2, nxt_b, wave, lane);
+    // B(kt+1) first, A(kt+2) second (NA = 3): vmcnt counts in issue order, so waiting for B(kt+1) (and the A(kt+1)
+    // issued a tile earlier) can leave A(kt+2)'s 4 pieces in flight.  (Spreading the 8 pieces one per 4-MFMA group
+    // instead of this burst measured neutral on forward/dgrad and 1.3-1.7x slower on the NA = 2 weight-gradient layout,
+    // whose vmcnt(0) then waits on the last, late piece.)
+    if (MODE != 7) {
+      if (NA == 3) {
+        if (more) db.tile(kbeg + (kt + 1) * TK2, nxt_b, wave);
+        if (more2) da.tile(kbeg + (kt + 2) * TK2, a_buf(kt + 2), wave);
+      } else if (more) {
+        da.tile(kbeg + (kt + 1) * TK2, nxt, wave);
+        db.tile(kbeg + (kt + 1) * TK2, nxt_b, wave);
+      }
     }
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bf0[j], acc[i][j], 0, 0, 0);
-      if (MODE == 8 && NA == 2 && more) {   // one DMA piece per 4 MFMAs: the issue cost interleaves with the MFMAs
-        if (i < 4) dma_piece<A_KC>(A, lda, bm, kbeg + (kt + 1) * TK2, nxt, wave, lane, i);
-        else dma_piece<B_KC>(B, ldb, bn, kbeg + (kt + 1) * TK2, nxt_b, wave, lane, i - 4);
-      }
       if (!A_KC && rs && wc == (i >> 1))
         accb[i & 1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], ones, accb[i & 1], 0, 0, 0);
       af[i] = frag256<A_KC>(a_s, wr * 128 + i * 16, 1, lane);
