@@ -1,7 +1,7 @@
-"""A/B two builds of libcmhar.so on every GEMM shape of the VideoMAE-B step in ONE process (interleaved rounds,
+"""A/B two (or more) builds of libcmhar.so on every GEMM shape of the VideoMAE-B step in ONE process (interleaved rounds,
 median per variant), so device/clock differences between boxes do not enter the comparison.
 
-    python tools/debug/gemm_ab.py path/to/libA.so path/to/libB.so [rounds]
+    python tools/debug/gemm_ab.py libA.so libB.so [libC.so ...] [--rounds R]
 """
 import ctypes as C
 import os
@@ -36,11 +36,17 @@ def timed(fn, reps=10):
 
 
 def main():
-    libs = [load(sys.argv[1]), load(sys.argv[2])]
-    rounds = int(sys.argv[3]) if len(sys.argv) > 3 else 7
+    args = sys.argv[1:]
+    rounds = 7
+    if '--rounds' in args:
+        i = args.index('--rounds')
+        rounds = int(args[i + 1])
+        del args[i:i + 2]
+    libs = [load(a) for a in args]
+    nv = len(libs)
     T = 50176
     lin = [('qkv', 2304, 768), ('out', 768, 768), ('fc1', 3072, 768), ('fc2', 768, 3072), ('embed', 768, 1536)]
-    tot = [0.0, 0.0]
+    tot = [0.0] * nv
     for name, n_out, n_in in lin:
         x = torch.randn(T, n_in, device='cuda').bfloat16()
         w = torch.randn(n_out, n_in, device='cuda').bfloat16()
@@ -55,25 +61,25 @@ def main():
             if name == 'embed' and tag == 'dgrad':
                 continue
             outs = []
-            for v in range(2):
+            for v in range(nv):
                 _lib._lib = libs[v]
                 for _ in range(3):
                     fn()
                 torch.cuda.synchronize()
                 outs.append(y.clone() if tag == 'fwd' else dx.clone() if tag == 'dgrad' else dw.clone())
-            same = torch.equal(outs[0], outs[1])
-            ts = [[], []]
+            same = all(torch.equal(outs[0], o) for o in outs[1:])
+            ts = [[] for _ in range(nv)]
             for _ in range(rounds):
-                for v in range(2):
+                for v in range(nv):
                     _lib._lib = libs[v]
                     ts[v].append(timed(fn))
             med = [statistics.median(t) for t in ts]
             mult = 1 if name == 'embed' else 12
-            for v in range(2):
+            for v in range(nv):
                 tot[v] += med[v] * mult
-            print(f'{name:6s} {tag:6s} A {med[0] * 1e3:8.1f} us {fl / med[0] / 1e9:6.0f} TF | B {med[1] * 1e3:8.1f} us '
-                  f'{fl / med[1] / 1e9:6.0f} TF | B/A {med[0] / med[1]:.3f}  bitwise-equal={same}', flush=True)
-    print(f'per-step GEMM total: A {tot[0]:.2f} ms  B {tot[1]:.2f} ms')
+            cols = ' | '.join(f'{chr(65 + v)} {med[v] * 1e3:7.1f} us {fl / med[v] / 1e9:5.0f} TF' for v in range(nv))
+            print(f'{name:6s} {tag:6s} {cols} | bitwise-equal={same}', flush=True)
+    print('per-step GEMM total: ' + '  '.join(f'{chr(65 + v)} {tot[v]:.2f} ms' for v in range(nv)))
 
 
 if __name__ == '__main__':
