@@ -13,6 +13,8 @@
 // and the tiny IMU attention (L = 13, d = 16), including counter-hash dropout regenerated in backward.
 #include "common.h"
 
+#include <type_traits>
+
 namespace {
 
 constexpr float LOG2E = 1.4426950408889634f;
@@ -143,8 +145,10 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_bf16(int H, int Lq, int Lk, i
   // A wave whose queries all lie past Lq (the ragged last workgroup of a head) still helps stage K/V tiles and
   // joins every barrier, but issues no MFMA / softmax work: its SIMD's matrix pipe goes to the co-resident waves.
   const bool active = q0 < Lq;
-  for (int kt = 0; kt < nt; ++kt) {
-    const int cur = kt & 1;
+  // One K/V tile; the LDS buffer index is a compile-time constant (the loop below runs the tiles in pairs), so
+  // every LDS address folds into the ds_read immediate offsets instead of a v_add per read.
+  auto tile = [&](auto CUR, int kt) __attribute__((always_inline)) {
+    constexpr int cur = decltype(CUR)::value;
     const bool more = kt + 1 < nt;
     // Sᵀ = K·Qᵀ for every q-block; each K fragment is read once and used QB times
     floatx16 s[QB][2];
@@ -233,6 +237,10 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_bf16(int H, int Lq, int Lk, i
       tv.store(Vs(cur ^ 1), tid);
     }
     __syncthreads();
+  };
+  for (int kt = 0; kt < nt; kt += 2) {
+    tile(std::integral_constant<int, 0>{}, kt);
+    if (kt + 1 < nt) tile(std::integral_constant<int, 1>{}, kt + 1);
   }
 #pragma unroll
   for (int j = 0; j < QB; ++j) {
@@ -313,8 +321,10 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_bf16(int H, int Lq, int 
   store_rows(0);
   __syncthreads();
   const bool active = k0 < Lk;      // waves past the last key only stage tiles and join barriers (see forward)
-  for (int qt = 0; qt < nt; ++qt) {
-    const int cur = qt & 1;
+  // one tile per call, LDS buffer index a compile-time constant (tiles run in pairs): LDS addresses fold into
+  // the ds_read immediate offsets
+  auto tile = [&](auto CUR, int qt) __attribute__((always_inline)) {
+    constexpr int cur = decltype(CUR)::value;
     const bool more = qt + 1 < nt;
     if (more) load_rows(qt + 1);
     const float* L_ = Ls + cur * 64;
@@ -353,6 +363,10 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_bf16(int H, int Lq, int 
     }
     if (more) store_rows(cur ^ 1);
     __syncthreads();
+  };
+  for (int qt = 0; qt < nt; qt += 2) {
+    tile(std::integral_constant<int, 0>{}, qt);
+    if (qt + 1 < nt) tile(std::integral_constant<int, 1>{}, qt + 1);
   }
   const int key = k0 + (lane & 31);
   if (key < Lk) {
@@ -422,8 +436,10 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_bf16(int H, int Lq, int Lk
   tv.store(Vs(0), tid);
   __syncthreads();
   const bool active = q0 < Lq;      // waves past the last query only stage tiles and join barriers (see forward)
-  for (int kt = 0; kt < nt; ++kt) {
-    const int cur = kt & 1;
+  // one tile per call, LDS buffer index a compile-time constant (tiles run in pairs): LDS addresses fold into
+  // the ds_read immediate offsets
+  auto tile = [&](auto CUR, int kt) __attribute__((always_inline)) {
+    constexpr int cur = decltype(CUR)::value;
     const bool more = kt + 1 < nt;
     if (more) {
       tk.load(Kb, ldk, (kt + 1) * 64, Lk, tid);
@@ -461,6 +477,10 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_bf16(int H, int Lq, int Lk
       tv.store(Vs(cur ^ 1), tid);
     }
     __syncthreads();
+  };
+  for (int kt = 0; kt < nt; kt += 2) {
+    tile(std::integral_constant<int, 0>{}, kt);
+    if (kt + 1 < nt) tile(std::integral_constant<int, 1>{}, kt + 1);
   }
   const int q = q0 + (lane & 31);
   if (q < Lq) {
