@@ -52,6 +52,26 @@ TRACE = Tracer()
 
 _GEMM_SYMBOL = {0: 'gemm_bf16_kernel<true,true,{o}>', 1: 'gemm_bf16_kernel<true,false,{o}>',
                 2: 'gemm_bf16_kernel<false,false,{o}>'}
+_PLAN = {}
+
+
+def _gemm_trace_name(layout, M, N, K, s, has_ws, rowsum, out_dtype):
+    """Trace label of a bf16 GEMM call: the kernel(s) the library's own plan (cmhar_gemm_bf16_plan) launches."""
+    key = (layout, M, N, K, s, has_ws, rowsum)
+    plan = _PLAN.get(key)
+    if plan is None:
+        plan = _PLAN[key] = int(L.lib().cmhar_gemm_bf16_plan(layout, M, N, K, s, int(has_ws), int(rowsum)))
+    o = 'float' if (plan in (3, 5) or out_dtype == torch.float32) else 'bf16'
+    if plan == 4:
+        return f'gemm8p_kernel<{"true" if layout == 0 else "false"},{o}>'
+    name = _GEMM_SYMBOL[layout].format(o=o)
+    if plan in (1, 2, 3):
+        name = name.replace('gemm_bf16_kernel', 'gemm256_kernel')
+    if plan == 2:
+        name += '+tail_reduce'
+    elif plan in (3, 5):
+        name += '+splitk_reduce'
+    return name
 
 # ------------------------------------------------------------------------------------------------------------
 # workspaces (one growing fp32 buffer per (device, stream))
@@ -191,11 +211,7 @@ def gemm(layout: int, a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, *, bi
                 ws = workspace(n, out.device)
         ev = name = None
         if TRACE.active:
-            name = _GEMM_SYMBOL[layout].format(o='float' if (s > 1 or out.dtype == torch.float32) else 'bf16')
-            if M % 256 == 0 and N % 256 == 0 and K % 64 == 0:
-                name = name.replace('gemm_bf16_kernel', 'gemm256_kernel')
-            if s > 1:
-                name += '+splitk_reduce'
+            name = _gemm_trace_name(layout, M, N, K, s, ws is not None, rowsum is not None, out.dtype)
             ev = TRACE.begin(name)
         call('cmhar_gemm_bf16', layout, L.dtype_code(out.dtype), M, N, K, ptr(a), a.stride(0), ptr(b), b.stride(0),
              ptr(out), out.stride(0), C.byref(epi), s, ptr(ws), st)

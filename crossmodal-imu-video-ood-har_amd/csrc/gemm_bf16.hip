@@ -618,6 +618,199 @@ __global__ __launch_bounds__(NT2, 2) void gemm256_kernel(int M, int N, int K, co
   }
 }
 
+// ---------------------------------------------------------------------------------------------------------------
+// Forward and dgrad layouts (A K-contiguous), whole K: the same 256² tile and wave layout, but the K loop is an
+// 8-interval-per-K-tile ping-pong.  The two wave groups (wr = 0: waves 0-3, wr = 1: waves 4-7 — one of each on
+// every SIMD) run one barrier interval apart, so in every interval one wave of each SIMD issues its 16 MFMAs (one
+// 64x32 quadrant of its 128x64 block, K = 64, at s_setprio 1) while the other issues its LDS fragment reads and
+// LDS-DMA pieces.  Per K-tile a wave runs 4 phases = quadrants (0,0) (0,1) (1,1) (1,0), reading A0+B0, B1, A1,
+// nothing.  Staging: K-tile t+1's A lower half is DMA'd in phase 1 of t, both B halves in phase 2; after phase 4's
+// vmcnt(0) (everything of t+1 landed) the A upper half of t+2 is issued into the buffer t just finished with (its
+// last read was group 0's phase 3, two intervals earlier).  Every region is restaged >= 2 intervals after its last
+// read and read >= 1 interval after the wait that retires it.  (Measured against gemm256_kernel in one process,
+// tools/debug/gemm_ab.py: forward 5-6 % faster at K = 768-1536; bit-identical — each output's k order is unchanged.)
+// ---------------------------------------------------------------------------------------------------------------
+// Per-lane offsets of this wave's 2 pieces of each half of an operand tile.  K-contiguous [256 rows][64 k]: half h =
+// rows 128h..128h+127.  Row-contraction [64 k][256 cols] (the dgrad weight operand): half h = k rows 32h..32h+31.
+template <bool KC>
+struct DmaHalf {
+  const char* base;
+  long kstride;
+  int voff[2][2];
+  __device__ __forceinline__ void init(const bf16* __restrict__ P, long ld, int r0, int wave, int lane) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const int i = 16 * h + 2 * wave + t;                   // 1 KiB piece index within the tile image
+        if (KC) {
+          const int row = 8 * i + (lane >> 3);
+          const int lc = (lane & 7) ^ ((row >> 1) & 7);
+          voff[h][t] = (int)(((long)row * ld + lc * 8) * 2);
+        } else {
+          const int k = 2 * i + (lane >> 5);
+          const int lc = (lane & 31) ^ mc_swz(k);
+          voff[h][t] = (int)(((long)k * ld + lc * 8) * 2);
+        }
+      }
+    base = (const char*)(KC ? P + (long)r0 * ld : P + r0);
+    kstride = KC ? 2 : ld * 2;
+  }
+  __device__ __forceinline__ void half(int k0, char* lds, int h, int wave) const {
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void*)(base + (long)k0 * kstride), (short)0,
+                                                                       0x7fffffff, 0x00020000);
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void_ptr)(lds + (16 * h + 2 * wave + t) * 1024), 16,
+                                               voff[h][t], 0, 0, 0);
+  }
+};
+
+template <bool B_KC, typename OutT>
+__global__ __launch_bounds__(NT2, 2) void gemm8p_kernel(int M, int N, int K, const bf16* __restrict__ A, long lda,
+                                                        const bf16* __restrict__ B, long ldb, OutT* __restrict__ C,
+                                                        long ldc, Epilogue e) {
+  __shared__ __attribute__((aligned(16))) char smem[SMEM2];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave >> 2, wc = wave & 3;
+  const int tiles_n = N / TN2;
+  const int bid = xcd_remap(blockIdx.x, (M / TM2) * tiles_n);
+  const int bm = (bid / tiles_n) * TM2, bn = (bid % tiles_n) * TN2;
+  const int nk = K / TK2;   // >= 2 (host-checked)
+  DmaHalf<true> da;
+  DmaHalf<B_KC> db;
+  da.init(A, lda, bm, wave, lane);
+  db.init(B, ldb, bn, wave, lane);
+  // buffer b: A image [256][64] at b*64 KiB, B image at b*64 KiB + 32 KiB
+  auto abuf = [&](int t) -> char* { return smem + (t & 1) * 65536; };
+  auto bbuf = [&](int t) -> char* { return smem + (t & 1) * 65536 + 32768; };
+
+  floatx4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+  bf16x8 af[2][4], b0[2][2], b1[2][2];
+
+  // prologue: K-tile 0 whole + K-tile 1's A upper half; wait for tile 0
+  da.half(0, abuf(0), 0, wave);
+  da.half(0, abuf(0), 1, wave);
+  db.half(0, bbuf(0), 0, wave);
+  db.half(0, bbuf(0), 1, wave);
+  da.half(TK2, abuf(1), 0, wave);
+  asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  if (wr == 1) __builtin_amdgcn_s_barrier();   // group 1 runs one interval behind
+  __builtin_amdgcn_sched_barrier(0);
+
+#define MFMA_Q(QM, BF)                                                                                        \
+  do {                                                                                                        \
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                                                        \
+    __builtin_amdgcn_sched_barrier(0);                                                                        \
+    __builtin_amdgcn_s_setprio(1);                                                                            \
+    _Pragma("unroll") for (int kk = 0; kk < 2; ++kk)                                                          \
+    _Pragma("unroll") for (int i = 0; i < 4; ++i)                                                             \
+    _Pragma("unroll") for (int j = 0; j < 2; ++j)                                                             \
+      acc[(QM) * 4 + i][qn_ * 2 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[kk][i], BF[kk][j],           \
+                                                                             acc[(QM) * 4 + i][qn_ * 2 + j], 0, 0, 0); \
+    __builtin_amdgcn_s_setprio(0);                                                                            \
+    __builtin_amdgcn_sched_barrier(0);                                                                        \
+    __builtin_amdgcn_s_barrier();                                                                             \
+    __builtin_amdgcn_sched_barrier(0);                                                                        \
+  } while (0)
+#define END_LOADS()                                                                                           \
+  do {                                                                                                        \
+    __builtin_amdgcn_sched_barrier(0);                                                                        \
+    __builtin_amdgcn_s_barrier();                                                                             \
+    __builtin_amdgcn_sched_barrier(0);                                                                        \
+  } while (0)
+
+  for (int t = 0; t < nk; ++t) {
+    const char* as = abuf(t);
+    const char* bs = bbuf(t);
+    const bool n1 = t + 1 < nk, n2 = t + 2 < nk;
+    const int k1 = (t + 1) * TK2, k2 = (t + 2) * TK2;
+    // phase 1: A0 + B0, stage A lower half of t+1; MFMA quadrant (0,0)
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j) b0[kk][j] = frag256<B_KC>(bs, wc * 64 + j * 16, kk, lane);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) af[kk][i] = frag256<true>(as, wr * 128 + i * 16, kk, lane);
+    }
+    if (n1) da.half(k1, abuf(t + 1), 1, wave);
+    END_LOADS();
+    {
+      constexpr int qn_ = 0;
+      MFMA_Q(0, b0);
+    }
+    // phase 2: B1, stage both B halves of t+1; quadrant (0,1)
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) b1[kk][j] = frag256<B_KC>(bs, wc * 64 + 32 + j * 16, kk, lane);
+    if (n1) {
+      db.half(k1, bbuf(t + 1), 0, wave);
+      db.half(k1, bbuf(t + 1), 1, wave);
+    }
+    END_LOADS();
+    {
+      constexpr int qn_ = 1;
+      MFMA_Q(0, b1);
+    }
+    // phase 3: A1 (its 8 reads are the phase's load work); quadrant (1,1)
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) af[kk][i] = frag256<true>(as, wr * 128 + 64 + i * 16, kk, lane);
+    END_LOADS();
+    {
+      constexpr int qn_ = 1;
+      MFMA_Q(1, b1);
+    }
+    // phase 4: no reads; all of t+1 landed (own pieces), then A upper half of t+2; quadrant (1,0)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (n2) da.half(k2, abuf(t + 2), 0, wave);
+    END_LOADS();
+    {
+      constexpr int qn_ = 0;
+      MFMA_Q(1, b0);
+    }
+  }
+#undef MFMA_Q
+#undef END_LOADS
+  if (wr == 0) __builtin_amdgcn_s_barrier();   // re-align the groups
+  __syncthreads();
+
+  // epilogue: as gemm256_kernel — per wave, two passes of 64x64 through a private LDS slab, 16-B stores
+  float* T = (float*)(smem + wave * 64 * EPI2_LD * 4);
+#pragma unroll
+  for (int pass = 0; pass < 2; ++pass) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          T[(i * 16 + 4 * (lane >> 4) + r) * EPI2_LD + j * 16 + (lane & 15)] = acc[pass * 4 + i][j][r];
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    const int cg = (lane & 7) * 8;
+    const int n0 = bn + wc * 64 + cg;
+#pragma unroll 2
+    for (int it = 0; it < 8; ++it) {
+      const int rr = it * 8 + (lane >> 3);
+      const int m = bm + wr * 128 + pass * 64 + rr;
+      const floatx4 lo = *(const floatx4*)&T[rr * EPI2_LD + cg], hi = *(const floatx4*)&T[rr * EPI2_LD + cg + 4];
+      float v[8];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) { v[j] = lo[j]; v[4 + j] = hi[j]; }
+      epilogue_store8<OutT>(e, C, ldc, m, n0, v);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  }
+}
+
 // Tail split for a whole-K 256² GEMM whose tile count leaves the last round of the chip mostly empty: keep full
 // rounds data-parallel and split the remaining tile rows along K to fill the last round.
 constexpr int kCUs = 256;
@@ -649,6 +842,40 @@ static TailSplit tail_split(int M, int N, int K) {
   return t;
 }
 
+// 8-phase ping-pong kernel for the forward layout; CMHAR_GEMM_8P=0/1 overrides the build default (A/B measurements).
+#ifndef CMHAR_GEMM_8P_DEFAULT
+#define CMHAR_GEMM_8P_DEFAULT 1
+#endif
+static bool use_8p() {
+  static const bool v = [] {
+    const char* s = getenv("CMHAR_GEMM_8P");
+    return s ? atoi(s) != 0 : CMHAR_GEMM_8P_DEFAULT != 0;
+  }();
+  return v;
+}
+
+// The dgrad layout (B row-contraction, transposed fragment reads) builds and is exact on the same kernel, but measured
+// 11 % slower on FC2 dgrad and neutral elsewhere: off unless CMHAR_GEMM_8P_DGRAD=1 at build time.
+#ifndef CMHAR_GEMM_8P_DGRAD
+#define CMHAR_GEMM_8P_DGRAD 0
+#endif
+static bool use_8p_dgrad() { return CMHAR_GEMM_8P_DGRAD != 0; }
+
+// Which kernel(s) a cmhar_gemm_bf16 call launches (also exported for trace labels: cmhar_gemm_bf16_plan).
+enum GemmPlan { PLAN_128 = 0, PLAN_256 = 1, PLAN_256_TAIL = 2, PLAN_256_SPLITK = 3, PLAN_8P = 4, PLAN_128_SPLITK = 5 };
+static int gemm_plan(bool ak, bool bkc, int M, int N, int K, int splits, bool has_ws, bool rowsum) {
+  const bool big = M % TM2 == 0 && N % TN2 == 0 && K % TK2 == 0;
+  if (!big) {
+    const int klen = splits > 1 ? cdiv(cdiv(K, splits), BK) * BK : K;
+    return cdiv(K, klen) > 1 ? PLAN_128_SPLITK : PLAN_128;
+  }
+  const int klen = splits > 1 ? cdiv(cdiv(K, splits), TK2) * TK2 : K;
+  if (cdiv(K, klen) > 1) return PLAN_256_SPLITK;
+  if (has_ws && !rowsum && tail_split(M, N, K).n_dp > 0) return PLAN_256_TAIL;   // (8-phase instead: FC2 fwd 5 % slower)
+  if (ak && K >= 2 * TK2 && use_8p() && (bkc || use_8p_dgrad())) return PLAN_8P;
+  return PLAN_256;
+}
+
 template <bool AK, bool BKc, typename OutT>
 int launch(int M, int N, int K, const bf16* A, long lda, const bf16* B, long ldb, OutT* C, long ldc,
            const Epilogue& e, int splits, float* ws, hipStream_t st) {
@@ -664,14 +891,17 @@ int launch(int M, int N, int K, const bf16* A, long lda, const bf16* B, long ldb
     if (splits > 1) klen = cdiv(cdiv(K, splits), TK2) * TK2;
     const int nsplit = cdiv(K, klen);
     dim3 grid((M / TM2) * (N / TN2), 1, nsplit);
-    const TailSplit ts = tail_split(M, N, K);
-    if (nsplit == 1 && ws && ts.n_dp > 0 && !e.rowsum) {
+    const int plan = gemm_plan(AK, BKc, M, N, K, splits, ws != nullptr, e.rowsum != nullptr);
+    if (plan == PLAN_256_TAIL) {
+      const TailSplit ts = tail_split(M, N, K);
       gemm256_kernel<AK, BKc, OutT, 0, kNA><<<ts.n_dp + ts.n_sk, NT2, 0, st>>>(M, N, K, A, lda, B, ldb, C, ldc, e, K, 0, 0, ws,
                                                                       ts.n_dp, ts.sk_klen);
       const int tail_rows = M - ts.tail_m0;
       splitk_reduce_kernel<OutT><<<reduce_blocks(tail_rows, N), 256, 0, st>>>(
           tail_rows, N, ts.nsplit, ws, (long)tail_rows * N, C, ldc, e, ts.tail_m0);
-    } else if (nsplit == 1) {
+    } else if (plan == PLAN_8P) {
+      gemm8p_kernel<BKc, OutT><<<grid, NT2, 0, st>>>(M, N, K, A, lda, B, ldb, C, ldc, e);
+    } else if (plan == PLAN_256) {
       gemm256_kernel<AK, BKc, OutT, 0, kNA><<<grid, NT2, 0, st>>>(M, N, K, A, lda, B, ldb, C, ldc, e, klen, 0, 0, nullptr, 0, 0);
     } else {
       gemm256_kernel<AK, BKc, float, 0, kNA><<<grid, NT2, 0, st>>>(M, N, K, A, lda, B, ldb, ws, N, e, klen, ss, 1, nullptr, 0,
@@ -707,6 +937,13 @@ int launch(int M, int N, int K, const bf16* A, long lda, const bf16* B, long ldb
 extern "C" long cmhar_gemm_bf16_ws(int M, int N, int K) {
   const TailSplit t = tail_split(M, N, K);
   return t.n_dp > 0 ? (long)t.nsplit * (M - t.tail_m0) * N : 0;
+}
+
+// The kernel plan of a cmhar_gemm_bf16 call with these arguments (GemmPlan: 0 = 128² tile, 1 = 256² tile, 2 = 256²
+// + tail split + reduce, 3 = 256² split-K + reduce, 4 = 8-phase 256², 5 = 128² split-K + reduce), -1 on a bad layout.
+extern "C" int cmhar_gemm_bf16_plan(int layout, int M, int N, int K, int splits, int has_ws, int rowsum) {
+  if (layout < 0 || layout > 2) return -1;
+  return gemm_plan(layout != 2, layout == 0, M, N, K, splits, has_ws != 0, rowsum != 0);
 }
 
 // layout: 0 = NT (A K-contig, B K-contig: Y = X Wᵀ), 1 = NN (A K-contig, B N-contig: dX = dY W),

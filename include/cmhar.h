@@ -60,6 +60,10 @@ int cmhar_gemm_bf16(int layout, int out_dtype, int M, int N, int K, const void* 
  * half full, the full rounds run whole-K and the remaining tile rows are split along K (partials in ws, reduced
  * with the epilogue).  0 = no workspace needed; a call with ws == NULL always runs whole-K. */
 long cmhar_gemm_bf16_ws(int M, int N, int K);
+/* The kernel plan cmhar_gemm_bf16 would run for these arguments (has_ws: ws != NULL; rowsum: epi->rowsum set):
+ * 0 = 128² tile, 1 = 256² tile, 2 = 256² + tail split + reduce, 3 = 256² split-K + reduce, 4 = 8-phase 256²
+ * (forward layout), 5 = 128² split-K + reduce; -1 = bad layout.  Used for trace labels (bench.py kernel breakdown). */
+int cmhar_gemm_bf16_plan(int layout, int M, int N, int K, int splits, int has_ws, int rowsum);
 
 /* Exact-fp32 (or mixed) strided batched GEMM: C[z][m,n] = epi(Σ_k A[z][m*sam+k*sak] B[z][k*sbk+n*sbn])
  * (replaces: the fp32 nn.Linear / IMU encoder / ProjectionHead matmuls, models.py:16-132, 221-234). */
