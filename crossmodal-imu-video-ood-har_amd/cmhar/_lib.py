@@ -71,6 +71,14 @@ _SIGS = {
     'cmhar_mt_grad_norm': (i32, [vp, vp, i32, vp, vp, f32, i32, vp]),
     'cmhar_mt_adamw': (i32, [vp, vp, i32, f32, f32, f32, f32, f32, f32, f32, vp, vp]),
     'cmhar_mt_cast_bf16': (i32, [vp, vp, i32, vp]),
+    'cmhar_conv3d_im2col': (i32, [i32, i32, vp, vp, vp, vp]),
+    'cmhar_conv3d_col2im': (i32, [i32, vp, vp, vp, i32, vp]),
+    'cmhar_bn_cl_ws': (i64, [i64, i32]),
+    'cmhar_bn_cl_fwd': (i32, [i32, i64, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, i32, f32, f32, i32, vp, vp, vp]),
+    'cmhar_bn_cl_bwd': (i32, [i32, i64, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, vp, vp]),
+    'cmhar_avgpool_cl': (i32, [i32, i32, i64, i32, vp, vp, vp]),
+    'cmhar_avgpool_cl_bwd': (i32, [i32, i32, i64, i32, vp, vp, vp]),
+    'cmhar_video_to_ndhwc': (i32, [i32, i32, i32, i32, i32, i32, vp, vp, vp]),
 }
 
 EXPORTED = tuple(_SIGS)

@@ -21,6 +21,7 @@ import torch.nn as nn
 from . import kernels as K
 from .heads import ProjectionHead, l2_normalize, run_head, _Seeds
 from .imu import IMUEncoder, PatchEmbedding
+from .r3d import R3D18, run_r3d
 from .videomae import VideoMAEBackbone, default_videomae_config, run_backbone
 
 __all__ = ['PatchEmbedding', 'IMUEncoder', 'VideoEncoder', 'ProjectionHead', 'CrossModalModel', 'IMUClassifier']
@@ -84,6 +85,10 @@ class VideoEncoder(nn.Module):
                                   f'initialised backbone of the configured geometry')
                 self.backbone = VideoMAEBackbone(_videomae_geometry(config), compute_dtype=dt)
             self.feature_dim = self.backbone.config.hidden_size
+        elif vb == 'r3d_18':
+            # north_star extension (no reference code): torchvision-layout R3D-18 on the HIP conv3d path
+            self.backbone = R3D18(None, compute_dtype=dt)
+            self.feature_dim = self.backbone.feature_dim
         elif vb in ('resnet18', 'mobilenet_v2'):
             raise NotImplementedError(f'{vb}: per-frame 2-D CNN backbones are not on the accelerated path '
                                       f'(torchvision is absent; see DESIGN.md scope)')
@@ -95,6 +100,8 @@ class VideoEncoder(nn.Module):
         """x (B, T, C, H, W) → (B, video_d_model)."""
         if x.dim() != 5:
             raise ValueError(f'expected (B, T, C, H, W) video, got {tuple(x.shape)}')
+        if not self.is_videomae:                                  # r3d_18: pooled 3-D CNN features
+            return linear_fp32(run_r3d(self.backbone, x, self.training), self.projection)
         feat = run_backbone(self.backbone, x, token0_only=True)   # last_hidden_state[:, 0]  (models.py:201)
         return linear_fp32(feat, self.projection)                 # models.py:202
 

@@ -1,0 +1,295 @@
+"""R3D-18 video backbone on the cmhar HIP library (north_star extension "VideoEncoder 3D-conv/R3D").
+
+The reference has no 3-D CNN (its CNN options are per-frame 2-D torchvision models, `models.py:160-216`, and
+torchvision is absent here), so this module follows torchvision's `models.video.r3d_18` architecture and
+state_dict names (`stem.0.weight`, `layer{i}.{j}.conv{1,2}.{0,1}.*`, `layer{i}.0.downsample.{0,1}.*`): BasicStem
+Conv3d(3,64,(3,7,7),s=(1,2,2),p=(1,3,3)) + BN + ReLU, four stages of two BasicBlocks (64/128/256/512 channels,
+stride 2 at stages 2-4 with a 1x1x1 strided downsample), global average pool; `fc` is dropped (the encoder's own
+projection follows).  Parity: unpinned w.r.t. the reference (no reference code); checked against the CPU
+restatement `oracle/r3d_cpu.py` (F.conv3d / F.batch_norm) in tests/test_r3d_gpu.py.
+
+Execution (MI355X): activations channels-last NDHWC in the compute dtype; every Conv3d is im2col
+(`cmhar_conv3d_im2col`) + the bf16 MFMA GEMM (layout 0) → BatchNorm3d with fused residual/ReLU
+(`cmhar_bn_cl_fwd`).  Backward: fused ReLU-mask BN backward (also emitting the residual-branch gradient), wgrad =
+dzᵀ·col (layout 2, col recomputed rather than kept), dgrad = dz·W (layout 1) gathered by `cmhar_conv3d_col2im`.
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+
+import torch
+import torch.nn as nn
+
+from . import _lib as L
+from . import kernels as K
+from ._lib import call, ptr
+
+
+def _r8(x):
+    return (x + 7) // 8 * 8
+
+
+class BasicBlock(nn.Module):
+    expansion = 1
+
+    def __init__(self, inplanes, planes, stride=1, downsample=None):
+        super().__init__()
+        self.conv1 = nn.Sequential(nn.Conv3d(inplanes, planes, 3, stride, 1, bias=False), nn.BatchNorm3d(planes),
+                                   nn.ReLU(inplace=True))
+        self.conv2 = nn.Sequential(nn.Conv3d(planes, planes, 3, 1, 1, bias=False), nn.BatchNorm3d(planes))
+        self.relu = nn.ReLU(inplace=True)
+        self.downsample = downsample
+        self.stride = stride
+
+
+class R3D18(nn.Module):
+    """torchvision `r3d_18(num_classes)` layout; `fc=None` → feature extractor returning (B, 512) fp32."""
+
+    def __init__(self, num_classes=None, compute_dtype='bf16'):
+        super().__init__()
+        self.compute_dtype = compute_dtype
+        self.stem = nn.Sequential(nn.Conv3d(3, 64, (3, 7, 7), (1, 2, 2), (1, 3, 3), bias=False), nn.BatchNorm3d(64),
+                                  nn.ReLU(inplace=True))
+        self.inplanes = 64
+        self.layer1 = self._make_layer(64, 1)
+        self.layer2 = self._make_layer(128, 2)
+        self.layer3 = self._make_layer(256, 2)
+        self.layer4 = self._make_layer(512, 2)
+        self.fc = nn.Linear(512, num_classes) if num_classes else None
+        self.feature_dim = 512
+        # keep every conv's im2col matrix from the forward for the weight gradient (~38 GB at 32 clips of 16x112²,
+        # sized for the 288 GB of HBM) instead of rebuilding it in the backward
+        self.keep_cols = True
+        for m in self.modules():     # torchvision VideoResNet.__init__ initialisation
+            if isinstance(m, nn.Conv3d):
+                nn.init.kaiming_normal_(m.weight, mode='fan_out', nonlinearity='relu')
+            elif isinstance(m, nn.BatchNorm3d):
+                nn.init.constant_(m.weight, 1)
+                nn.init.constant_(m.bias, 0)
+            elif isinstance(m, nn.Linear):
+                nn.init.normal_(m.weight, 0, 0.01)
+                nn.init.constant_(m.bias, 0)
+
+    def _make_layer(self, planes, stride):
+        ds = None
+        if stride != 1 or self.inplanes != planes:
+            ds = nn.Sequential(nn.Conv3d(self.inplanes, planes, 1, stride, bias=False), nn.BatchNorm3d(planes))
+        blocks = [BasicBlock(self.inplanes, planes, stride, ds), BasicBlock(planes, planes)]
+        self.inplanes = planes
+        return nn.Sequential(*blocks)
+
+    def blocks(self):
+        for layer in (self.layer1, self.layer2, self.layer3, self.layer4):
+            yield from layer
+
+    def forward(self, x):
+        """x: (B, C, T, H, W) as torchvision's VideoResNet.forward."""
+        feat = run_r3d(self, x.transpose(1, 2), self.training)
+        if self.fc is not None:
+            from .models import linear_fp32
+            feat = linear_fp32(feat, self.fc)
+        return feat
+
+
+# ------------------------------------------------------------------------------------------------------------
+# one Conv3d (+ BatchNorm3d [+ residual] [+ ReLU]) unit
+# ------------------------------------------------------------------------------------------------------------
+def _dims(shape, conv, Kp):
+    N, T, H, W, C = shape
+    kt, kh, kw = conv.kernel_size
+    st, sh, sw = conv.stride
+    pt, ph, pw = conv.padding
+    return (ctypes.c_int * 15)(N, T, H, W, C, kt, kh, kw, st, sh, sw, pt, ph, pw, Kp)
+
+
+def _out_shape(shape, conv):
+    N, T, H, W, _ = shape
+    o = [(s + 2 * p - k) // st + 1 for s, p, k, st in zip((T, H, W), conv.padding, conv.kernel_size, conv.stride)]
+    return (N, o[0], o[1], o[2], conv.out_channels)
+
+
+def _pack(conv, dt):
+    """[Cout, Cin, kt, kh, kw] fp32 master → [Cout, Kp] compute dtype in the im2col k order (kt, kh, kw, Cin)."""
+    w = conv.weight.detach()
+    co = w.shape[0]
+    k = w[0].numel()
+    wp = torch.zeros(co, _r8(k), dtype=dt, device=w.device)
+    wp[:, :k] = w.permute(0, 2, 3, 4, 1).reshape(co, k)
+    return wp
+
+
+def _im2col(x, shape, conv, Kp, rows):
+    dims = _dims(shape, conv, Kp)
+    M = math.prod(_out_shape(shape, conv)[:4])
+    col = torch.empty(rows, Kp, dtype=x.dtype, device=x.device)
+    if rows > M:
+        col[M:].zero_()
+    dc = L.dtype_code(x.dtype)
+    call('cmhar_conv3d_im2col', dc, dc, dims, ptr(x), ptr(col), L.stream(x.device))
+    return col
+
+
+def _bn_fwd(z, bn, res, relu, training):
+    M, Cc = z.shape
+    y = torch.empty_like(z)
+    sm = torch.empty(Cc, dtype=torch.float32, device=z.device)
+    sr = torch.empty(Cc, dtype=torch.float32, device=z.device)
+    ws = K.workspace(L.lib().cmhar_bn_cl_ws(M, Cc), z.device)
+    upd = training and bn.track_running_stats
+    call('cmhar_bn_cl_fwd', L.dtype_code(z.dtype), M, Cc, ptr(z), ptr(res), ptr(y), ptr(bn.weight), ptr(bn.bias),
+         ptr(bn.running_mean) if upd or not training else None, ptr(bn.running_var) if upd or not training else None,
+         ptr(sm), ptr(sr), int(training), bn.momentum if bn.momentum is not None else 0.1, bn.eps, int(relu),
+         ptr(bn.num_batches_tracked) if upd else None, ptr(ws), L.stream(z.device))
+    return y, sm, sr
+
+
+class _Unit:
+    """Forward state of one conv+BN unit (input, pre-BN output, BN output, batch statistics)."""
+    __slots__ = ('conv', 'bn', 'relu', 'shape', 'oshape', 'x', 'z', 'y', 'sm', 'sr', 'Kp', 'rows', 'wp', 'col')
+
+
+def _unit_fwd(x, shape, conv, bn, relu, training, save, res=None, wp=None, keep_col=True):
+    oshape = _out_shape(shape, conv)
+    M = math.prod(oshape[:4])
+    Kp = _r8(conv.weight[0].numel())
+    rows = _r8(M) if x.dtype == torch.bfloat16 else M
+    col = _im2col(x, shape, conv, Kp, rows)
+    z = torch.empty(M, conv.out_channels, dtype=x.dtype, device=x.device)
+    K.gemm(0, col[:M], wp, z)
+    y, sm, sr = _bn_fwd(z, bn, res, relu, training)
+    u = None
+    if save:
+        u = _Unit()
+        u.conv, u.bn, u.relu, u.shape, u.oshape, u.Kp, u.rows, u.wp = conv, bn, relu, shape, oshape, Kp, rows, wp
+        u.x, u.z, u.y, u.sm, u.sr = x, z, y, sm, sr
+        u.col = col if keep_col else None
+    return y, oshape, u
+
+
+def _unit_bwd(u, dy, grads, training, need_dx, want_dres, dx_acc=None):
+    """Returns (dx or None, dres or None); dx accumulates into dx_acc when given."""
+    M, Cc = u.z.shape
+    dt = u.z.dtype
+    dz = torch.empty(u.rows, Cc, dtype=dt, device=dy.device)
+    if u.rows > M:
+        dz[M:].zero_()
+    dres = torch.empty(M, Cc, dtype=dt, device=dy.device) if want_dres else None
+    dw_bn = torch.empty(Cc, dtype=torch.float32, device=dy.device)
+    db_bn = torch.empty(Cc, dtype=torch.float32, device=dy.device)
+    ws = K.workspace(L.lib().cmhar_bn_cl_ws(M, Cc), dy.device)
+    call('cmhar_bn_cl_bwd', L.dtype_code(dt), M, Cc, ptr(u.z), ptr(u.y), ptr(dy), ptr(u.bn.weight), ptr(u.sm),
+         ptr(u.sr), ptr(dz), ptr(dres), ptr(dw_bn), ptr(db_bn), int(training), int(u.relu), ptr(ws),
+         L.stream(dy.device))
+    grads[u.bn.weight] = dw_bn
+    grads[u.bn.bias] = db_bn
+    col = u.col if u.col is not None else _im2col(u.x, u.shape, u.conv, u.Kp, u.rows)
+    u.col = None
+    dwp = torch.empty(Cc, u.Kp, dtype=torch.float32, device=dy.device)
+    K.gemm(2, dz, col, dwp)
+    del col
+    w = u.conv.weight
+    k = w[0].numel()
+    grads[w] = dwp[:, :k].reshape(Cc, w.shape[2], w.shape[3], w.shape[4], w.shape[1]).permute(0, 4, 1, 2, 3)
+    dx = None
+    if need_dx:
+        dcol = torch.empty(M, u.Kp, dtype=dt, device=dy.device)
+        K.gemm(1, dz[:M], u.wp, dcol)
+        dx = dx_acc if dx_acc is not None else torch.empty_like(u.x)
+        call('cmhar_conv3d_col2im', L.dtype_code(dt), _dims(u.shape, u.conv, u.Kp), ptr(dcol), ptr(dx),
+             int(dx_acc is not None), L.stream(dy.device))
+    return dx, dres
+
+
+# ------------------------------------------------------------------------------------------------------------
+# whole backbone
+# ------------------------------------------------------------------------------------------------------------
+def _forward_impl(m: R3D18, video, training, save):
+    """video (B, T, C, H, W) fp32 → features (B, 512) fp32 (+ saved units)."""
+    dt = torch.bfloat16 if m.compute_dtype == 'bf16' else torch.float32
+    B, T, Cc, H, W = video.shape
+    x = torch.empty(B, T, H, W, Cc, dtype=dt, device=video.device)
+    call('cmhar_video_to_ndhwc', L.dtype_code(dt), B, T, Cc, H, W, ptr(video), ptr(x), L.stream(video.device))
+    shape = (B, T, H, W, Cc)
+    units = []
+    packs = {}
+
+    def unit(xin, shp, seq, relu, res=None):
+        conv, bn = seq[0], seq[1]
+        wp = packs[conv] = _pack(conv, dt)
+        y, osh, u = _unit_fwd(xin, shp, conv, bn, relu, training, save, res=res, wp=wp, keep_col=m.keep_cols)
+        units.append(u)
+        return y, osh
+
+    h, shape = unit(x, shape, m.stem, True)
+    for blk in m.blocks():
+        x_in, s_in = h, shape
+        h1, s1 = unit(x_in, s_in, blk.conv1, True)
+        if blk.downsample is not None:
+            idn, _ = unit(x_in, s_in, blk.downsample, False)
+        else:
+            idn = x_in
+        h, shape = unit(h1, s1, blk.conv2, True, res=idn)
+    N, To, Ho, Wo, Co = shape
+    feat = torch.empty(N, Co, dtype=torch.float32, device=video.device)
+    call('cmhar_avgpool_cl', L.dtype_code(dt), N, To * Ho * Wo, Co, ptr(h), ptr(feat), L.stream(video.device))
+    st = (units, shape) if save else None
+    return feat, st
+
+
+def _backward_impl(m: R3D18, st, dfeat, training):
+    units, shape = st
+    grads = {}
+    N, To, Ho, Wo, Co = shape
+    dt = units[-1].z.dtype
+    dh = torch.empty(N * To * Ho * Wo, Co, dtype=dt, device=dfeat.device)
+    call('cmhar_avgpool_cl_bwd', L.dtype_code(dt), N, To * Ho * Wo, Co, ptr(dfeat.contiguous()), ptr(dh),
+         L.stream(dfeat.device))
+    i = len(units) - 1
+    for blk in reversed(list(m.blocks())):
+        has_ds = blk.downsample is not None
+        u2 = units[i]
+        u_ds = units[i - 1] if has_ds else None
+        u1 = units[i - 2] if has_ds else units[i - 1]
+        i -= 3 if has_ds else 2
+        dh1, dres = _unit_bwd(u2, dh, grads, training, True, True)
+        if has_ds:
+            dx, _ = _unit_bwd(u_ds, dres, grads, training, True, False)
+            dx, _ = _unit_bwd(u1, dh1, grads, training, True, False, dx_acc=dx)
+        else:
+            dx, _ = _unit_bwd(u1, dh1, grads, training, True, False, dx_acc=dres)
+        dh = dx.reshape(-1, dx.shape[-1])
+    _unit_bwd(units[0], dh, grads, training, False, False)     # stem: no pixel gradient
+    return grads
+
+
+class _R3DFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, video, module, training, *params):
+        feat, st = _forward_impl(module, video.contiguous().float(), training, save=True)
+        ctx.module, ctx.st, ctx.training = module, st, training
+        return feat
+
+    @staticmethod
+    def backward(ctx, dfeat):
+        m = ctx.module
+        grads = _backward_impl(m, ctx.st, dfeat, ctx.training)
+        ctx.st = None
+        out = []
+        for p in m.parameters():
+            if m.fc is not None and (p is m.fc.weight or p is m.fc.bias):
+                out.append(None)
+            else:
+                out.append(grads.get(p) if p.requires_grad else None)
+        return (None, None, None, *out)
+
+
+def run_r3d(m: R3D18, video_btchw: torch.Tensor, training: bool) -> torch.Tensor:
+    """video (B, T, C, H, W) fp32 on the GPU → (B, 512) fp32 pooled features (autograd-aware)."""
+    if not video_btchw.is_cuda:
+        raise RuntimeError('R3D18 runs on the cmhar HIP library: move the module and input to the GPU')
+    params = list(m.parameters())
+    if torch.is_grad_enabled() and any(p.requires_grad for p in params):
+        return _R3DFn.apply(video_btchw, m, training, *params)
+    feat, _ = _forward_impl(m, video_btchw.contiguous().float(), training, save=False)
+    return feat

@@ -202,6 +202,32 @@ int cmhar_mt_adamw(const void* tens, const void* chunks, int nchunks, float lr, 
 /* refresh the compute shadows (p_bf16 / p_copy) from p, e.g. after a foreign optimizer updated p. */
 int cmhar_mt_cast_bf16(const void* tens, const void* chunks, int nchunks, hipStream_t stream);
 
+/* ---- R3D-18 video backbone (north_star extension; no reference code — the reference's CNN options are per-frame
+ * 2-D torchvision models, models.py:160-216; replaces torchvision.models.video.r3d_18's Conv3d / BatchNorm3d /
+ * AdaptiveAvgPool3d).  Activations are channels-last NDHWC.  dims: HOST int[15] =
+ * {N, T, H, W, C, kt, kh, kw, st, sh, sw, pt, ph, pw, Kp}; col is [N·To·Ho·Wo, Kp] with k = ((it·kh+ih)·kw+iw)·C + c
+ * (zero for k >= kt·kh·kw·C); the convolution itself is cmhar_gemm_bf16 / cmhar_gemm_generic over col. */
+int cmhar_conv3d_im2col(int in_dtype, int out_dtype, const int* dims, const void* x, void* col, hipStream_t stream);
+/* dx (NDHWC, dtype) = Σ over taps of dcol (+ dx when accumulate): the input gradient of the convolution. */
+int cmhar_conv3d_col2im(int dtype, const int* dims, const void* dcol, void* dx, int accumulate, hipStream_t stream);
+/* BatchNorm3d over the [M, C] channels-last view (C = 8·2^j ≤ 2048, M < 2^31), fused residual add + ReLU:
+ * y = relu?(bn(x) + res).  ws: cmhar_bn_cl_ws(M, C) floats.  Training updates rmean/rvar/num_batches_tracked. */
+long cmhar_bn_cl_ws(long M, int C);
+int cmhar_bn_cl_fwd(int dtype, long M, int C, const void* x, const void* res, void* y, const float* w,
+                    const float* b, float* rmean, float* rvar, float* smean, float* srstd, int training,
+                    float momentum, float eps, int relu, long long* num_batches_tracked, float* ws,
+                    hipStream_t stream);
+/* g = dy·[y > 0 if relu]; dres = g (optional); dx = BN input gradient; dw = Σg·x̂, db = Σg (fp32, overwritten). */
+int cmhar_bn_cl_bwd(int dtype, long M, int C, const void* x, const void* y, const void* dy, const float* w,
+                    const float* smean, const float* srstd, void* dx, void* dres, float* dw, float* db, int training,
+                    int relu, float* ws, hipStream_t stream);
+/* AdaptiveAvgPool3d(1): [N, S, C] → fp32 [N, C], and its backward (dx = dout / S broadcast). */
+int cmhar_avgpool_cl(int dtype, int N, long S, int C, const void* x, float* out, hipStream_t stream);
+int cmhar_avgpool_cl_bwd(int dtype, int N, long S, int C, const float* dout, void* dx, hipStream_t stream);
+/* (B, T, C, H, W) fp32 clip batch → (B, T, H, W, C) in the compute dtype (the backbone's input layout). */
+int cmhar_video_to_ndhwc(int out_dtype, int B, int T, int C, int H, int W, const float* video, void* out,
+                         hipStream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

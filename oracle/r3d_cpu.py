@@ -1,0 +1,41 @@
+"""ORACLE — test infrastructure only.  CPU fp32 restatement of the R3D-18 video backbone (north_star extension).
+
+Only `tests/` may import this module, as the checker.  Parity unpinned w.r.t. the reference: the reference has no
+3-D CNN (its CNN options are per-frame 2-D torchvision models, `src/models/models.py:160-216`) and torchvision is
+not installed here, so this restates torchvision `models/video/resnet.py` (VideoResNet with BasicStem,
+Conv3DSimple, BasicBlock [2, 2, 2, 2]; BN3d eps 1e-5, momentum 0.1; AdaptiveAvgPool3d(1)) functionally with
+`F.conv3d` / `F.batch_norm` on parameters taken from a `cmhar.r3d.R3D18` state_dict (same key names as torchvision).
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn.functional as F
+
+
+def _bn(x, sd, pre, training, stats):
+    rm, rv = sd[pre + 'running_mean'].clone(), sd[pre + 'running_var'].clone()
+    y = F.batch_norm(x, rm, rv, sd[pre + 'weight'], sd[pre + 'bias'], training=training, momentum=0.1, eps=1e-5)
+    stats[pre] = (rm, rv)
+    return y
+
+
+def r3d18_features(sd, video_bcthw, training=True, stats=None):
+    """video (B, 3, T, H, W) fp32 → pooled (B, 512).  `stats` collects updated running (mean, var) per BN prefix."""
+    stats = {} if stats is None else stats
+    x = F.conv3d(video_bcthw, sd['stem.0.weight'], stride=(1, 2, 2), padding=(1, 3, 3))
+    x = F.relu(_bn(x, sd, 'stem.1.', training, stats))
+    for li in range(1, 5):
+        for bi in range(2):
+            p = f'layer{li}.{bi}.'
+            stride = 2 if (li > 1 and bi == 0) else 1
+            h = F.conv3d(x, sd[p + 'conv1.0.weight'], stride=stride, padding=1)
+            h = F.relu(_bn(h, sd, p + 'conv1.1.', training, stats))
+            h = F.conv3d(h, sd[p + 'conv2.0.weight'], stride=1, padding=1)
+            h = _bn(h, sd, p + 'conv2.1.', training, stats)
+            if p + 'downsample.0.weight' in sd:
+                idn = F.conv3d(x, sd[p + 'downsample.0.weight'], stride=stride)
+                idn = _bn(idn, sd, p + 'downsample.1.', training, stats)
+            else:
+                idn = x
+            x = F.relu(h + idn)
+    return x.mean(dim=(2, 3, 4))

@@ -145,3 +145,18 @@ def test_loss_module_surface():
     assert sorted(k for k, _ in lf.named_parameters()) == ['bias', 'temperature']
     lf2 = SigmoidContrastiveLoss(learnable=False)
     assert sorted(lf2.state_dict()) == ['bias', 'temperature'] and not list(lf2.parameters())
+
+
+def test_r3d18_state_dict_matches_torchvision_layout():
+    """torchvision `r3d_18(num_classes=400)` has 33 371 472 parameters and 122 state_dict entries; the drop-in keeps
+    its key names so torchvision checkpoints load strict (the build constructs on CPU; compute needs the GPU)."""
+    from cmhar.r3d import R3D18
+    m = R3D18(400)
+    sd = m.state_dict()
+    assert sum(p.numel() for p in m.parameters()) == 33371472
+    assert len(sd) == 122
+    for k in ('stem.0.weight', 'stem.1.running_var', 'layer1.0.conv1.0.weight', 'layer1.1.conv2.1.bias',
+              'layer2.0.downsample.0.weight', 'layer4.1.conv2.0.weight', 'fc.weight'):
+        assert k in sd, k
+    assert tuple(sd['stem.0.weight'].shape) == (64, 3, 3, 7, 7)
+    assert tuple(sd['layer3.0.downsample.0.weight'].shape) == (256, 128, 1, 1, 1)

@@ -1,0 +1,111 @@
+"""BASELINE config 2 with its named backbone: CrossModalModel pretraining step with the R3D-18 video backbone
+(north_star extension, cmhar/r3d.py) at 16x112^2 clips + 6x200 IMU, batch 32, bf16, one MI355X.
+
+Same step as bench.py (forward, SigLIP loss, backward, clip 1.0, fused AdamW) on synthetic inputs resident in HBM.
+Prints one JSON line: clips/s, ms/step and the model's algorithmic TFLOP/s (conv FLOPs counted from the layer
+geometry: fwd 2·M·Cout·K per conv; fwd+bwd = 3x minus the stem's input gradient, which is not computed).
+    python tools/bench_r3d.py [--steps 10 --warmup 3 --batch 32 --frames 16 --image 112]
+"""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+import warnings
+
+import torch
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, 'crossmodal-imu-video-ood-har_amd'))
+from cmhar.config import Config  # noqa: E402
+from cmhar.losses import SigmoidContrastiveLoss  # noqa: E402
+from cmhar.models import CrossModalModel  # noqa: E402
+from cmhar.optim import FusedAdamW, clip_grad_norm_  # noqa: E402
+from cmhar.r3d import _out_shape  # noqa: E402
+
+PEAK_BF16_TFLOPS = 2500.0
+
+
+def r3d_flops(m, B, T, H, W):
+    """(forward, stem forward) FLOPs of the backbone for B clips."""
+    shape = (B, T, H, W, 3)
+    tot = 0
+
+    def conv(shp, c):
+        nonlocal tot
+        o = _out_shape(shp, c)
+        f = 2 * math.prod(o[:4]) * c.out_channels * c.weight[0].numel()
+        tot += f
+        return o, f
+
+    shape, stem = conv(shape, m.stem[0])
+    for blk in m.blocks():
+        s1, _ = conv(shape, blk.conv1[0])
+        if blk.downsample is not None:
+            conv(shape, blk.downsample[0])
+        shape, _ = conv(s1, blk.conv2[0])
+    return tot, stem
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--steps', type=int, default=10)
+    ap.add_argument('--warmup', type=int, default=3)
+    ap.add_argument('--batch', type=int, default=32)
+    ap.add_argument('--frames', type=int, default=16)
+    ap.add_argument('--image', type=int, default=112)
+    args = ap.parse_args()
+    dev = torch.device('cuda')
+    cfg = Config()
+    cfg.model.video_backbone = 'r3d_18'
+    cfg.model.compute_dtype = 'bf16'
+    cfg.data.video_frames_per_window = args.frames
+    cfg.data.video_resize = (args.image, args.image)
+    torch.manual_seed(0)
+    with warnings.catch_warnings():
+        warnings.simplefilter('ignore')
+        model = CrossModalModel(cfg).to(dev).train()
+    loss_fn = SigmoidContrastiveLoss().to(dev)
+    params = list(model.parameters())
+    opt = FusedAdamW(params, lr=1e-5, weight_decay=0.01)
+    g = torch.Generator(device=dev).manual_seed(1000)
+    B = args.batch
+    video = torch.randn(B, args.frames, 3, args.image, args.image, device=dev, generator=g)
+    imu = torch.randn(B, 6, 200, device=dev, generator=g)
+
+    def step():
+        a, b = model(imu, video)
+        loss = loss_fn(a, b)
+        opt.zero_grad(set_to_none=True)
+        loss.backward()
+        clip_grad_norm_(params, 1.0)
+        opt.step()
+        return loss
+
+    for _ in range(args.warmup):
+        loss = step()
+    torch.cuda.synchronize()
+    first = float(loss.item())
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loss = step()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    fwd, stem = r3d_flops(model.video_encoder.backbone, B, args.frames, args.image, args.image)
+    step_flops = 3 * fwd - stem
+    tf = step_flops * args.steps / el / 1e12
+    print(json.dumps({
+        'metric': f'clips/sec fwd+bwd, R3D-18 {args.frames}x{args.image}^2 video + 200x6 IMU, batch {B}, 1 GPU',
+        'value': round(B * args.steps / el, 3), 'unit': 'clips/sec', 'n_gpus': 1, 'steps': args.steps,
+        'warmup': args.warmup, 'ms_per_step': round(1000 * el / args.steps, 3), 'dtype': 'bf16',
+        'data': 'synthetic (randn video/IMU resident in HBM, random-init R3D-18)',
+        'config': {'workload': 'CrossModalModel pretrain step, video_backbone=r3d_18 (conv3d = im2col + MFMA GEMM)',
+                   'global_batch': B, 'parallelism': 'dp1'},
+        'model_gflop_per_clip': round(step_flops / B / 1e9, 2), 'model_tflops': round(tf, 1),
+        'mfma_frac': round(tf / PEAK_BF16_TFLOPS, 4), 'loss_after_warmup': first,
+        'max_mem_gb': round(torch.cuda.max_memory_allocated() / 2 ** 30, 1)}))
+
+
+if __name__ == '__main__':
+    main()
