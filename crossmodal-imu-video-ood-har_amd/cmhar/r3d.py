@@ -8,10 +8,12 @@ stride 2 at stages 2-4 with a 1x1x1 strided downsample), global average pool; `f
 projection follows).  Parity: unpinned w.r.t. the reference (no reference code); checked against the CPU
 restatement `oracle/r3d_cpu.py` (F.conv3d / F.batch_norm) in tests/test_r3d_gpu.py.
 
-Execution (MI355X): activations channels-last NDHWC in the compute dtype; every Conv3d is im2col
-(`cmhar_conv3d_im2col`) + the bf16 MFMA GEMM (layout 0) → BatchNorm3d with fused residual/ReLU
-(`cmhar_bn_cl_fwd`).  Backward: fused ReLU-mask BN backward (also emitting the residual-branch gradient), wgrad =
-dzᵀ·col (layout 2, col recomputed rather than kept), dgrad = dz·W (layout 1) gathered by `cmhar_conv3d_col2im`.
+Execution (MI355X): activations channels-last NDHWC in the compute dtype.  Convs with C % 64 == 0 (all but the
+stem) run as implicit GEMMs on MFMA (`cmhar_conv3d_fwd` / `cmhar_conv3d_wgrad`: the im2col gather happens in the
+operand loads, no column matrix in HBM); the stem (C = 3) and the fp32 parity mode use im2col
+(`cmhar_conv3d_im2col`, kept from the forward for the weight gradient) + the GEMM.  BatchNorm3d with fused
+residual/ReLU (`cmhar_bn_cl_fwd`); backward: fused ReLU-mask BN backward (also emitting the residual-branch
+gradient), dgrad = dz·W (layout 1) gathered by `cmhar_conv3d_col2im`.
 """
 from __future__ import annotations
 
@@ -146,7 +148,13 @@ def _bn_fwd(z, bn, res, relu, training):
 
 class _Unit:
     """Forward state of one conv+BN unit (input, pre-BN output, BN output, batch statistics)."""
-    __slots__ = ('conv', 'bn', 'relu', 'shape', 'oshape', 'x', 'z', 'y', 'sm', 'sr', 'Kp', 'rows', 'wp', 'col')
+    __slots__ = ('conv', 'bn', 'relu', 'shape', 'oshape', 'x', 'z', 'y', 'sm', 'sr', 'Kp', 'rows', 'wp', 'col',
+                 'igemm')
+
+
+def _igemm_ok(x, shape, conv, Kp):
+    """Implicit-GEMM conv (no column matrix in HBM): bf16, C % 64 == 0 (a 64-wide K-tile stays in one tap)."""
+    return x.dtype == torch.bfloat16 and shape[4] % 64 == 0 and Kp == conv.weight[0].numel()
 
 
 def _unit_fwd(x, shape, conv, bn, relu, training, save, res=None, wp=None, keep_col=True):
@@ -154,9 +162,15 @@ def _unit_fwd(x, shape, conv, bn, relu, training, save, res=None, wp=None, keep_
     M = math.prod(oshape[:4])
     Kp = _r8(conv.weight[0].numel())
     rows = _r8(M) if x.dtype == torch.bfloat16 else M
-    col = _im2col(x, shape, conv, Kp, rows)
     z = torch.empty(M, conv.out_channels, dtype=x.dtype, device=x.device)
-    K.gemm(0, col[:M], wp, z)
+    igemm = _igemm_ok(x, shape, conv, Kp)
+    if igemm:
+        col = None
+        call('cmhar_conv3d_fwd', _dims(shape, conv, Kp), conv.out_channels, ptr(x), ptr(wp), None, ptr(z),
+             L.stream(x.device))
+    else:
+        col = _im2col(x, shape, conv, Kp, rows)
+        K.gemm(0, col[:M], wp, z)
     y, sm, sr = _bn_fwd(z, bn, res, relu, training)
     u = None
     if save:
@@ -164,7 +178,30 @@ def _unit_fwd(x, shape, conv, bn, relu, training, save, res=None, wp=None, keep_
         u.conv, u.bn, u.relu, u.shape, u.oshape, u.Kp, u.rows, u.wp = conv, bn, relu, shape, oshape, Kp, rows, wp
         u.x, u.z, u.y, u.sm, u.sr = x, z, y, sm, sr
         u.col = col if keep_col else None
+        u.igemm = igemm
     return y, oshape, u
+
+
+def _dgrad_igemm_ok(conv):
+    return tuple(conv.stride) == (1, 1, 1) and conv.out_channels % 64 == 0 and \
+        all(2 * p == k - 1 for p, k in zip(conv.padding, conv.kernel_size))
+
+
+def _dgrad_igemm(dz, conv, oshape, x, dx_acc=None):
+    """Input gradient of a stride-1 'same' conv as the conv of dz (NDHWC [M, Cout] bf16) with the tap-flipped,
+    in/out-transposed weight (padding k-1-p = p): an implicit GEMM, no dcol / col2im; dx_acc (the residual-branch
+    gradient) is added in its epilogue.  Returns dx shaped like x."""
+    w = conv.weight.detach()
+    cin, cout = w.shape[1], w.shape[0]
+    wf = torch.empty(cin, w[0, 0].numel() * cout, dtype=dz.dtype, device=dz.device)
+    wf.view(cin, w.shape[2], w.shape[3], w.shape[4], cout).copy_(w.flip(2, 3, 4).permute(1, 2, 3, 4, 0))
+    N, To, Ho, Wo, _ = oshape
+    kt, kh, kw = conv.kernel_size
+    pt, ph, pw = conv.padding
+    dims = (ctypes.c_int * 15)(N, To, Ho, Wo, cout, kt, kh, kw, 1, 1, 1, pt, ph, pw, wf.shape[1])
+    dx = torch.empty_like(x)
+    call('cmhar_conv3d_fwd', dims, cin, ptr(dz), ptr(wf), ptr(dx_acc), ptr(dx), L.stream(dz.device))
+    return dx
 
 
 def _unit_bwd(u, dy, grads, training, need_dx, want_dres, dx_acc=None):
@@ -183,16 +220,24 @@ def _unit_bwd(u, dy, grads, training, need_dx, want_dres, dx_acc=None):
          L.stream(dy.device))
     grads[u.bn.weight] = dw_bn
     grads[u.bn.bias] = db_bn
-    col = u.col if u.col is not None else _im2col(u.x, u.shape, u.conv, u.Kp, u.rows)
-    u.col = None
     dwp = torch.empty(Cc, u.Kp, dtype=torch.float32, device=dy.device)
-    K.gemm(2, dz, col, dwp)
-    del col
+    if u.igemm:
+        dims = _dims(u.shape, u.conv, u.Kp)
+        n = L.lib().cmhar_conv3d_wgrad_ws(dims, Cc)
+        ws = K.workspace(n, dy.device) if n > 0 else None
+        call('cmhar_conv3d_wgrad', dims, Cc, ptr(u.x), ptr(dz), ptr(dwp), ptr(ws), L.stream(dy.device))
+    else:
+        col = u.col if u.col is not None else _im2col(u.x, u.shape, u.conv, u.Kp, u.rows)
+        u.col = None
+        K.gemm(2, dz, col, dwp)
+        del col
     w = u.conv.weight
     k = w[0].numel()
     grads[w] = dwp[:, :k].reshape(Cc, w.shape[2], w.shape[3], w.shape[4], w.shape[1]).permute(0, 4, 1, 2, 3)
     dx = None
-    if need_dx:
+    if need_dx and u.igemm and _dgrad_igemm_ok(u.conv):
+        dx = _dgrad_igemm(dz, u.conv, u.oshape, u.x, dx_acc)
+    elif need_dx:
         dcol = torch.empty(M, u.Kp, dtype=dt, device=dy.device)
         K.gemm(1, dz[:M], u.wp, dcol)
         dx = dx_acc if dx_acc is not None else torch.empty_like(u.x)

@@ -376,6 +376,238 @@ __global__ __launch_bounds__(256) void video_ndhwc_kernel(long total, int C, lon
   }
 }
 
+// ---- implicit-GEMM conv3d on MFMA (bf16, C % 64 == 0: a 64-wide K-tile never crosses a tap) ----------------------
+// Same tile machinery as gemm_bf16.hip's 128² kernel (128x128x64 tile, 4 waves of 64x64 = 4x4
+// mfma_f32_16x16x32_bf16, XOR-swizzled LDS images, register-staged double buffer, one barrier per K-tile), with the
+// column matrix never materialised: the im2col gather happens in the operand loads.
+//   forward  z[m, co]  = Σ_k col(m, k)·W[co, k]         A = col (gathered, K-contiguous), B = W [Cout][K]
+//   wgrad    dW[co, k] = Σ_m dz[m, co]·col(m, k)       A = dz (row-contraction), B = col (gathered, row-contraction)
+namespace ig {
+constexpr int BM = 128, BN = 128, BK = 64, NT = 256, EPI_LD = BN + 4;
+__device__ __forceinline__ int kc_off(int row, int chunk) { return row * 128 + ((chunk ^ ((row >> 1) & 7)) << 4); }
+__device__ __forceinline__ int mc_swz(int k) { return ((k & 3) | (((k >> 3) & 1) << 2)) << 1; }
+__device__ __forceinline__ int mc_off(int k, int chunk) { return k * 256 + ((chunk ^ mc_swz(k)) << 4); }
+
+template <bool KC>
+__device__ __forceinline__ bf16x8 frag(const char* lds, int r0, int kk, int lane) {
+  if (KC) {
+    return *(const bf16x8*)(lds + kc_off(r0 + (lane & 15), kk * 4 + (lane >> 4)));
+  } else {
+    const int gq = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+    const int chunk = (r0 >> 3) + (p >> 1);
+    const short4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        LDS_PTR(short4_t, lds + mc_off(kk * 32 + 8 * gq + q, chunk) + (p & 1) * 8));
+    const short4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        LDS_PTR(short4_t, lds + mc_off(kk * 32 + 8 * gq + 4 + q, chunk) + (p & 1) * 8));
+    short8_t v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    return __builtin_bit_cast(bf16x8, v);
+  }
+}
+
+// Input element offset of output position m for tap (it, ih, iw), or -1 when it falls in the zero padding.
+__device__ __forceinline__ long tap_src(const Geom& g, int n, int t0, int h0, int w0, int it, int ih, int iw) {
+  const int ti = t0 + it, hi = h0 + ih, wi = w0 + iw;
+  if (ti < 0 || ti >= g.T || hi < 0 || hi >= g.H || wi < 0 || wi >= g.W) return -1;
+  return ((((long)n * g.T + ti) * g.H + hi) * g.W + wi) * g.C;
+}
+__device__ __forceinline__ void out_pos(const Geom& g, int m, int& n, int& t0, int& h0, int& w0) {
+  int r = m;
+  const int wo = r % g.Wo; r /= g.Wo;
+  const int ho = r % g.Ho; r /= g.Ho;
+  const int to = r % g.To;
+  n = r / g.To;
+  t0 = to * g.st - g.pt; h0 = ho * g.sh - g.ph; w0 = wo * g.sw - g.pw;
+}
+
+template <bool AKC, bool BKC>
+__device__ __forceinline__ void mma_tile(const char* As, const char* Bs, int wr, int wc, int lane, floatx4 (&acc)[4][4]) {
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk) {
+    bf16x8 af[4], bfr[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) af[i] = frag<AKC>(As, wr * 64 + i * 16, kk, lane);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) bfr[j] = frag<BKC>(Bs, wc * 64 + j * 16, kk, lane);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+  }
+}
+
+// Stage the fp32 accumulators through LDS and emit rows [bm, min(bm+128, M)) x cols [bn, min(bn+128, N)) with
+// 8-column vectors (N % 8 == 0).
+template <typename OutT>
+__device__ __forceinline__ void store_tile(char* smem, const floatx4 (&acc)[4][4], int wr, int wc, int lane, int tid,
+                                           int bm, int bn, int M, int N, OutT* __restrict__ C, long ldc,
+                                           const OutT* __restrict__ res = nullptr) {
+  float* T = (float*)smem;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        T[(wr * 64 + i * 16 + 4 * (lane >> 4) + r) * EPI_LD + wc * 64 + j * 16 + (lane & 15)] = acc[i][j][r];
+  __syncthreads();
+  const int cg = (tid & 15) * 8, n0 = bn + cg;
+  if (n0 >= N) return;
+  for (int rr = tid >> 4; rr < BM; rr += NT / 16) {
+    const int m = bm + rr;
+    if (m >= M) break;
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = T[rr * EPI_LD + cg + j];
+    if (res) {
+      float r[8];
+      vload<OutT, 8>(res + (long)m * ldc + n0, r);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] += r[j];
+    }
+    vstore<OutT, 8>(C + (long)m * ldc + n0, v);
+  }
+}
+}  // namespace ig
+
+__global__ __launch_bounds__(256, 2) void conv3d_fwd_igemm(Geom g, int M, int Cout, const bf16* __restrict__ x,
+                                                           const bf16* __restrict__ Wt, const bf16* __restrict__ res,
+                                                           bf16* __restrict__ z) {
+  using namespace ig;
+  __shared__ __attribute__((aligned(16))) char smem[BM * EPI_LD * 4];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, wr = wave >> 1, wc = wave & 1;
+  const int tiles_n = (Cout + BN - 1) / BN, ntile = ((M + BM - 1) / BM) * tiles_n;
+  const int bid = xcd_remap(blockIdx.x, ntile);
+  const int bm = (bid / tiles_n) * BM, bn = (bid % tiles_n) * BN;
+  // this thread's four A rows (row = it*32 + tid/8) are fixed for the whole K loop: decompose them once
+  int an[4], at[4], ah[4], aw[4];
+  bool aok[4];
+#pragma unroll
+  for (int it = 0; it < 4; ++it) {
+    const int m = bm + it * 32 + (tid >> 3);
+    aok[it] = m < M;
+    out_pos(g, aok[it] ? m : 0, an[it], at[it], ah[it], aw[it]);
+  }
+  const int kk8 = (tid & 7) * 8;
+  uint4_t ra[4], rb[4];
+  auto load = [&](int k0) {
+    const int tap = k0 / g.C, c0 = k0 - tap * g.C + kk8;
+    const int iw = tap % g.kw, ih = (tap / g.kw) % g.kh, itp = tap / (g.kw * g.kh);
+#pragma unroll
+    for (int it = 0; it < 4; ++it) {
+      const long off = aok[it] ? tap_src(g, an[it], at[it], ah[it], aw[it], itp, ih, iw) : -1;
+      const uint4_t v = *(const uint4_t*)(x + (off >= 0 ? off + c0 : 0));
+      ra[it] = off >= 0 ? v : uint4_t{0u, 0u, 0u, 0u};
+      const int co = bn + it * 32 + (tid >> 3);
+      const uint4_t w = *(const uint4_t*)(Wt + (long)(co < Cout ? co : 0) * g.Kp + k0 + kk8);
+      rb[it] = co < Cout ? w : uint4_t{0u, 0u, 0u, 0u};
+    }
+  };
+  auto store = [&](int buf) {
+#pragma unroll
+    for (int it = 0; it < 4; ++it) {
+      const int off = kc_off(it * 32 + (tid >> 3), tid & 7);
+      *(uint4_t*)(smem + 16384 * buf + off) = ra[it];
+      *(uint4_t*)(smem + 32768 + 16384 * buf + off) = rb[it];
+    }
+  };
+  floatx4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+  const int nk = g.K / BK;
+  load(0);
+  store(0);
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    const bool more = kt + 1 < nk;
+    if (more) load((kt + 1) * BK);
+    mma_tile<true, true>(smem + 16384 * cur, smem + 32768 + 16384 * cur, wr, wc, lane, acc);
+    if (more) store(cur ^ 1);
+    __syncthreads();
+  }
+  store_tile<bf16>(smem, acc, wr, wc, lane, tid, bm, bn, M, Cout, z, Cout, res);
+}
+
+// dW partial over output rows [z·mlen, min(M, (z+1)·mlen)) into ws slab z (fp32 [Cout][K]).
+__global__ __launch_bounds__(256, 2) void conv3d_wgrad_igemm(Geom g, int M, int Cout, int mlen,
+                                                             const bf16* __restrict__ x, const bf16* __restrict__ dz,
+                                                             float* __restrict__ out) {
+  using namespace ig;
+  __shared__ __attribute__((aligned(16))) char smem[BM * EPI_LD * 4];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, wr = wave >> 1, wc = wave & 1;
+  const int tiles_n = (g.K + BN - 1) / BN, ntile = ((Cout + BM - 1) / BM) * tiles_n;
+  const int rl = xcd_remap(blockIdx.x + ntile * blockIdx.y, ntile * gridDim.y);
+  const int bid = rl % ntile, split = rl / ntile;
+  const int bm = (bid / tiles_n) * BM, bn = (bid % tiles_n) * BN;   // bm: Cout rows, bn: K columns
+  const int mbeg = split * mlen, mend = min(M, mbeg + mlen);
+  // this thread's B columns (8 consecutive k of one tap) are fixed: decompose the tap once
+  const int kq = (tid & 15) * 8;                  // non-K-contiguous image: 16 x 8 columns per row
+  const int kcol = bn + kq;
+  const bool kok = kcol < g.K;
+  const int tap = kok ? kcol / g.C : 0, cc = kok ? kcol - tap * g.C : 0;
+  const int iw = tap % g.kw, ih = (tap / g.kw) % g.kh, itp = tap / (g.kw * g.kh);
+  const int co = bm + kq;
+  const bool cok = co < Cout;
+  uint4_t ra[4], rb[4];
+  auto load = [&](int m0) {
+#pragma unroll
+    for (int it = 0; it < 4; ++it) {
+      const int m = m0 + it * 16 + (tid >> 4);
+      const bool mok = m < mend;
+      const uint4_t a = *(const uint4_t*)(dz + (long)(mok ? m : 0) * Cout + (cok ? co : 0));
+      ra[it] = mok && cok ? a : uint4_t{0u, 0u, 0u, 0u};
+      long off = -1;
+      if (mok && kok) {
+        int n, t0, h0, w0;
+        out_pos(g, m, n, t0, h0, w0);
+        off = tap_src(g, n, t0, h0, w0, itp, ih, iw);
+      }
+      const uint4_t b = *(const uint4_t*)(x + (off >= 0 ? off + cc : 0));
+      rb[it] = off >= 0 ? b : uint4_t{0u, 0u, 0u, 0u};
+    }
+  };
+  auto store = [&](int buf) {
+#pragma unroll
+    for (int it = 0; it < 4; ++it) {
+      const int off = mc_off(it * 16 + (tid >> 4), tid & 15);
+      *(uint4_t*)(smem + 16384 * buf + off) = ra[it];
+      *(uint4_t*)(smem + 32768 + 16384 * buf + off) = rb[it];
+    }
+  };
+  floatx4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+  const int nk = mend > mbeg ? (mend - mbeg + BK - 1) / BK : 0;
+  if (nk > 0) {
+    load(mbeg);
+    store(0);
+  }
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    const bool more = kt + 1 < nk;
+    if (more) load(mbeg + (kt + 1) * BK);
+    mma_tile<false, false>(smem + 16384 * cur, smem + 32768 + 16384 * cur, wr, wc, lane, acc);
+    if (more) store(cur ^ 1);
+    __syncthreads();
+  }
+  store_tile<float>(smem, acc, wr, wc, lane, tid, bm, bn, Cout, g.K, out + (long)split * Cout * g.K, g.K);
+}
+
+// dW = Σ_z ws[z] in a fixed order (deterministic), 4 floats per thread.
+__global__ __launch_bounds__(256) void conv3d_wgrad_reduce(long n4, int splits, long slab, const float* __restrict__ ws,
+                                                           float* __restrict__ dw) {
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (long)gridDim.x * blockDim.x) {
+    floatx4 s = *(const floatx4*)(ws + i * 4);
+    for (int z = 1; z < splits; ++z) s += *(const floatx4*)(ws + z * slab + i * 4);
+    *(floatx4*)(dw + i * 4) = s;
+  }
+}
+
 inline int grid_for(long work) {
   const long b = (work + 255) / 256;
   return (int)(b < 8192 ? (b > 0 ? b : 1) : 8192);
@@ -559,6 +791,63 @@ extern "C" int cmhar_video_to_ndhwc(int out_dtype, int B, int T, int C, int H, i
   else if (out_dtype == CMHAR_F32)
     video_ndhwc_kernel<float><<<grid_for(total), 256, 0, stream>>>(total, C, HW, video, (float*)out);
   else return -1;
+  CMHAR_CHECK_LAUNCH();
+  return 0;
+}
+
+// ---- implicit-GEMM entry points (bf16, C % 64 == 0, Kp == kt·kh·kw·C) ----
+static bool igemm_ok(const Geom& g, int Cout) {
+  return geom_ok(g) && g.C % 64 == 0 && g.Kp == g.K && Cout > 0 && Cout % 8 == 0 &&
+         (long)g.N * g.To * g.Ho * g.Wo < (1L << 31);
+}
+
+extern "C" int cmhar_conv3d_fwd(const int* dims, int Cout, const void* x, const void* w, const void* res, void* z,
+                                hipStream_t stream) {
+  const Geom g = make_geom(dims);
+  if (!igemm_ok(g, Cout)) return -1;
+  const int M = g.N * g.To * g.Ho * g.Wo;
+  const int tiles = ((M + 127) / 128) * ((Cout + 127) / 128);
+  conv3d_fwd_igemm<<<tiles, 256, 0, stream>>>(g, M, Cout, (const bf16*)x, (const bf16*)w, (const bf16*)res,
+                                               (bf16*)z);
+  CMHAR_CHECK_LAUNCH();
+  return 0;
+}
+
+// Split of the M contraction: about two workgroups per CU over the 256 CUs, slices of >= 512 rows (multiples of 64).
+static int wgrad_splits(const Geom& g, int Cout, int& mlen) {
+  const int M = g.N * g.To * g.Ho * g.Wo;
+  const int tiles = ((Cout + 127) / 128) * ((g.K + 127) / 128);
+  int s = (512 + tiles - 1) / tiles;
+  const int smax = (M + 511) / 512;
+  if (s > smax) s = smax;
+  if (s < 1) s = 1;
+  mlen = ((M + s - 1) / s + 63) / 64 * 64;
+  return (M + mlen - 1) / mlen;
+}
+
+extern "C" long cmhar_conv3d_wgrad_ws(const int* dims, int Cout) {
+  const Geom g = make_geom(dims);
+  if (!igemm_ok(g, Cout)) return -1;
+  int mlen;
+  const int s = wgrad_splits(g, Cout, mlen);
+  return s > 1 ? (long)s * Cout * g.K : 0;
+}
+
+extern "C" int cmhar_conv3d_wgrad(const int* dims, int Cout, const void* x, const void* dz, float* dw, float* ws,
+                                  hipStream_t stream) {
+  const Geom g = make_geom(dims);
+  if (!igemm_ok(g, Cout)) return -1;
+  const int M = g.N * g.To * g.Ho * g.Wo;
+  int mlen;
+  const int s = wgrad_splits(g, Cout, mlen);
+  if (s > 1 && !ws) return -2;
+  const int tiles = ((Cout + 127) / 128) * ((g.K + 127) / 128);
+  dim3 grid(tiles, s);
+  conv3d_wgrad_igemm<<<grid, 256, 0, stream>>>(g, M, Cout, mlen, (const bf16*)x, (const bf16*)dz, s > 1 ? ws : dw);
+  if (s > 1) {
+    const long slab = (long)Cout * g.K, n4 = slab / 4;
+    conv3d_wgrad_reduce<<<grid_for(n4), 256, 0, stream>>>(n4, s, slab, ws, dw);
+  }
   CMHAR_CHECK_LAUNCH();
   return 0;
 }

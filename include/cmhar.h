@@ -208,6 +208,15 @@ int cmhar_mt_cast_bf16(const void* tens, const void* chunks, int nchunks, hipStr
  * {N, T, H, W, C, kt, kh, kw, st, sh, sw, pt, ph, pw, Kp}; col is [N·To·Ho·Wo, Kp] with k = ((it·kh+ih)·kw+iw)·C + c
  * (zero for k >= kt·kh·kw·C); the convolution itself is cmhar_gemm_bf16 / cmhar_gemm_generic over col. */
 int cmhar_conv3d_im2col(int in_dtype, int out_dtype, const int* dims, const void* x, void* col, hipStream_t stream);
+/* Implicit-GEMM convolution on MFMA (bf16, C % 64 == 0, Kp == kt·kh·kw·C; no column matrix in HBM):
+ * z [M, Cout] = col(x) · Wᵀ (+ res [M, Cout], nullable) with W [Cout, Kp] in the im2col k order — also the input
+ * gradient of a stride-1 conv (x = dz, W = the tap-flipped, in/out-transposed weight); dw [Cout, Kp] fp32 =
+ * dzᵀ · col(x), split over M into ws (cmhar_conv3d_wgrad_ws floats; 0 = no workspace), reduced in a fixed order. */
+int cmhar_conv3d_fwd(const int* dims, int Cout, const void* x, const void* w, const void* res, void* z,
+                     hipStream_t stream);
+long cmhar_conv3d_wgrad_ws(const int* dims, int Cout);
+int cmhar_conv3d_wgrad(const int* dims, int Cout, const void* x, const void* dz, float* dw, float* ws,
+                       hipStream_t stream);
 /* dx (NDHWC, dtype) = Σ over taps of dcol (+ dx when accumulate): the input gradient of the convolution. */
 int cmhar_conv3d_col2im(int dtype, const int* dims, const void* dcol, void* dx, int accumulate, hipStream_t stream);
 /* BatchNorm3d over the [M, C] channels-last view (C = 8·2^j ≤ 2048, M < 2^31), fused residual add + ReLU:

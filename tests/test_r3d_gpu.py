@@ -181,3 +181,67 @@ def test_crossmodal_with_r3d_backbone_steps():
     for k, p in model.named_parameters():
         if k.startswith('video_encoder.backbone.'):
             assert p.grad is not None and torch.isfinite(p.grad).all(), k
+
+
+@pytest.mark.parametrize('cin,cout,k,s,p,shape', [(64, 64, 3, 1, 1, (3, 5, 9, 7)), (64, 128, 3, 2, 1, (2, 6, 11, 10)),
+                                                  (128, 256, 1, 2, 0, (2, 4, 7, 9)), (192, 72, 3, 1, 1, (1, 3, 6, 5))])
+def test_conv3d_implicit_gemm_fwd_wgrad(cin, cout, k, s, p, shape):
+    """Implicit-GEMM forward / weight gradient (bf16 operands, fp32 MFMA accumulation) vs F.conv3d in fp32 on the
+    same bf16-rounded operands: forward ≤ 5e-3 rel (bf16 output rounding), wgrad ≤ 1e-4 rel (fp32 output)."""
+    from cmhar import _lib as L
+    from cmhar import kernels as K
+    from cmhar import r3d
+    torch.manual_seed(4)
+    N, T, H, W = shape
+    conv = torch.nn.Conv3d(cin, cout, k, s, p, bias=False)
+    x = torch.randn(N, cin, T, H, W).bfloat16().float().requires_grad_(True)
+    wq = conv.weight.detach().bfloat16().float().requires_grad_(True)
+    ref = F.conv3d(x, wq, stride=s, padding=p)
+    dz = torch.randn_like(ref).bfloat16().float()
+    ref.backward(dz)
+    conv = conv.to(DEV)
+    xc = x.detach().permute(0, 2, 3, 4, 1).contiguous().to(DEV).bfloat16()
+    shp = tuple(xc.shape)
+    Kp = r3d._r8(conv.weight[0].numel())
+    assert r3d._igemm_ok(xc, shp, conv, Kp)
+    wp = r3d._pack(conv, torch.bfloat16)
+    osh = r3d._out_shape(shp, conv)
+    M = math.prod(osh[:4])
+    z = torch.empty(M, cout, dtype=torch.bfloat16, device=DEV)
+    dims = r3d._dims(shp, conv, Kp)
+    L.call('cmhar_conv3d_fwd', dims, cout, xc.data_ptr(), wp.data_ptr(), None, z.data_ptr(), L.stream(xc.device))
+    got = z.float().reshape(osh).permute(0, 4, 1, 2, 3).cpu()
+    assert rel(got, ref) < 5e-3
+    dzc = dz.permute(0, 2, 3, 4, 1).reshape(M, cout).contiguous().to(DEV).bfloat16()
+    dwp = torch.empty(cout, Kp, device=DEV)
+    n = L.lib().cmhar_conv3d_wgrad_ws(dims, cout)
+    ws = K.workspace(n, xc.device) if n > 0 else None
+    L.call('cmhar_conv3d_wgrad', dims, cout, xc.data_ptr(), dzc.data_ptr(), dwp.data_ptr(),
+           None if ws is None else ws.data_ptr(), L.stream(xc.device))
+    kk = conv.weight[0].numel()
+    dw = dwp[:, :kk].reshape(cout, *conv.kernel_size, cin).permute(0, 4, 1, 2, 3).cpu()
+    assert rel(dw, wq.grad) < 1e-4
+
+
+@pytest.mark.parametrize('cin,cout,shape,acc', [(64, 64, (2, 4, 9, 7), True), (128, 192, (1, 3, 5, 6), False)])
+def test_conv3d_implicit_gemm_dgrad(cin, cout, shape, acc):
+    """Stride-1 input gradient as the flipped-weight implicit GEMM (+ the residual-branch gradient in its epilogue)
+    vs torch autograd of F.conv3d on the same bf16-rounded operands: ≤ 5e-3 rel."""
+    from cmhar import r3d
+    torch.manual_seed(5)
+    N, T, H, W = shape
+    conv = torch.nn.Conv3d(cin, cout, 3, 1, 1, bias=False)
+    conv.weight.data = conv.weight.data.bfloat16().float()
+    x = torch.randn(N, cin, T, H, W).bfloat16().float().requires_grad_(True)
+    ref = F.conv3d(x, conv.weight, padding=1)
+    dz = torch.randn_like(ref).bfloat16().float()
+    ref.backward(dz)
+    res = torch.randn(N, T, H, W, cin).bfloat16() if acc else None
+    expect = x.grad.permute(0, 2, 3, 4, 1) + (res.float() if acc else 0)
+    conv = conv.to(DEV)
+    assert r3d._dgrad_igemm_ok(conv)
+    xc = x.detach().permute(0, 2, 3, 4, 1).reshape(-1, cin).contiguous().to(DEV).bfloat16()
+    dzc = dz.permute(0, 2, 3, 4, 1).reshape(-1, cout).contiguous().to(DEV).bfloat16()
+    dx = r3d._dgrad_igemm(dzc, conv, (N, T, H, W, cout), xc,
+                          None if res is None else res.reshape(-1, cin).contiguous().to(DEV))
+    assert rel(dx.float().reshape(N, T, H, W, cin), expect) < 5e-3

@@ -100,7 +100,7 @@ def main():
         'value': round(B * args.steps / el, 3), 'unit': 'clips/sec', 'n_gpus': 1, 'steps': args.steps,
         'warmup': args.warmup, 'ms_per_step': round(1000 * el / args.steps, 3), 'dtype': 'bf16',
         'data': 'synthetic (randn video/IMU resident in HBM, random-init R3D-18)',
-        'config': {'workload': 'CrossModalModel pretrain step, video_backbone=r3d_18 (conv3d = im2col + MFMA GEMM)',
+        'config': {'workload': 'CrossModalModel pretrain step, video_backbone=r3d_18 (implicit-GEMM conv3d on MFMA)',
                    'global_batch': B, 'parallelism': 'dp1'},
         'model_gflop_per_clip': round(step_flops / B / 1e9, 2), 'model_tflops': round(tf, 1),
         'mfma_frac': round(tf / PEAK_BF16_TFLOPS, 4), 'loss_after_warmup': first,
