@@ -419,40 +419,44 @@ __device__ __forceinline__ void out_pos(const Geom& g, int m, int& n, int& t0, i
   t0 = to * g.st - g.pt; h0 = ho * g.sh - g.ph; w0 = wo * g.sw - g.pw;
 }
 
-template <bool AKC, bool BKC>
-__device__ __forceinline__ void mma_tile(const char* As, const char* Bs, int wr, int wc, int lane, floatx4 (&acc)[4][4]) {
+// JN = 16-column blocks per wave: 4 (128-wide tile) or 2 (64-wide tile, for Cout = 64 convs)
+template <bool AKC, bool BKC, int JN>
+__device__ __forceinline__ void mma_tile(const char* As, const char* Bs, int wr, int wc, int lane,
+                                         floatx4 (&acc)[4][JN]) {
 #pragma unroll
   for (int kk = 0; kk < 2; ++kk) {
-    bf16x8 af[4], bfr[4];
+    bf16x8 af[4], bfr[JN];
 #pragma unroll
     for (int i = 0; i < 4; ++i) af[i] = frag<AKC>(As, wr * 64 + i * 16, kk, lane);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) bfr[j] = frag<BKC>(Bs, wc * 64 + j * 16, kk, lane);
+    for (int j = 0; j < JN; ++j) bfr[j] = frag<BKC>(Bs, wc * JN * 16 + j * 16, kk, lane);
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+      for (int j = 0; j < JN; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
   }
 }
 
 // Stage the fp32 accumulators through LDS and emit rows [bm, min(bm+128, M)) x cols [bn, min(bn+128, N)) with
 // 8-column vectors (N % 8 == 0).
-template <typename OutT>
-__device__ __forceinline__ void store_tile(char* smem, const floatx4 (&acc)[4][4], int wr, int wc, int lane, int tid,
+template <typename OutT, int JN>
+__device__ __forceinline__ void store_tile(char* smem, const floatx4 (&acc)[4][JN], int wr, int wc, int lane, int tid,
                                            int bm, int bn, int M, int N, OutT* __restrict__ C, long ldc,
                                            const OutT* __restrict__ res = nullptr) {
+  constexpr int TPR = JN * 4;                      // threads per output row (8 columns each)
   float* T = (float*)smem;
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
+    for (int j = 0; j < JN; ++j)
 #pragma unroll
       for (int r = 0; r < 4; ++r)
-        T[(wr * 64 + i * 16 + 4 * (lane >> 4) + r) * EPI_LD + wc * 64 + j * 16 + (lane & 15)] = acc[i][j][r];
+        T[(wr * 64 + i * 16 + 4 * (lane >> 4) + r) * EPI_LD + wc * JN * 16 + j * 16 + (lane & 15)] = acc[i][j][r];
   __syncthreads();
-  const int cg = (tid & 15) * 8, n0 = bn + cg;
+  const int cg = (tid % TPR) * 8, n0 = bn + cg;
   if (n0 >= N) return;
-  for (int rr = tid >> 4; rr < BM; rr += NT / 16) {
+  for (int rr = tid / TPR; rr < BM; rr += NT / TPR) {
     const int m = bm + rr;
     if (m >= M) break;
     float v[8];
@@ -469,15 +473,17 @@ __device__ __forceinline__ void store_tile(char* smem, const floatx4 (&acc)[4][4
 }
 }  // namespace ig
 
+template <int JN>
 __global__ __launch_bounds__(256, 2) void conv3d_fwd_igemm(Geom g, int M, int Cout, const bf16* __restrict__ x,
                                                            const bf16* __restrict__ Wt, const bf16* __restrict__ res,
                                                            bf16* __restrict__ z) {
   using namespace ig;
   __shared__ __attribute__((aligned(16))) char smem[BM * EPI_LD * 4];
+  constexpr int TN = JN * 32, NB = TN / 32;        // tile width (Cout) and B-row loads per thread
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, wr = wave >> 1, wc = wave & 1;
-  const int tiles_n = (Cout + BN - 1) / BN, ntile = ((M + BM - 1) / BM) * tiles_n;
+  const int tiles_n = (Cout + TN - 1) / TN, ntile = ((M + BM - 1) / BM) * tiles_n;
   const int bid = xcd_remap(blockIdx.x, ntile);
-  const int bm = (bid / tiles_n) * BM, bn = (bid % tiles_n) * BN;
+  const int bm = (bid / tiles_n) * BM, bn = (bid % tiles_n) * TN;
   // this thread's four A rows (row = it*32 + tid/8) are fixed for the whole K loop: decompose them once
   int an[4], at[4], ah[4], aw[4];
   bool aok[4];
@@ -497,6 +503,9 @@ __global__ __launch_bounds__(256, 2) void conv3d_fwd_igemm(Geom g, int M, int Co
       const long off = aok[it] ? tap_src(g, an[it], at[it], ah[it], aw[it], itp, ih, iw) : -1;
       const uint4_t v = *(const uint4_t*)(x + (off >= 0 ? off + c0 : 0));
       ra[it] = off >= 0 ? v : uint4_t{0u, 0u, 0u, 0u};
+    }
+#pragma unroll
+    for (int it = 0; it < NB; ++it) {
       const int co = bn + it * 32 + (tid >> 3);
       const uint4_t w = *(const uint4_t*)(Wt + (long)(co < Cout ? co : 0) * g.Kp + k0 + kk8);
       rb[it] = co < Cout ? w : uint4_t{0u, 0u, 0u, 0u};
@@ -507,14 +516,14 @@ __global__ __launch_bounds__(256, 2) void conv3d_fwd_igemm(Geom g, int M, int Co
     for (int it = 0; it < 4; ++it) {
       const int off = kc_off(it * 32 + (tid >> 3), tid & 7);
       *(uint4_t*)(smem + 16384 * buf + off) = ra[it];
-      *(uint4_t*)(smem + 32768 + 16384 * buf + off) = rb[it];
+      if (it < NB) *(uint4_t*)(smem + 32768 + 16384 * buf + off) = rb[it];
     }
   };
-  floatx4 acc[4][4];
+  floatx4 acc[4][JN];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < JN; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
   const int nk = g.K / BK;
   load(0);
   store(0);
@@ -523,11 +532,11 @@ __global__ __launch_bounds__(256, 2) void conv3d_fwd_igemm(Geom g, int M, int Co
     const int cur = kt & 1;
     const bool more = kt + 1 < nk;
     if (more) load((kt + 1) * BK);
-    mma_tile<true, true>(smem + 16384 * cur, smem + 32768 + 16384 * cur, wr, wc, lane, acc);
+    mma_tile<true, true, JN>(smem + 16384 * cur, smem + 32768 + 16384 * cur, wr, wc, lane, acc);
     if (more) store(cur ^ 1);
     __syncthreads();
   }
-  store_tile<bf16>(smem, acc, wr, wc, lane, tid, bm, bn, M, Cout, z, Cout, res);
+  store_tile<bf16, JN>(smem, acc, wr, wc, lane, tid, bm, bn, M, Cout, z, Cout, res);
 }
 
 // dW partial over output rows [z·mlen, min(M, (z+1)·mlen)) into ws slab z (fp32 [Cout][K]).
@@ -591,11 +600,11 @@ __global__ __launch_bounds__(256, 2) void conv3d_wgrad_igemm(Geom g, int M, int 
     const int cur = kt & 1;
     const bool more = kt + 1 < nk;
     if (more) load(mbeg + (kt + 1) * BK);
-    mma_tile<false, false>(smem + 16384 * cur, smem + 32768 + 16384 * cur, wr, wc, lane, acc);
+    mma_tile<false, false, 4>(smem + 16384 * cur, smem + 32768 + 16384 * cur, wr, wc, lane, acc);
     if (more) store(cur ^ 1);
     __syncthreads();
   }
-  store_tile<float>(smem, acc, wr, wc, lane, tid, bm, bn, Cout, g.K, out + (long)split * Cout * g.K, g.K);
+  store_tile<float, 4>(smem, acc, wr, wc, lane, tid, bm, bn, Cout, g.K, out + (long)split * Cout * g.K, g.K);
 }
 
 // dW = Σ_z ws[z] in a fixed order (deterministic), 4 floats per thread.
@@ -806,9 +815,16 @@ extern "C" int cmhar_conv3d_fwd(const int* dims, int Cout, const void* x, const 
   const Geom g = make_geom(dims);
   if (!igemm_ok(g, Cout)) return -1;
   const int M = g.N * g.To * g.Ho * g.Wo;
-  const int tiles = ((M + 127) / 128) * ((Cout + 127) / 128);
-  conv3d_fwd_igemm<<<tiles, 256, 0, stream>>>(g, M, Cout, (const bf16*)x, (const bf16*)w, (const bf16*)res,
-                                               (bf16*)z);
+  // Cout <= 64: 128x64 tiles (a 128-wide tile would leave half its MFMA work on padding columns)
+  if (Cout <= 64) {
+    const int tiles = (M + 127) / 128;
+    conv3d_fwd_igemm<2><<<tiles, 256, 0, stream>>>(g, M, Cout, (const bf16*)x, (const bf16*)w, (const bf16*)res,
+                                                   (bf16*)z);
+  } else {
+    const int tiles = ((M + 127) / 128) * ((Cout + 127) / 128);
+    conv3d_fwd_igemm<4><<<tiles, 256, 0, stream>>>(g, M, Cout, (const bf16*)x, (const bf16*)w, (const bf16*)res,
+                                                   (bf16*)z);
+  }
   CMHAR_CHECK_LAUNCH();
   return 0;
 }
