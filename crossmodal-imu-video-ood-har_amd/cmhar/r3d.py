@@ -146,6 +146,18 @@ def _bn_fwd(z, bn, res, relu, training):
     return y, sm, sr
 
 
+def _bn_fwd_tiles(z, bn, res, relu, tstats):
+    M, Cc = z.shape
+    y = torch.empty_like(z)
+    sm = torch.empty(Cc, dtype=torch.float32, device=z.device)
+    sr = torch.empty(Cc, dtype=torch.float32, device=z.device)
+    call('cmhar_bn_cl_fwd_tiles', M, Cc, ptr(tstats), ptr(z), ptr(res), ptr(y), ptr(bn.weight), ptr(bn.bias),
+         ptr(bn.running_mean), ptr(bn.running_var), ptr(sm), ptr(sr),
+         bn.momentum if bn.momentum is not None else 0.1, bn.eps, int(relu), ptr(bn.num_batches_tracked),
+         L.stream(z.device))
+    return y, sm, sr
+
+
 class _Unit:
     """Forward state of one conv+BN unit (input, pre-BN output, BN output, batch statistics)."""
     __slots__ = ('conv', 'bn', 'relu', 'shape', 'oshape', 'x', 'z', 'y', 'sm', 'sr', 'Kp', 'rows', 'wp', 'col',
@@ -164,14 +176,21 @@ def _unit_fwd(x, shape, conv, bn, relu, training, save, res=None, wp=None, keep_
     rows = _r8(M) if x.dtype == torch.bfloat16 else M
     z = torch.empty(M, conv.out_channels, dtype=x.dtype, device=x.device)
     igemm = _igemm_ok(x, shape, conv, Kp)
+    tstats = None
     if igemm:
         col = None
+        if training and bn.track_running_stats:      # BN statistics from the conv epilogue (no statistics pass)
+            ntile = (M + 127) // 128
+            tstats = K.workspace(2 * (ntile + (ntile + 63) // 64) * conv.out_channels, x.device)
         call('cmhar_conv3d_fwd', _dims(shape, conv, Kp), conv.out_channels, ptr(x), ptr(wp), None, ptr(z),
-             L.stream(x.device))
+             ptr(tstats), L.stream(x.device))
     else:
         col = _im2col(x, shape, conv, Kp, rows)
         K.gemm(0, col[:M], wp, z)
-    y, sm, sr = _bn_fwd(z, bn, res, relu, training)
+    if tstats is not None:
+        y, sm, sr = _bn_fwd_tiles(z, bn, res, relu, tstats)
+    else:
+        y, sm, sr = _bn_fwd(z, bn, res, relu, training)
     u = None
     if save:
         u = _Unit()
@@ -200,7 +219,7 @@ def _dgrad_igemm(dz, conv, oshape, x, dx_acc=None):
     pt, ph, pw = conv.padding
     dims = (ctypes.c_int * 15)(N, To, Ho, Wo, cout, kt, kh, kw, 1, 1, 1, pt, ph, pw, wf.shape[1])
     dx = torch.empty_like(x)
-    call('cmhar_conv3d_fwd', dims, cin, ptr(dz), ptr(wf), ptr(dx_acc), ptr(dx), L.stream(dz.device))
+    call('cmhar_conv3d_fwd', dims, cin, ptr(dz), ptr(wf), ptr(dx_acc), ptr(dx), None, L.stream(dz.device))
     return dx
 
 

@@ -268,6 +268,73 @@ __global__ __launch_bounds__(256) void bn_cl_final(int mode, long M, int C, int 
   }
 }
 
+// Combine per-tile (mean_t, M2_t) over the ntile row tiles of 128 rows (the last one ragged) with Chan's formula,
+// in a fixed order: mean = Σ n_t·mean_t / M,  M2 = Σ M2_t + n_t·(mean_t − mean)².  16 tile slots x 16 channels per
+// block.  Then rstd and the running statistics as bn_cl_final.
+// Level 1: one thread per (group of 64 tiles, channel) merges its tiles' (n, mean, M2) sequentially (Chan's update)
+// into the group's (mean, M2); out: [2][ngroup][C].
+__global__ __launch_bounds__(256) void bn_tile_group(long M, int C, int ntile, const float* __restrict__ ts,
+                                                     float* __restrict__ out) {
+  const int ngroup = (ntile + 63) / 64;
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long)ngroup * C) return;
+  const int g = (int)(i / C), c = (int)(i % C);
+  float n = 0.f, mu = 0.f, m2 = 0.f;
+  for (int t = g * 64; t < min(ntile, g * 64 + 64); ++t) {
+    const float nt = (float)min(128L, M - 128L * t), mt = ts[(long)t * C + c];
+    const float d = mt - mu, n2 = n + nt;
+    mu = fmaf(d, nt / n2, mu);
+    m2 += ts[((long)ntile + t) * C + c] + d * d * (n * nt / n2);
+    n = n2;
+  }
+  out[(long)g * C + c] = mu;
+  out[((long)ngroup + g) * C + c] = m2;
+}
+
+// Level 2 over the groups (rows_per: rows a group covers, the last one ragged).
+__global__ __launch_bounds__(256) void bn_tile_final(long M, int C, int ntile, long rows_per, const float* __restrict__ ts,
+                                                     float* __restrict__ mean, float* __restrict__ rstd,
+                                                     float* __restrict__ rmean, float* __restrict__ rvar,
+                                                     long long* __restrict__ nbt, float momentum, float eps) {
+  __shared__ float sh[256];
+  __shared__ float smu[16];
+  const int tid = threadIdx.x, cl = tid & 15, slot = tid >> 4;
+  const int c = blockIdx.x * 16 + cl;
+  auto nrows = [&](int t) { return (float)min(rows_per, M - rows_per * t); };
+  float a = 0.f;
+  if (c < C)
+    for (int t = slot; t < ntile; t += 16) a = fmaf(nrows(t), ts[(long)t * C + c], a);
+  sh[tid] = a;
+  __syncthreads();
+  if (slot == 0) {
+    float b = 0.f;
+    for (int k = 0; k < 16; ++k) b += sh[k * 16 + cl];
+    smu[cl] = b / (float)M;
+  }
+  __syncthreads();
+  const float mu = smu[cl];
+  float q = 0.f;
+  if (c < C)
+    for (int t = slot; t < ntile; t += 16) {
+      const float d = ts[(long)t * C + c] - mu;
+      q += ts[((long)ntile + t) * C + c] + nrows(t) * d * d;
+    }
+  __syncthreads();
+  sh[tid] = q;
+  __syncthreads();
+  if (slot || c >= C) return;
+  float m2 = 0.f;
+  for (int k = 0; k < 16; ++k) m2 += sh[k * 16 + cl];
+  const float var = m2 / (float)M;
+  mean[c] = mu;
+  rstd[c] = rsqrtf(var + eps);
+  if (rmean) {
+    rmean[c] = (1.f - momentum) * rmean[c] + momentum * mu;
+    rvar[c] = (1.f - momentum) * rvar[c] + momentum * var * ((float)M / (float)(M > 1 ? M - 1 : 1));
+  }
+  if (nbt && c == 0) *nbt += 1;
+}
+
 __global__ void bn_cl_eval_stats(int C, const float* __restrict__ rmean, const float* __restrict__ rvar, float eps,
                                  float* __restrict__ mean, float* __restrict__ rstd) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
@@ -476,7 +543,7 @@ __device__ __forceinline__ void store_tile(char* smem, const floatx4 (&acc)[4][J
 template <int JN>
 __global__ __launch_bounds__(256, 2) void conv3d_fwd_igemm(Geom g, int M, int Cout, const bf16* __restrict__ x,
                                                            const bf16* __restrict__ Wt, const bf16* __restrict__ res,
-                                                           bf16* __restrict__ z) {
+                                                           bf16* __restrict__ z, float* __restrict__ tstats) {
   using namespace ig;
   __shared__ __attribute__((aligned(16))) char smem[BM * EPI_LD * 4];
   constexpr int TN = JN * 32, NB = TN / 32;        // tile width (Cout) and B-row loads per thread
@@ -537,6 +604,25 @@ __global__ __launch_bounds__(256, 2) void conv3d_fwd_igemm(Geom g, int M, int Co
     __syncthreads();
   }
   store_tile<bf16, JN>(smem, acc, wr, wc, lane, tid, bm, bn, M, Cout, z, Cout, res);
+  if (tstats) {
+    // BatchNorm statistics of this tile's (bf16-rounded) outputs, per column: tile mean and Σ(v − mean)² over its
+    // valid rows, from the fp32 staging image still in LDS (combined across tiles by bn_tile_final, Chan's formula)
+    const float* T = (const float*)smem;
+    const int rows = min(BM, M - bm), tm = bm / BM, ntm = gridDim.x / ((Cout + TN - 1) / TN);
+    for (int c = tid; c < TN; c += NT) {
+      if (bn + c >= Cout) break;
+      float sum = 0.f;
+      for (int r = 0; r < rows; ++r) sum += (float)(bf16)T[r * EPI_LD + c];
+      const float mu = sum / (float)rows;
+      float m2 = 0.f;
+      for (int r = 0; r < rows; ++r) {
+        const float d = (float)(bf16)T[r * EPI_LD + c] - mu;
+        m2 = fmaf(d, d, m2);
+      }
+      tstats[(long)tm * Cout + bn + c] = mu;
+      tstats[((long)ntm + tm) * Cout + bn + c] = m2;
+    }
+  }
 }
 
 // dW partial over output rows [z·mlen, min(M, (z+1)·mlen)) into ws slab z (fp32 [Cout][K]).
@@ -739,6 +825,24 @@ extern "C" int cmhar_bn_cl_fwd(int dtype, long M, int C, const void* x, const vo
   return 0;
 }
 
+extern "C" int cmhar_bn_cl_fwd_tiles(long M, int C, float* tile_stats, const void* x, const void* res, void* y,
+                                     const float* w, const float* b, float* rmean, float* rvar, float* smean,
+                                     float* srstd, float momentum, float eps, int relu, long long* num_batches_tracked,
+                                     hipStream_t stream) {
+  if (M <= 0 || !bn_channels_ok(C) || !tile_stats) return -1;
+  if (M >= (1L << 31) || M * C / 8 >= (1L << 32)) return -2;
+  const int ntile = (int)((M + 127) / 128), ngroup = (ntile + 63) / 64;
+  float* groups = (float*)tile_stats + 2L * ntile * C;
+  bn_tile_group<<<cdiv((long)ngroup * C, 256), 256, 0, stream>>>(M, C, ntile, tile_stats, groups);
+  bn_tile_final<<<(C + 15) / 16, 256, 0, stream>>>(M, C, ngroup, 128L * 64, groups, smean, srstd, rmean, rvar,
+                                                   num_batches_tracked, momentum, eps);
+  const unsigned nvec = (unsigned)(M * C / 8);
+  bn_cl_apply<bf16><<<grid_for(nvec), 256, 0, stream>>>(nvec, C, (const bf16*)x, (const bf16*)res, smean, srstd, w,
+                                                        b, relu, (bf16*)y);
+  CMHAR_CHECK_LAUNCH();
+  return 0;
+}
+
 extern "C" int cmhar_bn_cl_bwd(int dtype, long M, int C, const void* x, const void* y, const void* dy,
                                const float* w, const float* smean, const float* srstd, void* dx, void* dres,
                                float* dw, float* db, int training, int relu, float* ws, hipStream_t stream) {
@@ -811,7 +915,7 @@ static bool igemm_ok(const Geom& g, int Cout) {
 }
 
 extern "C" int cmhar_conv3d_fwd(const int* dims, int Cout, const void* x, const void* w, const void* res, void* z,
-                                hipStream_t stream) {
+                                float* tile_stats, hipStream_t stream) {
   const Geom g = make_geom(dims);
   if (!igemm_ok(g, Cout)) return -1;
   const int M = g.N * g.To * g.Ho * g.Wo;
@@ -819,11 +923,11 @@ extern "C" int cmhar_conv3d_fwd(const int* dims, int Cout, const void* x, const 
   if (Cout <= 64) {
     const int tiles = (M + 127) / 128;
     conv3d_fwd_igemm<2><<<tiles, 256, 0, stream>>>(g, M, Cout, (const bf16*)x, (const bf16*)w, (const bf16*)res,
-                                                   (bf16*)z);
+                                                   (bf16*)z, tile_stats);
   } else {
     const int tiles = ((M + 127) / 128) * ((Cout + 127) / 128);
     conv3d_fwd_igemm<4><<<tiles, 256, 0, stream>>>(g, M, Cout, (const bf16*)x, (const bf16*)w, (const bf16*)res,
-                                                   (bf16*)z);
+                                                   (bf16*)z, tile_stats);
   }
   CMHAR_CHECK_LAUNCH();
   return 0;

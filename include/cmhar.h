@@ -213,7 +213,13 @@ int cmhar_conv3d_im2col(int in_dtype, int out_dtype, const int* dims, const void
  * gradient of a stride-1 conv (x = dz, W = the tap-flipped, in/out-transposed weight); dw [Cout, Kp] fp32 =
  * dzᵀ · col(x), split over M into ws (cmhar_conv3d_wgrad_ws floats; 0 = no workspace), reduced in a fixed order. */
 int cmhar_conv3d_fwd(const int* dims, int Cout, const void* x, const void* w, const void* res, void* z,
-                     hipStream_t stream);
+                     float* tile_stats, hipStream_t stream);
+/* tile_stats (nullable): 2·ceil(M/128)·Cout floats — per 128-row tile and channel, the mean and Σ(v − mean)² of the
+ * bf16 outputs, consumed by cmhar_bn_cl_fwd_tiles (training-mode BatchNorm3d of z without a statistics pass), which
+ * needs 2·(ntile + ceil(ntile/64))·C floats there (its group partials follow the tile partials). */
+int cmhar_bn_cl_fwd_tiles(long M, int C, float* tile_stats, const void* x, const void* res, void* y,
+                          const float* w, const float* b, float* rmean, float* rvar, float* smean, float* srstd,
+                          float momentum, float eps, int relu, long long* num_batches_tracked, hipStream_t stream);
 long cmhar_conv3d_wgrad_ws(const int* dims, int Cout);
 int cmhar_conv3d_wgrad(const int* dims, int Cout, const void* x, const void* dz, float* dw, float* ws,
                        hipStream_t stream);

@@ -184,6 +184,7 @@ def test_crossmodal_with_r3d_backbone_steps():
 
 
 @pytest.mark.parametrize('cin,cout,k,s,p,shape', [(64, 64, 3, 1, 1, (3, 5, 9, 7)), (64, 128, 3, 2, 1, (2, 6, 11, 10)),
+                                                  (64, 64, 3, 1, 1, (2, 12, 40, 38)),
                                                   (128, 256, 1, 2, 0, (2, 4, 7, 9)), (192, 72, 3, 1, 1, (1, 3, 6, 5))])
 def test_conv3d_implicit_gemm_fwd_wgrad(cin, cout, k, s, p, shape):
     """Implicit-GEMM forward / weight gradient (bf16 operands, fp32 MFMA accumulation) vs F.conv3d in fp32 on the
@@ -209,9 +210,20 @@ def test_conv3d_implicit_gemm_fwd_wgrad(cin, cout, k, s, p, shape):
     M = math.prod(osh[:4])
     z = torch.empty(M, cout, dtype=torch.bfloat16, device=DEV)
     dims = r3d._dims(shp, conv, Kp)
-    L.call('cmhar_conv3d_fwd', dims, cout, xc.data_ptr(), wp.data_ptr(), None, z.data_ptr(), L.stream(xc.device))
+    ntm = (M + 127) // 128
+    ts = torch.empty(2 * (ntm + (ntm + 63) // 64) * cout, device=DEV)
+    L.call('cmhar_conv3d_fwd', dims, cout, xc.data_ptr(), wp.data_ptr(), None, z.data_ptr(), ts.data_ptr(),
+           L.stream(xc.device))
     got = z.float().reshape(osh).permute(0, 4, 1, 2, 3).cpu()
     assert rel(got, ref) < 5e-3
+    # epilogue BatchNorm statistics (per-tile mean / M2 combined by cmhar_bn_cl_fwd_tiles) vs the two-pass kernel
+    bn_a, bn_b = torch.nn.BatchNorm3d(cout).to(DEV), torch.nn.BatchNorm3d(cout).to(DEV)
+    if cout % 8 == 0 and 256 % (cout // 8) == 0:
+        ya, sma, sra = r3d._bn_fwd(z, bn_a, None, True, True)
+        yb, smb, srb = r3d._bn_fwd_tiles(z, bn_b, None, True, ts)
+        assert rel(smb, sma) < 1e-5 and rel(srb, sra) < 1e-5
+        assert rel(bn_b.running_var, bn_a.running_var) < 1e-5 and int(bn_b.num_batches_tracked) == 1
+        assert rel(yb.float(), ya.float()) < 1e-2
     dzc = dz.permute(0, 2, 3, 4, 1).reshape(M, cout).contiguous().to(DEV).bfloat16()
     dwp = torch.empty(cout, Kp, device=DEV)
     n = L.lib().cmhar_conv3d_wgrad_ws(dims, cout)
