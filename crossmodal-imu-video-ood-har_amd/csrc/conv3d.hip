@@ -645,8 +645,10 @@ __global__ __launch_bounds__(256, 2) void conv3d_wgrad_igemm(Geom g, int M, int 
   const int iw = tap % g.kw, ih = (tap / g.kw) % g.kh, itp = tap / (g.kw * g.kh);
   const int co = bm + kq;
   const bool cok = co < Cout;
-  uint4_t ra[4], rb[4];
-  auto load = [&](int m0) {
+  // Two register sets: tile t+2's gather is issued while tile t is multiplied and tile t+1 (loaded one full
+  // iteration earlier) is written to LDS, so each scattered load has two MFMA phases to land.
+  uint4_t ra0[4], rb0[4], ra1[4], rb1[4];
+  auto load = [&](int m0, uint4_t (&ra)[4], uint4_t (&rb)[4]) {
 #pragma unroll
     for (int it = 0; it < 4; ++it) {
       const int m = m0 + it * 16 + (tid >> 4);
@@ -663,7 +665,7 @@ __global__ __launch_bounds__(256, 2) void conv3d_wgrad_igemm(Geom g, int M, int 
       rb[it] = off >= 0 ? b : uint4_t{0u, 0u, 0u, 0u};
     }
   };
-  auto store = [&](int buf) {
+  auto store = [&](int buf, const uint4_t (&ra)[4], const uint4_t (&rb)[4]) {
 #pragma unroll
     for (int it = 0; it < 4; ++it) {
       const int off = mc_off(it * 16 + (tid >> 4), tid & 15);
@@ -678,17 +680,21 @@ __global__ __launch_bounds__(256, 2) void conv3d_wgrad_igemm(Geom g, int M, int 
     for (int j = 0; j < 4; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
   const int nk = mend > mbeg ? (mend - mbeg + BK - 1) / BK : 0;
   if (nk > 0) {
-    load(mbeg);
-    store(0);
+    load(mbeg, ra0, rb0);
+    store(0, ra0, rb0);
+    if (nk > 1) load(mbeg + BK, ra1, rb1);
   }
   __syncthreads();
-  for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
-    const bool more = kt + 1 < nk;
-    if (more) load(mbeg + (kt + 1) * BK);
-    mma_tile<false, false, 4>(smem + 16384 * cur, smem + 32768 + 16384 * cur, wr, wc, lane, acc);
-    if (more) store(cur ^ 1);
+  // tile kt lives in LDS buffer kt&1 and was loaded into register set kt&1
+  auto step = [&](int kt, uint4_t (&rac)[4], uint4_t (&rbc)[4], uint4_t (&ran)[4], uint4_t (&rbn)[4]) {
+    if (kt + 2 < nk) load(mbeg + (kt + 2) * BK, rac, rbc);
+    mma_tile<false, false, 4>(smem + 16384 * (kt & 1), smem + 32768 + 16384 * (kt & 1), wr, wc, lane, acc);
+    if (kt + 1 < nk) store((kt + 1) & 1, ran, rbn);
     __syncthreads();
+  };
+  for (int kt = 0; kt < nk; kt += 2) {
+    step(kt, ra0, rb0, ra1, rb1);
+    if (kt + 1 < nk) step(kt + 1, ra1, rb1, ra0, rb0);
   }
   store_tile<float, 4>(smem, acc, wr, wc, lane, tid, bm, bn, Cout, g.K, out + (long)split * Cout * g.K, g.K);
 }
