@@ -64,7 +64,9 @@ def auroc(in_scores, out_scores) -> float:
 
 class OODEvaluator:
     """`Evaluator` (`src/eval/evaluator.py:18-53`) with energy scores: same constructor and `predict(dataloader)`
-    (batches with 'imu' and 'label'), returning (predictions, labels, logits, energies) numpy arrays."""
+    (batches with 'imu' and 'label'), returning (predictions, labels, logits, energies) numpy arrays.  Batches that
+    also carry 'video' are scored by a two-input model — `model(imu, video)`, e.g. the cross-attention fusion
+    classifier (`cmhar.fusion.CrossModalFusionClassifier`), whose class logits are the "fused logits" of config 5."""
 
     def __init__(self, model, config, device='cuda', temperature: float = 1.0):
         self.model = model.to(device)
@@ -78,7 +80,10 @@ class OODEvaluator:
         preds, labels, logits, energies = [], [], [], []
         for batch in dataloader:
             imu = batch['imu'].to(self.device)
-            out = self.model(imu)
+            if 'video' in batch:
+                out = self.model(imu, batch['video'].to(self.device))
+            else:
+                out = self.model(imu)
             p, e, _ = logits_energy(out.float(), self.temperature)
             preds.append(p.cpu().numpy())
             labels.append(np.asarray(batch['label']))

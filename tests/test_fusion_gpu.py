@@ -65,3 +65,29 @@ def test_fusion_classifier_end_to_end():
         if k.startswith('video_encoder.projection.'):      # the token path bypasses the CLS projection
             continue
         assert p.grad is not None and torch.isfinite(p.grad).all(), k
+
+
+def test_ood_evaluator_on_fusion_logits():
+    """Config 5 on the fused model: OODEvaluator over (imu, video) batches scores the fusion classifier's class
+    logits; energies equal −logsumexp of the returned logits, predictions their argmax (torch reference)."""
+    import numpy as np
+    from cmhar.config import Config
+    from cmhar.fusion import CrossModalFusionClassifier
+    from cmhar.ood import OODEvaluator
+    cfg = Config()
+    cfg.data.video_frames_per_window = 4
+    cfg.data.video_resize = (32, 32)
+    m = cfg.model
+    m.video_backbone = '/nonexistent/videomae-ood'
+    m.video_pretrained = False
+    m.videomae_hidden_size, m.videomae_num_layers, m.videomae_num_heads = 128, 2, 2
+    m.videomae_intermediate_size = 256
+    torch.manual_seed(2)
+    model = CrossModalFusionClassifier(cfg)
+    batches = [{'imu': torch.randn(4, 6, 200), 'video': torch.randn(4, 4, 3, 32, 32), 'label': np.arange(4)}
+               for _ in range(3)]
+    preds, labels, logits, energies = OODEvaluator(model, cfg, device=DEV).predict(batches)
+    assert logits.shape == (12, cfg.model.num_classes) and labels.shape == (12,)
+    lt = torch.from_numpy(logits).double()
+    assert np.allclose(energies, (-torch.logsumexp(lt, 1)).numpy(), rtol=1e-5, atol=1e-5)
+    assert (preds == lt.argmax(1).numpy()).all()

@@ -29,6 +29,9 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--clips', type=int, default=10000)
     ap.add_argument('--batch', type=int, default=32)
+    ap.add_argument('--model', choices=['siglip', 'fusion'], default='siglip',
+                    help='siglip: energy over the SigLIP logits of CrossModalModel; fusion: energy over the class '
+                         'logits of the cross-attention fusion classifier')
     args = ap.parse_args()
     dev = torch.device('cuda')
     cfg = Config()
@@ -36,7 +39,11 @@ def main():
     torch.manual_seed(0)
     with warnings.catch_warnings():
         warnings.simplefilter('ignore')
-        model = CrossModalModel(cfg).to(dev).eval()
+        if args.model == 'fusion':
+            from cmhar.fusion import CrossModalFusionClassifier
+            model = CrossModalFusionClassifier(cfg).to(dev).eval()
+        else:
+            model = CrossModalModel(cfg).to(dev).eval()
     B = args.batch
     g = torch.Generator(device=dev).manual_seed(5)
     video = torch.randn(B, 16, 3, 224, 224, device=dev, generator=g)
@@ -46,10 +53,16 @@ def main():
     S = torch.empty(B, B, device=dev)
     nb = math.ceil(args.clips / B)
 
+    last = {}
+
     def batch():
-        a, b = model(imu, video)
-        K.gemm(0, a, b, S, bias=bias, alpha=scale)
-        return logits_energy(S)
+        if args.model == 'fusion':
+            last['logits'] = model(imu, video)
+        else:
+            a, b = model(imu, video)
+            K.gemm(0, a, b, S, bias=bias, alpha=scale)
+            last['logits'] = S
+        return logits_energy(last['logits'])
 
     with torch.no_grad():
         for _ in range(3):
@@ -63,10 +76,11 @@ def main():
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
         for _ in range(100):
-            logits_energy(S)
+            logits_energy(last['logits'])
         e1.record()
         torch.cuda.synchronize()
-    print(json.dumps({'metric': 'clips/sec OOD energy-score eval stream (16x224^2 video + 6x200 IMU)',
+    what = 'fusion-classifier logits' if args.model == 'fusion' else 'SigLIP logits'
+    print(json.dumps({'metric': f'clips/sec OOD energy-score eval stream over {what} (16x224^2 video + 6x200 IMU)',
                       'value': round(nb * B / dt, 1), 'unit': 'clips/sec', 'clips': nb * B, 'batch': B,
                       'dtype': 'bf16', 'ms_per_batch': round(1e3 * dt / nb, 3),
                       'energy_kernel_us': round(e0.elapsed_time(e1) * 10, 2),
