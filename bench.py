@@ -52,8 +52,8 @@ def pmc_traffic(label):
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
-    ap.add_argument('--steps', type=int, default=10)
-    ap.add_argument('--warmup', type=int, default=3)
+    ap.add_argument('--steps', type=int, default=50)     # >= 50 timed steps after >= 10 warm-up
+    ap.add_argument('--warmup', type=int, default=10)
     ap.add_argument('--batch', type=int, default=32)
     ap.add_argument('--frames', type=int, default=16)
     ap.add_argument('--image', type=int, default=224)
