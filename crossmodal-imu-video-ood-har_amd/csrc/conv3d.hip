@@ -92,36 +92,6 @@ __global__ __launch_bounds__(256) void im2col3d_kernel(Geom g, int M, int tpr, c
   }
 }
 
-// Few input channels (the stem: C = 3): one thread per (row, it, ih) copies the kw·C elements of that tap row,
-// which are contiguous in both the NDHWC input and the column (clipped at the W padding).
-template <typename TI, typename TO>
-__global__ __launch_bounds__(256) void im2col3d_seg_kernel(Geom g, int M, const TI* __restrict__ x,
-                                                           TO* __restrict__ col) {
-  const int segs = g.kt * g.kh, seglen = g.kw * g.C;
-  const long total = (long)M * segs;
-  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
-    const int row = (int)(i / segs), sg = (int)(i - (long)row * segs);
-    const int it = sg / g.kh, ih = sg - it * g.kh;
-    int r = row;
-    const int wo = r % g.Wo; r /= g.Wo;
-    const int ho = r % g.Ho; r /= g.Ho;
-    const int to = r % g.To;
-    const int n = r / g.To;
-    const int ti = to * g.st - g.pt + it, hi = ho * g.sh - g.ph + ih, w0 = wo * g.sw - g.pw;
-    TO* dst = col + (long)row * g.Kp + sg * seglen;
-    const bool rowok = ti >= 0 && ti < g.T && hi >= 0 && hi < g.H;
-    const TI* src = x + ((((long)n * g.T + (rowok ? ti : 0)) * g.H + (rowok ? hi : 0)) * g.W) * g.C;
-    for (int e = 0; e < seglen; ++e) {
-      const int wi = w0 + e / g.C;
-      float v = 0.f;
-      if (rowok && wi >= 0 && wi < g.W) v = to_f<TI>(src[(long)wi * g.C + e % g.C]);
-      dst[e] = from_f<TO>(v);
-    }
-    if (sg == segs - 1)
-      for (int k = g.K; k < g.Kp; ++k) col[(long)row * g.Kp + k] = from_f<TO>(0.f);
-  }
-}
-
 // Gather form of col2im: every input element sums the (at most kt·kh·kw) column entries it fed, in tap order —
 // deterministic, no atomics.  dx = Σ (+ dx_old when accumulate).  32-bit position arithmetic (host-checked).
 template <typename T, int V>
@@ -751,16 +721,13 @@ extern "C" int cmhar_conv3d_im2col(int in_dtype, int out_dtype, const int* dims,
   if (Ml >= (1L << 31) || (long)g.N * g.T * g.H * g.W >= (1L << 31)) return -2;
   const int M = (int)Ml;
   const bool vec = g.C % 8 == 0 && g.Kp % 8 == 0;
-  const bool seg = false;   // measured: the coalesced per-element row kernel beats the per-thread segment copy
   const int kv = vec ? g.Kp / 8 : g.Kp;
   int tpr = 1;
   while (tpr < kv && tpr < 256) tpr <<= 1;
   const int rows_grid = grid_for((long)M * tpr);
-  const int seg_grid = grid_for((long)M * g.kt * g.kh);
 #define IM2COL(TI, TO)                                                                                          \
   do {                                                                                                          \
     if (vec) im2col3d_kernel<TI, TO, 8><<<rows_grid, 256, 0, stream>>>(g, M, tpr, (const TI*)x, (TO*)col);     \
-    else if (seg) im2col3d_seg_kernel<TI, TO><<<seg_grid, 256, 0, stream>>>(g, M, (const TI*)x, (TO*)col);    \
     else im2col3d_kernel<TI, TO, 1><<<rows_grid, 256, 0, stream>>>(g, M, tpr, (const TI*)x, (TO*)col);         \
   } while (0)
   if (in_dtype == CMHAR_BF16 && out_dtype == CMHAR_BF16) IM2COL(bf16, bf16);
@@ -939,11 +906,13 @@ extern "C" int cmhar_conv3d_fwd(const int* dims, int Cout, const void* x, const 
   return 0;
 }
 
-// Split of the M contraction: about two workgroups per CU over the 256 CUs, slices of >= 512 rows (multiples of 64).
+// Split of the M contraction: ~2048 workgroups (8 per CU), slices of >= 512 rows (multiples of 64).  Measured on the
+// R3D-18 step (tools/bench_r3d.py, ms/step): 256 WGs 46.5, 512 44.3, 1024 41.1, 2048 39.8, 4096 39.8, 8192 40.7 —
+// short slices keep each XCD's gathered input window inside its L2.
 static int wgrad_splits(const Geom& g, int Cout, int& mlen) {
   const int M = g.N * g.To * g.Ho * g.Wo;
   const int tiles = ((Cout + 127) / 128) * ((g.K + 127) / 128);
-  int s = (512 + tiles - 1) / tiles;
+  int s = (2048 + tiles - 1) / tiles;
   const int smax = (M + 511) / 512;
   if (s > smax) s = smax;
   if (s < 1) s = 1;
