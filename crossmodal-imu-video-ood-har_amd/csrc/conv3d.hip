@@ -482,6 +482,7 @@ __device__ __forceinline__ void store_tile(char* smem, const floatx4 (&acc)[4][J
                                            int bm, int bn, int M, int N, OutT* __restrict__ C, long ldc,
                                            const OutT* __restrict__ res = nullptr) {
   constexpr int TPR = JN * 4;                      // threads per output row (8 columns each)
+  constexpr int LD = JN * 32 + 4;                  // padded fp32 staging row
   float* T = (float*)smem;
 #pragma unroll
   for (int i = 0; i < 4; ++i)
@@ -489,7 +490,7 @@ __device__ __forceinline__ void store_tile(char* smem, const floatx4 (&acc)[4][J
     for (int j = 0; j < JN; ++j)
 #pragma unroll
       for (int r = 0; r < 4; ++r)
-        T[(wr * 64 + i * 16 + 4 * (lane >> 4) + r) * EPI_LD + wc * JN * 16 + j * 16 + (lane & 15)] = acc[i][j][r];
+        T[(wr * 64 + i * 16 + 4 * (lane >> 4) + r) * LD + wc * JN * 16 + j * 16 + (lane & 15)] = acc[i][j][r];
   __syncthreads();
   const int cg = (tid % TPR) * 8, n0 = bn + cg;
   if (n0 >= N) return;
@@ -498,7 +499,7 @@ __device__ __forceinline__ void store_tile(char* smem, const floatx4 (&acc)[4][J
     if (m >= M) break;
     float v[8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = T[rr * EPI_LD + cg + j];
+    for (int j = 0; j < 8; ++j) v[j] = T[rr * LD + cg + j];
     if (res) {
       float r[8];
       vload<OutT, 8>(res + (long)m * ldc + n0, r);
@@ -510,12 +511,21 @@ __device__ __forceinline__ void store_tile(char* smem, const floatx4 (&acc)[4][J
 }
 }  // namespace ig
 
+// LDS: A stages 2 x 16 KiB, B stages 2 x (JN·4 KiB), fp32 staging 128 x (32·JN + 4) — 48 KiB at JN = 2, so three
+// workgroups share a CU (vs two at JN = 4).
+template <int JN> struct FwdLds {
+  static constexpr int B0 = 32768, BSTAGE = JN * 4096;
+  static constexpr int OPS = B0 + 2 * BSTAGE, EPI = 128 * (JN * 32 + 4) * 4;
+  static constexpr int BYTES = OPS > EPI ? OPS : EPI;
+};
+
 template <int JN>
-__global__ __launch_bounds__(256, 2) void conv3d_fwd_igemm(Geom g, int M, int Cout, const bf16* __restrict__ x,
+__global__ __launch_bounds__(256, JN == 2 ? 3 : 2) void conv3d_fwd_igemm(Geom g, int M, int Cout, const bf16* __restrict__ x,
                                                            const bf16* __restrict__ Wt, const bf16* __restrict__ res,
                                                            bf16* __restrict__ z, float* __restrict__ tstats) {
   using namespace ig;
-  __shared__ __attribute__((aligned(16))) char smem[BM * EPI_LD * 4];
+  using Lds = FwdLds<JN>;
+  __shared__ __attribute__((aligned(16))) char smem[Lds::BYTES];
   constexpr int TN = JN * 32, NB = TN / 32;        // tile width (Cout) and B-row loads per thread
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, wr = wave >> 1, wc = wave & 1;
   const int tiles_n = (Cout + TN - 1) / TN, ntile = ((M + BM - 1) / BM) * tiles_n;
@@ -553,7 +563,7 @@ __global__ __launch_bounds__(256, 2) void conv3d_fwd_igemm(Geom g, int M, int Co
     for (int it = 0; it < 4; ++it) {
       const int off = kc_off(it * 32 + (tid >> 3), tid & 7);
       *(uint4_t*)(smem + 16384 * buf + off) = ra[it];
-      if (it < NB) *(uint4_t*)(smem + 32768 + 16384 * buf + off) = rb[it];
+      if (it < NB) *(uint4_t*)(smem + Lds::B0 + Lds::BSTAGE * buf + off) = rb[it];
     }
   };
   floatx4 acc[4][JN];
@@ -569,7 +579,7 @@ __global__ __launch_bounds__(256, 2) void conv3d_fwd_igemm(Geom g, int M, int Co
     const int cur = kt & 1;
     const bool more = kt + 1 < nk;
     if (more) load((kt + 1) * BK);
-    mma_tile<true, true, JN>(smem + 16384 * cur, smem + 32768 + 16384 * cur, wr, wc, lane, acc);
+    mma_tile<true, true, JN>(smem + 16384 * cur, smem + Lds::B0 + Lds::BSTAGE * cur, wr, wc, lane, acc);
     if (more) store(cur ^ 1);
     __syncthreads();
   }
@@ -582,11 +592,11 @@ __global__ __launch_bounds__(256, 2) void conv3d_fwd_igemm(Geom g, int M, int Co
     for (int c = tid; c < TN; c += NT) {
       if (bn + c >= Cout) break;
       float sum = 0.f;
-      for (int r = 0; r < rows; ++r) sum += (float)(bf16)T[r * EPI_LD + c];
+      for (int r = 0; r < rows; ++r) sum += (float)(bf16)T[r * (TN + 4) + c];
       const float mu = sum / (float)rows;
       float m2 = 0.f;
       for (int r = 0; r < rows; ++r) {
-        const float d = (float)(bf16)T[r * EPI_LD + c] - mu;
+        const float d = (float)(bf16)T[r * (TN + 4) + c] - mu;
         m2 = fmaf(d, d, m2);
       }
       tstats[(long)tm * Cout + bn + c] = mu;
