@@ -92,6 +92,42 @@ __global__ __launch_bounds__(256) void im2col3d_kernel(Geom g, int M, int tpr, c
   }
 }
 
+// Few input channels (the stem: C = 3, K = 441): each thread gathers 8 consecutive k of one row element by element
+// (tap / channel advanced incrementally) and writes them as one 16-B vector — the column matrix is the traffic here.
+template <typename TI, typename TO>
+__global__ __launch_bounds__(256) void im2col3d_vec_store_kernel(Geom g, int M, const TI* __restrict__ x,
+                                                                 TO* __restrict__ col) {
+  const int kv = g.Kp / 8;
+  const long total = (long)M * kv;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int row = (int)(i / kv), k0 = (int)(i - (long)row * kv) * 8;
+    int r = row;
+    const int wo = r % g.Wo; r /= g.Wo;
+    const int ho = r % g.Ho; r /= g.Ho;
+    const int to = r % g.To;
+    const int n = r / g.To;
+    const int t0 = to * g.st - g.pt, h0 = ho * g.sh - g.ph, w0 = wo * g.sw - g.pw;
+    int tap = k0 / g.C, c = k0 - tap * g.C;
+    int iw = tap % g.kw, ih = (tap / g.kw) % g.kh, it = tap / (g.kw * g.kh);
+    float v[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      float e = 0.f;
+      if (k0 + q < g.K) {
+        const int ti = t0 + it, hi = h0 + ih, wi = w0 + iw;
+        if (ti >= 0 && ti < g.T && hi >= 0 && hi < g.H && wi >= 0 && wi < g.W)
+          e = to_f<TI>(x[((((long)n * g.T + ti) * g.H + hi) * g.W + wi) * g.C + c]);
+      }
+      v[q] = e;
+      if (++c == g.C) {                       // next tap: (it, ih, iw) advance like an odometer
+        c = 0;
+        if (++iw == g.kw) { iw = 0; if (++ih == g.kh) { ih = 0; ++it; } }
+      }
+    }
+    vstore<TO, 8>(col + (long)row * g.Kp + k0, v);
+  }
+}
+
 // Gather form of col2im: every input element sums the (at most kt·kh·kw) column entries it fed, in tap order —
 // deterministic, no atomics.  dx = Σ (+ dx_old when accumulate).  32-bit position arithmetic (host-checked).
 template <typename T, int V>
@@ -738,6 +774,9 @@ extern "C" int cmhar_conv3d_im2col(int in_dtype, int out_dtype, const int* dims,
 #define IM2COL(TI, TO)                                                                                          \
   do {                                                                                                          \
     if (vec) im2col3d_kernel<TI, TO, 8><<<rows_grid, 256, 0, stream>>>(g, M, tpr, (const TI*)x, (TO*)col);     \
+    else if (g.Kp % 8 == 0)                                                                                   \
+      im2col3d_vec_store_kernel<TI, TO><<<grid_for((long)M * (g.Kp / 8)), 256, 0, stream>>>(g, M, (const TI*)x, \
+                                                                                             (TO*)col);        \
     else im2col3d_kernel<TI, TO, 1><<<rows_grid, 256, 0, stream>>>(g, M, tpr, (const TI*)x, (TO*)col);         \
   } while (0)
   if (in_dtype == CMHAR_BF16 && out_dtype == CMHAR_BF16) IM2COL(bf16, bf16);
