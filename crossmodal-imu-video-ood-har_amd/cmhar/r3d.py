@@ -248,7 +248,13 @@ def _unit_bwd(u, dy, grads, training, need_dx, want_dres, dx_acc=None):
     else:
         col = u.col if u.col is not None else _im2col(u.x, u.shape, u.conv, u.Kp, u.rows)
         u.col = None
-        K.gemm(2, dz, col, dwp)
+        splits = None
+        if dz.dtype == torch.bfloat16:
+            # the stem's weight gradient is a 64 x 448 output over ~1.6 M rows: ~1024 split-K slices of >= 4096 rows
+            # (the generic heuristic caps at 32 splits = 128 workgroups for this 4-tile output)
+            tiles = -(-Cc // 128) * -(-u.Kp // 128)
+            splits = max(1, min(1024 // tiles, u.rows // 4096))
+        K.gemm(2, dz, col, dwp, splits=splits)
         del col
     w = u.conv.weight
     k = w[0].numel()
