@@ -139,6 +139,7 @@ def main():
 
     def make_cfg():
         cfg = Config()
+        cfg.model.allow_random_init = True   # synthetic benchmark: random-init weights
         cfg.data.imu_window_size = args.imu_len
         cfg.data.video_frames_per_window = args.frames
         cfg.data.video_resize = (args.image, args.image)

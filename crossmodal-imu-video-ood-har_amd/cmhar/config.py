@@ -83,6 +83,10 @@ class ModelConfig:
     classifier_dropout: float = 0.3
     # ---- MI355X build knobs (not in the reference) ----
     compute_dtype: str = 'bf16'          # 'bf16' (MFMA bf16, fp32 accumulate) or 'fp32' (exact-f32 parity mode)
+    # video_pretrained=True with a hub name that cannot be loaded offline raises (as from_pretrained would);
+    # True (or env CMHAR_ALLOW_RANDOM_INIT=1) builds the configured architecture with random weights instead
+    # (benchmarks and tests, which use synthetic data)
+    allow_random_init: bool = False
     # VideoMAE geometry used when the backbone cannot be loaded from a local directory.  None -> taken from
     # DataConfig (frames / resize) and the videomae-base defaults (hidden 768, 12 layers, 12 heads, 3072).
     videomae_hidden_size: int = 768

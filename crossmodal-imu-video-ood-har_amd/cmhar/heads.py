@@ -42,6 +42,16 @@ class _Seeds:
         return (0x5DEECE66D * self.n + 0xB) & ((1 << 62) - 1)
 
 
+def bn_momentum(bn, updating: bool) -> float:
+    """The running-statistics factor torch's _BatchNorm.forward uses: `momentum`, or with momentum=None the
+    cumulative moving average 1 / num_batches_tracked (counted after this batch's increment; one host read)."""
+    if bn.momentum is not None:
+        return float(bn.momentum)
+    if not updating or bn.num_batches_tracked is None:
+        return 0.0
+    return 1.0 / float(int(bn.num_batches_tracked.item()) + 1)
+
+
 def _head_forward(seq, x, training, seed, save):
     blocks, final = _blocks(seq)
     h = x
@@ -52,7 +62,7 @@ def _head_forward(seq, x, training, seed, save):
         use_batch = training or not bn.track_running_stats
         y, sm, sr = K.batchnorm_fwd(z, bn.weight, bn.bias, bn.running_mean if upd or not use_batch else None,
                                     bn.running_var if upd or not use_batch else None, use_batch,
-                                    bn.momentum if bn.momentum is not None else 0.1, bn.eps, True,
+                                    bn_momentum(bn, upd), bn.eps, True,
                                     bn.num_batches_tracked if upd else None)
         pd = p if training else 0.0
         if pd > 0:

@@ -83,7 +83,8 @@ class _SigLIPFn(torch.autograd.Function):
 
 
 class SigmoidContrastiveLoss(nn.Module):
-    """Reference `losses.py:9-54`."""
+    """Reference `losses.py:9-54`.  `group`: process group of the global batch (None: `cmhar.dist`'s default, False:
+    this process's batch only)."""
 
     def __init__(self, init_temperature=10.0, init_bias=-10.0, learnable=True, group=None):
         super().__init__()
@@ -99,7 +100,9 @@ class SigmoidContrastiveLoss(nn.Module):
         if imu_embeds.shape != video_embeds.shape or imu_embeds.dim() != 2:
             raise ValueError('expected two (batch, dim) embedding matrices of equal shape')
         group = self.group
-        if group is None:
+        if group is False:                 # explicitly local: this process's batch only
+            group = None
+        elif group is None:
             from . import dist as _d
             group = _d.loss_group()
         return _SigLIPFn.apply(imu_embeds, video_embeds, self.temperature, self.bias, group)

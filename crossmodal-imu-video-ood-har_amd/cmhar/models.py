@@ -80,9 +80,16 @@ class VideoEncoder(nn.Module):
             if os.path.isdir(vb) and os.path.exists(os.path.join(vb, 'config.json')):
                 self.backbone = VideoMAEBackbone.from_pretrained(vb, compute_dtype=dt)
             else:
-                if model_cfg.video_pretrained and not os.path.isdir(vb):
+                if model_cfg.video_pretrained:
+                    allow = bool(getattr(model_cfg, 'allow_random_init', False)) or \
+                        os.environ.get('CMHAR_ALLOW_RANDOM_INIT', '') == '1'
+                    if not allow:   # VideoMAEModel.from_pretrained(vb) (models.py:157) would fail here too
+                        raise OSError(f'VideoMAE checkpoint {vb!r} cannot be loaded (not a local HF directory '
+                                      f'and no network); give a local directory, set video_pretrained=False, or '
+                                      f'opt in to random weights with model.allow_random_init=True / '
+                                      f'CMHAR_ALLOW_RANDOM_INIT=1')
                     warnings.warn(f'VideoMAE checkpoint {vb!r} is not available offline; using a randomly '
-                                  f'initialised backbone of the configured geometry')
+                                  f'initialised backbone of the configured geometry (allow_random_init)')
                 self.backbone = VideoMAEBackbone(_videomae_geometry(config), compute_dtype=dt)
             self.feature_dim = self.backbone.config.hidden_size
         elif vb == 'r3d_18':

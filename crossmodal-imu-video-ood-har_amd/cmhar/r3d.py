@@ -26,6 +26,7 @@ import torch.nn as nn
 from . import _lib as L
 from . import kernels as K
 from ._lib import call, ptr
+from .heads import bn_momentum
 
 
 def _r8(x):
@@ -139,9 +140,11 @@ def _bn_fwd(z, bn, res, relu, training):
     sr = torch.empty(Cc, dtype=torch.float32, device=z.device)
     ws = K.workspace(L.lib().cmhar_bn_cl_ws(M, Cc), z.device)
     upd = training and bn.track_running_stats
+    use_batch = training or not bn.track_running_stats     # torch: eval without running stats → batch statistics
     call('cmhar_bn_cl_fwd', L.dtype_code(z.dtype), M, Cc, ptr(z), ptr(res), ptr(y), ptr(bn.weight), ptr(bn.bias),
-         ptr(bn.running_mean) if upd or not training else None, ptr(bn.running_var) if upd or not training else None,
-         ptr(sm), ptr(sr), int(training), bn.momentum if bn.momentum is not None else 0.1, bn.eps, int(relu),
+         ptr(bn.running_mean) if upd or not use_batch else None,
+         ptr(bn.running_var) if upd or not use_batch else None,
+         ptr(sm), ptr(sr), int(use_batch), bn_momentum(bn, upd), bn.eps, int(relu),
          ptr(bn.num_batches_tracked) if upd else None, ptr(ws), L.stream(z.device))
     return y, sm, sr
 
@@ -153,7 +156,7 @@ def _bn_fwd_tiles(z, bn, res, relu, tstats):
     sr = torch.empty(Cc, dtype=torch.float32, device=z.device)
     call('cmhar_bn_cl_fwd_tiles', M, Cc, ptr(tstats), ptr(z), ptr(res), ptr(y), ptr(bn.weight), ptr(bn.bias),
          ptr(bn.running_mean), ptr(bn.running_var), ptr(sm), ptr(sr),
-         bn.momentum if bn.momentum is not None else 0.1, bn.eps, int(relu), ptr(bn.num_batches_tracked),
+         bn_momentum(bn, True), bn.eps, int(relu), ptr(bn.num_batches_tracked),
          L.stream(z.device))
     return y, sm, sr
 
@@ -235,7 +238,7 @@ def _unit_bwd(u, dy, grads, training, need_dx, want_dres, dx_acc=None):
     db_bn = torch.empty(Cc, dtype=torch.float32, device=dy.device)
     ws = K.workspace(L.lib().cmhar_bn_cl_ws(M, Cc), dy.device)
     call('cmhar_bn_cl_bwd', L.dtype_code(dt), M, Cc, ptr(u.z), ptr(u.y), ptr(dy), ptr(u.bn.weight), ptr(u.sm),
-         ptr(u.sr), ptr(dz), ptr(dres), ptr(dw_bn), ptr(db_bn), int(training), int(u.relu), ptr(ws),
+         ptr(u.sr), ptr(dz), ptr(dres), ptr(dw_bn), ptr(db_bn), int(training or not u.bn.track_running_stats), int(u.relu), ptr(ws),
          L.stream(dy.device))
     grads[u.bn.weight] = dw_bn
     grads[u.bn.bias] = db_bn

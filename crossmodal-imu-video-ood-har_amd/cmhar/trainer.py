@@ -12,7 +12,12 @@ switch by changing the import.  What differs is only what the MI355X wants:
 * the per-step `loss.item()` host syncs of the reference loop (`trainer.py:143-144,307-310`) are replaced by
   device-side accumulation; the epoch means are read once per epoch (same values);
 * data parallel: pass a `cmhar.dist.GradReducer` (one process per GPU, RCCL all-reduce SUM of gradients
-  overlapped with backward — `nn.DataParallel`'s reduce-add semantics) as `grad_reducer`.
+  overlapped with backward — `nn.DataParallel`'s reduce-add semantics) as `grad_reducer`.  The
+  single-writer semantics of the reference's one process (main.py:89-124) are kept: only rank 0 writes
+  checkpoints and `training_history.json`; BatchNorm running statistics are rank 0's (DataParallel keeps the
+  device-0 replica's) and are broadcast at the end of every training epoch, before validation and saving; losses
+  and metrics are those of the global batch (the classification loss is scaled by B_local / B_global so the
+  summed gradient is the global-batch mean's, as DataParallel's gather-then-mean gives).
 """
 from __future__ import annotations
 
@@ -24,6 +29,7 @@ import torch
 import torch.nn as nn
 from torch.optim.lr_scheduler import CosineAnnealingLR, LinearLR, SequentialLR
 
+from . import dist as D
 from . import kernels as K
 from .losses import CrossEntropyLoss
 from .optim import FusedAdamW, clip_grad_norm_
@@ -70,6 +76,8 @@ class BaseTrainer:
         self.history = {'train': [], 'val': []}
 
     def save_checkpoint(self, path: Path, extra: Optional[Dict[str, Any]] = None):
+        if not D.is_main():           # one writer under data parallelism (the reference is one process)
+            return
         path = Path(path)
         path.parent.mkdir(parents=True, exist_ok=True)
         ckpt = {'epoch': self.current_epoch, 'model_state_dict': self.model.state_dict(), 'history': self.history}
@@ -147,7 +155,8 @@ class CrossModalTrainer(BaseTrainer):
         total = _DeviceSum(self.device)
         for batch in _progress(dataloader, self.show_progress, f'[Pretrain] Epoch {self.current_epoch}'):
             total.add(self.train_step(*self._batch(batch)))
-        return total.value() / max(len(dataloader), 1)
+        D.broadcast_buffers(self.model)     # rank 0's BN running statistics (DataParallel's device-0 replica)
+        return total.value() / max(len(dataloader), 1)     # global-batch loss: identical on every rank
 
     @torch.no_grad()
     def validate(self, dataloader) -> float:
@@ -177,7 +186,8 @@ class CrossModalTrainer(BaseTrainer):
             self.history['train'].append(train_loss)
             self.history['val'].append(val_loss)
             self.scheduler.step()
-            print(f'[Pretrain] epoch={epoch} train_loss={train_loss:.4f} val_loss={val_loss:.4f}')
+            if D.is_main():
+                print(f'[Pretrain] epoch={epoch} train_loss={train_loss:.4f} val_loss={val_loss:.4f}')
             self.save_checkpoint(save_dir / 'last.pt', extra=self._extra())
             if val_loss < self.best_val_loss:
                 self.best_val_loss = val_loss
@@ -191,8 +201,9 @@ class CrossModalTrainer(BaseTrainer):
             if patience_counter >= patience:
                 print(f'[Pretrain] Early stopping at epoch {epoch}')
                 break
-        with open(save_dir / 'training_history.json', 'w') as f:
-            json.dump(self.history, f, indent=2)
+        if D.is_main():
+            with open(save_dir / 'training_history.json', 'w') as f:
+                json.dump(self.history, f, indent=2)
 
 
 # -----------------------------
@@ -248,9 +259,24 @@ class ClassificationTrainer(BaseTrainer):
         if preds is not None:
             preds.append(pred)
 
+    def _global_share(self, n_local):
+        """B_local / B_global as a device scalar (one all-reduce, no host sync); None without data parallelism."""
+        if D.world_size() == 1:
+            return None
+        t = torch.full((1,), float(n_local), dtype=torch.float32, device=self.device)
+        D.all_reduce_sum_(t)
+        return float(n_local) / t
+
     def train_step(self, imu, labels):
+        """trainer.py:296-305.  Under data parallelism the local mean CE is scaled by B_local / B_global: the
+        SUM all-reduce of the gradients then yields the gradient of the global-batch mean, which is what
+        DataParallel computes (outputs gathered on device 0, one CE mean over the whole batch).  Returns the
+        logits and this rank's share of the global-batch loss (the shares sum to the global loss)."""
         logits = self.model(imu)
         loss = self.loss_fn(logits, labels)
+        share = self._global_share(labels.shape[0])
+        if share is not None:
+            loss = loss * share
         self.optimizer.zero_grad(set_to_none=True)
         if self.grad_reducer is not None:
             self.grad_reducer.start_step()
@@ -271,7 +297,12 @@ class ClassificationTrainer(BaseTrainer):
             loss_sum.add(loss)
             self._score(logits, labels, correct)
             total += labels.shape[0]
-        n_ok = int(torch.cat(correct).sum().item()) if correct else 0
+        D.broadcast_buffers(self.model)     # rank 0's BN running statistics (DataParallel's device-0 replica)
+        counts = torch.tensor([float(torch.cat(correct).sum().item()) if correct else 0.0, float(total)],
+                              device=self.device)
+        D.all_reduce_sum_(counts)
+        D.all_reduce_sum_(loss_sum.t)
+        n_ok, total = counts.tolist()
         return {'loss': loss_sum.value() / max(len(dataloader), 1), 'accuracy': 100.0 * n_ok / max(total, 1)}
 
     @torch.no_grad()
@@ -282,7 +313,9 @@ class ClassificationTrainer(BaseTrainer):
         for batch in _progress(dataloader, self.show_progress, f'[Cls:{self.mode}] Val'):
             imu, labels = self._batch(batch)
             logits = self.model(imu)
-            loss_sum.add(self.loss_fn(logits, labels))
+            loss = self.loss_fn(logits, labels)
+            share = self._global_share(labels.shape[0])
+            loss_sum.add(loss if share is None else loss * share)
             self._score(logits, labels, correct, preds)
             labels_all.append(labels)
             total += labels.shape[0]
@@ -290,6 +323,14 @@ class ClassificationTrainer(BaseTrainer):
         all_preds = torch.cat(preds).cpu().numpy().tolist() if preds else []
         all_labels = torch.cat(labels_all).cpu().numpy().tolist() if labels_all else []
         n_ok = int(torch.cat(correct).sum().item()) if correct else 0
+        if D.world_size() > 1:         # metrics of the whole validation set (every rank's shard)
+            import torch.distributed as tdist
+            parts = [None] * D.world_size()
+            tdist.all_gather_object(parts, (all_preds, all_labels, n_ok, total))
+            all_preds = [x for pr in parts for x in pr[0]]
+            all_labels = [x for pr in parts for x in pr[1]]
+            n_ok, total = sum(pr[2] for pr in parts), sum(pr[3] for pr in parts)
+            D.all_reduce_sum_(loss_sum.t)
         return {'loss': loss_sum.value() / max(len(dataloader), 1),
                 'accuracy': 100.0 * n_ok / max(total, 1),
                 'balanced_accuracy': 100.0 * balanced_accuracy_score(all_labels, all_preds),
@@ -312,7 +353,8 @@ class ClassificationTrainer(BaseTrainer):
             self.history['train'].append(train_metrics)
             self.history['val'].append(val_metrics)
             self.scheduler.step()
-            print(f"[Cls:{self.mode}] epoch={epoch} "
+            if D.is_main():
+                print(f"[Cls:{self.mode}] epoch={epoch} "
                   f"train_loss={train_metrics['loss']:.4f} train_acc={train_metrics['accuracy']:.2f}% | "
                   f"val_loss={val_metrics['loss']:.4f} val_acc={val_metrics['accuracy']:.2f}% "
                   f"val_bal_acc={val_metrics['balanced_accuracy']:.2f}% val_f1={val_metrics['f1_macro']:.2f}%")
@@ -326,6 +368,7 @@ class ClassificationTrainer(BaseTrainer):
             if patience_counter >= patience:
                 print(f'[Cls:{self.mode}] Early stopping at epoch {epoch}')
                 break
-        with open(save_dir / 'training_history.json', 'w') as f:
-            json.dump(self.history, f, indent=2)
+        if D.is_main():
+            with open(save_dir / 'training_history.json', 'w') as f:
+                json.dump(self.history, f, indent=2)
         return self.best_bal_acc

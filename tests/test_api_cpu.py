@@ -160,3 +160,22 @@ def test_r3d18_state_dict_matches_torchvision_layout():
         assert k in sd, k
     assert tuple(sd['stem.0.weight'].shape) == (64, 3, 3, 7, 7)
     assert tuple(sd['layer3.0.downsample.0.weight'].shape) == (256, 128, 1, 1, 1)
+
+
+def test_unloadable_pretrained_backbone_raises(monkeypatch):
+    """video_pretrained=True with a hub name that cannot be loaded must fail like
+    VideoMAEModel.from_pretrained (reference models.py:157), unless random init is explicitly allowed."""
+    from cmhar.config import Config
+    from cmhar.models import VideoEncoder
+    monkeypatch.delenv('CMHAR_ALLOW_RANDOM_INIT', raising=False)
+    cfg = Config()
+    cfg.model.videomae_num_layers, cfg.model.videomae_hidden_size = 1, 64
+    cfg.model.videomae_num_heads, cfg.model.videomae_intermediate_size = 2, 128
+    with pytest.raises(OSError):
+        VideoEncoder(cfg)
+    cfg.model.allow_random_init = True
+    with pytest.warns(UserWarning):
+        VideoEncoder(cfg)
+    cfg.model.allow_random_init = False
+    cfg.model.video_pretrained = False
+    VideoEncoder(cfg)

@@ -161,7 +161,7 @@ def _bucket_worker(rank, world, port):
         assert beta == 0.0 and p.grad is not None
         dst.copy_(torch.full(p.shape, float(rank + 1)) * (i + 1))
         sink.done([p])
-    assert all(reducer._launched), 'every bucket must be in flight before finish()'
+    assert all(b.launched for b in reducer.buckets if b.kind == 'sink'), 'every sink bucket must be in flight'
     model.head.weight.grad = torch.full_like(model.head.weight, float(rank + 1))
     model.head.bias.grad = torch.full_like(model.head.bias, 2.0 * (rank + 1))
     reducer.finish()

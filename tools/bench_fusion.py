@@ -37,6 +37,7 @@ def main():
     args = ap.parse_args()
     dev = torch.device('cuda')
     cfg = Config()
+    cfg.model.allow_random_init = True   # synthetic benchmark: random-init weights
     cfg.model.compute_dtype = 'bf16'
     cfg.data.video_frames_per_window = args.frames
     cfg.data.video_resize = (args.image, args.image)

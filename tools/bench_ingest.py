@@ -43,6 +43,7 @@ def timed(fn, reps):
 def main():
     dev = torch.device('cuda')
     cfg = Config()
+    cfg.model.allow_random_init = True   # synthetic benchmark: random-init weights
     H0, W0, H, W, B, T = 1080, 1920, 224, 224, 32, 16
     npool = 400                                       # 16 s of 25 fps video, 2.5 GB of decoded frames
     g = torch.Generator(device=dev).manual_seed(0)

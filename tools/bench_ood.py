@@ -35,6 +35,7 @@ def main():
     args = ap.parse_args()
     dev = torch.device('cuda')
     cfg = Config()
+    cfg.model.allow_random_init = True   # synthetic benchmark: random-init weights
     cfg.model.compute_dtype = 'bf16'
     torch.manual_seed(0)
     with warnings.catch_warnings():

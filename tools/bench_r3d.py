@@ -58,6 +58,7 @@ def main():
     args = ap.parse_args()
     dev = torch.device('cuda')
     cfg = Config()
+    cfg.model.allow_random_init = True   # synthetic benchmark: random-init weights
     cfg.model.video_backbone = 'r3d_18'
     cfg.model.compute_dtype = 'bf16'
     cfg.data.video_frames_per_window = args.frames

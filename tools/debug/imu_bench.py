@@ -13,6 +13,7 @@ from cmhar.models import CrossModalModel  # noqa: E402
 
 def main():
     cfg = Config()
+    cfg.model.allow_random_init = True   # synthetic benchmark: random-init weights
     cfg.data.video_frames_per_window = 4
     cfg.data.video_resize = (32, 32)
     cfg.model.video_backbone = '/nonexistent'
