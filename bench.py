@@ -28,25 +28,28 @@ PEAK_BF16_TFLOPS = 2500.0      # MI355X dense bf16 MFMA (MI355X_MICROARCH.md; sp
 PEAK_HBM_GBS = 8000.0
 
 
-TRAFFIC_JSON = os.path.join(REPO, 'profiles', 'r01_pmc_traffic.json')
+TRAFFIC_JSON = os.path.join(REPO, 'profiles', 'r02_pmc_traffic.json')
 
 
-def pmc_traffic(label):
-    """HBM bytes per launch of the traced kernel `label` (e.g. 'gemm256_kernel<true,false,bf16>') from the committed
-    PMC summary of this same bench command (tools/pmc_traffic.py), or None when it has no entry."""
-    if not os.path.exists(TRAFFIC_JSON) or '<' not in label:
-        return None
+def pmc_traffic(label, path=TRAFFIC_JSON):
+    """HBM bytes per launch of the traced kernel `label` (e.g. 'gemm256_kernel<false,false,float>') from a committed
+    PMC summary of this same bench command (tools/pmc_traffic.py: FETCH_SIZE x2 + WRITE_SIZE per dispatch), with
+    the commit of the build it was measured on; None when the file or the kernel is absent."""
+    if not path or not os.path.exists(path) or '<' not in label:
+        return None, None
     base, args = label.split('<', 1)
     code = {'true': 'Lb1E', 'false': 'Lb0E', 'bf16': 'DF16b', 'float': 'f'}
     mangled = base + 'I' + ''.join(code[a.strip()] for a in args.rstrip('>').split(','))
-    with open(TRAFFIC_JSON) as f:
-        ks = json.load(f)['kernels']
+    with open(path) as f:
+        doc = json.load(f)
+    ks = doc['kernels']
     demangled = base + '<' + ', '.join(a.strip() for a in args.rstrip('>').split(','))   # rocprof demangles some
     hits = [v for k, v in ks.items() if mangled in k or demangled in k]
+    src = {'file': os.path.relpath(path, REPO), 'commit': doc.get('commit'), 'cmd': doc.get('cmd')}
     if not hits:
-        return None
+        return None, src
     n = sum(v['dispatches'] for v in hits)
-    return int(sum(v['hbm_bytes_per_launch'] * v['dispatches'] for v in hits) / n)
+    return int(sum(v['hbm_bytes_per_launch'] * v['dispatches'] for v in hits) / n), src
 
 
 def parse():
@@ -60,8 +63,10 @@ def parse():
     ap.add_argument('--imu-len', type=int, default=200)
     ap.add_argument('--dtype', default='bf16', choices=['bf16', 'fp32'])
     ap.add_argument('--no-cpu-baseline', action='store_true')
-    ap.add_argument('--cpu-batch', type=int, default=2)
-    ap.add_argument('--cpu-steps', type=int, default=2)
+    ap.add_argument('--cpu-batch', type=int, default=4)       # BASELINE.md CPU-baseline plan: batch 4,
+    ap.add_argument('--cpu-warmup', type=int, default=2)      # 2 warm-up + 3 timed steps, all host cores
+    ap.add_argument('--cpu-steps', type=int, default=3)
+    ap.add_argument('--traffic-json', default=TRAFFIC_JSON)
     ap.add_argument('--no-trace', action='store_true')
     ap.add_argument('--imu-stream', choices=['side', 'main'], default='side',
                     help='run the IMU branch on its own HIP stream (overlapping the video branch) or on the main one')
@@ -76,11 +81,42 @@ def videomae_flops_per_clip(T, H, W, hd=768, layers=12, inter=3072, P=16, tub=2,
     return embed, embed + layers * per_layer
 
 
-def cpu_baseline(cfg_builder, batch, steps, frames, image, imu_len):
-    """The CPU oracle (torch-eager fp32 restatement of the reference path) timed on the host cores."""
+def host_cpu():
+    """(model name, cores this process may run on): the box's CPU share, not the whole machine's count."""
+    name = 'unknown'
+    try:
+        with open('/proc/cpuinfo') as f:
+            for line in f:
+                if line.startswith('model name'):
+                    name = line.split(':', 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        cores = len(os.sched_getaffinity(0))
+    except AttributeError:
+        cores = os.cpu_count() or 1
+    try:                      # a cgroup CPU quota (e.g. '1600000 100000' = 16 cores) caps the usable cores
+        with open('/sys/fs/cgroup/cpu.max') as f:
+            quota, period = f.read().split()[:2]
+        if quota != 'max':
+            cores = max(1, min(cores, int(quota) // int(period)))
+    except (OSError, ValueError):
+        pass
+    return name, cores
+
+
+def log(msg):
+    print(f'[bench] {msg}', file=sys.stderr, flush=True)
+
+
+def cpu_baseline(cfg_builder, batch, warmup, steps, frames, image, imu_len):
+    """The CPU oracle (torch-eager fp32 restatement of the reference path, validated against the reference's
+    golden vectors) timed on every host core this process may use: the training step (fwd+bwd+clip+AdamW) and,
+    as a second row, the eval-mode forward."""
     sys.path.insert(0, REPO)
     from oracle import cpu_model as O
-    threads = min(16, os.cpu_count() or 1)
+    cpu_name, threads = host_cpu()
     torch.set_num_threads(threads)
     cfg = cfg_builder()
     from cmhar.models import CrossModalModel
@@ -111,14 +147,31 @@ def cpu_baseline(cfg_builder, batch, steps, frames, image, imu_len):
             O.clip_grad_norm(grads, 1.0)
             O.adamw_step([sd[k] for k in names], grads, m, v, i, lr=1e-5)
 
-    step(1)
+    def fwd():
+        with torch.no_grad():
+            O.crossmodal(sd, imu, video, mc, training=False)
+
+    log(f'cpu baseline: {threads} threads on {cpu_name}, batch {batch}, {warmup} + {steps} steps')
+    for i in range(warmup):
+        step(i + 1)
+        log(f'cpu warm-up step {i + 1} done')
     t0 = time.perf_counter()
     for i in range(steps):
-        step(i + 2)
+        step(warmup + i + 1)
+        log(f'cpu timed step {i + 1}: {time.perf_counter() - t0:.1f} s')
     dt = time.perf_counter() - t0
+    fwd()
+    t1 = time.perf_counter()
+    for i in range(steps):
+        fwd()
+        log(f'cpu eval forward {i + 1}: {time.perf_counter() - t1:.1f} s')
+    dte = time.perf_counter() - t1
     return {'value': round(batch * steps / dt, 4), 'unit': 'clips/sec', 'cores': threads, 'kind': 'port',
-            'sample': f'oracle/cpu_model.py fp32 fwd+bwd+clip+AdamW, batch {batch}, {steps} timed steps after '
-                      f'1 warm-up, {frames}x{image}^2 video + 6x{imu_len} IMU, {threads} threads'}
+            'cpu_model': cpu_name,
+            'eval_fwd_clips_per_sec': round(batch * steps / dte, 4),
+            'sample': f'oracle/cpu_model.py fp32 fwd+bwd+clip+AdamW, batch {batch}, {warmup} warm-up + {steps} timed '
+                      f'steps, {frames}x{image}^2 video + 6x{imu_len} IMU, {threads} threads on {cpu_name}; eval row: '
+                      f'eval-mode forward, {steps} timed batches after 1 warm-up'}
 
 
 def main():
@@ -192,7 +245,8 @@ def main():
             breakdown = K.TRACE.summary()
     torch.cuda.synchronize()
     first_loss = float(loss.item()) if args.warmup else float('nan')
-    single = {k: v for k, v in breakdown.items() if '+' not in k and '(' not in k}
+    # every traced label is one kernel symbol except the two-kernel attention backward entry
+    single = {k: v for k, v in breakdown.items() if '(' not in k}
     dominant = max(single.items(), key=lambda kv: kv[1][1])[0] if single else None
     if world > 1:
         dist.barrier()
@@ -200,11 +254,15 @@ def main():
     K.TRACE.records = []
     K.TRACE.only = {dominant} if dominant else None
     K.TRACE.active = not args.no_trace and dominant is not None
+    if rank == 0:
+        log(f'warm-up done ({args.warmup} steps, loss {first_loss:.5f}); timing {args.steps} steps')
     t0 = time.perf_counter()
     for _ in range(args.steps):
         loss = step()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    if rank == 0:
+        log(f'timed region: {elapsed:.3f} s')
     K.TRACE.active = False
     if world > 1:
         dist.barrier()
@@ -215,17 +273,19 @@ def main():
     value = clips / elapsed
     ms = 1000 * elapsed / args.steps
 
-    # dominant kernel: the single HIP kernel (not a multi-kernel entry such as attention backward or split-K +
-    # reduce) with the largest traced time in the traced warm-up step; achieved = its algorithmic FLOPs / its
-    # HIP-event-measured time over the timed region
+    # dominant kernel: the single HIP kernel with the largest traced time in the traced warm-up step (split-K GEMMs
+    # are traced without their reduce launch); achieved = its algorithmic FLOPs / its HIP-event-measured time over
+    # the timed region
     roof = None
     summ = K.TRACE.summary() if not args.no_trace else {}
     if dominant in summ:
         name = dominant
         n, tot_ms, fl, nb = summ[name]
         achieved = fl / (tot_ms / 1e3) / 1e12
+        traffic, tsrc = pmc_traffic(name, args.traffic_json)
         roof = {'bound': 'mfma', 'achieved': round(achieved, 1), 'peak': PEAK_BF16_TFLOPS, 'unit': 'TFLOP/s',
-                'frac': round(achieved / PEAK_BF16_TFLOPS, 4), 'traffic': pmc_traffic(name), 'kernel': name,
+                'frac': round(achieved / PEAK_BF16_TFLOPS, 4), 'traffic': traffic, 'traffic_source': tsrc,
+                'kernel': name,
                 'launches': n, 'avg_launch_ms': round(tot_ms / n, 4),
                 'algorithmic_bytes_per_launch': int(nb / n)}
     embed_f, fwd_f = videomae_flops_per_clip(args.frames, args.image, args.image)
@@ -245,8 +305,8 @@ def main():
            'first_warmup_loss': first_loss,
            'max_mem_gb': round(torch.cuda.max_memory_allocated(dev) / 2 ** 30, 1)}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        out['cpu_baseline'] = cpu_baseline(make_cfg, args.cpu_batch, args.cpu_steps, args.frames, args.image,
-                                           args.imu_len)
+        out['cpu_baseline'] = cpu_baseline(make_cfg, args.cpu_batch, args.cpu_warmup, args.cpu_steps, args.frames,
+                                           args.image, args.imu_len)
     if rank == 0:
         if breakdown:   # one traced warm-up step
             out['kernels'] = {k: {'launches': n, 'ms_per_step': round(tm, 3),

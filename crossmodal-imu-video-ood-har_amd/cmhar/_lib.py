@@ -30,6 +30,8 @@ class Epilogue(C.Structure):
 _SIGS = {
     'cmhar_version': (i32, []),
     'cmhar_gemm_bf16': (i32, [i32, i32, i32, i32, i32, vp, i64, vp, i64, vp, i64, C.POINTER(Epilogue), i32, vp, vp]),
+    'cmhar_gemm_bf16_phased': (i32, [i32, i32, i32, i32, i32, vp, i64, vp, i64, vp, i64, C.POINTER(Epilogue), i32, vp,
+                                     vp, i32]),
     'cmhar_gemm_bf16_ws': (i64, [i32, i32, i32]),
     'cmhar_gemm_bf16_plan': (i32, [i32, i32, i32, i32, i32, i32, i32]),
     'cmhar_gemm_generic': (i32, [i32, i32, i32, i32, i32, i32, vp, i64, i64, i64, vp, i64, i64, i64, vp, i64, i64,

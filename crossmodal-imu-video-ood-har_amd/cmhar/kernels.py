@@ -56,7 +56,9 @@ _PLAN = {}
 
 
 def _gemm_trace_name(layout, M, N, K, s, has_ws, rowsum, out_dtype):
-    """Trace label of a bf16 GEMM call: the kernel(s) the library's own plan (cmhar_gemm_bf16_plan) launches."""
+    """Trace label of a bf16 GEMM call: the GEMM kernel (template name as rocprofv3 lists it, without the trailing
+    integer parameters) that the library's own plan (cmhar_gemm_bf16_plan) launches; a split-K / tail reduce that
+    follows it is launched outside the traced interval."""
     key = (layout, M, N, K, s, has_ws, rowsum)
     plan = _PLAN.get(key)
     if plan is None:
@@ -67,11 +69,12 @@ def _gemm_trace_name(layout, M, N, K, s, has_ws, rowsum, out_dtype):
     name = _GEMM_SYMBOL[layout].format(o=o)
     if plan in (1, 2, 3):
         name = name.replace('gemm_bf16_kernel', 'gemm256_kernel')
-    if plan == 2:
-        name += '+tail_reduce'
-    elif plan in (3, 5):
-        name += '+splitk_reduce'
     return name
+
+
+def _gemm_has_reduce(layout, M, N, K, s, has_ws, rowsum):
+    """Whether the call's plan ends with a split-K / tail reduce launch (plans 2, 3, 5)."""
+    return _PLAN[(layout, M, N, K, s, has_ws, rowsum)] in (2, 3, 5)
 
 # ------------------------------------------------------------------------------------------------------------
 # workspaces (one growing fp32 buffer per (device, stream))
@@ -213,12 +216,19 @@ def gemm(layout: int, a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, *, bi
         if TRACE.active:
             name = _gemm_trace_name(layout, M, N, K, s, ws is not None, rowsum is not None, out.dtype)
             ev = TRACE.begin(name)
-        call('cmhar_gemm_bf16', layout, L.dtype_code(out.dtype), M, N, K, ptr(a), a.stride(0), ptr(b), b.stride(0),
-             ptr(out), out.stride(0), C.byref(epi), s, ptr(ws), st)
-        if ev is not None:
+        if ev is None:
+            call('cmhar_gemm_bf16', layout, L.dtype_code(out.dtype), M, N, K, ptr(a), a.stride(0), ptr(b),
+                 b.stride(0), ptr(out), out.stride(0), C.byref(epi), s, ptr(ws), st)
+        else:
+            # traced: the GEMM kernel alone between the events (phase 1), then its split-K / tail reduce (phase 2)
+            args = (layout, L.dtype_code(out.dtype), M, N, K, ptr(a), a.stride(0), ptr(b), b.stride(0), ptr(out),
+                    out.stride(0), C.byref(epi), s, ptr(ws), st)
+            call('cmhar_gemm_bf16_phased', *args, 1)
             # algorithmic bytes: operands once + output once + every epilogue tensor (residual / aux in / aux out)
             extra = sum(t.element_size() * M * N for t in (residual, aux_in, aux_out) if t is not None)
             TRACE.end(ev, name, 2 * M * N * K, 2 * (M * K + N * K) + out.element_size() * M * N + extra)
+            if _gemm_has_reduce(layout, M, N, K, s, ws is not None, rowsum is not None):
+                call('cmhar_gemm_bf16_phased', *args, 2)
     else:
         if layout == 0:
             sam, sak, sbk, sbn = a.stride(0), 1, 1, b.stride(0)

@@ -878,7 +878,10 @@ static int gemm_plan(bool ak, bool bkc, int M, int N, int K, int splits, bool ha
 
 template <bool AK, bool BKc, typename OutT>
 int launch(int M, int N, int K, const bf16* A, long lda, const bf16* B, long ldb, OutT* C, long ldc,
-           const Epilogue& e, int splits, float* ws, hipStream_t st) {
+           const Epilogue& e, int splits, float* ws, hipStream_t st, int phases) {
+  // phases: bit 0 = the GEMM kernel, bit 1 = the split-K / tail reduce (3 = both; the split lets a tracer time
+  // the GEMM kernel alone between the two launches)
+  const bool ph_gemm = phases & 1, ph_red = phases & 2;
   // triple-buffered A for the forward / dgrad layouts (7-14 % faster, tools/debug/gemm_ablate.py mode 9); the
   // weight-gradient layout (both operands row-contraction) runs out of registers with it and keeps two buffers
   constexpr int kNA = AK ? 3 : 2;
@@ -894,19 +897,24 @@ int launch(int M, int N, int K, const bf16* A, long lda, const bf16* B, long ldb
     const int plan = gemm_plan(AK, BKc, M, N, K, splits, ws != nullptr, e.rowsum != nullptr);
     if (plan == PLAN_256_TAIL) {
       const TailSplit ts = tail_split(M, N, K);
-      gemm256_kernel<AK, BKc, OutT, 0, kNA><<<ts.n_dp + ts.n_sk, NT2, 0, st>>>(M, N, K, A, lda, B, ldb, C, ldc, e, K, 0, 0, ws,
-                                                                      ts.n_dp, ts.sk_klen);
+      if (ph_gemm)
+        gemm256_kernel<AK, BKc, OutT, 0, kNA><<<ts.n_dp + ts.n_sk, NT2, 0, st>>>(M, N, K, A, lda, B, ldb, C, ldc, e, K, 0,
+                                                                                0, ws, ts.n_dp, ts.sk_klen);
       const int tail_rows = M - ts.tail_m0;
-      splitk_reduce_kernel<OutT><<<reduce_blocks(tail_rows, N), 256, 0, st>>>(
-          tail_rows, N, ts.nsplit, ws, (long)tail_rows * N, C, ldc, e, ts.tail_m0);
+      if (ph_red)
+        splitk_reduce_kernel<OutT><<<reduce_blocks(tail_rows, N), 256, 0, st>>>(
+            tail_rows, N, ts.nsplit, ws, (long)tail_rows * N, C, ldc, e, ts.tail_m0);
     } else if (plan == PLAN_8P) {
-      gemm8p_kernel<BKc, OutT><<<grid, NT2, 0, st>>>(M, N, K, A, lda, B, ldb, C, ldc, e);
+      if (ph_gemm) gemm8p_kernel<BKc, OutT><<<grid, NT2, 0, st>>>(M, N, K, A, lda, B, ldb, C, ldc, e);
     } else if (plan == PLAN_256) {
-      gemm256_kernel<AK, BKc, OutT, 0, kNA><<<grid, NT2, 0, st>>>(M, N, K, A, lda, B, ldb, C, ldc, e, klen, 0, 0, nullptr, 0, 0);
+      if (ph_gemm)
+        gemm256_kernel<AK, BKc, OutT, 0, kNA><<<grid, NT2, 0, st>>>(M, N, K, A, lda, B, ldb, C, ldc, e, klen, 0, 0, nullptr,
+                                                                   0, 0);
     } else {
-      gemm256_kernel<AK, BKc, float, 0, kNA><<<grid, NT2, 0, st>>>(M, N, K, A, lda, B, ldb, ws, N, e, klen, ss, 1, nullptr, 0,
-                                                           0);
-      splitk_reduce_kernel<OutT><<<reduce_blocks(M, N), 256, 0, st>>>(M, N, nsplit, ws, ss, C, ldc, e);
+      if (ph_gemm)
+        gemm256_kernel<AK, BKc, float, 0, kNA><<<grid, NT2, 0, st>>>(M, N, K, A, lda, B, ldb, ws, N, e, klen, ss, 1,
+                                                                    nullptr, 0, 0);
+      if (ph_red) splitk_reduce_kernel<OutT><<<reduce_blocks(M, N), 256, 0, st>>>(M, N, nsplit, ws, ss, C, ldc, e);
     }
     CMHAR_CHECK_LAUNCH();
     return 0;
@@ -919,6 +927,7 @@ int launch(int M, int N, int K, const bf16* A, long lda, const bf16* B, long ldb
   const bool full = (M % BM == 0) && (N % BN == 0) && (K % BK == 0) && (klen % BK == 0);
 #define GO(BND)                                                                                               \
   do {                                                                                                        \
+    if (!ph_gemm) break;                                                                                      \
     if (nsplit == 1)                                                                                          \
       gemm_bf16_kernel<AK, BKc, OutT, BND><<<grid, NT, 0, st>>>(M, N, K, A, lda, B, ldb, C, ldc, e, klen, 0, 0); \
     else                                                                                                      \
@@ -926,7 +935,8 @@ int launch(int M, int N, int K, const bf16* A, long lda, const bf16* B, long ldb
   } while (0)
   if (full) GO(false); else GO(true);
 #undef GO
-  if (nsplit > 1) splitk_reduce_kernel<OutT><<<reduce_blocks(M, N), 256, 0, st>>>(M, N, nsplit, ws, ss, C, ldc, e);
+  if (nsplit > 1 && ph_red)
+    splitk_reduce_kernel<OutT><<<reduce_blocks(M, N), 256, 0, st>>>(M, N, nsplit, ws, ss, C, ldc, e);
   CMHAR_CHECK_LAUNCH();
   return 0;
 }
@@ -946,12 +956,13 @@ extern "C" int cmhar_gemm_bf16_plan(int layout, int M, int N, int K, int splits,
   return gemm_plan(layout != 2, layout == 0, M, N, K, splits, has_ws != 0, rowsum != 0);
 }
 
-// layout: 0 = NT (A K-contig, B K-contig: Y = X Wᵀ), 1 = NN (A K-contig, B N-contig: dX = dY W),
-//         2 = TN (A M-contig, B N-contig: dW = dYᵀ X).  ws: fp32 workspace of splits*M*N floats when splits > 1.
-extern "C" int cmhar_gemm_bf16(int layout, int out_dtype, int M, int N, int K, const void* A, long lda, const void* B,
-                               long ldb, void* C, long ldc, const Epilogue* epi, int splits, void* ws,
-                               hipStream_t stream) {
+// cmhar_gemm_bf16 with a phase mask (bit 0 = GEMM kernel, bit 1 = split-K / tail reduce): phases 1 then 2 is the
+// same computation as one cmhar_gemm_bf16 call, split so that a tracer can bracket the GEMM kernel alone.
+extern "C" int cmhar_gemm_bf16_phased(int layout, int out_dtype, int M, int N, int K, const void* A, long lda,
+                                      const void* B, long ldb, void* C, long ldc, const Epilogue* epi, int splits,
+                                      void* ws, hipStream_t stream, int phases) {
   if (M <= 0 || N <= 0) return 0;
+  if (phases < 1 || phases > 3) return -1;
   const bf16* a = (const bf16*)A;
   const bf16* b = (const bf16*)B;
   float* w = (float*)ws;
@@ -959,8 +970,9 @@ extern "C" int cmhar_gemm_bf16(int layout, int out_dtype, int M, int N, int K, c
   plain.alpha = 1.f;
   const Epilogue& e = epi ? *epi : plain;             // NULL = the plain product
 #define DISPATCH(AK, BKc)                                                                                     \
-  return out_dtype == CMHAR_BF16 ? launch<AK, BKc, bf16>(M, N, K, a, lda, b, ldb, (bf16*)C, ldc, e, splits, w, stream) \
-                                 : launch<AK, BKc, float>(M, N, K, a, lda, b, ldb, (float*)C, ldc, e, splits, w, stream)
+  return out_dtype == CMHAR_BF16                                                                              \
+             ? launch<AK, BKc, bf16>(M, N, K, a, lda, b, ldb, (bf16*)C, ldc, e, splits, w, stream, phases)    \
+             : launch<AK, BKc, float>(M, N, K, a, lda, b, ldb, (float*)C, ldc, e, splits, w, stream, phases)
   switch (layout) {
     case 0: DISPATCH(true, true);
     case 1: DISPATCH(true, false);
@@ -968,4 +980,12 @@ extern "C" int cmhar_gemm_bf16(int layout, int out_dtype, int M, int N, int K, c
     default: return -1;
   }
 #undef DISPATCH
+}
+
+// layout: 0 = NT (A K-contig, B K-contig: Y = X Wᵀ), 1 = NN (A K-contig, B N-contig: dX = dY W),
+//         2 = TN (A M-contig, B N-contig: dW = dYᵀ X).  ws: fp32 workspace of splits*M*N floats when splits > 1.
+extern "C" int cmhar_gemm_bf16(int layout, int out_dtype, int M, int N, int K, const void* A, long lda, const void* B,
+                               long ldb, void* C, long ldc, const Epilogue* epi, int splits, void* ws,
+                               hipStream_t stream) {
+  return cmhar_gemm_bf16_phased(layout, out_dtype, M, N, K, A, lda, B, ldb, C, ldc, epi, splits, ws, stream, 3);
 }

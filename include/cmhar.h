@@ -64,6 +64,12 @@ long cmhar_gemm_bf16_ws(int M, int N, int K);
  * 0 = 128² tile, 1 = 256² tile, 2 = 256² + tail split + reduce, 3 = 256² split-K + reduce, 4 = 8-phase 256²
  * (forward layout), 5 = 128² split-K + reduce; -1 = bad layout.  Used for trace labels (bench.py kernel breakdown). */
 int cmhar_gemm_bf16_plan(int layout, int M, int N, int K, int splits, int has_ws, int rowsum);
+/* cmhar_gemm_bf16 restricted to a phase mask: bit 0 = the GEMM kernel, bit 1 = the split-K / tail reduce (3 = the
+ * whole call).  Calling phases 1 then 2 on one stream equals one cmhar_gemm_bf16 call; bench.py uses the split to
+ * time the GEMM kernel alone with HIP events.  Returns -1 for phases outside 1..3. */
+int cmhar_gemm_bf16_phased(int layout, int out_dtype, int M, int N, int K, const void* A, long lda, const void* B,
+                           long ldb, void* C, long ldc, const CmharEpilogue* epi, int splits, void* ws,
+                           hipStream_t stream, int phases);
 
 /* Exact-fp32 (or mixed) strided batched GEMM: C[z][m,n] = epi(Σ_k A[z][m*sam+k*sak] B[z][k*sbk+n*sbn])
  * (replaces: the fp32 nn.Linear / IMU encoder / ProjectionHead matmuls, models.py:16-132, 221-234). */
