@@ -14,7 +14,7 @@ import torch
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get('CMHAR_LIB', os.path.join(_HERE, 'libcmhar.so'))
 
-F32, BF16 = 0, 1
+F32, BF16, F16 = 0, 1, 2
 ACT_NONE, ACT_GELU, ACT_RELU, ACT_DGELU, ACT_DRELU, ACT_GELU_SAVEGRAD, ACT_MULAUX = 0, 1, 2, 3, 4, 5, 6
 
 vp, i32, i64, f32, u64 = C.c_void_p, C.c_int, C.c_long, C.c_float, C.c_ulonglong
@@ -32,6 +32,7 @@ _SIGS = {
     'cmhar_gemm_bf16': (i32, [i32, i32, i32, i32, i32, vp, i64, vp, i64, vp, i64, C.POINTER(Epilogue), i32, vp, vp]),
     'cmhar_gemm_bf16_phased': (i32, [i32, i32, i32, i32, i32, vp, i64, vp, i64, vp, i64, C.POINTER(Epilogue), i32, vp,
                                      vp, i32]),
+    'cmhar_gemm_f16': (i32, [i32, i32, i32, i32, i32, vp, i64, vp, i64, vp, i64, C.POINTER(Epilogue), i32, vp, vp]),
     'cmhar_gemm_bf16_ws': (i64, [i32, i32, i32]),
     'cmhar_gemm_bf16_plan': (i32, [i32, i32, i32, i32, i32, i32, i32]),
     'cmhar_gemm_generic': (i32, [i32, i32, i32, i32, i32, i32, vp, i64, i64, i64, vp, i64, i64, i64, vp, i64, i64,
@@ -128,6 +129,8 @@ def dtype_code(dt):
         return F32
     if dt == torch.bfloat16:
         return BF16
+    if dt == torch.float16:
+        return F16
     raise TypeError(f'unsupported dtype {dt}')
 
 

@@ -82,7 +82,8 @@ class ModelConfig:
     classifier_hidden_dims: List[int] = field(default_factory=lambda: [256, 128])
     classifier_dropout: float = 0.3
     # ---- MI355X build knobs (not in the reference) ----
-    compute_dtype: str = 'bf16'          # 'bf16' (MFMA bf16, fp32 accumulate) or 'fp32' (exact-f32 parity mode)
+    compute_dtype: str = 'bf16'          # 'bf16' (MFMA bf16, fp32 accumulate), 'fp32' (exact-f32 parity mode) or
+    #                                      'fp16' (MFMA fp16, fp32 accumulate; VideoMAE inference only — config 5)
     # video_pretrained=True with a hub name that cannot be loaded offline raises (as from_pretrained would);
     # True (or env CMHAR_ALLOW_RANDOM_INIT=1) builds the configured architecture with random weights instead
     # (benchmarks and tests, which use synthetic data)

@@ -40,9 +40,12 @@ class _LinearFn(torch.autograd.Function):
     def forward(ctx, x, weight, bias, residual, dt, out_dt):
         xc = _cast(x, dt)
         wc = _cast(weight.detach(), dt)
-        y = torch.empty(xc.shape[0], wc.shape[0], dtype=out_dt, device=x.device)
+        # the exact-fp32 GEMM writes fp32 / bf16; an fp16 result of it (fp16 inference path) is cast afterwards
+        gemm_dt = torch.float32 if (dt == torch.float32 and out_dt == torch.float16) else out_dt
+        y = torch.empty(xc.shape[0], wc.shape[0], dtype=gemm_dt, device=x.device)
         K.gemm(0, xc, wc, y, bias=None if bias is None else bias.detach(),
-               residual=None if residual is None else _cast(residual, out_dt))
+               residual=None if residual is None else _cast(residual, gemm_dt))
+        y = _cast(y, out_dt)
         ctx.save_for_backward(xc, wc)
         ctx.dt, ctx.x_dtype, ctx.has_bias, ctx.has_res = dt, x.dtype, bias is not None, residual is not None
         return y
@@ -136,8 +139,8 @@ class CrossAttentionFusion(nn.Module):
         super().__init__()
         if d_model % num_heads or d_model // num_heads not in (8, 16, 32, 64):
             raise ValueError('head dim must be 8/16/32/64')
-        if compute_dtype == 'bf16' and d_model // num_heads != 64:
-            raise ValueError('bf16 (MFMA flash) attention needs head dim 64')
+        if compute_dtype in ('bf16', 'fp16') and d_model // num_heads != 64:
+            raise ValueError(f'{compute_dtype} (MFMA flash) attention needs head dim 64')
         self.d_model, self.num_heads, self.eps, self.compute_dtype = d_model, num_heads, eps, compute_dtype
         self.q_proj = nn.Linear(imu_dim, d_model)
         self.kv_proj = nn.Linear(video_dim, 2 * d_model)      # rows [0, d): K, [d, 2d): V
@@ -153,7 +156,7 @@ class CrossAttentionFusion(nn.Module):
         B, Lq, _ = imu_tokens.shape
         Lk = video_tokens.shape[1]
         d, H = self.d_model, self.num_heads
-        dt = torch.bfloat16 if self.compute_dtype == 'bf16' else torch.float32
+        dt = {'bf16': torch.bfloat16, 'fp16': torch.float16}.get(self.compute_dtype, torch.float32)
         xi = imu_tokens.reshape(B * Lq, -1).float()
         xv = video_tokens.reshape(B * Lk, -1)
         f32 = torch.float32

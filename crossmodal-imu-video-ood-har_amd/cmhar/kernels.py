@@ -197,6 +197,25 @@ def gemm(layout: int, a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, *, bi
     epi = L.epilogue(bias, residual, aux_in, aux_out, rowadd, rowadd_mod, act, alpha, beta, pdrop, seed, rowsum,
                      rowsum_beta)
     st = L.stream(out.device)
+    if a.dtype == torch.float16:
+        # fp16 inference path (BASELINE config 5): the bf16 kernels on the fp16 MFMA, forward layout only
+        if layout != 0 or rowsum is not None:
+            raise ValueError('fp16 GEMM: forward layout 0 only (inference path)')
+        _check_bf16_operand(a, 'A')
+        _check_bf16_operand(b, 'B')
+        if K % 8:
+            raise ValueError('fp16 GEMM needs K to be a multiple of 8')
+        if out.dtype not in (torch.float16, torch.float32):
+            raise TypeError('fp16 GEMM output must be fp16 or fp32')
+        s = 1 if splits is None else splits
+        ws = workspace(s * M * N, out.device) if s > 1 else None
+        if s == 1 and splits is None:
+            n = _tail_ws(M, N, K)
+            if n:
+                ws = workspace(n, out.device)
+        call('cmhar_gemm_f16', layout, L.dtype_code(out.dtype), M, N, K, ptr(a), a.stride(0), ptr(b), b.stride(0),
+             ptr(out), out.stride(0), C.byref(epi), s, ptr(ws), st)
+        return out
     if a.dtype == torch.bfloat16:
         _check_bf16_operand(a, 'A')
         _check_bf16_operand(b, 'B')
@@ -312,7 +331,7 @@ def attention_fwd(q, k, v, out, lse, *, B, H, Lq, Lk, D, scale, pdrop=0.0, seed=
     dt = L.dtype_code(q.dtype)
     if D not in (8, 16, 32, 64):
         raise ValueError(f'head dim {D} not supported')
-    if dt == L.BF16 and D == 64 and pdrop == 0.0:     # flash (MFMA) path: 16-B aligned rows
+    if dt in (L.BF16, L.F16) and D == 64 and pdrop == 0.0:     # flash (MFMA) path: 16-B aligned rows
         for t, n in ((q, 'q'), (k, 'k'), (v, 'v'), (out, 'o')):
             _check_bf16_operand(t, n)
     ev = TRACE.begin('attn_fwd_bf16') if (dt == L.BF16 and D == 64 and pdrop == 0.0) else None
@@ -329,6 +348,8 @@ def attention_bwd(q, k, v, o, do, lse, dq, dk, dv, *, B, H, Lq, Lk, D, scale, pd
     dt = L.dtype_code(q.dtype)
     if D not in (8, 16, 32, 64):
         raise ValueError(f'head dim {D} not supported')
+    if dt == L.F16:
+        raise ValueError('fp16 is the inference-only path: no attention backward')
     flash = dt == L.BF16 and D == 64 and pdrop == 0.0
     if flash:
         for t, n in ((q, 'q'), (k, 'k'), (v, 'v'), (o, 'o'), (do, 'do'), (dq, 'dq'), (dk, 'dk'), (dv, 'dv')):

@@ -92,6 +92,8 @@ class VideoEncoder(nn.Module):
                                   f'initialised backbone of the configured geometry (allow_random_init)')
                 self.backbone = VideoMAEBackbone(_videomae_geometry(config), compute_dtype=dt)
             self.feature_dim = self.backbone.config.hidden_size
+        elif dt == 'fp16':
+            raise ValueError("compute_dtype 'fp16' (inference path) covers the VideoMAE backbone only")
         elif vb == 'r3d_18':
             # north_star extension (no reference code): torchvision-layout R3D-18 on the HIP conv3d path
             self.backbone = R3D18(None, compute_dtype=dt)

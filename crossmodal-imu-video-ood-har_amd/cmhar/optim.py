@@ -83,7 +83,7 @@ class FusedAdamW(torch.optim.Optimizer):
         packs = []
         for m in self.shadow_sources:
             pk = getattr(m, '_packs', None)
-            if pk is not None:
+            if pk is not None and pk.dtype != torch.float16:   # fp16 (inference) packs are refreshed by version
                 slots.update(pk.slots)
                 packs.append(pk)
         return slots, packs

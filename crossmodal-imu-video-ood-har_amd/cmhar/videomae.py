@@ -11,8 +11,9 @@ autograd node whose body is a sequence of HIP launches:
   → out-proj GEMM(+bias +residual) → LN → FC1 GEMM(+bias, GELU, pre-act saved) → FC2 GEMM(+bias +residual)]
 
 and the mirrored backward (dgrad GEMMs with fused GELU'/residual epilogues, split-K fp32 wgrad GEMMs that also
-emit the bias gradients, flash attention backward, fused LN backward with the residual gradient).  Compute dtype: bf16 (MFMA, fp32 accumulate)
-or fp32 (exact parity mode); master weights and their gradients stay fp32.
+emit the bias gradients, flash attention backward, fused LN backward with the residual gradient).  Compute dtype: bf16 (MFMA, fp32 accumulate),
+fp32 (exact parity mode), or fp16 (MFMA, fp32 accumulate; forward only — the inference path of BASELINE config 5);
+master weights and their gradients stay fp32.
 """
 from __future__ import annotations
 
@@ -104,6 +105,9 @@ def default_videomae_config(**kw):
     return types.SimpleNamespace(**cfg)
 
 
+_DTYPES = {'bf16': torch.bfloat16, 'fp16': torch.float16, 'fp32': torch.float32}
+
+
 class VideoMAEOutput:
     def __init__(self, last_hidden_state):
         self.last_hidden_state = last_hidden_state
@@ -167,7 +171,7 @@ class VideoMAEBackbone(nn.Module):
     # ------------------------------------------------------------------------------------------------------
     def _weights(self):
         """Packed compute-dtype weights (QKV concatenated), refreshed when the fp32 masters change."""
-        dt = torch.bfloat16 if self.compute_dtype == 'bf16' else torch.float32
+        dt = _DTYPES.get(self.compute_dtype, torch.float32)
         dev = self.embeddings.patch_embeddings.projection.weight.device
         if self._packs is None or self._packs.device != dev or self._packs.dtype != dt:
             self._packs = PackedWeights(dev, dt)
@@ -399,6 +403,9 @@ def run_backbone(m: VideoMAEBackbone, video: torch.Tensor, token0_only: bool) ->
     (`last_hidden_state[:, 0]`, models.py:201) or the full fp32 last_hidden_state (B, L, Hd)."""
     params = list(m.parameters())
     if torch.is_grad_enabled() and any(p.requires_grad for p in params):
+        if m.compute_dtype == 'fp16':
+            raise RuntimeError("compute_dtype 'fp16' is the inference-only path (BASELINE config 5): run it under "
+                               "torch.no_grad() / with frozen parameters, or use 'bf16' / 'fp32' for training")
         return _BackboneFn.apply(video, m, token0_only, *params)
     with torch.no_grad():
         x, st = _forward_impl(m, video, save=False)

@@ -102,8 +102,17 @@ class PackedWeights:
                 tab[i]['pbf'] = bf
                 tab[i]['pcopy'] = cp
                 tab[i]['n'] = p.numel()
-            ch = chunk_list([p.numel() for p in stale])
-            dt = to_device_bytes(tab, self.device)
-            dc = to_device_bytes(ch, self.device)
-            L.call('cmhar_mt_cast_bf16', dt.data_ptr(), dc.data_ptr(), len(ch), L.stream(self.device))
+            if self.dtype == torch.float16:
+                # fp16 inference packs (refreshed only when the weights change): one cast launch per parameter
+                for p in stale:
+                    h, cp = self.slots[p]
+                    rows = p.shape[0]
+                    cols = p.numel() // rows
+                    L.call('cmhar_copy2d', L.F32, L.F16 if h else L.F32, rows, cols, p.data_ptr(), cols, h or cp,
+                           cols, 1.0, 0.0, 0.0, 0, L.stream(self.device))
+            else:
+                ch = chunk_list([p.numel() for p in stale])
+                dt = to_device_bytes(tab, self.device)
+                dc = to_device_bytes(ch, self.device)
+                L.call('cmhar_mt_cast_bf16', dt.data_ptr(), dc.data_ptr(), len(ch), L.stream(self.device))
         self._versions = vers

@@ -69,12 +69,13 @@ __device__ __forceinline__ bf16x8 tr_frag(const char* lds, int r0, int s, int c0
   return __builtin_bit_cast(bf16x8, v);
 }
 
-// Accumulator registers 8s..8s+7 → bf16 operand fragment.
+// Accumulator registers 8s..8s+7 → 16-bit operand fragment in format E (bf16, or fp16 on the inference path).
+template <typename E = bf16>
 __device__ __forceinline__ bf16x8 pack8(const floatx16& a, int s) {
-  bf16x8 v;
+  float x[8];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) v[j] = (bf16)a[8 * s + j];
-  return v;
+  for (int j = 0; j < 8; ++j) x[j] = a[8 * s + j];
+  return pack_frag8<E>(x);
 }
 
 // accumulator register r of lane-half h ↔ row index (r&3) + 8(r>>2) + 4h
@@ -100,10 +101,11 @@ __device__ __forceinline__ BlkIdx flash_block(int H) {
 // LDS feeds QB MFMA chains, so LDS read traffic per MFMA is 1/QB of the one-block form (at QB = 1 the reads
 // alone saturate the CU's 128 B/clk LDS port at the MFMA rate).  A workgroup = 4 waves = 128·QB queries starting
 // at q_base; K/V tiles of 64 keys are register-staged into a double-buffered LDS pair (issue early, write late).
-template <int QB>
+// E: the 16-bit number format of Q/K/V/O (bf16 training path; fp16 for the fp16 inference path).
+template <typename E, int QB>
 __global__ __launch_bounds__(256, 2) void attn_fwd_bf16(int H, int Lq, int Lk, int q_base, const bf16* __restrict__ Q,
                                                         long ldq, const bf16* __restrict__ K, long ldk,
-                                                        const bf16* __restrict__ V, long ldv, bf16* __restrict__ O,
+                                                        const bf16* __restrict__ V, long ldv, E* __restrict__ O,
                                                         long ldo, float* __restrict__ lse, float scale) {
   __shared__ __attribute__((aligned(16))) char smem[4 * 8192];
 #define Ks(buf) (smem + 8192 * (buf))
@@ -164,7 +166,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_bf16(int H, int Lq, int Lk, i
         const bf16x8 kf = row_frag(Ks(cur), kb * 32, t, lane);
 #pragma unroll
         for (int j = 0; j < QB; ++j)
-          s[j][kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[j][t], s[j][kb], 0, 0, 0);
+          s[j][kb] = mma32<E>(kf, qf[j][t], s[j][kb]);
       }
     }
     }
@@ -216,7 +218,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_bf16(int H, int Lq, int Lk, i
           l[j] += p;
         }
 #pragma unroll
-        for (int ss = 0; ss < 2; ++ss) pb[j][kb][ss] = pack8(s[j][kb], ss);   // P leaves fp32 registers here
+        for (int ss = 0; ss < 2; ++ss) pb[j][kb][ss] = pack8<E>(s[j][kb], ss);   // P leaves fp32 registers here
       }
     }
     // Oᵀ += Vᵀ·Pᵀ; each V transposed fragment is read once and used QB times
@@ -229,7 +231,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_bf16(int H, int Lq, int Lk, i
           const bf16x8 vf = tr_frag(Vs(cur), kb * 32, ss, d * 32, lane);
 #pragma unroll
           for (int j = 0; j < QB; ++j)
-            o[j][d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pb[j][kb][ss], o[j][d], 0, 0, 0);
+            o[j][d] = mma32<E>(vf, pb[j][kb][ss], o[j][d]);
         }
     }
     if (more) {
@@ -248,15 +250,16 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_bf16(int H, int Lq, int Lk, i
     const float inv = 1.f / lj;
     const int q = q0 + 32 * j + (lane & 31);
     if (q < Lq) {
-      bf16* orow = O + ((long)b * Lq + q) * ldo + hd * 64;
+      E* orow = O + ((long)b * Lq + q) * ldo + hd * 64;
 #pragma unroll
       for (int d = 0; d < 2; ++d)
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
-          bf16x4 v;
+          typedef E __attribute__((ext_vector_type(4))) e4;
+          e4 v;
 #pragma unroll
-          for (int jj = 0; jj < 4; ++jj) v[jj] = (bf16)(o[j][d][4 * g + jj] * inv);
-          *(bf16x4*)(orow + d * 32 + 8 * g + 4 * h) = v;
+          for (int jj = 0; jj < 4; ++jj) v[jj] = (E)(o[j][d][4 * g + jj] * inv);
+          *(e4*)(orow + d * 32 + 8 * g + 4 * h) = v;
         }
       if (h == 0) lse[((long)b * H + hd) * Lq + q] = m[j] + log2f(lj);   // log2-domain LSE of (scale*log2e)*s
     }
@@ -680,17 +683,22 @@ extern "C" int cmhar_attention_fwd(int dtype, int B, int H, int Lq, int Lk, int 
                                    const void* K, long ldk, const void* V, long ldv, void* O, long ldo, float* lse,
                                    float scale, float pdrop, unsigned long long seed, hipStream_t st) {
   if (B <= 0 || Lq <= 0) return 0;
-  if (dtype == CMHAR_BF16 && D == 64 && pdrop == 0.f) {
+  if ((dtype == CMHAR_BF16 || dtype == CMHAR_F16) && D == 64 && pdrop == 0.f) {
     // 256-query workgroups (64 rows per wave) over the bulk, 128-query workgroups (32 rows per wave, waves past Lq
     // skip the math) for the rest
     const int bulk = (Lq / 256) * 256;
-    if (bulk > 0)
-      attn_fwd_bf16<2><<<dim3(bulk / 256, H, B), 256, 0, st>>>(H, Lq, Lk, 0, (const bf16*)Q, ldq, (const bf16*)K, ldk,
-                                                               (const bf16*)V, ldv, (bf16*)O, ldo, lse, scale);
-    if (Lq > bulk)
-      attn_fwd_bf16<1><<<dim3(cdiv(Lq - bulk, 128), H, B), 256, 0, st>>>(H, Lq, Lk, bulk, (const bf16*)Q, ldq,
-                                                                         (const bf16*)K, ldk, (const bf16*)V, ldv,
-                                                                         (bf16*)O, ldo, lse, scale);
+#define FL(E)                                                                                                    \
+  do {                                                                                                           \
+    if (bulk > 0)                                                                                                \
+      attn_fwd_bf16<E, 2><<<dim3(bulk / 256, H, B), 256, 0, st>>>(H, Lq, Lk, 0, (const bf16*)Q, ldq, (const bf16*)K, \
+                                                                  ldk, (const bf16*)V, ldv, (E*)O, ldo, lse, scale); \
+    if (Lq > bulk)                                                                                               \
+      attn_fwd_bf16<E, 1><<<dim3(cdiv(Lq - bulk, 128), H, B), 256, 0, st>>>(H, Lq, Lk, bulk, (const bf16*)Q, ldq,   \
+                                                                            (const bf16*)K, ldk, (const bf16*)V, ldv, \
+                                                                            (E*)O, ldo, lse, scale);             \
+  } while (0)
+    if (dtype == CMHAR_F16) FL(f16); else FL(bf16);
+#undef FL
   } else {
     // exact-fp32 math path (fp32 storage, or bf16 storage with a head dim / dropout the flash kernel lacks);
     // its LSE is in natural-log units and is only ever consumed by the matching backward below
@@ -700,7 +708,7 @@ extern "C" int cmhar_attention_fwd(int dtype, int B, int H, int Lq, int Lk, int 
                                             (TT*)O, ldo, lse, scale, pdrop, seed)
 #define SW(TT) switch (D) { case 8: F(TT, 8); break; case 16: F(TT, 16); break; case 32: F(TT, 32); break;  \
                             case 64: F(TT, 64); break; default: return -1; }
-    if (dtype == CMHAR_BF16) { SW(bf16) } else { SW(float) }
+    if (dtype == CMHAR_BF16) { SW(bf16) } else if (dtype == CMHAR_F16) { SW(f16) } else { SW(float) }
 #undef SW
 #undef F
   }
@@ -715,6 +723,7 @@ extern "C" int cmhar_attention_bwd(int dtype, int B, int H, int Lq, int Lk, int 
                                    void* dK, long lddk, void* dV, long lddv, float scale, float pdrop,
                                    unsigned long long seed, hipStream_t st) {
   if (B <= 0 || Lq <= 0) return 0;
+  if (dtype == CMHAR_F16) return -1;   // fp16 is the inference-only path
   if (dtype == CMHAR_BF16 && D == 64 && pdrop == 0.f) {
     attn_bwd_dq_bf16<<<dim3(cdiv(Lq, 128), H, B), 256, 0, st>>>(H, Lq, Lk, (const bf16*)Q, ldq, (const bf16*)K, ldk,
                                                                 (const bf16*)V, ldv, (const bf16*)O, ldo,

@@ -6,6 +6,9 @@
 typedef __bf16 bf16;
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
 typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+typedef _Float16 f16;
+typedef __attribute__((ext_vector_type(8))) _Float16 f16x8;
+typedef __attribute__((ext_vector_type(4))) _Float16 f16x4;
 typedef __attribute__((ext_vector_type(4))) short short4_t;
 typedef __attribute__((ext_vector_type(8))) short short8_t;
 typedef __attribute__((ext_vector_type(4))) float floatx4;
@@ -16,7 +19,7 @@ typedef __attribute__((ext_vector_type(2))) unsigned uint2_t;
 #define LDS_PTR(T, p) ((__attribute__((address_space(3))) T*)(p))
 
 // dtype codes used across the C ABI
-enum { CMHAR_F32 = 0, CMHAR_BF16 = 1 };
+enum { CMHAR_F32 = 0, CMHAR_BF16 = 1, CMHAR_F16 = 2 };
 
 // activation / epilogue codes
 enum {
@@ -40,9 +43,37 @@ __device__ __forceinline__ bf16 f2bf(float x) { return (bf16)x; }
 template <typename T> __device__ __forceinline__ float to_f(T x);
 template <> __device__ __forceinline__ float to_f<float>(float x) { return x; }
 template <> __device__ __forceinline__ float to_f<bf16>(bf16 x) { return (float)x; }
+template <> __device__ __forceinline__ float to_f<f16>(f16 x) { return (float)x; }
 template <typename T> __device__ __forceinline__ T from_f(float x);
 template <> __device__ __forceinline__ float from_f<float>(float x) { return x; }
 template <> __device__ __forceinline__ bf16 from_f<bf16>(float x) { return (bf16)x; }
+template <> __device__ __forceinline__ f16 from_f<f16>(float x) { return (f16)x; }
+
+// 16-bit MFMA operands travel as raw 16-B fragments (bf16x8 carriers: LDS-DMA, ds_read and the transposing
+// ds_read_tr16 move bits, not numbers); E picks the number format the matrix core reads them in — bf16 for training,
+// fp16 for the fp16 inference path (BASELINE config 5).
+template <typename E> __device__ __forceinline__ floatx4 mma16(bf16x8 a, bf16x8 b, floatx4 c);
+template <> __device__ __forceinline__ floatx4 mma16<bf16>(bf16x8 a, bf16x8 b, floatx4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+template <> __device__ __forceinline__ floatx4 mma16<f16>(bf16x8 a, bf16x8 b, floatx4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c, 0, 0, 0);
+}
+template <typename E> __device__ __forceinline__ floatx16 mma32(bf16x8 a, bf16x8 b, floatx16 c);
+template <> __device__ __forceinline__ floatx16 mma32<bf16>(bf16x8 a, bf16x8 b, floatx16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+template <> __device__ __forceinline__ floatx16 mma32<f16>(bf16x8 a, bf16x8 b, floatx16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c, 0, 0, 0);
+}
+// 8 fp32 values → one 16-B fragment in format E
+template <typename E> __device__ __forceinline__ bf16x8 pack_frag8(const float (&x)[8]) {
+  typedef E __attribute__((ext_vector_type(8))) v8;
+  v8 v;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] = (E)x[j];
+  return __builtin_bit_cast(bf16x8, v);
+}
 
 // GELU(erf) and its derivative from ONE shared set of transcendentals.  Φ(x) = ½·erfc(−x/√2) with erfc(z), z ≥ 0,
 // from the Chebyshev-fitted form erfc(z) = t·exp(−z² + R(t)), t = 1/(1 + z/2) (Numerical Recipes `erfcc`,

@@ -88,7 +88,8 @@ __device__ __forceinline__ bf16x8 frag(const char* lds, int r0, int kk, int lane
 template <typename OutT>
 __device__ __forceinline__ void load8(const OutT* __restrict__ p, float (&x)[8]) {
   if constexpr (sizeof(OutT) == 2) {
-    const bf16x8 v = *(const bf16x8*)p;
+    typedef OutT __attribute__((ext_vector_type(8))) v8;
+    const v8 v = *(const v8*)p;
 #pragma unroll
     for (int j = 0; j < 8; ++j) x[j] = (float)v[j];
   } else {
@@ -100,10 +101,11 @@ __device__ __forceinline__ void load8(const OutT* __restrict__ p, float (&x)[8])
 template <typename OutT>
 __device__ __forceinline__ void store8(OutT* __restrict__ p, const float (&x)[8]) {
   if constexpr (sizeof(OutT) == 2) {
-    bf16x8 v;
+    typedef OutT __attribute__((ext_vector_type(8))) v8;
+    v8 v;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = (bf16)x[j];
-    *(bf16x8*)p = v;
+    for (int j = 0; j < 8; ++j) v[j] = (OutT)x[j];
+    *(v8*)p = v;
   } else {
     *(floatx4*)p = floatx4{x[0], x[1], x[2], x[3]};
     *(floatx4*)(p + 4) = floatx4{x[4], x[5], x[6], x[7]};
@@ -175,7 +177,7 @@ __device__ __forceinline__ void epilogue_store8(const Epilogue& e, OutT* __restr
 constexpr int EPI_LD = BN + 4;                       // padded fp32 staging row: conflict-free acc writes
 constexpr int SMEM_BYTES = BM * EPI_LD * 4;          // 67584 B ≥ the 64 KiB of double-buffered A/B stages
 
-template <bool A_KC, bool B_KC, typename OutT, bool BOUNDS>
+template <typename E, bool A_KC, bool B_KC, typename OutT, bool BOUNDS>
 __global__ __launch_bounds__(NT, 2) void gemm_bf16_kernel(int M, int N, int K, const bf16* __restrict__ A, long lda,
                                                           const bf16* __restrict__ B, long ldb,
                                                           OutT* __restrict__ C, long ldc, Epilogue e, int klen,
@@ -233,7 +235,7 @@ __global__ __launch_bounds__(NT, 2) void gemm_bf16_kernel(int M, int N, int K, c
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+        for (int j = 0; j < 4; ++j) acc[i][j] = mma16<E>(af[i], bfr[j], acc[i][j]);
     }
     if (more) {
       sa.store(As(cur ^ 1), tid);
@@ -397,7 +399,7 @@ __device__ __forceinline__ bf16x8 frag256(const char* lds, int r0, int kk, int l
 // NA: A-operand LDS buffers.  2 = tile k+1 streams in while tile k is consumed (A and B double-buffered, 128 KiB);
 // 3 = the A tile (the HBM-streamed activation panel) is fetched TWO tiles ahead — three 32 KiB A buffers + two
 // 32 KiB B buffers = the whole 160 KiB LDS — so its longer HBM/MALL latency has two K-tiles of MFMAs to hide under.
-template <bool A_KC, bool B_KC, typename OutT, int MODE = 0, int NA = 2>
+template <typename E, bool A_KC, bool B_KC, typename OutT, int MODE = 0, int NA = 2>
 __global__ __launch_bounds__(NT2, 2) void gemm256_kernel(int M, int N, int K, const bf16* __restrict__ A, long lda,
                                                          const bf16* __restrict__ B, long ldb, OutT* __restrict__ C,
                                                          long ldc, Epilogue e, int klen, long split_stride,
@@ -448,7 +450,8 @@ __global__ __launch_bounds__(NT2, 2) void gemm256_kernel(int M, int N, int K, co
   // A fragment against an all-ones B fragment.  One block per row panel (tn == tm % tiles_n, spreading the panels
   // over the column tiles) does it, each of its waves for 2 of its 8 A fragments: +2 MFMAs per 32 on those blocks.
   const bool rs = !A_KC && e.rowsum != nullptr && tn == tm % tiles_n;
-  const bf16x8 ones = {(bf16)1.f, (bf16)1.f, (bf16)1.f, (bf16)1.f, (bf16)1.f, (bf16)1.f, (bf16)1.f, (bf16)1.f};
+  const float one8[8] = {1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f};
+  const bf16x8 ones = pack_frag8<E>(one8);
   floatx4 accb[2] = {floatx4{0.f, 0.f, 0.f, 0.f}, floatx4{0.f, 0.f, 0.f, 0.f}};
 
   floatx4 acc[8][4];
@@ -516,18 +519,18 @@ __global__ __launch_bounds__(NT2, 2) void gemm256_kernel(int M, int N, int K, co
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bf0[j], acc[i][j], 0, 0, 0);
+      for (int j = 0; j < 4; ++j) acc[i][j] = mma16<E>(af[i], bf0[j], acc[i][j]);
       if (!A_KC && rs && wc == (i >> 1))
-        accb[i & 1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], ones, accb[i & 1], 0, 0, 0);
+        accb[i & 1] = mma16<E>(af[i], ones, accb[i & 1]);
       af[i] = frag256<A_KC>(a_s, wr * 128 + i * 16, 1, lane);
       __builtin_amdgcn_sched_barrier(0);
     }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bf1[j], acc[i][j], 0, 0, 0);
+      for (int j = 0; j < 4; ++j) acc[i][j] = mma16<E>(af[i], bf1[j], acc[i][j]);
       if (!A_KC && rs && wc == (i >> 1))
-        accb[i & 1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], ones, accb[i & 1], 0, 0, 0);
+        accb[i & 1] = mma16<E>(af[i], ones, accb[i & 1]);
     }
     __builtin_amdgcn_sched_barrier(0);
     if (more) {
@@ -540,9 +543,9 @@ __global__ __launch_bounds__(NT2, 2) void gemm256_kernel(int M, int N, int K, co
 #pragma unroll
     for (int i = 4; i < 8; ++i) {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bf1[j], acc[i][j], 0, 0, 0);
+      for (int j = 0; j < 4; ++j) acc[i][j] = mma16<E>(af[i], bf1[j], acc[i][j]);
       if (!A_KC && rs && wc == (i >> 1))
-        accb[i & 1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], ones, accb[i & 1], 0, 0, 0);
+        accb[i & 1] = mma16<E>(af[i], ones, accb[i & 1]);
       if (more) af[i] = frag256<A_KC>(nxt, wr * 128 + i * 16, 0, lane);
       __builtin_amdgcn_sched_barrier(0);
     }
@@ -666,7 +669,7 @@ struct DmaHalf {
   }
 };
 
-template <bool B_KC, typename OutT>
+template <typename E, bool B_KC, typename OutT>
 __global__ __launch_bounds__(NT2, 2) void gemm8p_kernel(int M, int N, int K, const bf16* __restrict__ A, long lda,
                                                         const bf16* __restrict__ B, long ldb, OutT* __restrict__ C,
                                                         long ldc, Epilogue e) {
@@ -712,8 +715,8 @@ __global__ __launch_bounds__(NT2, 2) void gemm8p_kernel(int M, int N, int K, con
     _Pragma("unroll") for (int kk = 0; kk < 2; ++kk)                                                          \
     _Pragma("unroll") for (int i = 0; i < 4; ++i)                                                             \
     _Pragma("unroll") for (int j = 0; j < 2; ++j)                                                             \
-      acc[(QM) * 4 + i][qn_ * 2 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[kk][i], BF[kk][j],           \
-                                                                             acc[(QM) * 4 + i][qn_ * 2 + j], 0, 0, 0); \
+      acc[(QM) * 4 + i][qn_ * 2 + j] = mma16<E>(af[kk][i], BF[kk][j],           \
+                                                                             acc[(QM) * 4 + i][qn_ * 2 + j]); \
     __builtin_amdgcn_s_setprio(0);                                                                            \
     __builtin_amdgcn_sched_barrier(0);                                                                        \
     __builtin_amdgcn_s_barrier();                                                                             \
@@ -876,7 +879,7 @@ static int gemm_plan(bool ak, bool bkc, int M, int N, int K, int splits, bool ha
   return PLAN_256;
 }
 
-template <bool AK, bool BKc, typename OutT>
+template <typename E, bool AK, bool BKc, typename OutT>
 int launch(int M, int N, int K, const bf16* A, long lda, const bf16* B, long ldb, OutT* C, long ldc,
            const Epilogue& e, int splits, float* ws, hipStream_t st, int phases) {
   // phases: bit 0 = the GEMM kernel, bit 1 = the split-K / tail reduce (3 = both; the split lets a tracer time
@@ -898,21 +901,21 @@ int launch(int M, int N, int K, const bf16* A, long lda, const bf16* B, long ldb
     if (plan == PLAN_256_TAIL) {
       const TailSplit ts = tail_split(M, N, K);
       if (ph_gemm)
-        gemm256_kernel<AK, BKc, OutT, 0, kNA><<<ts.n_dp + ts.n_sk, NT2, 0, st>>>(M, N, K, A, lda, B, ldb, C, ldc, e, K, 0,
+        gemm256_kernel<E, AK, BKc, OutT, 0, kNA><<<ts.n_dp + ts.n_sk, NT2, 0, st>>>(M, N, K, A, lda, B, ldb, C, ldc, e, K, 0,
                                                                                 0, ws, ts.n_dp, ts.sk_klen);
       const int tail_rows = M - ts.tail_m0;
       if (ph_red)
         splitk_reduce_kernel<OutT><<<reduce_blocks(tail_rows, N), 256, 0, st>>>(
             tail_rows, N, ts.nsplit, ws, (long)tail_rows * N, C, ldc, e, ts.tail_m0);
     } else if (plan == PLAN_8P) {
-      if (ph_gemm) gemm8p_kernel<BKc, OutT><<<grid, NT2, 0, st>>>(M, N, K, A, lda, B, ldb, C, ldc, e);
+      if (ph_gemm) gemm8p_kernel<E, BKc, OutT><<<grid, NT2, 0, st>>>(M, N, K, A, lda, B, ldb, C, ldc, e);
     } else if (plan == PLAN_256) {
       if (ph_gemm)
-        gemm256_kernel<AK, BKc, OutT, 0, kNA><<<grid, NT2, 0, st>>>(M, N, K, A, lda, B, ldb, C, ldc, e, klen, 0, 0, nullptr,
+        gemm256_kernel<E, AK, BKc, OutT, 0, kNA><<<grid, NT2, 0, st>>>(M, N, K, A, lda, B, ldb, C, ldc, e, klen, 0, 0, nullptr,
                                                                    0, 0);
     } else {
       if (ph_gemm)
-        gemm256_kernel<AK, BKc, float, 0, kNA><<<grid, NT2, 0, st>>>(M, N, K, A, lda, B, ldb, ws, N, e, klen, ss, 1,
+        gemm256_kernel<E, AK, BKc, float, 0, kNA><<<grid, NT2, 0, st>>>(M, N, K, A, lda, B, ldb, ws, N, e, klen, ss, 1,
                                                                     nullptr, 0, 0);
       if (ph_red) splitk_reduce_kernel<OutT><<<reduce_blocks(M, N), 256, 0, st>>>(M, N, nsplit, ws, ss, C, ldc, e);
     }
@@ -929,9 +932,9 @@ int launch(int M, int N, int K, const bf16* A, long lda, const bf16* B, long ldb
   do {                                                                                                        \
     if (!ph_gemm) break;                                                                                      \
     if (nsplit == 1)                                                                                          \
-      gemm_bf16_kernel<AK, BKc, OutT, BND><<<grid, NT, 0, st>>>(M, N, K, A, lda, B, ldb, C, ldc, e, klen, 0, 0); \
+      gemm_bf16_kernel<E, AK, BKc, OutT, BND><<<grid, NT, 0, st>>>(M, N, K, A, lda, B, ldb, C, ldc, e, klen, 0, 0); \
     else                                                                                                      \
-      gemm_bf16_kernel<AK, BKc, float, BND><<<grid, NT, 0, st>>>(M, N, K, A, lda, B, ldb, ws, N, e, klen, ss, 1); \
+      gemm_bf16_kernel<E, AK, BKc, float, BND><<<grid, NT, 0, st>>>(M, N, K, A, lda, B, ldb, ws, N, e, klen, ss, 1); \
   } while (0)
   if (full) GO(false); else GO(true);
 #undef GO
@@ -971,8 +974,8 @@ extern "C" int cmhar_gemm_bf16_phased(int layout, int out_dtype, int M, int N, i
   const Epilogue& e = epi ? *epi : plain;             // NULL = the plain product
 #define DISPATCH(AK, BKc)                                                                                     \
   return out_dtype == CMHAR_BF16                                                                              \
-             ? launch<AK, BKc, bf16>(M, N, K, a, lda, b, ldb, (bf16*)C, ldc, e, splits, w, stream, phases)    \
-             : launch<AK, BKc, float>(M, N, K, a, lda, b, ldb, (float*)C, ldc, e, splits, w, stream, phases)
+             ? launch<bf16, AK, BKc, bf16>(M, N, K, a, lda, b, ldb, (bf16*)C, ldc, e, splits, w, stream, phases)    \
+             : launch<bf16, AK, BKc, float>(M, N, K, a, lda, b, ldb, (float*)C, ldc, e, splits, w, stream, phases)
   switch (layout) {
     case 0: DISPATCH(true, true);
     case 1: DISPATCH(true, false);
@@ -988,4 +991,22 @@ extern "C" int cmhar_gemm_bf16(int layout, int out_dtype, int M, int N, int K, c
                                long ldb, void* C, long ldc, const Epilogue* epi, int splits, void* ws,
                                hipStream_t stream) {
   return cmhar_gemm_bf16_phased(layout, out_dtype, M, N, K, A, lda, B, ldb, C, ldc, epi, splits, ws, stream, 3);
+}
+
+// fp16 operands (the fp16 inference path, BASELINE config 5): the same kernels with the fp16 MFMA, forward layout
+// only (Y = X·Wᵀ, A and B K-contiguous), output fp16 or fp32.  Same arguments and return codes as cmhar_gemm_bf16.
+extern "C" int cmhar_gemm_f16(int layout, int out_dtype, int M, int N, int K, const void* A, long lda, const void* B,
+                              long ldb, void* C, long ldc, const Epilogue* epi, int splits, void* ws,
+                              hipStream_t stream) {
+  if (M <= 0 || N <= 0) return 0;
+  if (layout != 0 || (out_dtype != CMHAR_F16 && out_dtype != CMHAR_F32)) return -1;
+  Epilogue plain{};
+  plain.alpha = 1.f;
+  const Epilogue& e = epi ? *epi : plain;
+  if (e.rowsum) return -3;
+  const bf16* a = (const bf16*)A;
+  const bf16* b = (const bf16*)B;
+  return out_dtype == CMHAR_F16
+             ? launch<f16, true, true, f16>(M, N, K, a, lda, b, ldb, (f16*)C, ldc, e, splits, (float*)ws, stream, 3)
+             : launch<f16, true, true, float>(M, N, K, a, lda, b, ldb, (float*)C, ldc, e, splits, (float*)ws, stream, 3);
 }

@@ -235,6 +235,8 @@ extern "C" int cmhar_tubelet_im2col(int out_dtype, int B, int T, int C, int H, i
   if (total == 0) return 0;
   if (out_dtype == CMHAR_BF16)
     tubelet_im2col_kernel<bf16><<<cdiv(total, 256), 256, 0, st>>>(B, T, C, H, W, tub, P, video, (bf16*)out);
+  else if (out_dtype == CMHAR_F16)
+    tubelet_im2col_kernel<f16><<<cdiv(total, 256), 256, 0, st>>>(B, T, C, H, W, tub, P, video, (f16*)out);
   else
     tubelet_im2col_kernel<float><<<cdiv(total, 256), 256, 0, st>>>(B, T, C, H, W, tub, P, video, (float*)out);
   CMHAR_CHECK_LAUNCH();
@@ -277,7 +279,11 @@ extern "C" int cmhar_copy2d(int in_dtype, int out_dtype, int rows, int cols, con
   if (in_dtype == CMHAR_F32 && out_dtype == CMHAR_F32) C2(float, float);
   else if (in_dtype == CMHAR_F32 && out_dtype == CMHAR_BF16) C2(float, bf16);
   else if (in_dtype == CMHAR_BF16 && out_dtype == CMHAR_F32) C2(bf16, float);
-  else C2(bf16, bf16);
+  else if (in_dtype == CMHAR_F16 && out_dtype == CMHAR_F32) C2(f16, float);
+  else if (in_dtype == CMHAR_F32 && out_dtype == CMHAR_F16) C2(float, f16);
+  else if (in_dtype == CMHAR_F16 && out_dtype == CMHAR_F16) C2(f16, f16);
+  else if (in_dtype == CMHAR_BF16 && out_dtype == CMHAR_BF16) C2(bf16, bf16);
+  else return -1;
 #undef C2
   CMHAR_CHECK_LAUNCH();
   return 0;

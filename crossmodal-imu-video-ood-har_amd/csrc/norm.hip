@@ -365,6 +365,8 @@ extern "C" int cmhar_layernorm_fwd(int dtype, int M, int N, const void* a, long 
     const int G = N / 256;
     if (dtype == CMHAR_BF16) {
       switch (G) { case 1: LF(bf16, 1); break; case 2: LF(bf16, 2); break; case 3: LF(bf16, 3); break; default: LF(bf16, 4); }
+    } else if (dtype == CMHAR_F16) {
+      switch (G) { case 1: LF(f16, 1); break; case 2: LF(f16, 2); break; case 3: LF(f16, 3); break; default: LF(f16, 4); }
     } else {
       switch (G) { case 1: LF(float, 1); break; case 2: LF(float, 2); break; case 3: LF(float, 3); break; default: LF(float, 4); }
     }
@@ -372,6 +374,9 @@ extern "C" int cmhar_layernorm_fwd(int dtype, int M, int N, const void* a, long 
   } else if (dtype == CMHAR_BF16)
     ln_fwd_kernel<bf16><<<grid, 256, 0, st>>>(M, N, (const bf16*)a, lda, (const bf16*)b, ldb, pdrop, seed,
                                               (bf16*)h_out, ldh, (bf16*)y, ldy, gamma, beta, mean, rstd, eps);
+  else if (dtype == CMHAR_F16)
+    ln_fwd_kernel<f16><<<grid, 256, 0, st>>>(M, N, (const f16*)a, lda, (const f16*)b, ldb, pdrop, seed,
+                                             (f16*)h_out, ldh, (f16*)y, ldy, gamma, beta, mean, rstd, eps);
   else
     ln_fwd_kernel<float><<<grid, 256, 0, st>>>(M, N, (const float*)a, lda, (const float*)b, ldb, pdrop, seed,
                                                (float*)h_out, ldh, (float*)y, ldy, gamma, beta, mean, rstd, eps);

@@ -10,7 +10,7 @@
  * Conventions: all pointers are device pointers (HBM) unless stated; `stream` is a hipStream_t (the caller's
  * current stream); functions never allocate or synchronise — workspaces are passed in; return 0 on success,
  * a negative value for an unsupported argument combination, or a positive hipError_t from the launch.
- * dtype codes: 0 = fp32, 1 = bf16.  Matrices are row-major with explicit leading dimensions (elements).
+ * dtype codes: 0 = fp32, 1 = bf16, 2 = fp16 (inference path only).  Matrices are row-major with explicit leading dimensions (elements).
  */
 #ifndef CMHAR_H
 #define CMHAR_H
@@ -70,6 +70,12 @@ int cmhar_gemm_bf16_plan(int layout, int M, int N, int K, int splits, int has_ws
 int cmhar_gemm_bf16_phased(int layout, int out_dtype, int M, int N, int K, const void* A, long lda, const void* B,
                            long ldb, void* C, long ldc, const CmharEpilogue* epi, int splits, void* ws,
                            hipStream_t stream, int phases);
+/* fp16 MFMA GEMM, forward layout 0 only (C = A[M,K]·B[N,K]ᵀ, fp16 operands, out_dtype 2 = fp16 or 0 = fp32): the
+ * fp16 inference path of BASELINE config 5 (replaces: the same VideoMAE nn.Linear / tubelet Conv3d forwards under
+ * the reference's Evaluator.predict, src/eval/evaluator.py:28-53, run in half precision).  Arguments, workspace and
+ * return codes as cmhar_gemm_bf16 (rowsum unsupported: -3; other layouts / dtypes: -1). */
+int cmhar_gemm_f16(int layout, int out_dtype, int M, int N, int K, const void* A, long lda, const void* B, long ldb,
+                   void* C, long ldc, const CmharEpilogue* epi, int splits, void* ws, hipStream_t stream);
 
 /* Exact-fp32 (or mixed) strided batched GEMM: C[z][m,n] = epi(Σ_k A[z][m*sam+k*sak] B[z][k*sbk+n*sbn])
  * (replaces: the fp32 nn.Linear / IMU encoder / ProjectionHead matmuls, models.py:16-132, 221-234). */
@@ -83,7 +89,8 @@ int cmhar_gemm_generic_splitk(int in_dtype, int out_dtype, int M, int N, int K, 
                               const CmharEpilogue* epi, float* ws, hipStream_t stream);
 
 /* Attention softmax(scale·QKᵀ)V per (batch, head); Q/K/V/O rows [B*L, ld] with head h at cols h*D.
- * bf16: D = 64 flash kernels (no dropout).  fp32: D in {8,16,32,64}, attention-prob dropout pdrop.
+ * bf16: D = 64 flash kernels (no dropout).  fp16 (forward only; backward returns -1): the D = 64 flash kernel on
+ * the fp16 MFMA, else the exact-f32-math kernel on fp16 storage.  fp32: D in {8,16,32,64}, attention-prob dropout pdrop.
  * lse: fp32 [B*H*Lq] (replaces: VideoMAESelfAttention modeling_videomae.py:209-258 and
  * nn.MultiheadAttention inside nn.TransformerEncoderLayer, models.py:85-95). */
 int cmhar_attention_fwd(int dtype, int B, int H, int Lq, int Lk, int D, const void* Q, long ldq, const void* K,

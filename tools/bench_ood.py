@@ -1,10 +1,13 @@
 """BASELINE config 5: OOD evaluation stream — energy score over the cross-modal ("fused") logits of a 10k-clip
-synthetic stream, inference only (no autograd), bf16 MFMA compute (the fp16 of the config: same MFMA rate and
-width on gfx950; the model's trained weights are bf16-packed).
+synthetic stream, inference only (no autograd), fp16 MFMA compute (`compute_dtype='fp16'`: fp16 weight packs and
+activations, fp32 accumulation; `--dtype bf16` for the training dtype).
 
-Per batch of 32 clips: CrossModalModel.forward(imu, video) in eval mode → imu_proj, video_proj (unit rows) →
-logits S = exp(t)·imu_proj·video_projᵀ + bias (the SigLIP logits of src/models/losses.py:37-41, one row per IMU
-clip over the batch's video clips) → per-row prediction + energy E = −logsumexp(S) (cmhar_logits_energy).
+The stream cycles through a ring of `--ring` (default 8) DISTINCT resident batches of synthetic clips (randn video
+and IMU, 32 clips each), so consecutive batches never re-score the same inputs.  Per batch:
+CrossModalModel.forward(imu, video) in eval mode → imu_proj, video_proj (unit rows) → logits
+S = exp(t)·imu_proj·video_projᵀ + bias (the SigLIP logits of src/models/losses.py:37-41, one row per IMU clip over the
+batch's video clips) → per-row prediction + energy E = −logsumexp(S) (cmhar_logits_energy); or, with
+`--model fusion`, the cross-attention fusion classifier's class logits.
 Prints one JSON line: clips/s and the energy-score kernel's share.   python tools/bench_ood.py [--clips 10000]
 """
 import argparse
@@ -32,11 +35,13 @@ def main():
     ap.add_argument('--model', choices=['siglip', 'fusion'], default='siglip',
                     help='siglip: energy over the SigLIP logits of CrossModalModel; fusion: energy over the class '
                          'logits of the cross-attention fusion classifier')
+    ap.add_argument('--dtype', choices=['fp16', 'bf16'], default='fp16')
+    ap.add_argument('--ring', type=int, default=8, help='distinct resident input batches cycled by the stream')
     args = ap.parse_args()
     dev = torch.device('cuda')
     cfg = Config()
     cfg.model.allow_random_init = True   # synthetic benchmark: random-init weights
-    cfg.model.compute_dtype = 'bf16'
+    cfg.model.compute_dtype = args.dtype
     torch.manual_seed(0)
     with warnings.catch_warnings():
         warnings.simplefilter('ignore')
@@ -47,8 +52,8 @@ def main():
             model = CrossModalModel(cfg).to(dev).eval()
     B = args.batch
     g = torch.Generator(device=dev).manual_seed(5)
-    video = torch.randn(B, 16, 3, 224, 224, device=dev, generator=g)
-    imu = torch.randn(B, 6, 200, device=dev, generator=g)
+    ring = [(torch.randn(B, 6, 200, device=dev, generator=g), torch.randn(B, 16, 3, 224, 224, device=dev, generator=g))
+            for _ in range(args.ring)]
     scale = math.exp(math.log(10.0))
     bias = torch.full((B,), -10.0, device=dev)
     S = torch.empty(B, B, device=dev)
@@ -56,7 +61,8 @@ def main():
 
     last = {}
 
-    def batch():
+    def batch(i):
+        imu, video = ring[i % len(ring)]
         if args.model == 'fusion':
             last['logits'] = model(imu, video)
         else:
@@ -66,12 +72,12 @@ def main():
         return logits_energy(last['logits'])
 
     with torch.no_grad():
-        for _ in range(3):
-            batch()
+        for i in range(3):
+            batch(i)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        for _ in range(nb):
-            pred, energy, _ = batch()
+        for i in range(nb):
+            pred, energy, _ = batch(i)
         torch.cuda.synchronize()
         dt = time.perf_counter() - t0
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -83,7 +89,7 @@ def main():
     what = 'fusion-classifier logits' if args.model == 'fusion' else 'SigLIP logits'
     print(json.dumps({'metric': f'clips/sec OOD energy-score eval stream over {what} (16x224^2 video + 6x200 IMU)',
                       'value': round(nb * B / dt, 1), 'unit': 'clips/sec', 'clips': nb * B, 'batch': B,
-                      'dtype': 'bf16', 'ms_per_batch': round(1e3 * dt / nb, 3),
+                      'dtype': args.dtype, 'distinct_batches': args.ring, 'ms_per_batch': round(1e3 * dt / nb, 3),
                       'energy_kernel_us': round(e0.elapsed_time(e1) * 10, 2),
                       'energy_mean': float(energy.mean()), 'pred_sample': pred[:8].tolist()}))
 
