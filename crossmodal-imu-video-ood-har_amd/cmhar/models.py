@@ -21,6 +21,8 @@ import torch.nn as nn
 from . import kernels as K
 from .heads import ProjectionHead, l2_normalize, run_head, _Seeds
 from .imu import IMUEncoder, PatchEmbedding
+from .cnn2d import MobileNetV2Features, ResNet18Features, run_cnn2d
+from .fusion import _TokenMeanFn
 from .r3d import R3D18, run_r3d
 from .videomae import VideoMAEBackbone, default_videomae_config, run_backbone
 
@@ -64,9 +66,10 @@ def _videomae_geometry(config):
 
 
 class VideoEncoder(nn.Module):
-    """models.py:137-216 (VideoMAE branch).  A local HF-format directory is loaded (config.json +
-    safetensors / .bin via weights-only loaders); a hub name cannot be fetched offline, so the VideoMAE
-    architecture is built from `config.model.videomae_*` / the data geometry with HF's random init."""
+    """models.py:137-216.  VideoMAE branch: a local HF-format directory is loaded (config.json + safetensors / .bin
+    via weights-only loaders); a hub name cannot be fetched offline, so the VideoMAE architecture is built from
+    `config.model.videomae_*` / the data geometry with HF's random init.  'resnet18' / 'mobilenet_v2': the per-frame
+    torchvision CNNs (cmhar.cnn2d, torchvision state_dict names).  'r3d_18': the north_star R3D-18 extension."""
 
     def __init__(self, config):
         super().__init__()
@@ -99,16 +102,33 @@ class VideoEncoder(nn.Module):
             self.backbone = R3D18(None, compute_dtype=dt)
             self.feature_dim = self.backbone.feature_dim
         elif vb in ('resnet18', 'mobilenet_v2'):
-            raise NotImplementedError(f'{vb}: per-frame 2-D CNN backbones are not on the accelerated path '
-                                      f'(torchvision is absent; see DESIGN.md scope)')
+            # models.py:163-173: torchvision resnet18 children()[:-2] / mobilenet_v2 .features, run per frame
+            if model_cfg.video_pretrained:
+                allow = bool(getattr(model_cfg, 'allow_random_init', False)) or \
+                    os.environ.get('CMHAR_ALLOW_RANDOM_INIT', '') == '1'
+                if not allow:   # models.resnet18(pretrained=True) downloads ImageNet weights: not possible offline
+                    raise OSError(f'{vb}: ImageNet weights cannot be fetched offline; set video_pretrained=False '
+                                  f'(then load a torchvision state_dict into video_encoder.backbone), or opt in to '
+                                  f'random weights with model.allow_random_init=True / CMHAR_ALLOW_RANDOM_INIT=1')
+                warnings.warn(f'{vb}: pretrained ImageNet weights are not available offline; random init '
+                              f'(allow_random_init)')
+            self.backbone = (ResNet18Features if vb == 'resnet18' else MobileNetV2Features)(compute_dtype=dt)
+            self.feature_dim = self.backbone.feature_dim
         else:
             raise ValueError(f'Backbone inconnu: {vb}')
         self.projection = nn.Linear(self.feature_dim, model_cfg.video_d_model)
+        if vb in ('resnet18', 'mobilenet_v2'):
+            self.temporal_pool = nn.AdaptiveAvgPool1d(1)            # models.py:182-183 (no parameters)
 
     def forward(self, x):
         """x (B, T, C, H, W) → (B, video_d_model)."""
         if x.dim() != 5:
             raise ValueError(f'expected (B, T, C, H, W) video, got {tuple(x.shape)}')
+        if isinstance(self.backbone, (ResNet18Features, MobileNetV2Features)):
+            # models.py:208-216: per-frame CNN + 2-D average pool → per-frame projection → mean over the T frames
+            B, T = x.shape[:2]
+            feats = linear_fp32(run_cnn2d(self.backbone, x, self.training), self.projection)   # (B·T, d)
+            return _TokenMeanFn.apply(feats, B, T)
         if not self.is_videomae:                                  # r3d_18: pooled 3-D CNN features
             return linear_fp32(run_r3d(self.backbone, x, self.training), self.projection)
         feat = run_backbone(self.backbone, x, token0_only=True)   # last_hidden_state[:, 0]  (models.py:201)

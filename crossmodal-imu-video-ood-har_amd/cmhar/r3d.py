@@ -112,14 +112,29 @@ def _out_shape(shape, conv):
     return (N, o[0], o[1], o[2], conv.out_channels)
 
 
-def _pack(conv, dt):
-    """[Cout, Cin, kt, kh, kw] fp32 master → [Cout, Kp] compute dtype in the im2col k order (kt, kh, kw, Cin)."""
+def _pack(conv, dt, flip=False):
+    """[Cout, Cin, kt, kh, kw] fp32 master → [Cout, Kp] compute dtype in the im2col k order (kt, kh, kw, Cin), zero
+    padded to Kp; with flip also the tap-flipped, in/out-transposed [Cin, taps·Cout] weight of the stride-1 input
+    gradient — both from one cmhar_conv_pack_weight pass (no torch permute / copy kernels on the step).
+    Returns wp, or (wp, wf) when flip."""
     w = conv.weight.detach()
-    co = w.shape[0]
-    k = w[0].numel()
-    wp = torch.zeros(co, _r8(k), dtype=dt, device=w.device)
-    wp[:, :k] = w.permute(0, 2, 3, 4, 1).reshape(co, k)
-    return wp
+    if not w.is_contiguous():
+        w = w.contiguous()
+    co, ci, kt, kh, kw = w.shape
+    kp = _r8(w[0].numel())
+    wp = torch.empty(co, kp, dtype=dt, device=w.device)
+    wf = torch.empty(ci, kt * kh * kw * co, dtype=dt, device=w.device) if flip else None
+    call('cmhar_conv_pack_weight', L.dtype_code(dt), co, ci, kt, kh, kw, kp, ptr(w), ptr(wp), ptr(wf),
+         L.stream(w.device))
+    return (wp, wf) if flip else wp
+
+
+def _pack_flip(conv, dt):
+    w = conv.weight.detach().contiguous()
+    co, ci, kt, kh, kw = w.shape
+    wf = torch.empty(ci, kt * kh * kw * co, dtype=dt, device=w.device)
+    call('cmhar_conv_pack_weight', L.dtype_code(dt), co, ci, kt, kh, kw, 0, ptr(w), None, ptr(wf), L.stream(w.device))
+    return wf
 
 
 def _im2col(x, shape, conv, Kp, rows):
@@ -164,7 +179,13 @@ def _bn_fwd_tiles(z, bn, res, relu, tstats):
 class _Unit:
     """Forward state of one conv+BN unit (input, pre-BN output, BN output, batch statistics)."""
     __slots__ = ('conv', 'bn', 'relu', 'shape', 'oshape', 'x', 'z', 'y', 'sm', 'sr', 'Kp', 'rows', 'wp', 'col',
-                 'igemm')
+                 'igemm', 'wf')
+
+
+def _pointwise(conv, shape, Kp, M, rows):
+    """1×1×1, stride 1, no padding, Kp == C, no row padding: the im2col matrix IS the input viewed [M, C]."""
+    return tuple(conv.kernel_size) == (1, 1, 1) and tuple(conv.stride) == (1, 1, 1) and \
+        tuple(conv.padding) == (0, 0, 0) and Kp == shape[4] and rows == M
 
 
 def _igemm_ok(x, shape, conv, Kp):
@@ -172,7 +193,7 @@ def _igemm_ok(x, shape, conv, Kp):
     return x.dtype == torch.bfloat16 and shape[4] % 64 == 0 and Kp == conv.weight[0].numel()
 
 
-def _unit_fwd(x, shape, conv, bn, relu, training, save, res=None, wp=None, keep_col=True):
+def _unit_fwd(x, shape, conv, bn, relu, training, save, res=None, wp=None, keep_col=True, wf=None):
     oshape = _out_shape(shape, conv)
     M = math.prod(oshape[:4])
     Kp = _r8(conv.weight[0].numel())
@@ -187,6 +208,9 @@ def _unit_fwd(x, shape, conv, bn, relu, training, save, res=None, wp=None, keep_
             tstats = K.workspace(2 * (ntile + (ntile + 63) // 64) * conv.out_channels, x.device)
         call('cmhar_conv3d_fwd', _dims(shape, conv, Kp), conv.out_channels, ptr(x), ptr(wp), None, ptr(z),
              ptr(tstats), L.stream(x.device))
+    elif _pointwise(conv, shape, Kp, M, rows):
+        col = x.reshape(M, Kp)
+        K.gemm(0, col, wp, z)
     else:
         col = _im2col(x, shape, conv, Kp, rows)
         K.gemm(0, col[:M], wp, z)
@@ -201,6 +225,7 @@ def _unit_fwd(x, shape, conv, bn, relu, training, save, res=None, wp=None, keep_
         u.x, u.z, u.y, u.sm, u.sr = x, z, y, sm, sr
         u.col = col if keep_col else None
         u.igemm = igemm
+        u.wf = wf
     return y, oshape, u
 
 
@@ -209,14 +234,13 @@ def _dgrad_igemm_ok(conv):
         all(2 * p == k - 1 for p, k in zip(conv.padding, conv.kernel_size))
 
 
-def _dgrad_igemm(dz, conv, oshape, x, dx_acc=None):
+def _dgrad_igemm(dz, conv, oshape, x, dx_acc=None, wf=None):
     """Input gradient of a stride-1 'same' conv as the conv of dz (NDHWC [M, Cout] bf16) with the tap-flipped,
     in/out-transposed weight (padding k-1-p = p): an implicit GEMM, no dcol / col2im; dx_acc (the residual-branch
     gradient) is added in its epilogue.  Returns dx shaped like x."""
-    w = conv.weight.detach()
-    cin, cout = w.shape[1], w.shape[0]
-    wf = torch.empty(cin, w[0, 0].numel() * cout, dtype=dz.dtype, device=dz.device)
-    wf.view(cin, w.shape[2], w.shape[3], w.shape[4], cout).copy_(w.flip(2, 3, 4).permute(1, 2, 3, 4, 0))
+    cin, cout = conv.weight.shape[1], conv.weight.shape[0]
+    if wf is None:
+        wf = _pack_flip(conv, dz.dtype)
     N, To, Ho, Wo, _ = oshape
     kt, kh, kw = conv.kernel_size
     pt, ph, pw = conv.padding
@@ -261,10 +285,25 @@ def _unit_bwd(u, dy, grads, training, need_dx, want_dres, dx_acc=None):
         del col
     w = u.conv.weight
     k = w[0].numel()
-    grads[w] = dwp[:, :k].reshape(Cc, w.shape[2], w.shape[3], w.shape[4], w.shape[1]).permute(0, 4, 1, 2, 3)
+    g5 = dwp[:, :k].reshape(Cc, w.shape[2], w.shape[3], w.shape[4], w.shape[1]).permute(0, 4, 1, 2, 3)
+    p = getattr(u.conv, 'param', None)          # a 2-D conv run as (1, kh, kw): gradient in the parameter's shape
+    if p is None:
+        grads[w] = g5
+    else:
+        grads[p] = g5.reshape(p.shape)
     dx = None
     if need_dx and u.igemm and _dgrad_igemm_ok(u.conv):
-        dx = _dgrad_igemm(dz, u.conv, u.oshape, u.x, dx_acc)
+        dx = _dgrad_igemm(dz, u.conv, u.oshape, u.x, dx_acc, u.wf)
+    elif need_dx and _pointwise(u.conv, u.shape, u.Kp, M, u.rows):
+        # 1×1 stride-1: dx = dz·W directly (the col2im of a pointwise conv is the identity); the residual-branch
+        # gradient is added in the GEMM epilogue (element-wise read-then-write of the same buffer)
+        if dx_acc is not None:
+            dxv = dx_acc.reshape(M, u.Kp)
+            K.gemm(1, dz[:M], u.wp, dxv, residual=dxv)
+            dx = dx_acc
+        else:
+            dx = torch.empty_like(u.x)
+            K.gemm(1, dz[:M], u.wp, dx.reshape(M, u.Kp))
     elif need_dx:
         dcol = torch.empty(M, u.Kp, dtype=dt, device=dy.device)
         K.gemm(1, dz[:M], u.wp, dcol)
@@ -289,8 +328,13 @@ def _forward_impl(m: R3D18, video, training, save):
 
     def unit(xin, shp, seq, relu, res=None):
         conv, bn = seq[0], seq[1]
-        wp = packs[conv] = _pack(conv, dt)
-        y, osh, u = _unit_fwd(xin, shp, conv, bn, relu, training, save, res=res, wp=wp, keep_col=m.keep_cols)
+        wf = None
+        if save and dt == torch.bfloat16 and _dgrad_igemm_ok(conv) and shp[4] % 64 == 0:
+            wp, wf = _pack(conv, dt, flip=True)      # the backward's flipped weight from the same pass
+        else:
+            wp = _pack(conv, dt)
+        packs[conv] = wp
+        y, osh, u = _unit_fwd(xin, shp, conv, bn, relu, training, save, res=res, wp=wp, keep_col=m.keep_cols, wf=wf)
         units.append(u)
         return y, osh
 

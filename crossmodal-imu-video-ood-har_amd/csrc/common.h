@@ -147,6 +147,36 @@ __device__ __forceinline__ void epilogue_store(const Epilogue& e, OutT* __restri
   *p = from_f<OutT>(v);
 }
 
+// 8-element vector access (16 B for bf16, 32 B for fp32); every call site is 8-element aligned (C % 8 == 0).
+template <typename T> struct Vec8;
+template <> struct Vec8<bf16> {
+  static __device__ __forceinline__ void load(const bf16* p, float* v) {
+    const bf16x8 r = *(const bf16x8*)p;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = (float)r[j];
+  }
+  static __device__ __forceinline__ void store(bf16* p, const float* v) {
+    bf16x8 r;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) r[j] = (bf16)v[j];
+    *(bf16x8*)p = r;
+  }
+};
+template <> struct Vec8<float> {
+  static __device__ __forceinline__ void load(const float* p, float* v) {
+    const floatx4 a = *(const floatx4*)p, b = *(const floatx4*)(p + 4);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { v[j] = a[j]; v[4 + j] = b[j]; }
+  }
+  static __device__ __forceinline__ void store(float* p, const float* v) {
+    floatx4 a, b;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { a[j] = v[j]; b[j] = v[4 + j]; }
+    *(floatx4*)p = a;
+    *(floatx4*)(p + 4) = b;
+  }
+};
+
 // XCD-aware bijective block remap: workgroups are dispatched round-robin over the 8 XCDs by linear block id, so
 // id → (id % 8)'s contiguous chunk of the logical index space; logically adjacent blocks (sharing operand panels,
 // or the K/V of one attention head) then run on one XCD and share its L2.

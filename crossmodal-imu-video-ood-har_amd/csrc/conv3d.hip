@@ -12,35 +12,6 @@
 
 namespace {
 
-// 8-element vector access (16 B for bf16, 32 B for fp32); every call site is 8-element aligned (C % 8 == 0).
-template <typename T> struct Vec8;
-template <> struct Vec8<bf16> {
-  static __device__ __forceinline__ void load(const bf16* p, float* v) {
-    const bf16x8 r = *(const bf16x8*)p;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = (float)r[j];
-  }
-  static __device__ __forceinline__ void store(bf16* p, const float* v) {
-    bf16x8 r;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) r[j] = (bf16)v[j];
-    *(bf16x8*)p = r;
-  }
-};
-template <> struct Vec8<float> {
-  static __device__ __forceinline__ void load(const float* p, float* v) {
-    const floatx4 a = *(const floatx4*)p, b = *(const floatx4*)(p + 4);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) { v[j] = a[j]; v[4 + j] = b[j]; }
-  }
-  static __device__ __forceinline__ void store(float* p, const float* v) {
-    floatx4 a, b;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) { a[j] = v[j]; b[j] = v[4 + j]; }
-    *(floatx4*)p = a;
-    *(floatx4*)(p + 4) = b;
-  }
-};
 template <typename T, int V> __device__ __forceinline__ void vload(const T* p, float* v) {
   if constexpr (V == 8) Vec8<T>::load(p, v);
   else for (int j = 0; j < V; ++j) v[j] = to_f<T>(p[j]);
@@ -183,7 +154,8 @@ __global__ __launch_bounds__(256) void col2im3d_kernel(Geom g, const T* __restri
 // ---- BatchNorm over the [M, C] channels-last view ----------------------------------------------------------------
 // Column partial sums over a chunk of rows: each thread reads 8 consecutive channels of a row (one 16-B bf16
 // vector), TPR = C/8 threads cover a row and the block's RPI = 256/TPR row slots are combined in a fixed order.
-// mode 0: Σx; mode 1: Σ(x−mean)²; mode 2: Σg, Σg·x̂ with g = dy·[y > 0 if relu].  part: [2][nchunk][C].
+// mode 0: Σx; mode 1: Σ(x−mean)²; mode 2: Σg, Σg·x̂ with g = dy·act'(y) (relu 1: [y > 0]; relu 2 = ReLU6:
+// [0 < y < 6]).  part: [2][nchunk][C].  C/8 need not divide 256: the 256 % TPR spare threads only add zeros.
 template <typename T>
 __global__ __launch_bounds__(256) void bn_cl_partial(int mode, int M, int C, int rows_per_chunk,
                                                      const T* __restrict__ x, const T* __restrict__ y,
@@ -196,6 +168,7 @@ __global__ __launch_bounds__(256) void bn_cl_partial(int mode, int M, int C, int
   const int slot = tid / TPR, c0 = (tid % TPR) * 8;
   const int r0 = blockIdx.x * rows_per_chunk;
   const int r1 = min(r0 + rows_per_chunk, M);
+  const int rs0 = slot < RPI ? r0 + slot : r1;
   float mu[8], rs[8], a0[8], a1[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
@@ -203,7 +176,7 @@ __global__ __launch_bounds__(256) void bn_cl_partial(int mode, int M, int C, int
     rs[j] = mode == 2 ? rstd[c0 + j] : 0.f;
     a0[j] = a1[j] = 0.f;
   }
-  for (int r = r0 + slot; r < r1; r += RPI) {
+  for (int r = rs0; r < r1; r += RPI) {
     const long off = (long)r * C + c0;
     float v[8], gv[8], yv[8];
     Vec8<T>::load(x + off, v);
@@ -219,7 +192,7 @@ __global__ __launch_bounds__(256) void bn_cl_partial(int mode, int M, int C, int
         const float d = v[j] - mu[j];
         a0[j] = fmaf(d, d, a0[j]);
       } else {
-        const float gj = relu && yv[j] <= 0.f ? 0.f : gv[j];
+        const float gj = (relu && yv[j] <= 0.f) || (relu == 2 && yv[j] >= 6.f) ? 0.f : gv[j];
         a0[j] += gj;
         a1[j] = fmaf(gj, (v[j] - mu[j]) * rs[j], a1[j]);
       }
@@ -347,7 +320,7 @@ __global__ void bn_cl_eval_stats(int C, const float* __restrict__ rmean, const f
   if (c < C) { mean[c] = rmean[c]; rstd[c] = rsqrtf(rvar[c] + eps); }
 }
 
-// y = relu?((x − mean)·rstd·w + b + res), 8 channels per thread
+// y = act((x − mean)·rstd·w + b + res), act = identity / ReLU (relu 1) / ReLU6 (relu 2), 8 channels per thread
 template <typename T>
 __global__ __launch_bounds__(256) void bn_cl_apply(unsigned nvec, int C, const T* __restrict__ x,
                                                    const T* __restrict__ res, const float* __restrict__ mean,
@@ -357,15 +330,21 @@ __global__ __launch_bounds__(256) void bn_cl_apply(unsigned nvec, int C, const T
   for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < nvec; i += gridDim.x * blockDim.x) {
     const int c0 = (int)(i % cv) * 8;
     const long off = (long)i * 8;
-    float v[8], rv[8];
+    float v[8], rv[8], mu[8], rs[8], ww[8], bb[8];
     Vec8<T>::load(x + off, v);
     if (res) Vec8<T>::load(res + off, rv);
+    // per-channel constants as explicit 16-B loads (c0 % 8 == 0; the per-element form lost its vectorisation
+    // once the activation became a two-way choice: 34 vs 10 loads per 8 channels, 4x slower)
+    Vec8<float>::load(mean + c0, mu);
+    Vec8<float>::load(rstd + c0, rs);
+    Vec8<float>::load(w + c0, ww);
+    Vec8<float>::load(b + c0, bb);
+    const float lo = relu ? 0.f : -INFINITY, hi = relu == 2 ? 6.f : INFINITY;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      const int c = c0 + j;
-      v[j] = fmaf((v[j] - mean[c]) * rstd[c], w[c], b[c]);
+      v[j] = fmaf((v[j] - mu[j]) * rs[j], ww[j], bb[j]);
       if (res) v[j] += rv[j];
-      if (relu) v[j] = fmaxf(v[j], 0.f);
+      v[j] = fminf(fmaxf(v[j], lo), hi);
     }
     Vec8<T>::store(y + off, v);
   }
@@ -384,20 +363,27 @@ __global__ __launch_bounds__(256) void bn_cl_bwd_apply(unsigned nvec, int M, int
   for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < nvec; i += gridDim.x * blockDim.x) {
     const int c0 = (int)(i % cv) * 8;
     const long off = (long)i * 8;
-    float gv[8], yv[8], xv[8], out[8];
+    float gv[8], yv[8], xv[8], out[8], rs[8], ww[8], mu[8], sw[8], sb[8];
     Vec8<T>::load(dy + off, gv);
     if (relu) Vec8<T>::load(y + off, yv);
     if (training) Vec8<T>::load(x + off, xv);
+    // per-channel constants as explicit 16-B loads (c0 % 8 == 0): per element they compiled to 40 scalar loads
+    Vec8<float>::load(rstd + c0, rs);
+    Vec8<float>::load(w + c0, ww);
+    if (training) {
+      Vec8<float>::load(mean + c0, mu);
+      Vec8<float>::load(dw + c0, sw);
+      Vec8<float>::load(db + c0, sb);
+    }
+    const float lo = relu ? 0.f : -INFINITY, hi = relu == 2 ? 6.f : INFINITY;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      const int c = c0 + j;
-      if (relu && yv[j] <= 0.f) gv[j] = 0.f;
-      const float rs = rstd[c];
+      if (relu && !(yv[j] > lo && yv[j] < hi)) gv[j] = 0.f;
       if (training) {
-        const float xh = (xv[j] - mean[c]) * rs;
-        out[j] = w[c] * rs * (gv[j] - db[c] * inv - xh * dw[c] * inv);
+        const float xh = (xv[j] - mu[j]) * rs[j];
+        out[j] = ww[j] * rs[j] * (gv[j] - sb[j] * inv - xh * sw[j] * inv);
       } else {
-        out[j] = w[c] * rs * gv[j];
+        out[j] = ww[j] * rs[j] * gv[j];
       }
     }
     if (dres) Vec8<T>::store(dres + off, gv);
@@ -414,10 +400,11 @@ __global__ __launch_bounds__(256) void avgpool_cl_fwd(int N, long S, int C, cons
   const int CB = C < 256 ? C : 256, RPI = 256 / CB, slot = tid / CB, cc = tid % CB;
   for (int c0 = blockIdx.x * CB; c0 < C; c0 += gridDim.x * CB) {
     float a = 0.f;
-    for (long s = slot; s < S; s += RPI) a += to_f<T>(x[((long)n * S + s) * C + c0 + cc]);
+    if (slot < RPI && c0 + cc < C)      // (C not a multiple of CB / CB not dividing 256: spare threads add 0)
+      for (long s = slot; s < S; s += RPI) a += to_f<T>(x[((long)n * S + s) * C + c0 + cc]);
     sh[tid] = a;
     __syncthreads();
-    if (slot == 0) {
+    if (slot == 0 && c0 + cc < C) {
       float b = 0.f;
       for (int k = 0; k < RPI; ++k) b += sh[k * CB + cc];
       out[(long)n * C + c0 + cc] = b / (float)S;
@@ -730,7 +717,7 @@ inline int grid_for(long work) {
   return (int)(b < 8192 ? (b > 0 ? b : 1) : 8192);
 }
 
-inline bool bn_channels_ok(int C) { return C >= 8 && C % 8 == 0 && C <= 2048 && 256 % (C / 8) == 0; }
+inline bool bn_channels_ok(int C) { return C >= 8 && C % 8 == 0 && C <= 2048; }
 
 inline int bn_chunks(long M) {   // ≤ 512 chunks of ≥ 512 rows: enough blocks to stream M·C, few partials to combine
   const long c = (M + 511) / 512;
@@ -816,7 +803,7 @@ extern "C" int cmhar_bn_cl_fwd(int dtype, long M, int C, const void* x, const vo
                                float momentum, float eps, int relu, long long* num_batches_tracked, float* ws,
                                hipStream_t stream) {
   if (M <= 0 || !bn_channels_ok(C) || !ws) return -1;
-  if (M >= (1L << 31) || M * C / 8 >= (1L << 32)) return -2;
+  if (M >= (1L << 31) || M * C / 8 >= (1L << 31)) return -2;   // unsigned grid-stride loops never wrap
   const int nch = bn_chunks(M);
   const int rpc = (int)((M + nch - 1) / nch);
   const int fgrid = (C + 63) / 64;
@@ -852,7 +839,7 @@ extern "C" int cmhar_bn_cl_fwd_tiles(long M, int C, float* tile_stats, const voi
                                      float* srstd, float momentum, float eps, int relu, long long* num_batches_tracked,
                                      hipStream_t stream) {
   if (M <= 0 || !bn_channels_ok(C) || !tile_stats) return -1;
-  if (M >= (1L << 31) || M * C / 8 >= (1L << 32)) return -2;
+  if (M >= (1L << 31) || M * C / 8 >= (1L << 31)) return -2;   // unsigned grid-stride loops never wrap
   const int ntile = (int)((M + 127) / 128), ngroup = (ntile + 63) / 64;
   float* groups = (float*)tile_stats + 2L * ntile * C;
   bn_tile_group<<<cdiv((long)ngroup * C, 256), 256, 0, stream>>>(M, C, ntile, tile_stats, groups);
@@ -869,7 +856,7 @@ extern "C" int cmhar_bn_cl_bwd(int dtype, long M, int C, const void* x, const vo
                                const float* w, const float* smean, const float* srstd, void* dx, void* dres,
                                float* dw, float* db, int training, int relu, float* ws, hipStream_t stream) {
   if (M <= 0 || !bn_channels_ok(C) || !ws || !dw || !db) return -1;
-  if (M >= (1L << 31) || M * C / 8 >= (1L << 32)) return -2;
+  if (M >= (1L << 31) || M * C / 8 >= (1L << 31)) return -2;   // unsigned grid-stride loops never wrap
   const int nch = bn_chunks(M);
   const int rpc = (int)((M + nch - 1) / nch);
   if (dtype == CMHAR_BF16)
@@ -897,7 +884,7 @@ extern "C" int cmhar_bn_cl_bwd(int dtype, long M, int C, const void* x, const vo
 extern "C" int cmhar_avgpool_cl(int dtype, int N, long S, int C, const void* x, float* out, hipStream_t stream) {
   if (N <= 0 || S <= 0 || !bn_channels_ok(C)) return -1;
   const int CB = C < 256 ? C : 256;
-  dim3 grid(C / CB, N);
+  dim3 grid(cdiv(C, CB), N);
   if (dtype == CMHAR_BF16) avgpool_cl_fwd<bf16><<<grid, 256, 0, stream>>>(N, S, C, (const bf16*)x, out);
   else if (dtype == CMHAR_F32) avgpool_cl_fwd<float><<<grid, 256, 0, stream>>>(N, S, C, (const float*)x, out);
   else return -1;

@@ -238,20 +238,46 @@ int cmhar_conv3d_wgrad(const int* dims, int Cout, const void* x, const void* dz,
                        hipStream_t stream);
 /* dx (NDHWC, dtype) = Σ over taps of dcol (+ dx when accumulate): the input gradient of the convolution. */
 int cmhar_conv3d_col2im(int dtype, const int* dims, const void* dcol, void* dx, int accumulate, hipStream_t stream);
-/* BatchNorm3d over the [M, C] channels-last view (C = 8·2^j ≤ 2048, M < 2^31), fused residual add + ReLU:
- * y = relu?(bn(x) + res).  ws: cmhar_bn_cl_ws(M, C) floats.  Training updates rmean/rvar/num_batches_tracked. */
+/* BatchNorm3d / BatchNorm2d over the [M, C] channels-last view (C % 8 == 0, C ≤ 2048, M < 2^31), fused residual add
+ * + activation: y = act(bn(x) + res), relu 0 = none, 1 = ReLU, 2 = ReLU6 (MobileNetV2).  ws: cmhar_bn_cl_ws(M, C) floats.  Training updates rmean/rvar/num_batches_tracked. */
 long cmhar_bn_cl_ws(long M, int C);
 int cmhar_bn_cl_fwd(int dtype, long M, int C, const void* x, const void* res, void* y, const float* w,
                     const float* b, float* rmean, float* rvar, float* smean, float* srstd, int training,
                     float momentum, float eps, int relu, long long* num_batches_tracked, float* ws,
                     hipStream_t stream);
-/* g = dy·[y > 0 if relu]; dres = g (optional); dx = BN input gradient; dw = Σg·x̂, db = Σg (fp32, overwritten). */
+/* g = dy·act'(y) ([y > 0] for relu 1, [0 < y < 6] for relu 2); dres = g (optional); dx = BN input gradient; dw = Σg·x̂, db = Σg (fp32, overwritten). */
 int cmhar_bn_cl_bwd(int dtype, long M, int C, const void* x, const void* y, const void* dy, const float* w,
                     const float* smean, const float* srstd, void* dx, void* dres, float* dw, float* db, int training,
                     int relu, float* ws, hipStream_t stream);
 /* AdaptiveAvgPool3d(1): [N, S, C] → fp32 [N, C], and its backward (dx = dout / S broadcast). */
 int cmhar_avgpool_cl(int dtype, int N, long S, int C, const void* x, float* out, hipStream_t stream);
 int cmhar_avgpool_cl_bwd(int dtype, int N, long S, int C, const float* dout, void* dx, hipStream_t stream);
+/* Weight packs for the conv kernels, from the fp32 master w [Cout, Cin, kt, kh, kw] in one pass (either output
+ * nullable): out [Cout, Kp] (out_dtype) in the im2col k order ((it·kh + ih)·kw + iw)·Cin + ci, zero for k ≥ K;
+ * out_flip [Cin, taps·Cout]: the tap-flipped, in/out-transposed weight (k = tap·Cout + co) the stride-1 input
+ * gradient convolves dz with.  taps = kt·kh·kw ≤ 384. */
+int cmhar_conv_pack_weight(int out_dtype, int Cout, int Cin, int kt, int kh, int kw, int Kp, const float* w,
+                           void* out, void* out_flip, hipStream_t stream);
+
+/* ---- per-frame 2-D CNN video backbones (replaces: torchvision resnet18 children[:-2] / mobilenet_v2 .features under
+ * VideoEncoder, models.py:163-173,208-216).  Dense Conv2d = the conv3d entry points above with kt = 1; BatchNorm2d =
+ * cmhar_bn_cl_* (relu 2 = ReLU6).  Activations NHWC [N, H, W, C], C % 8 == 0, window k·k ≤ 9, 2p ≤ k.
+ * MaxPool2d(k, s, p): argmax = uint8 [N, Ho, Wo, C] tap index of the first maximum (torch's tie rule); the backward
+ * gathers dy into dx (overwritten). */
+int cmhar_maxpool2d_cl_fwd(int dtype, int N, int H, int W, int C, int k, int s, int p, const void* x, void* y,
+                           unsigned char* argmax, hipStream_t stream);
+int cmhar_maxpool2d_cl_bwd(int dtype, int N, int H, int W, int C, int k, int s, int p, const void* dy,
+                           const unsigned char* argmax, void* dx, hipStream_t stream);
+/* Depthwise Conv2d(C, C, k, s, p, groups = C, bias = False); w = the fp32 parameter [C, 1, k, k].  dgrad overwrites
+ * dx; wgrad overwrites dw (fp32 [C, k, k]) through ws (cmhar_dwconv2d_cl_wgrad_ws floats), fixed-order sums. */
+int cmhar_dwconv2d_cl_fwd(int dtype, int N, int H, int W, int C, int k, int s, int p, const void* x, const float* w,
+                          void* z, hipStream_t stream);
+int cmhar_dwconv2d_cl_dgrad(int dtype, int N, int H, int W, int C, int k, int s, int p, const void* dz,
+                            const float* w, void* dx, hipStream_t stream);
+long cmhar_dwconv2d_cl_wgrad_ws(int N, int H, int W, int C, int k, int s, int p);
+int cmhar_dwconv2d_cl_wgrad(int dtype, int N, int H, int W, int C, int k, int s, int p, const void* x, const void* dz,
+                            float* dw, float* ws, hipStream_t stream);
+
 /* (B, T, C, H, W) fp32 clip batch → (B, T, H, W, C) in the compute dtype (the backbone's input layout). */
 int cmhar_video_to_ndhwc(int out_dtype, int B, int T, int C, int H, int W, const float* video, void* out,
                          hipStream_t stream);

@@ -5,11 +5,36 @@ Only `tests/` may import this module, as the checker.  Parity unpinned w.r.t. th
 not installed here, so this restates torchvision `models/video/resnet.py` (VideoResNet with BasicStem,
 Conv3DSimple, BasicBlock [2, 2, 2, 2]; BN3d eps 1e-5, momentum 0.1; AdaptiveAvgPool3d(1)) functionally with
 `F.conv3d` / `F.batch_norm` on parameters taken from a `cmhar.r3d.R3D18` state_dict (same key names as torchvision).
+
+`q` (optional): a rounding applied at every point where the HIP bf16 path stores a tensor in bf16 — the network input,
+each conv output z (and, in the backward, dz), each BN/activation output y (and the gradient flowing into it) —
+`bf16_storage` emulates that storage in the fp32 restatement.  It separates the error bf16 storage itself causes
+(ill-conditioned gradients amplify it) from any kernel error (tests/test_r3d_gpu.py, tests/test_cnn2d_gpu.py).
 """
 from __future__ import annotations
 
 import torch
 import torch.nn.functional as F
+
+
+class _RoundBF16(torch.autograd.Function):
+    """Forward value and backward gradient both rounded to bf16 (round-to-nearest-even), kept in fp32."""
+
+    @staticmethod
+    def forward(ctx, x):
+        return x.bfloat16().float()
+
+    @staticmethod
+    def backward(ctx, g):
+        return g.bfloat16().float()
+
+
+def bf16_storage(x):
+    return _RoundBF16.apply(x)
+
+
+def _id(x):
+    return x
 
 
 def _bn(x, sd, pre, training, stats):
@@ -19,23 +44,25 @@ def _bn(x, sd, pre, training, stats):
     return y
 
 
-def r3d18_features(sd, video_bcthw, training=True, stats=None):
-    """video (B, 3, T, H, W) fp32 → pooled (B, 512).  `stats` collects updated running (mean, var) per BN prefix."""
+def r3d18_features(sd, video_bcthw, training=True, stats=None, q=None):
+    """video (B, 3, T, H, W) fp32 → pooled (B, 512).  `stats` collects updated running (mean, var) per BN prefix;
+    `q` marks the bf16 storage points of the HIP path (module docstring)."""
     stats = {} if stats is None else stats
-    x = F.conv3d(video_bcthw, sd['stem.0.weight'], stride=(1, 2, 2), padding=(1, 3, 3))
-    x = F.relu(_bn(x, sd, 'stem.1.', training, stats))
+    q = q or _id
+    x = q(F.conv3d(q(video_bcthw), sd['stem.0.weight'], stride=(1, 2, 2), padding=(1, 3, 3)))
+    x = q(F.relu(_bn(x, sd, 'stem.1.', training, stats)))
     for li in range(1, 5):
         for bi in range(2):
             p = f'layer{li}.{bi}.'
             stride = 2 if (li > 1 and bi == 0) else 1
-            h = F.conv3d(x, sd[p + 'conv1.0.weight'], stride=stride, padding=1)
-            h = F.relu(_bn(h, sd, p + 'conv1.1.', training, stats))
-            h = F.conv3d(h, sd[p + 'conv2.0.weight'], stride=1, padding=1)
+            h = q(F.conv3d(x, sd[p + 'conv1.0.weight'], stride=stride, padding=1))
+            h = q(F.relu(_bn(h, sd, p + 'conv1.1.', training, stats)))
+            h = q(F.conv3d(h, sd[p + 'conv2.0.weight'], stride=1, padding=1))
             h = _bn(h, sd, p + 'conv2.1.', training, stats)
             if p + 'downsample.0.weight' in sd:
-                idn = F.conv3d(x, sd[p + 'downsample.0.weight'], stride=stride)
-                idn = _bn(idn, sd, p + 'downsample.1.', training, stats)
+                idn = q(F.conv3d(x, sd[p + 'downsample.0.weight'], stride=stride))
+                idn = q(_bn(idn, sd, p + 'downsample.1.', training, stats))
             else:
                 idn = x
-            x = F.relu(h + idn)
+            x = q(F.relu(h + idn))
     return x.mean(dim=(2, 3, 4))

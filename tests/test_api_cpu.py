@@ -179,3 +179,41 @@ def test_unloadable_pretrained_backbone_raises(monkeypatch):
     cfg.model.allow_random_init = False
     cfg.model.video_pretrained = False
     VideoEncoder(cfg)
+
+
+def test_cnn2d_backbones_torchvision_layout():
+    """resnet18 children()[:-2] / mobilenet_v2 .features (models.py:163-173): torchvision parameter counts and key
+    names; hub / ImageNet weights are not fetchable offline, so video_pretrained=True raises unless opted in."""
+    import pytest
+    import torch
+    from cmhar.cnn2d import MobileNetV2Features, ResNet18Features
+    from cmhar.config import Config
+    from cmhar.models import VideoEncoder
+    from oracle import cnn2d_cpu as O
+    r, m = ResNet18Features(), MobileNetV2Features()
+    assert sum(p.numel() for p in r.parameters()) == 11_176_512     # resnet18 (11 689 512) minus fc (513 000)
+    assert sum(p.numel() for p in m.parameters()) == 2_223_872      # mobilenet_v2 (3 504 872) minus classifier
+    rk, mk = list(r.state_dict()), list(m.state_dict())
+    assert rk[:2] == ['0.weight', '1.weight'] and '5.0.downsample.0.weight' in rk and '7.1.bn2.running_var' in rk
+    assert mk[0] == '0.0.weight' and '1.conv.0.0.weight' in mk and '2.conv.3.running_mean' in mk
+    assert mk[-1] == '18.1.num_batches_tracked' and len(m) == 19
+    with torch.no_grad():
+        fr = O.resnet18_features({k: v for k, v in r.state_dict().items()}, torch.randn(2, 3, 64, 64), False)
+        fm = O.mobilenet_v2_features({k: v for k, v in m.state_dict().items()}, torch.randn(2, 3, 64, 64), False)
+    assert fr.shape == (2, 512, 2, 2) and fm.shape == (2, 1280, 2, 2)
+    cfg = Config()
+    cfg.model.video_backbone = 'resnet18'
+    cfg.model.video_pretrained = True
+    cfg.model.allow_random_init = False
+    import os
+    old = os.environ.pop('CMHAR_ALLOW_RANDOM_INIT', None)
+    try:
+        with pytest.raises(OSError):
+            VideoEncoder(cfg)
+    finally:
+        if old is not None:
+            os.environ['CMHAR_ALLOW_RANDOM_INIT'] = old
+    cfg.model.video_pretrained = False
+    venc = VideoEncoder(cfg)
+    assert venc.feature_dim == 512 and hasattr(venc, 'temporal_pool')
+    assert all(k.startswith(('backbone.', 'projection.')) for k in venc.state_dict())

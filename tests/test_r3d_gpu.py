@@ -5,7 +5,10 @@ Kernel level (fp32, exact-fp32 GEMM): conv3d = im2col + GEMM vs F.conv3d (≤ 1e
 vectorised (C % 8 == 0) paths with stride/padding; col2im is the adjoint of im2col (<im2col x, c> = <x, col2im c>);
 channels-last BatchNorm3d (+ residual + ReLU) forward / backward vs torch autograd (≤ 1e-5).
 Backbone: fp32 mode features ≤ 1e-4 rel, running stats ≤ 1e-5, every parameter gradient ≤ 2e-3 rel; bf16 mode
-(throughput) features ≤ 5e-2 rel, gradients cosine ≥ 0.9 and ≤ 0.5 rel; eval mode (running statistics) ≤ 1e-4 rel."""
+(throughput): every parameter gradient within 3× (+1e-2) of the error bf16 storage alone causes for that parameter
+(the fp32 oracle re-run with bf16 rounding at the HIP path's storage points — `bf16_storage_bound` documents why the
+stem / early-BN gradients are the ill-conditioned ones); eval mode (running statistics) ≤ 1e-4 rel.  The stem
+weight gradient's ~1024-way split-K at production row counts ≤ 1e-4 vs the fp32 product of the same operands."""
 import math
 
 import pytest
@@ -97,9 +100,9 @@ def test_bn_channels_last_fwd_bwd(C, relu, res):
         assert rel(dres, rr.grad) < 1e-6
 
 
-def _backbone_case(dtype, training=True, B=2, T=4, S=32):
+def _backbone_case(dtype, training=True, B=2, T=4, S=32, emulate=False):
     from cmhar.r3d import R3D18, run_r3d
-    from oracle.r3d_cpu import r3d18_features
+    from oracle.r3d_cpu import bf16_storage, r3d18_features
     torch.manual_seed(2)
     m = R3D18(None, compute_dtype=dtype)
     with torch.no_grad():     # non-trivial BN affine parameters / running stats
@@ -112,14 +115,21 @@ def _backbone_case(dtype, training=True, B=2, T=4, S=32):
     sd = {k: v.clone() for k, v in m.state_dict().items()}
     video = torch.randn(B, T, 3, S, S)      # (B, T, C, H, W)
     R = torch.randn(B, 512)
-    sd_p = {k: (v.clone().requires_grad_(True) if v.is_floating_point() and 'running' not in k else v.clone())
-            for k, v in sd.items()}
-    stats = {}
-    ref = r3d18_features(sd_p, video.transpose(1, 2), training=training, stats=stats)
-    (ref * R).sum().backward()
+
+    def oracle(q):
+        sd_p = {k: (v.clone().requires_grad_(True) if v.is_floating_point() and 'running' not in k else v.clone())
+                for k, v in sd.items()}
+        stats = {}
+        ref = r3d18_features(sd_p, video.transpose(1, 2), training=training, stats=stats, q=q)
+        (ref * R).sum().backward()
+        return sd_p, stats, ref
+
+    sd_p, stats, ref = oracle(None)
     m = m.to(DEV).train(training)
     feat = run_r3d(m, video.to(DEV), training)
     (feat * R.to(DEV)).sum().backward()
+    if emulate:
+        return m, sd_p, stats, ref, feat, oracle(bf16_storage)
     return m, sd_p, stats, ref, feat
 
 
@@ -137,19 +147,51 @@ def test_r3d18_fp32_matches_oracle():
         assert int(bufs[pre + 'num_batches_tracked']) == 1
 
 
-def test_r3d18_bf16_close_to_oracle():
-    # bf16 activations through 17 batch-normalised layers: the rounding noise grows towards the stem in the backward
-    # (at B = 2, 32² the stem gradient was 0.35 rel off), so the bound is per-parameter cosine ≥ 0.9 plus a loose norm
-    # bound; the exact path is the fp32 test above
-    m, sd_p, _, ref, feat = _backbone_case('bf16', B=4, T=4, S=48)
-    assert rel(feat, ref) < 5e-2
-    worst = []
-    for k, p in m.named_parameters():
-        g, r = p.grad.double().cpu().flatten(), sd_p[k].grad.double().flatten()
-        cos = (g @ r / (g.norm() * r.norm()).clamp_min(1e-30)).item()
-        worst.append((cos, rel(g, r), k))
-        assert cos > 0.9 and rel(g, r) < 0.5, (k, cos, rel(g, r))
-    print('worst cosine', min(worst))
+def bf16_storage_bound(gpu_grads, fp32_grads, emul_grads, slack=3.0, floor=1e-2):
+    """Per-parameter check of a bf16-storage path against the fp32 oracle, with the bound set by the error that bf16
+    STORAGE ITSELF causes for that parameter: the fp32 restatement run with bf16 rounding at the HIP path's storage
+    points (oracle q = bf16_storage) shows e_p = rel(emulated, fp32).  Root cause of the large stem / early-BN errors
+    (r01's 0.35): the next training-mode BatchNorm's backward removes each channel's mean gradient, so the gradients of
+    the layers before it are small residuals of large cancelling sums, and the 2^-9 relative rounding of the stored
+    dz / dx does not cancel — e_p is large exactly for those parameters and ~1e-2 elsewhere.  A kernel error shows as
+    rel(gpu, fp32) >> e_p on a well-conditioned parameter."""
+    rows = []
+    for k in fp32_grads:
+        e_p = rel(emul_grads[k], fp32_grads[k])
+        e_g = rel(gpu_grads[k], fp32_grads[k])
+        rows.append((e_g, e_p, k))
+        assert e_g <= slack * e_p + floor, (k, e_g, e_p)
+    return sorted(rows, reverse=True)
+
+
+def test_r3d18_bf16_error_is_bf16_storage():
+    m, sd_p, _, ref, feat, (sd_q, _, ref_q) = _backbone_case('bf16', B=4, T=4, S=48, emulate=True)
+    e_feat = rel(ref_q, ref)
+    assert rel(feat, ref) < 3 * e_feat + 1e-2, (rel(feat, ref), e_feat)
+    grads = {k: p.grad for k, p in m.named_parameters()}
+    rows = bf16_storage_bound(grads, {k: sd_p[k].grad for k in grads}, {k: sd_q[k].grad for k in grads})
+    print('worst (gpu err, bf16-storage err, param):', rows[:4])
+
+
+def test_r3d_stem_weight_gradient_split_k_production_rows():
+    """the stem weight gradient (C = 3, Kp = 448 → 64 × 448 over ~1.6 M rows) at the production clip
+    geometry, i.e. the ~1024-way split-K of r3d.py's stem path (K.gemm layout 2 with `splits`), against the fp32
+    product of the same bf16 operands (torch matmul on the device): ≤ 1e-4 rel."""
+    from cmhar import kernels as K
+    from cmhar import r3d
+    torch.manual_seed(7)
+    rows = 32 * 16 * 56 * 56                                  # B = 32 clips, 16 × 112² → 16 × 56² outputs
+    Kp, Cc = 448, 64
+    col = torch.randn(rows, Kp, device=DEV).bfloat16()
+    dz = torch.randn(rows, Cc, device=DEV).bfloat16()
+    tiles = -(-Cc // 128) * -(-Kp // 128)
+    splits = max(1, min(1024 // tiles, rows // 4096))
+    assert splits >= 256
+    dw = torch.empty(Cc, Kp, device=DEV)
+    K.gemm(2, dz, col, dw, splits=splits)
+    ref = dz.float().T @ col.float()
+    assert rel(dw, ref) < 1e-4
+    assert r3d._r8(3 * 3 * 7 * 7) == Kp                      # the stem's padded K
 
 
 def test_r3d18_eval_running_stats():
