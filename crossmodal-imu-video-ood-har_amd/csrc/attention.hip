@@ -30,24 +30,36 @@ __device__ __forceinline__ int att_off(int row, int chunk) {
   return row * 128 + ((chunk ^ f) << 4);
 }
 
-// Stage a [64][64] bf16 tile (rows r0.. of a [rows][ld] matrix, column offset col0) into registers: 2 chunks/thread.
-struct Tile64 {
-  uint4_t r[2];
-  __device__ __forceinline__ void load(const bf16* __restrict__ base, long ld, int r0, int rows_total, int tid) {
+typedef __attribute__((address_space(3))) void* att_lds_ptr;
+
+// The same [64][64] tile image written by LDS-DMA (buffer_load_dwordx4 ... lds: global → LDS without a VGPR round
+// trip, no ds_write): each wave issues 2 of the tile's 8 pieces of 1 KiB (8 rows × 128 B); the DMA's LDS destination
+// is lane-linear, so the att_off XOR swizzle is applied to each lane's SOURCE chunk (an involution).  Rows at or past
+// `rows_total` fall outside the buffer resource's num_records and read as zero.  Per-lane offsets are computed once; a tile costs two scalar resource updates and 2 DMA instructions.
+struct TileDma {
+  const char* base;   // row 0 of the head slice
+  long row_bytes;     // ld * 2
+  long valid;         // bytes of the slice that exist: (rows_total - 1) * row_bytes + 128
+  int voff[2];
+  __device__ __forceinline__ void init(const bf16* __restrict__ P, long ld, int rows_total, int wave, int lane) {
+    base = (const char*)P;
+    row_bytes = ld * 2;
+    valid = rows_total > 0 ? (long)(rows_total - 1) * row_bytes + 128 : 0;
 #pragma unroll
-    for (int it = 0; it < 2; ++it) {
-      const int c = it * 256 + tid;
-      const int row = c >> 3, ch = c & 7;
-      if (r0 + row < rows_total) r[it] = *(const uint4_t*)(base + (long)(r0 + row) * ld + ch * 8);
-      else r[it] = uint4_t{0u, 0u, 0u, 0u};
+    for (int t = 0; t < 2; ++t) {
+      const int row = 8 * (2 * wave + t) + (lane >> 3);
+      const int f = (((row >> 1) & 1) << 2) | ((row >> 3) & 3);
+      voff[t] = (int)(row * row_bytes + (((lane & 7) ^ f) << 4));
     }
   }
-  __device__ __forceinline__ void store(char* lds, int tid) const {
+  __device__ __forceinline__ void tile(int r0, char* lds, int wave) const {
+    const long off = (long)r0 * row_bytes;
+    const long left = valid - off;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(base + off), (short)0, (int)(left > 0 ? (left < 0x7fffffff ? left : 0x7fffffff) : 0), 0x00020000);
 #pragma unroll
-    for (int it = 0; it < 2; ++it) {
-      const int c = it * 256 + tid;
-      *(uint4_t*)(lds + att_off(c >> 3, c & 7)) = r[it];
-    }
+    for (int t = 0; t < 2; ++t)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (att_lds_ptr)(lds + (2 * wave + t) * 1024), 16, voff[t], 0, 0, 0);
   }
 };
 
@@ -138,11 +150,12 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_bf16(int H, int Lq, int Lk, i
   for (int j = 0; j < QB; ++j) { m[j] = -INFINITY; l[j] = 0.f; }
 
   const int nt = (Lk + 63) / 64;
-  Tile64 tk, tv;
-  tk.load(Kb, ldk, 0, Lk, tid);
-  tv.load(Vb, ldv, 0, Lk, tid);
-  tk.store(Ks(0), tid);
-  tv.store(Vs(0), tid);
+  TileDma tk, tv;
+  tk.init(Kb, ldk, Lk, wave, lane);
+  tv.init(Vb, ldv, Lk, wave, lane);
+  tk.tile(0, Ks(0), wave);
+  tv.tile(0, Vs(0), wave);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   // A wave whose queries all lie past Lq (the ragged last workgroup of a head) still helps stage K/V tiles and
   // joins every barrier, but issues no MFMA / softmax work: its SIMD's matrix pipe goes to the co-resident waves.
@@ -170,9 +183,9 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_bf16(int H, int Lq, int Lk, i
       }
     }
     }
-    if (more) {   // next tile's global loads fly under the softmax and P·V (written to LDS after them)
-      tk.load(Kb, ldk, (kt + 1) * 64, Lk, tid);
-      tv.load(Vb, ldv, (kt + 1) * 64, Lk, tid);
+    if (more) {   // next tile DMA'd into the other buffer under the softmax and P·V
+      tk.tile((kt + 1) * 64, Ks(cur ^ 1), wave);
+      tv.tile((kt + 1) * 64, Vs(cur ^ 1), wave);
     }
     if (active) {
     const int kbase = kt * 64;
@@ -234,10 +247,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_bf16(int H, int Lq, int Lk, i
             o[j][d] = mma32<E>(vf, pb[j][kb][ss], o[j][d]);
         }
     }
-    if (more) {
-      tk.store(Ks(cur ^ 1), tid);
-      tv.store(Vs(cur ^ 1), tid);
-    }
+    if (more) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // own pieces of the next tile landed
     __syncthreads();
   };
   for (int kt = 0; kt < nt; kt += 2) {
@@ -267,7 +277,12 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_bf16(int H, int Lq, int Lk, i
 }
 
 // dK, dV: one wave = 32 keys (K, V fragments in registers as B operands), q tiles of 64 staged in LDS.
-__global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_bf16(int H, int Lq, int Lk, const bf16* __restrict__ Q,
+// Three waves per SIMD for the dK/dV kernel (168 VGPRs, 12 B/lane spilled): its LDS-DMA staging freed the 64
+// register-staged tile VGPRs; measured 4-7 % faster than two waves per SIMD (tools/debug/attn_ab.py)
+#ifndef CMHAR_DKDV_OCC
+#define CMHAR_DKDV_OCC 3
+#endif
+__global__ __launch_bounds__(256, CMHAR_DKDV_OCC) void attn_bwd_dkdv_bf16(int H, int Lq, int Lk, const bf16* __restrict__ Q,
                                                              long ldq, const bf16* __restrict__ K, long ldk,
                                                              const bf16* __restrict__ V, long ldv,
                                                              const bf16* __restrict__ dO, long lddo,
@@ -304,11 +319,13 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_bf16(int H, int Lq, int 
     for (int r = 0; r < 16; ++r) { dk[d][r] = 0.f; dv[d][r] = 0.f; }
 
   const int nt = (Lq + 63) / 64;
-  Tile64 tq, tg;
+  TileDma tq, tg;            // Q / dO tiles by LDS-DMA (see TileDma)
+  tq.init(Qb, ldq, Lq, wave, lane);
+  tg.init(Gb, lddo, Lq, wave, lane);
   float lv = 0.f, dv_ = 0.f;
-  auto load_rows = [&](int qt) {
-    tq.load(Qb, ldq, qt * 64, Lq, tid);
-    tg.load(Gb, lddo, qt * 64, Lq, tid);
+  auto load_rows = [&](int qt, char* qs, char* gs) {
+    tq.tile(qt * 64, qs, wave);
+    tg.tile(qt * 64, gs, wave);
     if (tid < 64) {   // row constants staged pre-negated (and -lse pre-divided by c): accumulator seeds
       const int q = qt * 64 + tid;
       lv = q < Lq ? -lseb[q] * inv_c : -INFINITY;
@@ -316,12 +333,11 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_bf16(int H, int Lq, int 
     }
   };
   auto store_rows = [&](int buf) {
-    tq.store(Qs(buf), tid);
-    tg.store(Gs(buf), tid);
     if (tid < 64) { Ls[buf * 64 + tid] = lv; Ds[buf * 64 + tid] = dv_; }
   };
-  load_rows(0);
+  load_rows(0, Qs(0), Gs(0));
   store_rows(0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   const bool active = k0 < Lk;      // waves past the last key only stage tiles and join barriers (see forward)
   // one tile per call, LDS buffer index a compile-time constant (tiles run in pairs): LDS addresses fold into
@@ -329,7 +345,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_bf16(int H, int Lq, int 
   auto tile = [&](auto CUR, int qt) __attribute__((always_inline)) {
     constexpr int cur = decltype(CUR)::value;
     const bool more = qt + 1 < nt;
-    if (more) load_rows(qt + 1);
+    if (more) load_rows(qt + 1, Qs(cur ^ 1), Gs(cur ^ 1));
     const float* L_ = Ls + cur * 64;
     const float* D_ = Ds + cur * 64;
 #pragma unroll
@@ -364,7 +380,10 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_bf16(int H, int Lq, int 
         }
       }
     }
-    if (more) store_rows(cur ^ 1);
+    if (more) {
+      store_rows(cur ^ 1);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // own DMA pieces of the next tile landed
+    }
     __syncthreads();
   };
   for (int qt = 0; qt < nt; qt += 2) {
@@ -388,10 +407,19 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_bf16(int H, int Lq, int 
   }
 }
 
-// dQ: one wave = 32 queries (Q, dO fragments in registers), K/V tiles of 64 keys in LDS.
+// dQ: one wave = QB blocks of 32 queries (Q, dO fragments in registers), K/V tiles of 64 keys in LDS.  With QB = 2
+// every K / V row fragment and K transposed fragment read from LDS feeds two MFMA chains: the kernel's LDS read
+// traffic per MFMA halves (at QB = 1 the 4 waves' reads of the shared K/V tiles took as many LDS cycles as the MFMAs
+// took matrix-pipe cycles).  A workgroup = 4 waves = 128·QB queries starting at q_base.
 // δ = rowsum(dO ∘ O) is computed here from the query rows this wave owns anyway (no separate pass over O and dO)
 // and written for the dK/dV kernel, which runs after this one on the same stream.
-__global__ __launch_bounds__(256, 2) void attn_bwd_dq_bf16(int H, int Lq, int Lk, const bf16* __restrict__ Q, long ldq,
+// (three waves per SIMD for dQ spills 60 B/lane and measured 19 % slower)
+#ifndef CMHAR_DQ_OCC
+#define CMHAR_DQ_OCC 2
+#endif
+template <int QB>
+__global__ __launch_bounds__(256, QB == 1 ? CMHAR_DQ_OCC : 2) void attn_bwd_dq_bf16(int H, int Lq, int Lk, int q_base,
+                                                           const bf16* __restrict__ Q, long ldq,
                                                            const bf16* __restrict__ K, long ldk,
                                                            const bf16* __restrict__ V, long ldv,
                                                            const bf16* __restrict__ O, long ldo,
@@ -405,38 +433,46 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_bf16(int H, int Lq, int Lk
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5;
   const BlkIdx bi = flash_block(H);
   const int hd = bi.hd, b = bi.b;
-  const int q0 = bi.blk * 128 + wave * 32;
+  const int q0 = q_base + bi.blk * (128 * QB) + wave * (32 * QB);
   const bf16* Kb = K + (long)b * Lk * ldk + hd * 64;
   const bf16* Vb = V + (long)b * Lk * ldv + hd * 64;
   const float c = scale * LOG2E;
-  const int myq = min(q0 + (lane & 31), Lq - 1);
-  bf16x8 qf[4], gf[4];
+  bf16x8 qf[QB][4], gf[QB][4];
+  float sL[QB], Dl[QB];
 #pragma unroll
-  for (int t = 0; t < 4; ++t) {
-    qf[t] = *(const bf16x8*)(Q + ((long)b * Lq + myq) * ldq + hd * 64 + 16 * t + 8 * h);
-    gf[t] = *(const bf16x8*)(dO + ((long)b * Lq + myq) * lddo + hd * 64 + 16 * t + 8 * h);
+  for (int j = 0; j < QB; ++j) {
+    const int myq = min(q0 + 32 * j + (lane & 31), Lq - 1);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      qf[j][t] = *(const bf16x8*)(Q + ((long)b * Lq + myq) * ldq + hd * 64 + 16 * t + 8 * h);
+      gf[j][t] = *(const bf16x8*)(dO + ((long)b * Lq + myq) * lddo + hd * 64 + 16 * t + 8 * h);
+    }
+    sL[j] = -lse[((long)b * H + hd) * Lq + myq] / c;    // accumulator seed: p = exp2(c·acc)
+    float d_ = 0.f;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const bf16x8 ov = *(const bf16x8*)(O + ((long)b * Lq + myq) * ldo + hd * 64 + 16 * t + 8 * h);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) d_ = fmaf((float)gf[j][t][e], (float)ov[e], d_);
+    }
+    d_ += xhalf(d_);
+    Dl[j] = d_;
+    if (h == 0 && q0 + 32 * j + (lane & 31) < Lq) delta[((long)b * H + hd) * Lq + myq] = d_;
   }
-  const float L2 = lse[((long)b * H + hd) * Lq + myq];
-  float Dl = 0.f;
+  floatx16 dq[QB][2];
 #pragma unroll
-  for (int t = 0; t < 4; ++t) {
-    const bf16x8 ov = *(const bf16x8*)(O + ((long)b * Lq + myq) * ldo + hd * 64 + 16 * t + 8 * h);
+  for (int j = 0; j < QB; ++j)
 #pragma unroll
-    for (int j = 0; j < 8; ++j) Dl = fmaf((float)gf[t][j], (float)ov[j], Dl);
-  }
-  Dl += xhalf(Dl);
-  if (h == 0 && q0 + (lane & 31) < Lq) delta[((long)b * H + hd) * Lq + myq] = Dl;
-  floatx16 dq[2];
+    for (int d = 0; d < 2; ++d)
 #pragma unroll
-  for (int d = 0; d < 2; ++d)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) dq[d][r] = 0.f;
+      for (int r = 0; r < 16; ++r) dq[j][d][r] = 0.f;
   const int nt = (Lk + 63) / 64;
-  Tile64 tk, tv;
-  tk.load(Kb, ldk, 0, Lk, tid);
-  tv.load(Vb, ldv, 0, Lk, tid);
-  tk.store(Ks(0), tid);
-  tv.store(Vs(0), tid);
+  TileDma tk, tv;
+  tk.init(Kb, ldk, Lk, wave, lane);
+  tv.init(Vb, ldv, Lk, wave, lane);
+  tk.tile(0, Ks(0), wave);
+  tv.tile(0, Vs(0), wave);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   const bool active = q0 < Lq;      // waves past the last query only stage tiles and join barriers (see forward)
   // one tile per call, LDS buffer index a compile-time constant (tiles run in pairs): LDS addresses fold into
@@ -444,61 +480,79 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_bf16(int H, int Lq, int Lk
   auto tile = [&](auto CUR, int kt) __attribute__((always_inline)) {
     constexpr int cur = decltype(CUR)::value;
     const bool more = kt + 1 < nt;
-    if (more) {
-      tk.load(Kb, ldk, (kt + 1) * 64, Lk, tid);
-      tv.load(Vb, ldv, (kt + 1) * 64, Lk, tid);
+    if (more) {   // next tile DMA'd into the other buffer (its last reader passed the previous tile's barrier)
+      tk.tile((kt + 1) * 64, Ks(cur ^ 1), wave);
+      tv.tile((kt + 1) * 64, Vs(cur ^ 1), wave);
     }
     const int kbase = kt * 64;
-#pragma unroll
+    // (kb not unrolled: unrolled, the compiler hoisted the second key block's fragment reads over the first block's
+    // MFMAs and spilled 560 B/lane)
+#pragma unroll 1
     for (int kb = 0; kb < 2; ++kb) {
       if (!active) break;
-      floatx16 s, dp;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) { s[r] = -L2 / c; dp[r] = -Dl; }
+      // this key block's K / V row fragments and K transposed fragments, read once and used by all QB q-blocks
+      bf16x8 kfr[4], vfr[4], ktr[2][2];
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
-        s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag(Ks(cur), kb * 32, t, lane), qf[t], s, 0, 0, 0);
-        dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag(Vs(cur), kb * 32, t, lane), gf[t], dp, 0, 0, 0);
-      }
-      if (kbase + 64 > Lk) {   // ragged last tile only (wave-uniform branch)
-#pragma unroll
-        for (int r = 0; r < 16; ++r)
-          if (kbase + kb * 32 + acc_row(r, h) >= Lk) s[r] = -INFINITY;
+        kfr[t] = row_frag(Ks(cur), kb * 32, t, lane);
+        vfr[t] = row_frag(Vs(cur), kb * 32, t, lane);
       }
 #pragma unroll
-      for (int r = 0; r < 16; ++r) dp[r] = fexp2(s[r] * c) * dp[r];
+      for (int ss = 0; ss < 2; ++ss)
 #pragma unroll
-      for (int ss = 0; ss < 2; ++ss) {
-        const bf16x8 db = pack8(dp, ss);
+        for (int d = 0; d < 2; ++d) ktr[ss][d] = tr_frag(Ks(cur), kb * 32, ss, d * 32, lane);
 #pragma unroll
-        for (int d = 0; d < 2; ++d)
-          dq[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_frag(Ks(cur), kb * 32, ss, d * 32, lane), db, dq[d], 0, 0, 0);
+      for (int j = 0; j < QB; ++j) {
+        floatx16 s, dp;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) { s[r] = sL[j]; dp[r] = -Dl[j]; }
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kfr[t], qf[j][t], s, 0, 0, 0);
+          dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vfr[t], gf[j][t], dp, 0, 0, 0);
+        }
+        if (kbase + 64 > Lk) {   // ragged last tile only (wave-uniform branch)
+#pragma unroll
+          for (int r = 0; r < 16; ++r)
+            if (kbase + kb * 32 + acc_row(r, h) >= Lk) s[r] = -INFINITY;
+        }
+#pragma unroll
+        for (int r = 0; r < 16; ++r) dp[r] = fexp2(s[r] * c) * dp[r];
+#pragma unroll
+        for (int ss = 0; ss < 2; ++ss) {
+          const bf16x8 db = pack8(dp, ss);
+#pragma unroll
+          for (int d = 0; d < 2; ++d)
+            dq[j][d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ktr[ss][d], db, dq[j][d], 0, 0, 0);
+        }
       }
     }
-    if (more) {
-      tk.store(Ks(cur ^ 1), tid);
-      tv.store(Vs(cur ^ 1), tid);
-    }
+    if (more) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // own pieces of the next tile landed
     __syncthreads();
   };
   for (int kt = 0; kt < nt; kt += 2) {
     tile(std::integral_constant<int, 0>{}, kt);
     if (kt + 1 < nt) tile(std::integral_constant<int, 1>{}, kt + 1);
   }
-  const int q = q0 + (lane & 31);
-  if (q < Lq) {
-    bf16* row = dQ + ((long)b * Lq + q) * lddq + hd * 64;
 #pragma unroll
-    for (int d = 0; d < 2; ++d)
+  for (int j = 0; j < QB; ++j) {
+    const int q = q0 + 32 * j + (lane & 31);
+    if (q < Lq) {
+      bf16* row = dQ + ((long)b * Lq + q) * lddq + hd * 64;
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        bf16x4 v;
+      for (int d = 0; d < 2; ++d)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) v[j] = (bf16)(dq[d][4 * g + j] * scale);
-        *(bf16x4*)(row + d * 32 + 8 * g + 4 * h) = v;
-      }
+        for (int g = 0; g < 4; ++g) {
+          bf16x4 v;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = (bf16)(dq[j][d][4 * g + e] * scale);
+          *(bf16x4*)(row + d * 32 + 8 * g + 4 * h) = v;
+        }
+    }
   }
 }
+#undef Ks
+#undef Vs
 
 // ---------------------------------------------------------------------------------------------------------------
 // exact fp32 path (any head dim <= 64), with optional attention-prob dropout (nn.MultiheadAttention semantics)
@@ -675,6 +729,12 @@ __global__ __launch_bounds__(64) void attn_bwd_dkdv_f32(int H, int Lq, int Lk, c
 #undef Gs
 }  // namespace
 
+// QB = 2 for the dQ kernel does not fit 256 registers (spills at occupancy 2; at occupancy 1 it measured 16 % slower
+// than QB = 1): off unless CMHAR_ATTN_DQ_QB=2 at build time (A/B builds only)
+#ifndef CMHAR_ATTN_DQ_QB
+#define CMHAR_ATTN_DQ_QB 1
+#endif
+
 // ----------------------------------------------------------------------------------------------------------------
 // C ABI.  Tensors are [B*L, ld] row-major with head h at columns h*D .. h*D+D-1.
 // lse / delta: fp32 [B*H*Lq] workspaces owned by the caller.
@@ -725,10 +785,18 @@ extern "C" int cmhar_attention_bwd(int dtype, int B, int H, int Lq, int Lk, int 
   if (B <= 0 || Lq <= 0) return 0;
   if (dtype == CMHAR_F16) return -1;   // fp16 is the inference-only path
   if (dtype == CMHAR_BF16 && D == 64 && pdrop == 0.f) {
-    attn_bwd_dq_bf16<<<dim3(cdiv(Lq, 128), H, B), 256, 0, st>>>(H, Lq, Lk, (const bf16*)Q, ldq, (const bf16*)K, ldk,
-                                                                (const bf16*)V, ldv, (const bf16*)O, ldo,
-                                                                (const bf16*)dO, lddo, lse, delta, (bf16*)dQ, lddq,
-                                                                scale);
+    // 256-query workgroups (QB = 2) over the bulk, 128-query workgroups for the rest (as the forward)
+    const int bulk = CMHAR_ATTN_DQ_QB == 2 ? (Lq / 256) * 256 : 0;
+    if (bulk > 0)
+      attn_bwd_dq_bf16<2><<<dim3(bulk / 256, H, B), 256, 0, st>>>(H, Lq, Lk, 0, (const bf16*)Q, ldq, (const bf16*)K,
+                                                                  ldk, (const bf16*)V, ldv, (const bf16*)O, ldo,
+                                                                  (const bf16*)dO, lddo, lse, delta, (bf16*)dQ, lddq,
+                                                                  scale);
+    if (Lq > bulk)
+      attn_bwd_dq_bf16<1><<<dim3(cdiv(Lq - bulk, 128), H, B), 256, 0, st>>>(H, Lq, Lk, bulk, (const bf16*)Q, ldq,
+                                                                            (const bf16*)K, ldk, (const bf16*)V, ldv,
+                                                                            (const bf16*)O, ldo, (const bf16*)dO, lddo,
+                                                                            lse, delta, (bf16*)dQ, lddq, scale);
     attn_bwd_dkdv_bf16<<<dim3(cdiv(Lk, 128), H, B), 256, 0, st>>>(H, Lq, Lk, (const bf16*)Q, ldq, (const bf16*)K, ldk,
                                                                   (const bf16*)V, ldv, (const bf16*)dO, lddo, lse,
                                                                   delta, (bf16*)dK, lddk, (bf16*)dV, lddv, scale);
