@@ -114,8 +114,17 @@ __device__ __forceinline__ BlkIdx flash_block(int H) {
 // alone saturate the CU's 128 B/clk LDS port at the MFMA rate).  A workgroup = 4 waves = 128·QB queries starting
 // at q_base; K/V tiles of 64 keys are register-staged into a double-buffered LDS pair (issue early, write late).
 // E: the 16-bit number format of Q/K/V/O (bf16 training path; fp16 for the fp16 inference path).
+// Forward per 32-key half at 3 waves per SIMD (168 VGPRs): 4 % faster than scoring whole 64-key tiles at 2 waves
+// per SIMD (tools/debug/attn_ab.py; the lazy-rescale points move, so not bit-identical to that form).  One launch
+// with the last 256-query workgroup of each head partly idle instead of the 128-query tail launch: 1 % slower.
+#ifndef CMHAR_ATTN_FWD_PERKB
+#define CMHAR_ATTN_FWD_PERKB 1
+#endif
+#ifndef CMHAR_ATTN_FWD_ONE_LAUNCH
+#define CMHAR_ATTN_FWD_ONE_LAUNCH 0
+#endif
 template <typename E, int QB>
-__global__ __launch_bounds__(256, 2) void attn_fwd_bf16(int H, int Lq, int Lk, int q_base, const bf16* __restrict__ Q,
+__global__ __launch_bounds__(256, CMHAR_ATTN_FWD_PERKB ? 3 : 2) void attn_fwd_bf16(int H, int Lq, int Lk, int q_base, const bf16* __restrict__ Q,
                                                         long ldq, const bf16* __restrict__ K, long ldk,
                                                         const bf16* __restrict__ V, long ldv, E* __restrict__ O,
                                                         long ldo, float* __restrict__ lse, float scale) {
@@ -165,6 +174,75 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_bf16(int H, int Lq, int Lk, i
   auto tile = [&](auto CUR, int kt) __attribute__((always_inline)) {
     constexpr int cur = decltype(CUR)::value;
     const bool more = kt + 1 < nt;
+#if CMHAR_ATTN_FWD_PERKB
+    // Per 32-key half (kb): Sᵀ for every q-block (each K fragment read once, used QB times), its softmax, then
+    // Oᵀ += Vᵀ·Pᵀ for that half — only one half's scores are live (32 fewer VGPRs than scoring the whole 64-key
+    // tile first), which lets QB = 2 run at 3 waves per SIMD.
+    if (more) {   // next tile DMA'd into the other buffer under this tile's math
+      tk.tile((kt + 1) * 64, Ks(cur ^ 1), wave);
+      tv.tile((kt + 1) * 64, Vs(cur ^ 1), wave);
+    }
+    if (active) {
+      const int kbase = kt * 64;
+#pragma unroll 1
+      for (int kb = 0; kb < 2; ++kb) {
+        floatx16 s[QB];
+#pragma unroll
+        for (int j = 0; j < QB; ++j)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) s[j][r] = 0.f;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          const bf16x8 kf = row_frag(Ks(cur), kb * 32, t, lane);
+#pragma unroll
+          for (int j = 0; j < QB; ++j) s[j] = mma32<E>(kf, qf[j][t], s[j]);
+        }
+        if (kbase + kb * 32 + 32 > Lk) {   // ragged last half-tile only (wave-uniform branch)
+#pragma unroll
+          for (int j = 0; j < QB; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r)
+              if (kbase + kb * 32 + acc_row(r, h) >= Lk) s[j][r] = -INFINITY;
+        }
+        bf16x8 pb[QB][2];
+#pragma unroll
+        for (int j = 0; j < QB; ++j) {
+          float mt = -INFINITY;
+#pragma unroll
+          for (int r = 0; r < 16; ++r) mt = fmaxf(mt, s[j][r]);
+          mt = fmaxf(mt, xhalf(mt)) * c;
+          // lazy rescale (see below): the running max moves only when a row's half-tile max exceeds it by > 8
+          if (__builtin_amdgcn_ballot_w64(mt > m[j] + 8.f) != 0) {
+            const float mn = fmaxf(m[j], mt);
+            const float alpha = fexp2(m[j] - mn);
+            m[j] = mn;
+            l[j] *= alpha;
+#pragma unroll
+            for (int d = 0; d < 2; ++d)
+#pragma unroll
+              for (int r = 0; r < 16; ++r) o[j][d][r] *= alpha;
+          }
+          const float mn = m[j];
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const float p = fexp2(fmaf(s[j][r], c, -mn));
+            s[j][r] = p;
+            l[j] += p;
+          }
+#pragma unroll
+          for (int ss = 0; ss < 2; ++ss) pb[j][ss] = pack8<E>(s[j], ss);
+        }
+#pragma unroll
+        for (int ss = 0; ss < 2; ++ss)
+#pragma unroll
+          for (int d = 0; d < 2; ++d) {
+            const bf16x8 vf = tr_frag(Vs(cur), kb * 32, ss, d * 32, lane);
+#pragma unroll
+            for (int j = 0; j < QB; ++j) o[j][d] = mma32<E>(vf, pb[j][ss], o[j][d]);
+          }
+      }
+    }
+#else
     // Sᵀ = K·Qᵀ for every q-block; each K fragment is read once and used QB times
     floatx16 s[QB][2];
     if (active) {
@@ -247,6 +325,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_bf16(int H, int Lq, int Lk, i
             o[j][d] = mma32<E>(vf, pb[j][kb][ss], o[j][d]);
         }
     }
+#endif
     if (more) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // own pieces of the next tile landed
     __syncthreads();
   };
@@ -748,7 +827,8 @@ extern "C" int cmhar_attention_fwd(int dtype, int B, int H, int Lq, int Lk, int 
   if ((dtype == CMHAR_BF16 || dtype == CMHAR_F16) && D == 64 && pdrop == 0.f) {
     // 256-query workgroups (64 rows per wave) over the bulk, 128-query workgroups (32 rows per wave, waves past Lq
     // skip the math) for the rest
-    const int bulk = (Lq / 256) * 256;
+    // (CMHAR_ATTN_FWD_ONE_LAUNCH: 256-query workgroups everywhere, the last one per head partly idle)
+    const int bulk = CMHAR_ATTN_FWD_ONE_LAUNCH ? cdiv(Lq, 256) * 256 : (Lq / 256) * 256;
 #define FL(E)                                                                                                    \
   do {                                                                                                           \
     if (bulk > 0)                                                                                                \
