@@ -31,6 +31,8 @@ __device__ __forceinline__ int att_off(int row, int chunk) {
 }
 
 typedef __attribute__((address_space(3))) void* att_lds_ptr;
+typedef __attribute__((ext_vector_type(2))) float float2_t;
+typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2_t;
 
 // The same [64][64] tile image written by LDS-DMA (buffer_load_dwordx4 ... lds: global → LDS without a VGPR round
 // trip, no ds_write): each wave issues 2 of the tile's 8 pieces of 1 KiB (8 rows × 128 B); the DMA's LDS destination
@@ -443,15 +445,25 @@ __global__ __launch_bounds__(256, CMHAR_DKDV_OCC) void attn_bwd_dkdv_bf16(int H,
         s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag(Qs(cur), qb * 32, t, lane), kf[t], s, 0, 0, 0);
         dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag(Gs(cur), qb * 32, t, lane), vf[t], dp, 0, 0, 0);
       }
+      // p = exp2(c·s), dS = P ∘ (dP − δ), then both packed to bf16 — written in aligned register pairs (one
+      // v_pk_mul_f32 + one v_cvt_pk_bf16_f32 per pair; element-wise, the compiler paired (1,2),(3,4),... and spent
+      // v_mov / v_alignbit / v_perm re-pairing them for the packs; the backward got 3 % faster, bit-identical.  The
+      // same rewrite of the forward's softmax measured 5 % slower and is not used)
+      bf16x8 pbv[2], dbv[2];
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const float p = fexp2(s[r] * c);
-        s[r] = p;
-        dp[r] = p * dp[r];   // dS = P ∘ (dP − δ)
+      for (int r = 0; r < 16; r += 2) {
+        const float2_t pv = {fexp2(s[r] * c), fexp2(s[r + 1] * c)};
+        const float2_t dv2 = pv * float2_t{dp[r], dp[r + 1]};
+        const bf16x2_t pp = __builtin_convertvector(pv, bf16x2_t);
+        const bf16x2_t dd = __builtin_convertvector(dv2, bf16x2_t);
+        pbv[r >> 3][r & 7] = pp[0];
+        pbv[r >> 3][(r & 7) + 1] = pp[1];
+        dbv[r >> 3][r & 7] = dd[0];
+        dbv[r >> 3][(r & 7) + 1] = dd[1];
       }
 #pragma unroll
       for (int ss = 0; ss < 2; ++ss) {
-        const bf16x8 pb = pack8(s, ss), db = pack8(dp, ss);
+        const bf16x8 pb = pbv[ss], db = dbv[ss];
 #pragma unroll
         for (int d = 0; d < 2; ++d) {
           dv[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_frag(Gs(cur), qb * 32, ss, d * 32, lane), pb, dv[d], 0, 0, 0);
@@ -594,9 +606,12 @@ __global__ __launch_bounds__(256, QB == 1 ? CMHAR_DQ_OCC : 2) void attn_bwd_dq_b
 #pragma unroll
       for (int j = 0; j < QB; ++j) {
 #pragma unroll
-        for (int r = 0; r < 16; ++r) dp[j][r] = fexp2(s[j][r] * c) * dp[j][r];
-#pragma unroll
-        for (int ss = 0; ss < 2; ++ss) db[j][ss] = pack8(dp[j], ss);
+        for (int r = 0; r < 16; r += 2) {   // aligned pairs: one v_pk_mul_f32 + one v_cvt_pk_bf16_f32 each
+          const float2_t pv = {fexp2(s[j][r] * c), fexp2(s[j][r + 1] * c)};
+          const bf16x2_t dd = __builtin_convertvector(pv * float2_t{dp[j][r], dp[j][r + 1]}, bf16x2_t);
+          db[j][r >> 3][r & 7] = dd[0];
+          db[j][r >> 3][(r & 7) + 1] = dd[1];
+        }
       }
 #pragma unroll
       for (int ss = 0; ss < 2; ++ss)
