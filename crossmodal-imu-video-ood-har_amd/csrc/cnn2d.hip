@@ -250,26 +250,29 @@ __global__ __launch_bounds__(256) void dwconv_cl_wgrad_partial(Pool g, int rows_
   }
 }
 
-// dw[c, tap] = Σ_chunks part[chunk][tap][c]: one block per 64 (c, tap) outputs, 4 chunk slots of 64 lanes summing
-// strided chunks in a fixed order, then the 4 slots in a fixed order
+// dw[c, tap] = Σ_chunks part[chunk][tap][c]: a block sums 32 channels (lanes, coalesced 128-B rows of the slab) of one
+// tap over 8 chunk slots in a fixed order, then the slots in a fixed order
 __global__ __launch_bounds__(256) void dwconv_cl_wgrad_final(int C, int kk, int nchunk, const float* __restrict__ part,
                                                              float* __restrict__ dw) {
   __shared__ float sh[256];
-  const int tid = threadIdx.x, ol = tid & 63, slot = tid >> 6;
-  const int o = blockIdx.x * 64 + ol;                      // output index c·kk + t
+  const int tid = threadIdx.x, cl = tid & 31, slot = tid >> 5;
+  const int c = blockIdx.x * 32 + cl, t = blockIdx.y;
   float a = 0.f;
-  if (o < C * kk) {
-    const int c = o / kk, t = o % kk;
-    for (int b = slot; b < nchunk; b += 4) a += part[((long)b * kk + t) * C + c];
-  }
+  if (c < C)
+    for (int b = slot; b < nchunk; b += 8) a += part[((long)b * kk + t) * C + c];
   sh[tid] = a;
   __syncthreads();
-  if (slot == 0 && o < C * kk) dw[o] = sh[ol] + sh[64 + ol] + sh[128 + ol] + sh[192 + ol];
+  if (slot == 0 && c < C) {
+    float r = 0.f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) r += sh[k * 32 + cl];
+    dw[c * kk + t] = r;
+  }
 }
 
-inline int dw_chunks(long M) {   // ≤ 4096 chunks of ≥ 256 rows (≥ 16 blocks per CU at production sizes)
+inline int dw_chunks(long M) {   // ≤ 2048 chunks of ≥ 256 rows (≥ 8 blocks per CU at production sizes)
   const long c = (M + 255) / 256;
-  return (int)(c < 4096 ? (c > 0 ? c : 1) : 4096);
+  return (int)(c < 2048 ? (c > 0 ? c : 1) : 2048);
 }
 
 // ---- weight packing -------------------------------------------------------------------------------------------
@@ -407,7 +410,7 @@ extern "C" int cmhar_dwconv2d_cl_wgrad(int dtype, int N, int H, int W, int C, in
   DT_SWITCH(dtype, F);
 #undef F
 #undef FK
-  dwconv_cl_wgrad_final<<<cdiv((long)C * k * k, 64), 256, 0, stream>>>(C, k * k, nch, ws, dw);
+  dwconv_cl_wgrad_final<<<dim3(cdiv(C, 32), k * k), 256, 0, stream>>>(C, k * k, nch, ws, dw);
   CMHAR_CHECK_LAUNCH();
   return 0;
 }
