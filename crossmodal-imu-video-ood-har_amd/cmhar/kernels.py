@@ -133,8 +133,15 @@ def _generic_splits(M, N, K):
     workgroups with >= 64 k per slice.  The IMU encoder's token GEMMs (M = 13·batch) keep the single-pass order:
     their backward through post-LN layers amplifies summation-order differences (measured: split-K moved g1's
     bias gradients by up to 9e-4 relative, deterministically, vs 1e-6 single-pass)."""
+    if _NO_GENERIC_SPLIT:
+        return 1
+    if M >= 256 and N >= 256 and K >= 4096:
+        # fp32 weight gradients of the VideoMAE Linears (M, N = 768..3072, K = tokens): 36-144 tiles of 128² on the
+        # f32 MFMA kernel; split K into slices of >= 1024 to put ~512 workgroups on the chip
+        tiles = math.ceil(M / 128) * math.ceil(N / 128)
+        return 1 if tiles >= 256 else max(1, min(32, math.ceil(512 / tiles), K // 1024))
     tiles = math.ceil(M / 64) * math.ceil(N / 64)
-    if M > 64 or N < 256 or tiles >= 64 or K < 512 or _NO_GENERIC_SPLIT:
+    if M > 64 or N < 256 or tiles >= 64 or K < 512:
         return 1
     return max(1, min(32, math.ceil(128 / tiles), K // 64))
 

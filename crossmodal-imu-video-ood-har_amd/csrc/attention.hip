@@ -13,7 +13,9 @@
 // and the tiny IMU attention (L = 13, d = 16), including counter-hash dropout regenerated in backward.
 #include "common.h"
 
+#include <initializer_list>
 #include <type_traits>
+#include <utility>
 
 namespace {
 
@@ -96,17 +98,6 @@ __device__ __forceinline__ bf16x8 pack8(const floatx16& a, int s) {
 __device__ __forceinline__ int acc_row(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
 
 __device__ __forceinline__ float xhalf(float v) { return __shfl_xor(v, 32); }
-
-// (block, head, batch) of a flash workgroup with every block of one (batch, head) on the same XCD (K/V, or Q/dO,
-// of that head is then fetched into one L2 and re-read from it by the head's other blocks).
-struct BlkIdx { int blk, hd, b; };
-__device__ __forceinline__ BlkIdx flash_block(int H) {
-  const int nb = gridDim.x;
-  const int lin = blockIdx.x + nb * (blockIdx.y + gridDim.y * blockIdx.z);
-  const int r = xcd_remap(lin, nb * gridDim.y * gridDim.z);
-  const int bh = r / nb;
-  return {r % nb, bh % H, bh / H};
-}
 
 // ---------------------------------------------------------------------------------------------------------------
 // forward
@@ -831,6 +822,22 @@ __global__ __launch_bounds__(64) void attn_bwd_dkdv_f32(int H, int Lq, int Lk, c
 #define CMHAR_ATTN_DQ_QB 1
 #endif
 
+// f32-MFMA flash kernels (csrc/attention_f32.hip) for fp32 storage, D = 64, no dropout
+void cmhar_attn_f32m_fwd(int B, int H, int Lq, int Lk, const float* Q, long ldq, const float* K, long ldk,
+                         const float* V, long ldv, float* O, long ldo, float* lse, float scale, hipStream_t st);
+void cmhar_attn_f32m_bwd(int B, int H, int Lq, int Lk, const float* Q, long ldq, const float* K, long ldk,
+                         const float* V, long ldv, const float* O, long ldo, const float* dO, long lddo,
+                         const float* lse, float* delta, float* dQ, long lddq, float* dK, long lddk, float* dV,
+                         long lddv, float scale, hipStream_t st);
+
+// every operand a 16-B aligned base with a row stride of whole 16-B chunks (the f32 flash tiles load float4s)
+static bool f32m_ok(int dtype, int D, float pdrop, std::initializer_list<std::pair<const void*, long>> ops) {
+  if (dtype != CMHAR_F32 || D != 64 || pdrop != 0.f || !cmhar_f32_mfma()) return false;
+  for (const auto& o : ops)
+    if (((uintptr_t)o.first & 15) || (o.second & 3)) return false;
+  return true;
+}
+
 // ----------------------------------------------------------------------------------------------------------------
 // C ABI.  Tensors are [B*L, ld] row-major with head h at columns h*D .. h*D+D-1.
 // lse / delta: fp32 [B*H*Lq] workspaces owned by the caller.
@@ -856,6 +863,9 @@ extern "C" int cmhar_attention_fwd(int dtype, int B, int H, int Lq, int Lk, int 
   } while (0)
     if (dtype == CMHAR_F16) FL(f16); else FL(bf16);
 #undef FL
+  } else if (f32m_ok(dtype, D, pdrop, {{Q, ldq}, {K, ldk}, {V, ldv}, {O, ldo}})) {
+    cmhar_attn_f32m_fwd(B, H, Lq, Lk, (const float*)Q, ldq, (const float*)K, ldk, (const float*)V, ldv, (float*)O, ldo,
+                        lse, scale, st);
   } else {
     // exact-fp32 math path (fp32 storage, or bf16 storage with a head dim / dropout the flash kernel lacks);
     // its LSE is in natural-log units and is only ever consumed by the matching backward below
@@ -897,6 +907,11 @@ extern "C" int cmhar_attention_bwd(int dtype, int B, int H, int Lq, int Lk, int 
     attn_bwd_dkdv_bf16<<<dim3(cdiv(Lk, 128), H, B), 256, 0, st>>>(H, Lq, Lk, (const bf16*)Q, ldq, (const bf16*)K, ldk,
                                                                   (const bf16*)V, ldv, (const bf16*)dO, lddo, lse,
                                                                   delta, (bf16*)dK, lddk, (bf16*)dV, lddv, scale);
+  } else if (f32m_ok(dtype, D, pdrop, {{Q, ldq}, {K, ldk}, {V, ldv}, {O, ldo}, {dO, lddo}, {dQ, lddq}, {dK, lddk},
+                                       {dV, lddv}})) {
+    cmhar_attn_f32m_bwd(B, H, Lq, Lk, (const float*)Q, ldq, (const float*)K, ldk, (const float*)V, ldv,
+                        (const float*)O, ldo, (const float*)dO, lddo, lse, delta, (float*)dQ, lddq, (float*)dK, lddk,
+                        (float*)dV, lddv, scale, st);
   } else {
 #define F(TT, DD)                                                                                               \
   attn_bwd_dq_f32<TT, DD><<<dim3(cdiv(Lq, 64), H, B), 64, 0, st>>>(H, Lq, Lk, (const TT*)Q, ldq, (const TT*)K, ldk,   \

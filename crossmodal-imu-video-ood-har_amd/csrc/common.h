@@ -185,6 +185,28 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8;
 }
 
+// (block, head, batch) of a flash-attention workgroup on a (blocks, H, B) grid, with every block of one (batch, head)
+// on the same XCD (K/V, or Q/dO, of that head is then fetched into one L2 and re-read from it by the head's other
+// blocks).
+struct BlkIdx { int blk, hd, b; };
+__device__ __forceinline__ BlkIdx flash_block(int H) {
+  const int nb = gridDim.x;
+  const int lin = blockIdx.x + nb * (blockIdx.y + gridDim.y * blockIdx.z);
+  const int r = xcd_remap(lin, nb * gridDim.y * gridDim.z);
+  const int bh = r / nb;
+  return {r % nb, bh % H, bh / H};
+}
+
+// The exact-fp32 parity mode runs its large GEMMs and its D = 64 attention on the f32-input MFMA; CMHAR_F32_MFMA=0
+// (read once per process) routes them to the exact-f32 VALU kernels instead (A/B tests: identical GEMM bits).
+static inline bool cmhar_f32_mfma() {
+  static const bool on = [] {
+    const char* v = getenv("CMHAR_F32_MFMA");
+    return !(v && v[0] == '0');
+  }();
+  return on;
+}
+
 #define CMHAR_CHECK_LAUNCH() do { hipError_t _e = hipGetLastError(); if (_e != hipSuccess) return (int)_e; } while (0)
 
 static inline int cdiv(long a, long b) { return (int)((a + b - 1) / b); }

@@ -1,8 +1,13 @@
-// Generic strided GEMM with fp32 accumulation (VALU FMA, LDS-tiled).
+// Generic strided GEMM with fp32 accumulation.
 //
 // Used for (a) the exact-fp32 parity mode of every Linear on the path and (b) the small, latency-bound
 // GEMMs of the IMU encoder / projection heads (M = batch*13 or batch rows), where an MFMA tile would idle.
 // C[m,n] = epilogue( sum_k A[m*sam + k*sak] * B[k*sbk + n*sbn] ), batched over blockIdx.z.
+//
+// Two kernels, ONE numerics: every output is the k-ordered fmaf chain from 0.  The VALU kernel does it with fmaf;
+// the f32-input MFMA (v_mfma_f32_32x32x2_f32, 157 TF/s, bitwise the k-ordered fmaf chain: lanes 0-31 carry k, lanes
+// 32-63 carry k+1, applied in that order) does it for every f32 GEMM with >= 64 output tiles of 128², so the fp32
+// parity mode's VideoMAE GEMMs move to the matrix cores with bit-identical results.
 #include "common.h"
 
 namespace {
@@ -92,6 +97,149 @@ __global__ __launch_bounds__(NTH) void gemm_generic_kernel(
     }
 }
 
+// ---- f32 MFMA kernel --------------------------------------------------------------------------------------------
+// 128 x 128 output tile per 256-thread block, 32-k steps; wave (wm, wn) owns a 64 x 64 quadrant = 2 x 2 blocks of
+// 32 x 32 accumulators (64 acc VGPRs).  Operand panels are staged global → registers → LDS as [k][row] (the MFMA
+// reads one f32 per lane: row l&31 of k = 2p + (l>>5)), double-buffered with one barrier per k-step; the next panel's
+// global loads are in flight during the current one's 64 MFMAs per wave.
+constexpr int FM = 128, FK = 32, FNT = 256;
+#ifndef CMHAR_F32_PF
+#define CMHAR_F32_PF 1
+#endif
+
+// One 128-row x 32-k operand panel.  KC: element (r, k) at P[r*ld + k] (k contiguous; 16-B loads along k, written
+// transposed); else at P[k*ld + r] (rows contiguous; 16-B loads and 16-B LDS writes along r).
+template <bool KC>
+struct F32Panel {
+  static constexpr int LD = KC ? FM + 1 : FM + 4;   // LDS stride of one k row (floats): +1 spreads the transposed
+                                                    // scalar writes over banks, +4 keeps 16-B writes aligned
+  static constexpr int FLOATS = FK * LD;
+  floatx4 v[4];
+  __device__ __forceinline__ void load(const float* __restrict__ P, long ld, int R, int K, int r0, int k0, int tid) {
+#pragma unroll
+    for (int it = 0; it < 4; ++it) {
+      const int i = it * FNT + tid;
+      int r, k;
+      if (KC) { r = i >> 3; k = (i & 7) * 4; } else { k = i >> 5; r = (i & 31) * 4; }
+      const int gr = r0 + r, gk = k0 + k;
+      // K (KC) or R (!KC) is a multiple of 4 (host-checked): a 16-B vector is wholly inside or wholly outside
+      const bool ok = gr < R && gk < K;
+      const float* src = KC ? P + (long)gr * ld + gk : P + (long)gk * ld + gr;
+      v[it] = ok ? *(const floatx4*)src : floatx4{0.f, 0.f, 0.f, 0.f};
+    }
+  }
+  __device__ __forceinline__ void store(float* __restrict__ S, int tid) const {
+#pragma unroll
+    for (int it = 0; it < 4; ++it) {
+      const int i = it * FNT + tid;
+      if (KC) {
+        const int r = i >> 3, k = (i & 7) * 4;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) S[(k + j) * LD + r] = v[it][j];
+      } else {
+        *(floatx4*)(S + (i >> 5) * LD + (i & 31) * 4) = v[it];
+      }
+    }
+  }
+};
+
+template <bool A_KC, bool B_KC, typename OutT>
+__global__ __launch_bounds__(FNT, 2) void gemm_f32_mfma_kernel(
+    int M, int N, int K, const float* __restrict__ A, long lda, long sAb, const float* __restrict__ B, long ldb,
+    long sBb, OutT* __restrict__ C, long ldc, long sCb, Epilogue e) {
+  typedef F32Panel<A_KC> PA;
+  typedef F32Panel<B_KC> PB;
+  constexpr int TLD = FM + 1;                          // epilogue staging stride (the tile reuses the panels' LDS)
+  static_assert(2 * (PA::FLOATS + PB::FLOATS) >= FM * TLD, "epilogue tile must fit the panel LDS");
+  __shared__ float smem[2 * (PA::FLOATS + PB::FLOATS)];
+  float* const As0 = smem;                             // panel buffers: A[0], A[1], B[0], B[1]
+  float* const Bs0 = smem + 2 * PA::FLOATS;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int wm = w >> 1, wn = w & 1, r = lane & 31, h = lane >> 5;
+  const int bm = blockIdx.y * FM, bn = blockIdx.x * FM;
+  A += blockIdx.z * sAb;
+  B += blockIdx.z * sBb;
+  C += blockIdx.z * sCb;
+  floatx16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) acc[i][j][q] = 0.f;
+  const int nk = (K + FK - 1) / FK;
+  PA pa;
+  PB pb;
+  pa.load(A, lda, M, K, bm, 0, tid);
+  pb.load(B, ldb, N, K, bn, 0, tid);
+  pa.store(As0, tid);
+  pb.store(Bs0, tid);
+  __syncthreads();
+  const int ao = wm * 64 + r, bo = wn * 64 + r;
+  for (int t = 0; t < nk; ++t) {
+    const int cur = t & 1;
+    if (t + 1 < nk) {
+      pa.load(A, lda, M, K, bm, (t + 1) * FK, tid);
+      pb.load(B, ldb, N, K, bn, (t + 1) * FK, tid);
+    }
+    const float* as = As0 + cur * PA::FLOATS;
+    const float* bs = Bs0 + cur * PB::FLOATS;
+#if CMHAR_F32_PF
+    // operands of all 16 k-pairs read up front: the MFMAs wait on lgkmcnt for their own pair only
+    float fa0[FK / 2], fa1[FK / 2], fb0[FK / 2], fb1[FK / 2];
+#pragma unroll
+    for (int p = 0; p < FK / 2; ++p) {
+      const int k = 2 * p + h;
+      fa0[p] = as[k * PA::LD + ao];
+      fa1[p] = as[k * PA::LD + ao + 32];
+      fb0[p] = bs[k * PB::LD + bo];
+      fb1[p] = bs[k * PB::LD + bo + 32];
+    }
+    __builtin_amdgcn_sched_barrier(0);   // keep the reads ahead of the MFMAs (the scheduler sinks them otherwise)
+#pragma unroll
+    for (int p = 0; p < FK / 2; ++p) {
+      acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa0[p], fb0[p], acc[0][0], 0, 0, 0);
+      acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa0[p], fb1[p], acc[0][1], 0, 0, 0);
+      acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa1[p], fb0[p], acc[1][0], 0, 0, 0);
+      acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa1[p], fb1[p], acc[1][1], 0, 0, 0);
+    }
+#else
+#pragma unroll
+    for (int p = 0; p < FK / 2; ++p) {
+      const int k = 2 * p + h;
+      const float a0 = as[k * PA::LD + ao], a1 = as[k * PA::LD + ao + 32];
+      const float b0 = bs[k * PB::LD + bo], b1 = bs[k * PB::LD + bo + 32];
+      acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0, acc[0][0], 0, 0, 0);
+      acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b1, acc[0][1], 0, 0, 0);
+      acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b0, acc[1][0], 0, 0, 0);
+      acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc[1][1], 0, 0, 0);
+    }
+#endif
+    if (t + 1 < nk) {
+      pa.store(As0 + (cur ^ 1) * PA::FLOATS, tid);
+      pb.store(Bs0 + (cur ^ 1) * PB::FLOATS, tid);
+    }
+    __syncthreads();
+  }
+  // Stage the 128² tile through LDS (C/D map of the 32x32 forms: col = lane&31, row = (q&3) + 8(q>>2) + 4(lane>>5)),
+  // then apply the epilogue row-contiguously: coalesced C / residual / aux traffic, and no dynamic indexing of the
+  // accumulators (the epilogue body is too large to unroll 64 times).  The loop's last barrier freed the panels.
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int q = 0; q < 16; ++q)
+        smem[(wm * 64 + 32 * i + (q & 3) + 8 * (q >> 2) + 4 * h) * TLD + wn * 64 + 32 * j + r] = acc[i][j][q];
+  __syncthreads();
+#pragma unroll 4
+  for (int it = 0; it < FM * FM / FNT; ++it) {
+    const int idx = it * FNT + tid, row = idx >> 7, col = idx & (FM - 1);
+    const int m = bm + row, n = bn + col;
+    if (m < M && n < N) epilogue_store<OutT>(e, C, ldc, m, n, smem[row * TLD + col]);
+  }
+}
+
 // Split-K combine: C = epilogue(Σ_s P[s]) in a fixed split order (deterministic).
 template <typename TOut>
 __global__ __launch_bounds__(256) void generic_splitk_reduce(int M, int N, int S, const float* __restrict__ P,
@@ -105,6 +253,36 @@ __global__ __launch_bounds__(256) void generic_splitk_reduce(int M, int N, int S
 }
 
 }  // namespace
+
+static bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+
+// The f32 MFMA kernel takes f32 operands whose contiguous dimension allows 16-B loads: that dimension a multiple of
+// 4 elements, the other stride and the batch stride multiples of 4, 16-B aligned bases; and enough 128² tiles
+// (>= 64 over the batch) to fill the chip — the IMU encoder's few-tile GEMMs stay on the VALU kernel.
+static bool f32_mfma_ok(int M, int N, int K, int batch, const void* A, long sam, long sak, long sAb, const void* B,
+                        long sbk, long sbn, long sBb) {
+  if (!cmhar_f32_mfma()) return false;
+  if ((long)cdiv(M, FM) * cdiv(N, FM) * batch < 64) return false;
+  if (!al16(A) || !al16(B) || (sAb & 3) || (sBb & 3)) return false;
+  const bool akc = sak == 1, bkc = sbk == 1;
+  if (!(akc || sam == 1) || !(bkc || sbn == 1)) return false;
+  const long a_ld = akc ? sam : sak, b_ld = bkc ? sbn : sbk;
+  if ((a_ld & 3) || (b_ld & 3)) return false;
+  if ((akc && (K & 3)) || (!akc && (M & 3)) || (bkc && (K & 3)) || (!bkc && (N & 3))) return false;
+  return true;
+}
+
+template <typename TO>
+static void launch_f32_mfma(dim3 grid, hipStream_t stream, int M, int N, int K, const float* A, long sam, long sak,
+                            long sAb, const float* B, long sbk, long sbn, long sBb, TO* C, long ldc, long sCb,
+                            const Epilogue& e) {
+  const bool akc = sak == 1, bkc = sbk == 1;
+  const long a_ld = akc ? sam : sak, b_ld = bkc ? sbn : sbk;
+  if (akc && bkc) gemm_f32_mfma_kernel<true, true, TO><<<grid, FNT, 0, stream>>>(M, N, K, A, a_ld, sAb, B, b_ld, sBb, C, ldc, sCb, e);
+  else if (akc) gemm_f32_mfma_kernel<true, false, TO><<<grid, FNT, 0, stream>>>(M, N, K, A, a_ld, sAb, B, b_ld, sBb, C, ldc, sCb, e);
+  else if (bkc) gemm_f32_mfma_kernel<false, true, TO><<<grid, FNT, 0, stream>>>(M, N, K, A, a_ld, sAb, B, b_ld, sBb, C, ldc, sCb, e);
+  else gemm_f32_mfma_kernel<false, false, TO><<<grid, FNT, 0, stream>>>(M, N, K, A, a_ld, sAb, B, b_ld, sBb, C, ldc, sCb, e);
+}
 
 // Skinny GEMMs (a handful of 64x64 output tiles over a long K: the video projection / projection heads at M = batch
 // rows, K = 768) are bound by the latency of their K loop on a few CUs.  Split K over `splits` batched slices into
@@ -122,26 +300,36 @@ extern "C" int cmhar_gemm_generic_splitk(int in_dtype, int out_dtype, int M, int
   const int S = cdiv(K, klen);
   Epilogue plain{};
   plain.alpha = 1.f;
-  const int esz = in_dtype == CMHAR_BF16 ? 2 : 4;
   // slice s: A advanced by s*klen along k, B likewise; the last slice's K is clamped by running it separately
   const int full = K / klen;                           // slices of exactly klen
-  dim3 grid(cdiv(N, TN), cdiv(M, TM), full);
+  // every slice on one kernel (both give the k-ordered chain per slice, so the choice never changes a bit)
+  const bool mf = in_dtype == CMHAR_F32 && f32_mfma_ok(M, N, klen, S, A, sam, sak, (long)klen * sak, B, sbk, sbn,
+                                                       (long)klen * sbk);
+  const int tile = mf ? FM : TN;
+  dim3 grid(cdiv(N, tile), cdiv(M, tile), full);
 #define LAUNCH(TI, GRID, KK, AOFF, BOFF, POFF)                                                                  \
-  gemm_generic_kernel<TI, float><<<GRID, 256, 0, stream>>>(M, N, KK, (const TI*)A + (AOFF), sam, sak,           \
-                                                           (long)klen * sak, (const TI*)B + (BOFF), sbk, sbn,   \
-                                                           (long)klen * sbk, ws + (POFF), N, (long)M * N, plain)
+  do {                                                                                                          \
+    if (mf)                                                                                                     \
+      launch_f32_mfma<float>(GRID, stream, M, N, KK, (const float*)A + (AOFF), sam, sak, (long)klen * sak,     \
+                             (const float*)B + (BOFF), sbk, sbn, (long)klen * sbk, ws + (POFF), N,             \
+                             (long)M * N, plain);                                                               \
+    else                                                                                                        \
+      gemm_generic_kernel<TI, float><<<GRID, 256, 0, stream>>>(M, N, KK, (const TI*)A + (AOFF), sam, sak,       \
+                                                               (long)klen * sak, (const TI*)B + (BOFF), sbk,    \
+                                                               sbn, (long)klen * sbk, ws + (POFF), N,           \
+                                                               (long)M * N, plain);                             \
+  } while (0)
   if (full > 0) {
     if (in_dtype == CMHAR_F32) LAUNCH(float, grid, klen, 0, 0, 0);
     else LAUNCH(bf16, grid, klen, 0, 0, 0);
   }
   if (full < S) {
     const long k0 = (long)full * klen;
-    dim3 g1(cdiv(N, TN), cdiv(M, TM), 1);
+    dim3 g1(cdiv(N, tile), cdiv(M, tile), 1);
     if (in_dtype == CMHAR_F32) LAUNCH(float, g1, (int)(K - k0), k0 * sak, k0 * sbk, (long)full * M * N);
     else LAUNCH(bf16, g1, (int)(K - k0), k0 * sak, k0 * sbk, (long)full * M * N);
   }
 #undef LAUNCH
-  (void)esz;
   const int blocks = min(1024, cdiv((long)M * N, 256));
   if (out_dtype == CMHAR_F32) generic_splitk_reduce<float><<<blocks, 256, 0, stream>>>(M, N, S, ws, (float*)C, ldc, e);
   else generic_splitk_reduce<bf16><<<blocks, 256, 0, stream>>>(M, N, S, ws, (bf16*)C, ldc, e);
@@ -169,7 +357,16 @@ extern "C" int cmhar_gemm_generic(int in_dtype, int out_dtype, int M, int N, int
       gemm_generic_kernel<TI, TO><<<grid, 256, 0, stream>>>(M, N, K, (const TI*)A, sam, sak, sAb, (const TI*)B, \
                                                             sbk, sbn, sBb, (TO*)C, ldc, sCb, e);                \
   } while (0)
-  if (in_dtype == CMHAR_F32 && out_dtype == CMHAR_F32) LAUNCH(float, float);
+  if (in_dtype == CMHAR_F32 && f32_mfma_ok(M, N, K, batch, A, sam, sak, sAb, B, sbk, sbn, sBb) &&
+      (out_dtype == CMHAR_F32 || out_dtype == CMHAR_BF16)) {
+    dim3 g(cdiv(N, FM), cdiv(M, FM), batch);
+    if (out_dtype == CMHAR_F32)
+      launch_f32_mfma<float>(g, stream, M, N, K, (const float*)A, sam, sak, sAb, (const float*)B, sbk, sbn, sBb,
+                             (float*)C, ldc, sCb, e);
+    else
+      launch_f32_mfma<bf16>(g, stream, M, N, K, (const float*)A, sam, sak, sAb, (const float*)B, sbk, sbn, sBb,
+                            (bf16*)C, ldc, sCb, e);
+  } else if (in_dtype == CMHAR_F32 && out_dtype == CMHAR_F32) LAUNCH(float, float);
   else if (in_dtype == CMHAR_BF16 && out_dtype == CMHAR_BF16) LAUNCH(bf16, bf16);
   else if (in_dtype == CMHAR_BF16 && out_dtype == CMHAR_F32) LAUNCH(bf16, float);
   else if (in_dtype == CMHAR_F32 && out_dtype == CMHAR_BF16) LAUNCH(float, bf16);
