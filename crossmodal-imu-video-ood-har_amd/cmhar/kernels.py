@@ -137,9 +137,10 @@ def _generic_splits(M, N, K):
         return 1
     if M >= 256 and N >= 256 and K >= 4096:
         # fp32 weight gradients of the VideoMAE Linears (M, N = 768..3072, K = tokens): 36-144 tiles of 128² on the
-        # f32 MFMA kernel; split K into slices of >= 1024 to put ~512 workgroups on the chip
+        # f32 MFMA kernel (3 workgroups per CU = 768 slots); split K into slices of >= 512 so that the grid fills
+        # the slots once (not 1.05 times: a second, nearly empty round)
         tiles = math.ceil(M / 128) * math.ceil(N / 128)
-        return 1 if tiles >= 256 else max(1, min(32, math.ceil(512 / tiles), K // 1024))
+        return 1 if tiles >= 384 else max(1, min(32, 768 // tiles, K // 512))
     tiles = math.ceil(M / 64) * math.ceil(N / 64)
     if M > 64 or N < 256 or tiles >= 64 or K < 512:
         return 1

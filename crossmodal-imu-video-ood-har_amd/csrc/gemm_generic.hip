@@ -98,29 +98,45 @@ __global__ __launch_bounds__(NTH) void gemm_generic_kernel(
 }
 
 // ---- f32 MFMA kernel --------------------------------------------------------------------------------------------
-// 128 x 128 output tile per 256-thread block, 32-k steps; wave (wm, wn) owns a 64 x 64 quadrant = 2 x 2 blocks of
-// 32 x 32 accumulators (64 acc VGPRs).  Operand panels are staged global → registers → LDS as [k][row] (the MFMA
-// reads one f32 per lane: row l&31 of k = 2p + (l>>5)), double-buffered with one barrier per k-step; the next panel's
-// global loads are in flight during the current one's 64 MFMAs per wave.
-constexpr int FM = 128, FK = 32, FNT = 256;
-#ifndef CMHAR_F32_PF
-#define CMHAR_F32_PF 1
+// (64·WM) x (64·WN) output tile per block of WM x WN waves, 32-k steps; wave (wm, wn) owns a 64 x 64 quadrant = 2 x 2
+// blocks of 32 x 32 accumulators (64 acc VGPRs).  Operand panels are staged global → registers → LDS as [k][row]
+// (the MFMA reads one f32 per lane: row l&31 of k = 2p + (l>>5)), double-buffered with one barrier per k-step; the
+// next panel's global loads are in flight during the current one's 64 MFMAs per wave.  Tiles are walked in groups
+// of FGROUP tile-rows (every group column-by-column) in XCD-contiguous chunks, so the blocks co-resident on one XCD
+// share A and B panels through its L2 instead of streaming them from the Infinity Cache.
+// 16-k steps at 3 blocks per CU: 5 % faster than 32-k steps at 2 (double-buffered panels 33 KB vs 66 KB per block;
+// tools/debug/gemm_ab.py --dtype fp32, bit-identical results)
+#ifndef CMHAR_F32_BK
+#define CMHAR_F32_BK 16
 #endif
+#ifndef CMHAR_F32_OCC
+#define CMHAR_F32_OCC 3
+#endif
+constexpr int FK = CMHAR_F32_BK;
+#ifndef CMHAR_F32_WM
+#define CMHAR_F32_WM 2
+#endif
+#ifndef CMHAR_F32_GROUP
+#define CMHAR_F32_GROUP 8
+#endif
+constexpr int FWM = CMHAR_F32_WM, FWN = 2, FGROUP = CMHAR_F32_GROUP;
 
-// One 128-row x 32-k operand panel.  KC: element (r, k) at P[r*ld + k] (k contiguous; 16-B loads along k, written
+// One ROWS-row x 32-k operand panel.  KC: element (r, k) at P[r*ld + k] (k contiguous; 16-B loads along k, written
 // transposed); else at P[k*ld + r] (rows contiguous; 16-B loads and 16-B LDS writes along r).
-template <bool KC>
+template <bool KC, int ROWS, int NT>
 struct F32Panel {
-  static constexpr int LD = KC ? FM + 1 : FM + 4;   // LDS stride of one k row (floats): +1 spreads the transposed
-                                                    // scalar writes over banks, +4 keeps 16-B writes aligned
+  static constexpr int LD = KC ? ROWS + 1 : ROWS + 4;   // LDS stride of one k row (floats): +1 spreads the
+                                                        // transposed scalar writes over banks, +4 keeps 16-B writes aligned
   static constexpr int FLOATS = FK * LD;
-  floatx4 v[4];
+  static constexpr int PER = ROWS * FK / 4 / NT;        // float4 per thread
+  static constexpr int RQ = ROWS / 4, KQ = FK / 4;
+  floatx4 v[PER];
   __device__ __forceinline__ void load(const float* __restrict__ P, long ld, int R, int K, int r0, int k0, int tid) {
 #pragma unroll
-    for (int it = 0; it < 4; ++it) {
-      const int i = it * FNT + tid;
+    for (int it = 0; it < PER; ++it) {
+      const int i = it * NT + tid;
       int r, k;
-      if (KC) { r = i >> 3; k = (i & 7) * 4; } else { k = i >> 5; r = (i & 31) * 4; }
+      if (KC) { r = i / KQ; k = (i % KQ) * 4; } else { k = i / RQ; r = (i % RQ) * 4; }
       const int gr = r0 + r, gk = k0 + k;
       // K (KC) or R (!KC) is a multiple of 4 (host-checked): a 16-B vector is wholly inside or wholly outside
       const bool ok = gr < R && gk < K;
@@ -130,33 +146,39 @@ struct F32Panel {
   }
   __device__ __forceinline__ void store(float* __restrict__ S, int tid) const {
 #pragma unroll
-    for (int it = 0; it < 4; ++it) {
-      const int i = it * FNT + tid;
+    for (int it = 0; it < PER; ++it) {
+      const int i = it * NT + tid;
       if (KC) {
-        const int r = i >> 3, k = (i & 7) * 4;
+        const int r = i / KQ, k = (i % KQ) * 4;
 #pragma unroll
         for (int j = 0; j < 4; ++j) S[(k + j) * LD + r] = v[it][j];
       } else {
-        *(floatx4*)(S + (i >> 5) * LD + (i & 31) * 4) = v[it];
+        *(floatx4*)(S + (i / RQ) * LD + (i % RQ) * 4) = v[it];
       }
     }
   }
 };
 
-template <bool A_KC, bool B_KC, typename OutT>
-__global__ __launch_bounds__(FNT, 2) void gemm_f32_mfma_kernel(
+template <int WM, int WN, bool A_KC, bool B_KC, typename OutT>
+__global__ __launch_bounds__(64 * WM * WN, WM * WN == 4 ? CMHAR_F32_OCC : 1) void gemm_f32_mfma_kernel(
     int M, int N, int K, const float* __restrict__ A, long lda, long sAb, const float* __restrict__ B, long ldb,
     long sBb, OutT* __restrict__ C, long ldc, long sCb, Epilogue e) {
-  typedef F32Panel<A_KC> PA;
-  typedef F32Panel<B_KC> PB;
-  constexpr int TLD = FM + 1;                          // epilogue staging stride (the tile reuses the panels' LDS)
-  static_assert(2 * (PA::FLOATS + PB::FLOATS) >= FM * TLD, "epilogue tile must fit the panel LDS");
-  __shared__ float smem[2 * (PA::FLOATS + PB::FLOATS)];
+  constexpr int BM = 64 * WM, BN = 64 * WN, NT = 64 * WM * WN;
+  typedef F32Panel<A_KC, BM, NT> PA;
+  typedef F32Panel<B_KC, BN, NT> PB;
+  constexpr int ELD = 65;                              // epilogue staging: 32 rows x 64 (+1) per wave
+  constexpr int PANELS = 2 * (PA::FLOATS + PB::FLOATS), STAGE = WM * WN * 32 * ELD;
+  __shared__ float smem[PANELS > STAGE ? PANELS : STAGE];
   float* const As0 = smem;                             // panel buffers: A[0], A[1], B[0], B[1]
   float* const Bs0 = smem + 2 * PA::FLOATS;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int wm = w >> 1, wn = w & 1, r = lane & 31, h = lane >> 5;
-  const int bm = blockIdx.y * FM, bn = blockIdx.x * FM;
+  const int wm = w / WN, wn = w % WN, r = lane & 31, h = lane >> 5;
+  // XCD-contiguous, row-grouped tile order
+  const int tn_count = (N + BN - 1) / BN, tm_count = (M + BM - 1) / BM;
+  const int t = xcd_remap(blockIdx.x, gridDim.x);
+  const int per_group = FGROUP * tn_count, g = t / per_group;
+  const int gm = min(FGROUP, tm_count - g * FGROUP), tin = t - g * per_group;
+  const int bm = (g * FGROUP + tin % gm) * BM, bn = (tin / gm) * BN;
   A += blockIdx.z * sAb;
   B += blockIdx.z * sBb;
   C += blockIdx.z * sCb;
@@ -176,34 +198,14 @@ __global__ __launch_bounds__(FNT, 2) void gemm_f32_mfma_kernel(
   pb.store(Bs0, tid);
   __syncthreads();
   const int ao = wm * 64 + r, bo = wn * 64 + r;
-  for (int t = 0; t < nk; ++t) {
-    const int cur = t & 1;
-    if (t + 1 < nk) {
-      pa.load(A, lda, M, K, bm, (t + 1) * FK, tid);
-      pb.load(B, ldb, N, K, bn, (t + 1) * FK, tid);
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) {
+      pa.load(A, lda, M, K, bm, (kt + 1) * FK, tid);
+      pb.load(B, ldb, N, K, bn, (kt + 1) * FK, tid);
     }
     const float* as = As0 + cur * PA::FLOATS;
     const float* bs = Bs0 + cur * PB::FLOATS;
-#if CMHAR_F32_PF
-    // operands of all 16 k-pairs read up front: the MFMAs wait on lgkmcnt for their own pair only
-    float fa0[FK / 2], fa1[FK / 2], fb0[FK / 2], fb1[FK / 2];
-#pragma unroll
-    for (int p = 0; p < FK / 2; ++p) {
-      const int k = 2 * p + h;
-      fa0[p] = as[k * PA::LD + ao];
-      fa1[p] = as[k * PA::LD + ao + 32];
-      fb0[p] = bs[k * PB::LD + bo];
-      fb1[p] = bs[k * PB::LD + bo + 32];
-    }
-    __builtin_amdgcn_sched_barrier(0);   // keep the reads ahead of the MFMAs (the scheduler sinks them otherwise)
-#pragma unroll
-    for (int p = 0; p < FK / 2; ++p) {
-      acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa0[p], fb0[p], acc[0][0], 0, 0, 0);
-      acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa0[p], fb1[p], acc[0][1], 0, 0, 0);
-      acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa1[p], fb0[p], acc[1][0], 0, 0, 0);
-      acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa1[p], fb1[p], acc[1][1], 0, 0, 0);
-    }
-#else
 #pragma unroll
     for (int p = 0; p < FK / 2; ++p) {
       const int k = 2 * p + h;
@@ -214,29 +216,29 @@ __global__ __launch_bounds__(FNT, 2) void gemm_f32_mfma_kernel(
       acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b0, acc[1][0], 0, 0, 0);
       acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc[1][1], 0, 0, 0);
     }
-#endif
-    if (t + 1 < nk) {
+    if (kt + 1 < nk) {
       pa.store(As0 + (cur ^ 1) * PA::FLOATS, tid);
       pb.store(Bs0 + (cur ^ 1) * PB::FLOATS, tid);
     }
     __syncthreads();
   }
-  // Stage the 128² tile through LDS (C/D map of the 32x32 forms: col = lane&31, row = (q&3) + 8(q>>2) + 4(lane>>5)),
-  // then apply the epilogue row-contiguously: coalesced C / residual / aux traffic, and no dynamic indexing of the
-  // accumulators (the epilogue body is too large to unroll 64 times).  The loop's last barrier freed the panels.
+  // Epilogue per wave, one 32-row half of its quadrant at a time, staged through a wave-private LDS region (C/D map
+  // of the 32x32 forms: col = lane&31, row = (q&3) + 8(q>>2) + 4(lane>>5)) so that each lane applies the epilogue to
+  // one column of a 256-B row — coalesced C / residual / aux traffic, and no dynamic indexing of the accumulators
+  // (the epilogue body is too large to unroll 64 times).  The loop's last barrier freed the panels.
+  float* const st = smem + w * 32 * ELD;
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < 2; ++i) {
 #pragma unroll
     for (int j = 0; j < 2; ++j)
 #pragma unroll
-      for (int q = 0; q < 16; ++q)
-        smem[(wm * 64 + 32 * i + (q & 3) + 8 * (q >> 2) + 4 * h) * TLD + wn * 64 + 32 * j + r] = acc[i][j][q];
-  __syncthreads();
+      for (int q = 0; q < 16; ++q) st[((q & 3) + 8 * (q >> 2) + 4 * h) * ELD + 32 * j + r] = acc[i][j][q];
+    __builtin_amdgcn_wave_barrier();   // wave-private region: one wave's LDS ops complete in order
+    const int m0 = bm + wm * 64 + 32 * i, n = bn + wn * 64 + lane;
 #pragma unroll 4
-  for (int it = 0; it < FM * FM / FNT; ++it) {
-    const int idx = it * FNT + tid, row = idx >> 7, col = idx & (FM - 1);
-    const int m = bm + row, n = bn + col;
-    if (m < M && n < N) epilogue_store<OutT>(e, C, ldc, m, n, smem[row * TLD + col]);
+    for (int row = 0; row < 32; ++row)
+      if (m0 + row < M && n < N) epilogue_store<OutT>(e, C, ldc, m0 + row, n, st[row * ELD + lane]);
+    __builtin_amdgcn_wave_barrier();
   }
 }
 
@@ -262,7 +264,7 @@ static bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 static bool f32_mfma_ok(int M, int N, int K, int batch, const void* A, long sam, long sak, long sAb, const void* B,
                         long sbk, long sbn, long sBb) {
   if (!cmhar_f32_mfma()) return false;
-  if ((long)cdiv(M, FM) * cdiv(N, FM) * batch < 64) return false;
+  if ((long)cdiv(M, 128) * cdiv(N, 128) * batch < 64) return false;
   if (!al16(A) || !al16(B) || (sAb & 3) || (sBb & 3)) return false;
   const bool akc = sak == 1, bkc = sbk == 1;
   if (!(akc || sam == 1) || !(bkc || sbn == 1)) return false;
@@ -273,15 +275,21 @@ static bool f32_mfma_ok(int M, int N, int K, int batch, const void* A, long sam,
 }
 
 template <typename TO>
-static void launch_f32_mfma(dim3 grid, hipStream_t stream, int M, int N, int K, const float* A, long sam, long sak,
+static void launch_f32_mfma(int batch, hipStream_t stream, int M, int N, int K, const float* A, long sam, long sak,
                             long sAb, const float* B, long sbk, long sbn, long sBb, TO* C, long ldc, long sCb,
                             const Epilogue& e) {
   const bool akc = sak == 1, bkc = sbk == 1;
   const long a_ld = akc ? sam : sak, b_ld = bkc ? sbn : sbk;
-  if (akc && bkc) gemm_f32_mfma_kernel<true, true, TO><<<grid, FNT, 0, stream>>>(M, N, K, A, a_ld, sAb, B, b_ld, sBb, C, ldc, sCb, e);
-  else if (akc) gemm_f32_mfma_kernel<true, false, TO><<<grid, FNT, 0, stream>>>(M, N, K, A, a_ld, sAb, B, b_ld, sBb, C, ldc, sCb, e);
-  else if (bkc) gemm_f32_mfma_kernel<false, true, TO><<<grid, FNT, 0, stream>>>(M, N, K, A, a_ld, sAb, B, b_ld, sBb, C, ldc, sCb, e);
-  else gemm_f32_mfma_kernel<false, false, TO><<<grid, FNT, 0, stream>>>(M, N, K, A, a_ld, sAb, B, b_ld, sBb, C, ldc, sCb, e);
+  const dim3 grid(cdiv(M, 64 * FWM) * cdiv(N, 64 * FWN), 1, batch);
+  const int nt = 64 * FWM * FWN;
+#define FL(AK, BK)                                                                                               \
+  gemm_f32_mfma_kernel<FWM, FWN, AK, BK, TO><<<grid, nt, 0, stream>>>(M, N, K, A, a_ld, sAb, B, b_ld, sBb, C, ldc,  \
+                                                                      sCb, e)
+  if (akc && bkc) FL(true, true);
+  else if (akc) FL(true, false);
+  else if (bkc) FL(false, true);
+  else FL(false, false);
+#undef FL
 }
 
 // Skinny GEMMs (a handful of 64x64 output tiles over a long K: the video projection / projection heads at M = batch
@@ -305,12 +313,11 @@ extern "C" int cmhar_gemm_generic_splitk(int in_dtype, int out_dtype, int M, int
   // every slice on one kernel (both give the k-ordered chain per slice, so the choice never changes a bit)
   const bool mf = in_dtype == CMHAR_F32 && f32_mfma_ok(M, N, klen, S, A, sam, sak, (long)klen * sak, B, sbk, sbn,
                                                        (long)klen * sbk);
-  const int tile = mf ? FM : TN;
-  dim3 grid(cdiv(N, tile), cdiv(M, tile), full);
+  dim3 grid(cdiv(N, TN), cdiv(M, TM), full);
 #define LAUNCH(TI, GRID, KK, AOFF, BOFF, POFF)                                                                  \
   do {                                                                                                          \
     if (mf)                                                                                                     \
-      launch_f32_mfma<float>(GRID, stream, M, N, KK, (const float*)A + (AOFF), sam, sak, (long)klen * sak,     \
+      launch_f32_mfma<float>(GRID.z, stream, M, N, KK, (const float*)A + (AOFF), sam, sak, (long)klen * sak,   \
                              (const float*)B + (BOFF), sbk, sbn, (long)klen * sbk, ws + (POFF), N,             \
                              (long)M * N, plain);                                                               \
     else                                                                                                        \
@@ -325,7 +332,7 @@ extern "C" int cmhar_gemm_generic_splitk(int in_dtype, int out_dtype, int M, int
   }
   if (full < S) {
     const long k0 = (long)full * klen;
-    dim3 g1(cdiv(N, tile), cdiv(M, tile), 1);
+    dim3 g1(cdiv(N, TN), cdiv(M, TM), 1);
     if (in_dtype == CMHAR_F32) LAUNCH(float, g1, (int)(K - k0), k0 * sak, k0 * sbk, (long)full * M * N);
     else LAUNCH(bf16, g1, (int)(K - k0), k0 * sak, k0 * sbk, (long)full * M * N);
   }
@@ -359,12 +366,11 @@ extern "C" int cmhar_gemm_generic(int in_dtype, int out_dtype, int M, int N, int
   } while (0)
   if (in_dtype == CMHAR_F32 && f32_mfma_ok(M, N, K, batch, A, sam, sak, sAb, B, sbk, sbn, sBb) &&
       (out_dtype == CMHAR_F32 || out_dtype == CMHAR_BF16)) {
-    dim3 g(cdiv(N, FM), cdiv(M, FM), batch);
     if (out_dtype == CMHAR_F32)
-      launch_f32_mfma<float>(g, stream, M, N, K, (const float*)A, sam, sak, sAb, (const float*)B, sbk, sbn, sBb,
+      launch_f32_mfma<float>(batch, stream, M, N, K, (const float*)A, sam, sak, sAb, (const float*)B, sbk, sbn, sBb,
                              (float*)C, ldc, sCb, e);
     else
-      launch_f32_mfma<bf16>(g, stream, M, N, K, (const float*)A, sam, sak, sAb, (const float*)B, sbk, sbn, sBb,
+      launch_f32_mfma<bf16>(batch, stream, M, N, K, (const float*)A, sam, sak, sAb, (const float*)B, sbk, sbn, sBb,
                             (bf16*)C, ldc, sCb, e);
   } else if (in_dtype == CMHAR_F32 && out_dtype == CMHAR_F32) LAUNCH(float, float);
   else if (in_dtype == CMHAR_BF16 && out_dtype == CMHAR_BF16) LAUNCH(bf16, bf16);
