@@ -25,6 +25,7 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 PEAK_BF16_TFLOPS = 2500.0      # MI355X dense bf16 MFMA (MI355X_MICROARCH.md; sparsity excluded)
+PEAK_F32_TFLOPS = 157.3        # f32-input MFMA (= the f32 vector rate; no xf32 on gfx950)
 PEAK_HBM_GBS = 8000.0
 
 
@@ -301,7 +302,8 @@ def main():
                       'global_batch': world * B, 'per_gpu_batch': B, 'parallelism': f'dp{world}'},
            'roofline': roof,
            'whole_step_model_tflops': round(whole_tflops, 1),
-           'whole_step_mfma_frac': round(whole_tflops / PEAK_BF16_TFLOPS, 4),
+           'whole_step_mfma_frac': round(whole_tflops / (PEAK_F32_TFLOPS if args.dtype == 'fp32' else PEAK_BF16_TFLOPS),
+                                         4),
            'first_warmup_loss': first_loss,
            'max_mem_gb': round(torch.cuda.max_memory_allocated(dev) / 2 ** 30, 1)}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
