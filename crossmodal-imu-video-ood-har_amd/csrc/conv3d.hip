@@ -702,6 +702,181 @@ __global__ __launch_bounds__(256, 2) void conv3d_wgrad_igemm(Geom g, int M, int 
   store_tile<float, 4>(smem, acc, wr, wc, lane, tid, bm, bn, Cout, g.K, out + (long)split * Cout * g.K, g.K);
 }
 
+// ---- weight gradient of the k x k x 3 convolutions from input row slabs ------------------------------------------
+// dW[co, (it, ih, iw), c] = Σ_m dz[m, co] · x[in(m, it, ih) + iw, c].  The generic kernel above gathers a fresh
+// input row for every (m, tap) of its 128-column tile, so the input is read once per tap (27× per conv).  Here a
+// workgroup owns one (it, ih) tap pair, one 64-channel slice and all three kw taps (192 dW columns), and walks the
+// output rows in chunks of R = ⌊64 / Wo⌋ whole rows: per chunk it stages the chunk's dz rows (a contiguous
+// [R·Wo][Cout-tile] block) and, per output row, the ONE input row segment its three kw taps read (Ls = (Wo−1)·sw + 3
+// positions) — the kw taps are then row shifts of the same LDS slab.  The input is read kt·kh = 9 times instead of
+// 27, dz 9 times per Cout tile instead of once per 128-column tile, and no MFMA work is spent on padding columns.
+namespace wr {
+constexpr int SLOTS = 64, MAXQ = 136, RS = 144;   // RS: LDS row stride in bytes (128 + 16 pad)
+// [row][64 bf16] images with 144-B rows: every fragment address is a per-lane base plus a compile-time offset (no
+// per-(tap, column block) address registers), and the 16 rows of one transposed read (rows 8g + q of a half-wave)
+// start 36 banks apart: at most 2 lanes of a 32-lane half per bank for unit and stride-2 row steps
+// (cdna_hip_programming.md: ds_read_b64_tr_b16 banks are (a/4) % 64 per 32-lane half).
+// 16x16x32 operand fragment: 4 bf16 of rows lo and hi (lo = k 8g + q, hi = k 8g + 4 + q of this lane) at column
+// block offset; `lo`/`hi` are byte addresses of this lane's rows + its chunk / half offset
+__device__ __forceinline__ bf16x8 frag_at(const char* lo, const char* hi) {
+  const short4_t a = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(short4_t, lo));
+  const short4_t b = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(short4_t, hi));
+  short8_t v = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+  return __builtin_bit_cast(bf16x8, v);
+}
+}  // namespace wr
+
+// COT = Cout tile (64 or 128): dz image COT/64 sub-images of [64 slots][64].  G = kh taps per workgroup (1, or 3:
+// the whole kh column for one it — the dz chunk then feeds 576 dW columns); SQ = slab rows per tap; NW waves split
+// the G·12 16-column blocks evenly, each covering every Cout row of the tile.  Operands are register-staged one chunk
+// ahead (an LDS-DMA ring 2–3 chunks ahead at one workgroup per CU measured 1.2–2.2× slower: its per-piece issue
+// cost and the single wave per SIMD outweigh the deeper prefetch).  Every division of the gather is done once per
+// thread (the chunk-invariant slot → row / position map) or once per chunk (the chunk's first output row).
+template <int COT, int G, int SQ, int NW>
+__global__ __launch_bounds__(64 * NW, 2) void conv3d_wgrad_rows(Geom g, int Cout, int R, int Ls, int rows_total,
+                                                               int chunks_per_split, const bf16* __restrict__ x,
+                                                               const bf16* __restrict__ dz, float* __restrict__ out) {
+  using namespace wr;
+  constexpr int NT = 64 * NW, NCB = COT / 16, NJ = 12 * G / NW, DZ_SUB = SLOTS * RS, DZ_BYTES = (COT / 64) * DZ_SUB;
+  static_assert(NJ * NW == 12 * G, "column blocks must split evenly over the waves");
+  constexpr int SLAB_BYTES = G * SQ * RS, DZ_N = SLOTS * COT / 8, SL_N = G * SQ * 8;
+  constexpr int DZ_PER = (DZ_N + NT - 1) / NT, SL_PER = (SL_N + NT - 1) / NT;
+  constexpr int BUF = DZ_BYTES + SLAB_BYTES;
+  __shared__ __attribute__((aligned(16))) char smem[2 * BUF];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int nct = g.C / 64, ncot = Cout / COT, ngrp = g.kt * (g.kh / G), ntile = ngrp * nct * ncot;
+  const int lin = xcd_remap(blockIdx.x + ntile * blockIdx.y, ntile * gridDim.y);   // one split's tiles per XCD
+  const int split = lin / ntile;
+  int tl = lin % ntile;
+  const int cot = tl % ncot; tl /= ncot;
+  const int ct = tl % nct; tl /= nct;
+  const int ih0 = (tl % (g.kh / G)) * G, it = tl / (g.kh / G);
+  const int nchunk = (rows_total + R - 1) / R;
+  const int c_beg = split * chunks_per_split, c_end = min(nchunk, c_beg + chunks_per_split);
+  const int M = rows_total * g.Wo, used = R * g.Wo, nq = R * Ls;
+  // chunk-invariant part of this thread's slab loads: output row r within the chunk (-1: none), input position
+  // wi, input row offset hi − ho·sh (the tap), column
+  int sr[SL_PER], swi[SL_PER], sdh[SL_PER];
+#pragma unroll
+  for (int i = 0; i < SL_PER; ++i) {
+    const int e = i * NT + tid, qq = e >> 3;
+    const int gi = qq / SQ, q2 = qq - gi * SQ;
+    sr[i] = -1; swi[i] = 0; sdh[i] = 0;
+    if (e < SL_N && gi < G && q2 < nq) {
+      const int r = q2 / Ls;
+      sr[i] = r;
+      swi[i] = q2 - r * Ls - g.pw;
+      sdh[i] = ih0 + gi - g.ph;
+    }
+  }
+  // this lane's fragment rows: dz slot rows k = 32kk + 8g + 4hh + q; slab rows of tap iw = 0 for those slots (slots
+  // past R·Wo read row 0: their dz is zero).  Byte offsets include the lane's chunk (p>>1) and half (p&1).
+  const int gq = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
+  const int lane_col = (p >> 1) * 16 + (p & 1) * 8;
+  int sl_off[2][2];
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh) {
+      const int k = 32 * kk + 8 * gq + 4 * hh + q;
+      sl_off[kk][hh] = (k < used ? (k / g.Wo) * Ls + (k % g.Wo) * g.sw : 0) * RS + lane_col;
+    }
+  const int dz_off = (8 * gq + q) * RS + lane_col;
+  uint4_t rdz[DZ_PER], rsl[SL_PER];
+  auto load = [&](int c) {
+    const int rho0 = c * R;
+    const long m0 = (long)rho0 * g.Wo;
+    const int ho0 = rho0 % g.Ho, tn0 = rho0 / g.Ho, to0 = tn0 % g.To, n0 = tn0 / g.To;
+#pragma unroll
+    for (int i = 0; i < DZ_PER; ++i) {
+      const int e = i * NT + tid, j = e / (COT / 8), ch = e % (COT / 8);
+      const bool ok = e < DZ_N && j < used && m0 + j < M;
+      const uint4_t v = *(const uint4_t*)(dz + (ok ? (m0 + j) * Cout : 0) + cot * COT + ch * 8);
+      rdz[i] = ok ? v : uint4_t{0u, 0u, 0u, 0u};
+    }
+#pragma unroll
+    for (int i = 0; i < SL_PER; ++i) {
+      long off = -1;
+      if (sr[i] >= 0 && rho0 + sr[i] < rows_total) {
+        int ho = ho0 + sr[i], to = to0, n = n0;
+        while (ho >= g.Ho) {          // at most R / Ho + 1 wraps
+          ho -= g.Ho;
+          if (++to == g.To) { to = 0; ++n; }
+        }
+        const int ti = to * g.st - g.pt + it, hi = ho * g.sh + sdh[i], wi = swi[i];
+        if (ti >= 0 && ti < g.T && hi >= 0 && hi < g.H && wi >= 0 && wi < g.W)
+          off = ((((long)n * g.T + ti) * g.H + hi) * g.W + wi) * g.C + ct * 64 + ((i * NT + tid) & 7) * 8;
+      }
+      const uint4_t v = *(const uint4_t*)(x + (off >= 0 ? off : 0));
+      rsl[i] = off >= 0 ? v : uint4_t{0u, 0u, 0u, 0u};
+    }
+  };
+  auto store = [&](int buf) {
+    char* base = smem + buf * BUF;
+#pragma unroll
+    for (int i = 0; i < DZ_PER; ++i) {
+      const int e = i * NT + tid, j = e / (COT / 8), ch = e % (COT / 8);
+      if (e < DZ_N) *(uint4_t*)(base + (ch >> 3) * DZ_SUB + j * RS + (ch & 7) * 16) = rdz[i];
+    }
+#pragma unroll
+    for (int i = 0; i < SL_PER; ++i) {
+      const int e = i * NT + tid, qq = e >> 3, ch = e & 7;
+      if (e < SL_N) *(uint4_t*)(base + DZ_BYTES + qq * RS + ch * 16) = rsl[i];
+    }
+  };
+  floatx4 acc[NCB][NJ];
+#pragma unroll
+  for (int i = 0; i < NCB; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+  if (c_beg < c_end) {
+    load(c_beg);
+    store(0);
+  }
+  __syncthreads();
+  for (int c = c_beg; c < c_end; ++c) {
+    const int cur = (c - c_beg) & 1;
+    const bool more = c + 1 < c_end;
+    if (more) load(c + 1);
+    const char* dzs = smem + cur * BUF;
+    const char* sls = dzs + DZ_BYTES;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      bf16x8 af[NCB];
+#pragma unroll
+      for (int i = 0; i < NCB; ++i) {
+        const char* a = dzs + (i >> 2) * DZ_SUB + dz_off + 32 * kk * RS + (i & 3) * 32;
+        af[i] = frag_at(a, a + 4 * RS);
+      }
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const int cb = NJ * wave + j, gi = cb / 12, iw = (cb % 12) >> 2;
+        const int cofs = (gi * SQ + iw) * RS + (cb & 3) * 32;
+        const bf16x8 bf = frag_at(sls + sl_off[kk][0] + cofs, sls + sl_off[kk][1] + cofs);
+#pragma unroll
+        for (int i = 0; i < NCB; ++i) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bf, acc[i][j], 0, 0, 0);
+      }
+    }
+    if (more) store(cur ^ 1);
+    __syncthreads();
+  }
+  // partial dW of this split: rows co = cot·COT + 16i + 4(lane>>4) + r, columns k = ((it·kh + ih)·kw + iw)·C +
+  // ct·64 + 16(cb&3) + (lane&15)
+  float* o = out + (long)split * Cout * g.K;
+#pragma unroll
+  for (int i = 0; i < NCB; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int cb = NJ * wave + j, gi = cb / 12, iw = (cb % 12) >> 2;
+      const long col = ((long)(it * g.kh + ih0 + gi) * g.kw + iw) * g.C + ct * 64 + (cb & 3) * 16 + (lane & 15);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int co = cot * COT + 16 * i + 4 * (lane >> 4) + r;
+        o[(long)co * g.K + col] = acc[i][j][r];
+      }
+    }
+}
+
 // dW = Σ_z ws[z] in a fixed order (deterministic), 4 floats per thread.
 __global__ __launch_bounds__(256) void conv3d_wgrad_reduce(long n4, int splits, long slab, const float* __restrict__ ws,
                                                            float* __restrict__ dw) {
@@ -956,9 +1131,42 @@ static int wgrad_splits(const Geom& g, int Cout, int& mlen) {
   return (M + mlen - 1) / mlen;
 }
 
+// Row-slab weight-gradient plan (conv3d_wgrad_rows): kw = 3, whole output rows of <= 64 positions per chunk, the
+// chunk's input slab within MAXQ rows, Cout a multiple of 64.  Splits of the output-row chunks give ~2048 workgroups
+// (>= 4 chunks each); every split writes a full [Cout][K] partial (the kernel covers all K columns of its tiles).
+struct RowsPlan { int R, Ls, rows, cps, splits, cot, grp; };
+static bool rows_plan(const Geom& g, int Cout, RowsPlan& p) {
+  static const bool on = [] {
+    const char* v = getenv("CMHAR_WGRAD_ROWS");
+    return !(v && v[0] == '0');
+  }();
+  if (!on || g.kw != 3 || g.Wo > wr::SLOTS || Cout % 64 || g.C % 64) return false;
+  p.R = wr::SLOTS / g.Wo;
+  p.Ls = (g.Wo - 1) * g.sw + g.kw;
+  if (p.R * p.Ls > wr::MAXQ) return false;
+  p.rows = g.N * g.To * g.Ho;
+  p.cot = Cout % 128 == 0 ? 128 : 64;
+  // Cout = 64: three kh taps per workgroup when their slabs fit 64 rows each
+  // one kh tap per workgroup: three (the whole kh column, 576 dW columns per staged dz chunk) measured 4 % slower on
+  // the R3D-18 step — one workgroup per CU at 213 VGPRs, and a third of the workgroups to hide the gather latency
+  p.grp = 1;
+  const int nchunk = (p.rows + p.R - 1) / p.R;
+  const int tiles = g.kt * (g.kh / p.grp) * (g.C / 64) * (Cout / p.cot);
+  // ~2048 workgroups, >= 8 chunks each, and at most ~48 MB of fp32 partials (every split adds a Cout x K slab that
+  // is written here and read back by the reduce: at 2048 workgroups that was ~200 MB per conv, 1.7 ms per step)
+  int s = (2048 + tiles - 1) / tiles;
+  s = min(s, (int)((48L << 20) / ((long)Cout * g.K * 4)));
+  s = max(1, min(s, nchunk / 8));
+  p.cps = (nchunk + s - 1) / s;
+  p.splits = (nchunk + p.cps - 1) / p.cps;
+  return true;
+}
+
 extern "C" long cmhar_conv3d_wgrad_ws(const int* dims, int Cout) {
   const Geom g = make_geom(dims);
   if (!igemm_ok(g, Cout)) return -1;
+  RowsPlan rp;
+  if (rows_plan(g, Cout, rp)) return rp.splits > 1 ? (long)rp.splits * Cout * g.K : 0;
   int mlen;
   const int s = wgrad_splits(g, Cout, mlen);
   return s > 1 ? (long)s * Cout * g.K : 0;
@@ -969,6 +1177,25 @@ extern "C" int cmhar_conv3d_wgrad(const int* dims, int Cout, const void* x, cons
   const Geom g = make_geom(dims);
   if (!igemm_ok(g, Cout)) return -1;
   const int M = g.N * g.To * g.Ho * g.Wo;
+  RowsPlan rp;
+  if (rows_plan(g, Cout, rp)) {
+    if (rp.splits > 1 && !ws) return -2;
+    const int tiles = g.kt * (g.kh / rp.grp) * (g.C / 64) * (Cout / rp.cot);
+    float* dst = rp.splits > 1 ? ws : dw;
+    const dim3 grid(tiles, rp.splits);
+#define WR(COT, G, SQ, NW)                                                                                       \
+  conv3d_wgrad_rows<COT, G, SQ, NW><<<grid, 64 * NW, 0, stream>>>(g, Cout, rp.R, rp.Ls, rp.rows, rp.cps,          \
+                                                                  (const bf16*)x, (const bf16*)dz, dst)
+    if (rp.cot == 128) WR(128, 1, 136, 4);
+    else WR(64, 1, 136, 4);
+#undef WR
+    if (rp.splits > 1) {
+      const long slab = (long)Cout * g.K, n4 = slab / 4;
+      conv3d_wgrad_reduce<<<grid_for(n4), 256, 0, stream>>>(n4, rp.splits, slab, ws, dw);
+    }
+    CMHAR_CHECK_LAUNCH();
+    return 0;
+  }
   int mlen;
   const int s = wgrad_splits(g, Cout, mlen);
   if (s > 1 && !ws) return -2;

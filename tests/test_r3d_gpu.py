@@ -227,10 +227,15 @@ def test_crossmodal_with_r3d_backbone_steps():
 
 @pytest.mark.parametrize('cin,cout,k,s,p,shape', [(64, 64, 3, 1, 1, (3, 5, 9, 7)), (64, 128, 3, 2, 1, (2, 6, 11, 10)),
                                                   (64, 64, 3, 1, 1, (2, 12, 40, 38)),
-                                                  (128, 256, 1, 2, 0, (2, 4, 7, 9)), (192, 72, 3, 1, 1, (1, 3, 6, 5))])
+                                                  (128, 256, 1, 2, 0, (2, 4, 7, 9)), (192, 72, 3, 1, 1, (1, 3, 6, 5)),
+                                                  (128, 128, 3, 1, 1, (2, 4, 28, 28)), (64, 64, 3, 1, 1, (1, 4, 10, 56)),
+                                                  (256, 512, 3, 2, 1, (1, 4, 14, 14))])
 def test_conv3d_implicit_gemm_fwd_wgrad(cin, cout, k, s, p, shape):
     """Implicit-GEMM forward / weight gradient (bf16 operands, fp32 MFMA accumulation) vs F.conv3d in fp32 on the
-    same bf16-rounded operands: forward ≤ 5e-3 rel (bf16 output rounding), wgrad ≤ 1e-4 rel (fp32 output)."""
+    same bf16-rounded operands: forward ≤ 5e-3 rel (bf16 output rounding), wgrad ≤ 1e-4 rel (fp32 output).  The
+    k = 3 cases with Cout % 64 == 0 take the row-slab weight gradient (conv3d_wgrad_rows: whole output rows per chunk
+    — Wo = 7 / 38 / 56 / 28 give 9 / 1 / 1 / 2 rows per chunk, stride 2 slabs of 2·Wo + 1 positions, Cout tiles of
+    64 and 128, one and two 64-channel slices); 1x1x1 and Cout = 72 the generic gather kernel."""
     from cmhar import _lib as L
     from cmhar import kernels as K
     from cmhar import r3d
