@@ -877,6 +877,172 @@ __global__ __launch_bounds__(64 * NW, 2) void conv3d_wgrad_rows(Geom g, int Cout
     }
 }
 
+// ---- forward (and stride-1 input gradient) of the k x k x 3 convolutions from input row slabs -------------------
+// z[m, co] = Σ_(it, ih) Σ_iw Σ_c x[in(m, it, ih) + iw, c] · W[co, (it, ih, iw), c].  The generic kernel gathers one
+// tap's 128 input rows per K-step; here a 256-row tile of M stages, per (it, ih, 64-channel slice), the input row
+// segments of the output rows it touches ONCE (Ls = (Wo−1)·sw + 3 positions each) plus the three kw taps' weights,
+// and the kw taps become row shifts of the slab: a third of the input gather per FLOP.  4 waves, each 64 rows x 64
+// Cout of the tile (4 x 4 blocks of mfma_f32_16x16x32_bf16); LDS single-buffered with a register prefetch of the
+// next step (2 workgroups per CU); 128-row BatchNorm tile statistics as conv3d_fwd_igemm's.
+namespace fr {
+constexpr int TM = 256, TN = 64, NT = 256, SQ = 352, RS = 144;
+constexpr int SLAB = SQ * RS, WB = 3 * TN * RS;
+constexpr int SL_PER = (SQ * 8 + NT - 1) / NT, W_PER = 3 * TN * 8 / NT, ELD = TN + 4;
+constexpr int LDS = SLAB + WB + 2 * 64 * 4;   // + per-output-row table
+static_assert(TM * ELD * 4 <= SLAB + WB, "epilogue staging must fit the operand LDS");
+}  // namespace fr
+
+__global__ __launch_bounds__(256, 2) void conv3d_fwd_rows(Geom g, int M, int Cout, int Ls, const bf16* __restrict__ x,
+                                                          const bf16* __restrict__ Wt, const bf16* __restrict__ res,
+                                                          bf16* __restrict__ z, float* __restrict__ tstats) {
+  using namespace fr;
+  __shared__ __attribute__((aligned(16))) char smem[LDS];
+  char* const slab = smem;
+  char* const wl = smem + SLAB;
+  int* const tab = (int*)(smem + SLAB + WB);       // per output row r: [0][r] input-row base (position index),
+                                                   // [1][r] t0 | h0 << 16 (biased by 0x8000)
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tiles_n = Cout / TN, ntile = ((M + TM - 1) / TM) * tiles_n;
+  const int bid = xcd_remap(blockIdx.x, ntile);
+  const int bm = (bid / tiles_n) * TM, bn = (bid % tiles_n) * TN;
+  const int rho_first = bm / g.Wo, rho_last = (min(M, bm + TM) - 1) / g.Wo, nr = rho_last - rho_first + 1;
+  const int nq = nr * Ls;
+  if (tid < nr) {
+    const int rho = rho_first + tid;
+    const int ho = rho % g.Ho, tn = rho / g.Ho, to = tn % g.To, n = tn / g.To;
+    const int t0 = to * g.st - g.pt, h0 = ho * g.sh - g.ph;
+    tab[tid] = ((n * g.T + t0) * g.H + h0) * g.W - g.pw;   // position of (t0, h0, w = −pw); t0/h0 may be negative
+    tab[64 + tid] = (int)((unsigned)(t0 + 0x8000) | ((unsigned)(h0 + 0x8000) << 16));
+  }
+  // this thread's slab slots: (output row r, position) — fixed for the whole K loop
+  int spos[SL_PER];
+#pragma unroll
+  for (int i = 0; i < SL_PER; ++i) {
+    const int q = (i * NT + tid) >> 3;
+    spos[i] = -1;
+    if (q < nq) {
+      const int r = q / Ls;
+      spos[i] = (r << 8) | (q - r * Ls);
+    }
+  }
+  // A fragment rows of this lane (slots 64·wave + 16i + lane&15 → slab row of tap iw = 0)
+  int a_off[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int m = bm + 64 * wave + 16 * i + (lane & 15);
+    const int row = m < M ? (m / g.Wo - rho_first) * Ls + (m % g.Wo) * g.sw : 0;
+    a_off[i] = row * RS + (lane >> 4) * 16;
+  }
+  const int b_off = (lane & 15) * RS + (lane >> 4) * 16;
+  const int ncc = g.C / 64, nks = g.kt * g.kh * ncc;
+  uint4_t rsl[SL_PER], rw[W_PER];
+  __syncthreads();   // the row table
+  auto load = [&](int ks) {
+    const int cc = ks % ncc, tap = ks / ncc, ih = tap % g.kh, it = tap / g.kh;
+#pragma unroll
+    for (int i = 0; i < SL_PER; ++i) {
+      long off = -1;
+      if (spos[i] >= 0) {
+        const int r = spos[i] >> 8, pos = spos[i] & 255;
+        const unsigned th = (unsigned)tab[64 + r];
+        const int ti = (int)(th & 0xffffu) - 0x8000 + it, hi = (int)(th >> 16) - 0x8000 + ih, wi = pos - g.pw;
+        if (ti >= 0 && ti < g.T && hi >= 0 && hi < g.H && wi >= 0 && wi < g.W)
+          off = ((long)tab[r] + ((long)it * g.H + ih) * g.W + pos) * g.C + cc * 64 + ((i * NT + tid) & 7) * 8;
+      }
+      const uint4_t v = *(const uint4_t*)(x + (off >= 0 ? off : 0));
+      rsl[i] = off >= 0 ? v : uint4_t{0u, 0u, 0u, 0u};
+    }
+#pragma unroll
+    for (int i = 0; i < W_PER; ++i) {
+      const int e = i * NT + tid, iw = e >> 9, co = (e >> 3) & 63, ch = e & 7;
+      rw[i] = *(const uint4_t*)(Wt + (long)(bn + co) * g.Kp + ((it * g.kh + ih) * g.kw + iw) * g.C + cc * 64 + ch * 8);
+    }
+  };
+  auto store = [&]() {
+#pragma unroll
+    for (int i = 0; i < SL_PER; ++i) {
+      const int e = i * NT + tid, q = e >> 3, ch = e & 7;
+      if (q < SQ) *(uint4_t*)(slab + q * RS + ch * 16) = rsl[i];
+    }
+#pragma unroll
+    for (int i = 0; i < W_PER; ++i) {
+      const int e = i * NT + tid;
+      *(uint4_t*)(wl + (e >> 3) * RS + (e & 7) * 16) = rw[i];
+    }
+  };
+  floatx4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+  load(0);
+  store();
+  __syncthreads();
+  for (int ks = 0; ks < nks; ++ks) {
+    const bool more = ks + 1 < nks;
+    if (more) load(ks + 1);
+#pragma unroll
+    for (int iw = 0; iw < 3; ++iw)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        bf16x8 af[4], bfr[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) af[i] = *(const bf16x8*)(slab + a_off[i] + iw * RS + kk * 64);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) bfr[j] = *(const bf16x8*)(wl + (iw * TN + 16 * j) * RS + b_off + kk * 64);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+      }
+    __syncthreads();
+    if (more) store();
+    __syncthreads();
+  }
+  // epilogue: fp32 tile through LDS, 8-column bf16 vectors (+ residual), then the 128-row BatchNorm tile statistics
+  float* T = (float*)smem;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) T[(64 * wave + 16 * i + 4 * (lane >> 4) + r) * ELD + 16 * j + (lane & 15)] = acc[i][j][r];
+  __syncthreads();
+  const int cg = (tid & 7) * 8;
+  for (int rr = tid >> 3; rr < TM; rr += NT / 8) {
+    const int m = bm + rr;
+    if (m >= M) break;
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = T[rr * ELD + cg + j];
+    if (res) {
+      float q[8];
+      vload<bf16, 8>(res + (long)m * Cout + bn + cg, q);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] += q[j];
+    }
+    vstore<bf16, 8>(z + (long)m * Cout + bn + cg, v);
+  }
+  if (tstats) {
+    const int ntm = (M + 127) / 128;
+    for (int w = tid; w < 2 * TN; w += NT) {
+      const int half = w / TN, c = w % TN, r0 = half * 128, tm = bm / 128 + half;
+      const int rows = min(128, M - (bm + r0));
+      if (rows <= 0) continue;
+      float sum = 0.f;
+      for (int r = 0; r < rows; ++r) sum += (float)(bf16)T[(r0 + r) * ELD + c];
+      const float mu = sum / (float)rows;
+      float m2 = 0.f;
+      for (int r = 0; r < rows; ++r) {
+        const float d = (float)(bf16)T[(r0 + r) * ELD + c] - mu;
+        m2 = fmaf(d, d, m2);
+      }
+      tstats[(long)tm * Cout + bn + c] = mu;
+      tstats[((long)ntm + tm) * Cout + bn + c] = m2;
+    }
+  }
+}
+
 // dW = Σ_z ws[z] in a fixed order (deterministic), 4 floats per thread.
 __global__ __launch_bounds__(256) void conv3d_wgrad_reduce(long n4, int splits, long slab, const float* __restrict__ ws,
                                                            float* __restrict__ dw) {
@@ -1103,6 +1269,22 @@ extern "C" int cmhar_conv3d_fwd(const int* dims, int Cout, const void* x, const 
   const Geom g = make_geom(dims);
   if (!igemm_ok(g, Cout)) return -1;
   const int M = g.N * g.To * g.Ho * g.Wo;
+  // row-slab kernel: kw = 3, the input row segments of a 256-row tile's output rows within fr::SQ slab rows, whole
+  // 64-wide Cout tiles (CMHAR_FWD_ROWS=0: the generic gather kernel, A/B runs)
+  static const bool rows_on = [] {
+    const char* v = getenv("CMHAR_FWD_ROWS");
+    return !(v && v[0] == '0');
+  }();
+  const int Ls = (g.Wo - 1) * g.sw + g.kw;
+  const int max_rows = (fr::TM + g.Wo - 2) / g.Wo + 1;      // output rows a 256-row tile can touch
+  if (rows_on && g.kw == 3 && Cout % fr::TN == 0 && (long)max_rows * Ls <= fr::SQ && g.Wo <= 255 && Ls <= 255 &&
+      (long)g.N * g.T * g.H * g.W < (1L << 30)) {
+    const int tiles = ((M + fr::TM - 1) / fr::TM) * (Cout / fr::TN);
+    conv3d_fwd_rows<<<tiles, 256, 0, stream>>>(g, M, Cout, Ls, (const bf16*)x, (const bf16*)w, (const bf16*)res,
+                                               (bf16*)z, tile_stats);
+    CMHAR_CHECK_LAUNCH();
+    return 0;
+  }
   // Cout <= 64: 128x64 tiles (a 128-wide tile would leave half its MFMA work on padding columns)
   if (Cout <= 64) {
     const int tiles = (M + 127) / 128;
