@@ -885,23 +885,32 @@ __global__ __launch_bounds__(64 * NW, 2) void conv3d_wgrad_rows(Geom g, int Cout
 // Cout of the tile (4 x 4 blocks of mfma_f32_16x16x32_bf16); LDS single-buffered with a register prefetch of the
 // next step (2 workgroups per CU); 128-row BatchNorm tile statistics as conv3d_fwd_igemm's.
 namespace fr {
-constexpr int TM = 256, TN = 64, NT = 256, SQ = 352, RS = 144;
-constexpr int SLAB = SQ * RS, WB = 3 * TN * RS;
-constexpr int SL_PER = (SQ * 8 + NT - 1) / NT, W_PER = 3 * TN * 8 / NT, ELD = TN + 4;
-constexpr int LDS = SLAB + WB + 2 * 64 * 4;   // + per-output-row table
-static_assert(TM * ELD * 4 <= SLAB + WB, "epilogue staging must fit the operand LDS");
+constexpr int TN = 64, NT = 256, RS = 144;
+// TM = 256 (4 waves x 64 rows, all 64 Cout each) or 128 (2 x 2 waves of 64 rows x 32 Cout: twice the workgroups for
+// the small-M layers); SQ = slab rows for the output rows a tile can touch (1 + ⌈(TM−1)/Wo⌉ rows of Ls positions)
+template <int TM> struct Cfg {
+  static constexpr int WR = TM / 64, WC = 4 / WR, JB = 4 / WC, SQ = TM == 256 ? 352 : 184;
+  static constexpr int SLAB = SQ * RS, WB = 3 * TN * RS;
+  static constexpr int SL_PER = (SQ * 8 + NT - 1) / NT, W_PER = 3 * TN * 8 / NT, ELD = TN + 4;
+  static constexpr int LDS = SLAB + WB + 2 * 64 * 4;   // + per-output-row table
+  static_assert(TM * ELD * 4 <= SLAB + WB, "epilogue staging must fit the operand LDS");
+};
 }  // namespace fr
 
+template <int TM>
 __global__ __launch_bounds__(256, 2) void conv3d_fwd_rows(Geom g, int M, int Cout, int Ls, const bf16* __restrict__ x,
                                                           const bf16* __restrict__ Wt, const bf16* __restrict__ res,
                                                           bf16* __restrict__ z, float* __restrict__ tstats) {
   using namespace fr;
-  __shared__ __attribute__((aligned(16))) char smem[LDS];
+  typedef Cfg<TM> CF;
+  constexpr int SQ = CF::SQ, SLAB = CF::SLAB, WB = CF::WB, SL_PER = CF::SL_PER, W_PER = CF::W_PER, ELD = CF::ELD;
+  constexpr int JB = CF::JB;
+  __shared__ __attribute__((aligned(16))) char smem[CF::LDS];
   char* const slab = smem;
   char* const wl = smem + SLAB;
   int* const tab = (int*)(smem + SLAB + WB);       // per output row r: [0][r] input-row base (position index),
                                                    // [1][r] t0 | h0 << 16 (biased by 0x8000)
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, wr = wave / CF::WC, wc = wave % CF::WC;
   const int tiles_n = Cout / TN, ntile = ((M + TM - 1) / TM) * tiles_n;
   const int bid = xcd_remap(blockIdx.x, ntile);
   const int bm = (bid / tiles_n) * TM, bn = (bid % tiles_n) * TN;
@@ -929,7 +938,7 @@ __global__ __launch_bounds__(256, 2) void conv3d_fwd_rows(Geom g, int M, int Cou
   int a_off[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    const int m = bm + 64 * wave + 16 * i + (lane & 15);
+    const int m = bm + 64 * wr + 16 * i + (lane & 15);
     const int row = m < M ? (m / g.Wo - rho_first) * Ls + (m % g.Wo) * g.sw : 0;
     a_off[i] = row * RS + (lane >> 4) * 16;
   }
@@ -970,11 +979,11 @@ __global__ __launch_bounds__(256, 2) void conv3d_fwd_rows(Geom g, int M, int Cou
       *(uint4_t*)(wl + (e >> 3) * RS + (e & 7) * 16) = rw[i];
     }
   };
-  floatx4 acc[4][4];
+  floatx4 acc[4][JB];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < JB; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
   load(0);
   store();
   __syncthreads();
@@ -985,15 +994,16 @@ __global__ __launch_bounds__(256, 2) void conv3d_fwd_rows(Geom g, int M, int Cou
     for (int iw = 0; iw < 3; ++iw)
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk) {
-        bf16x8 af[4], bfr[4];
+        bf16x8 af[4], bfr[JB];
 #pragma unroll
         for (int i = 0; i < 4; ++i) af[i] = *(const bf16x8*)(slab + a_off[i] + iw * RS + kk * 64);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) bfr[j] = *(const bf16x8*)(wl + (iw * TN + 16 * j) * RS + b_off + kk * 64);
+        for (int j = 0; j < JB; ++j)
+          bfr[j] = *(const bf16x8*)(wl + (iw * TN + 16 * JB * wc + 16 * j) * RS + b_off + kk * 64);
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
-          for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+          for (int j = 0; j < JB; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
       }
     __syncthreads();
     if (more) store();
@@ -1004,9 +1014,10 @@ __global__ __launch_bounds__(256, 2) void conv3d_fwd_rows(Geom g, int M, int Cou
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
+    for (int j = 0; j < JB; ++j)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) T[(64 * wave + 16 * i + 4 * (lane >> 4) + r) * ELD + 16 * j + (lane & 15)] = acc[i][j][r];
+      for (int r = 0; r < 4; ++r)
+        T[(64 * wr + 16 * i + 4 * (lane >> 4) + r) * ELD + 16 * JB * wc + 16 * j + (lane & 15)] = acc[i][j][r];
   __syncthreads();
   const int cg = (tid & 7) * 8;
   for (int rr = tid >> 3; rr < TM; rr += NT / 8) {
@@ -1025,7 +1036,7 @@ __global__ __launch_bounds__(256, 2) void conv3d_fwd_rows(Geom g, int M, int Cou
   }
   if (tstats) {
     const int ntm = (M + 127) / 128;
-    for (int w = tid; w < 2 * TN; w += NT) {
+    for (int w = tid; w < (TM / 128) * TN; w += NT) {
       const int half = w / TN, c = w % TN, r0 = half * 128, tm = bm / 128 + half;
       const int rows = min(128, M - (bm + r0));
       if (rows <= 0) continue;
@@ -1276,14 +1287,23 @@ extern "C" int cmhar_conv3d_fwd(const int* dims, int Cout, const void* x, const 
     return !(v && v[0] == '0');
   }();
   const int Ls = (g.Wo - 1) * g.sw + g.kw;
-  const int max_rows = (fr::TM + g.Wo - 2) / g.Wo + 1;      // output rows a 256-row tile can touch
-  if (rows_on && g.kw == 3 && Cout % fr::TN == 0 && (long)max_rows * Ls <= fr::SQ && g.Wo <= 255 && Ls <= 255 &&
+  auto fits = [&](int tm, int sq) { return (long)((tm + g.Wo - 2) / g.Wo + 1) * Ls <= sq; };   // rows a tile touches
+  if (rows_on && g.kw == 3 && Cout % fr::TN == 0 && g.Wo <= 255 && Ls <= 255 &&
       (long)g.N * g.T * g.H * g.W < (1L << 30)) {
-    const int tiles = ((M + fr::TM - 1) / fr::TM) * (Cout / fr::TN);
-    conv3d_fwd_rows<<<tiles, 256, 0, stream>>>(g, M, Cout, Ls, (const bf16*)x, (const bf16*)w, (const bf16*)res,
-                                               (bf16*)z, tile_stats);
-    CMHAR_CHECK_LAUNCH();
-    return 0;
+    // 256-row tiles while they give every CU a workgroup, else 128-row tiles (R3D-18 layer 4: 268 -> 164 us; layer 3
+    // at 392 256-row tiles measured 167 vs 199 us, so it keeps them)
+    const long t256 = (long)((M + 255) / 256) * (Cout / fr::TN);
+    const bool small = t256 < 256 && fits(128, fr::Cfg<128>::SQ);
+    if (small || fits(256, fr::Cfg<256>::SQ)) {
+      if (small)
+        conv3d_fwd_rows<128><<<((M + 127) / 128) * (Cout / fr::TN), 256, 0, stream>>>(
+            g, M, Cout, Ls, (const bf16*)x, (const bf16*)w, (const bf16*)res, (bf16*)z, tile_stats);
+      else
+        conv3d_fwd_rows<256><<<(int)t256, 256, 0, stream>>>(g, M, Cout, Ls, (const bf16*)x, (const bf16*)w,
+                                                            (const bf16*)res, (bf16*)z, tile_stats);
+      CMHAR_CHECK_LAUNCH();
+      return 0;
+    }
   }
   // Cout <= 64: 128x64 tiles (a 128-wide tile would leave half its MFMA work on padding columns)
   if (Cout <= 64) {
