@@ -877,6 +877,149 @@ __global__ __launch_bounds__(64 * NW, 2) void conv3d_wgrad_rows(Geom g, int Cout
     }
 }
 
+// Cout = 64, stride-1 H/W variant: a workgroup owns one it, one 64-channel slice and ALL nine (ih, iw) taps (576 dW
+// columns, 12 waves x 3 column blocks), and a chunk is up to R = ⌊256 / Wo⌋ consecutive output rows of one frame:
+// output row r and tap ih read input row r + ih, so the chunk's R + 2 input row segments serve all 3·R (row, ih)
+// pairs (the one-tap-row kernel stages 3·R) and each staged dz row feeds 576 columns instead of 192 — 2.3x the
+// MFMA work per staged byte for R3D-18 layer 1 (R = 4).
+namespace wr3 {
+constexpr int SLOTS = 256, SQ = 352, NW = 12, NT = 64 * NW, RS = 144;
+constexpr int DZB = SLOTS * RS, SLB = SQ * RS;
+constexpr int DZ_N = SLOTS * 8, SL_N = SQ * 8, DZ_PER = (DZ_N + NT - 1) / NT, SL_PER = (SL_N + NT - 1) / NT;
+}  // namespace wr3
+
+__global__ __launch_bounds__(768, 1) void conv3d_wgrad_rows3(Geom g, int Cout, int R, int Ls, int cpf, int nchunk,
+                                                             int chunks_per_split, const bf16* __restrict__ x,
+                                                             const bf16* __restrict__ dz, float* __restrict__ out) {
+  using namespace wr3;
+  __shared__ __attribute__((aligned(16))) char smem[DZB + SLB];
+  char* const dzs = smem;
+  char* const sls = smem + DZB;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int nct = g.C / 64, ncot = Cout / 64, ntile = g.kt * nct * ncot;
+  const int lin = xcd_remap(blockIdx.x + ntile * blockIdx.y, ntile * gridDim.y);
+  const int split = lin / ntile;
+  int tl = lin % ntile;
+  const int cot = tl % ncot; tl /= ncot;
+  const int ct = tl % nct;
+  const int it = tl / nct;
+  const int c_beg = split * chunks_per_split, c_end = min(nchunk, c_beg + chunks_per_split);
+  // chunk-invariant slab slots: (input row u, position)
+  int su[SL_PER], sp[SL_PER];
+#pragma unroll
+  for (int i = 0; i < SL_PER; ++i) {
+    const int q = (i * NT + tid) >> 3;
+    su[i] = q / Ls;
+    sp[i] = q - su[i] * Ls - g.pw;
+  }
+  // fragment rows of this lane: slot k → (r, wo) → slab row r·Ls + wo (+ ih·Ls + iw per column block); slots past
+  // the chunk's rows read row 0 (their dz is zero)
+  const int gq = lane >> 4, q4 = (lane & 15) >> 2, p = lane & 3;
+  const int lane_col = (p >> 1) * 16 + (p & 1) * 8;
+  const int used_max = R * g.Wo;
+  int sl_off[8][2];
+#pragma unroll
+  for (int kk = 0; kk < 8; ++kk)
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh) {
+      const int k = 32 * kk + 8 * gq + 4 * hh + q4;
+      sl_off[kk][hh] = (k < used_max ? (k / g.Wo) * Ls + (k % g.Wo) : 0) * RS + lane_col;
+    }
+  const int dz_off = (8 * gq + q4) * RS + lane_col;
+  uint4_t rdz[DZ_PER], rsl[SL_PER];
+  auto load = [&](int c) {
+    const int f = c / cpf, ho0 = (c - f * cpf) * R, nr = min(R, g.Ho - ho0);
+    const int to = f % g.To, n = f / g.To;
+    const long m0 = ((long)f * g.Ho + ho0) * g.Wo;
+    const int used = nr * g.Wo;
+#pragma unroll
+    for (int i = 0; i < DZ_PER; ++i) {
+      const int e = i * NT + tid, j = e >> 3, ch = e & 7;
+      const bool ok = e < DZ_N && j < used;
+      const uint4_t v = *(const uint4_t*)(dz + (ok ? (m0 + j) * Cout : 0) + cot * 64 + ch * 8);
+      rdz[i] = ok ? v : uint4_t{0u, 0u, 0u, 0u};
+    }
+    const int ti = to * g.st - g.pt + it;
+    const bool tok = ti >= 0 && ti < g.T;
+#pragma unroll
+    for (int i = 0; i < SL_PER; ++i) {
+      const int hi = ho0 - g.ph + su[i], wi = sp[i];
+      long off = -1;
+      if (tok && su[i] < nr + 2 && hi >= 0 && hi < g.H && wi >= 0 && wi < g.W)
+        off = ((((long)n * g.T + ti) * g.H + hi) * g.W + wi) * g.C + ct * 64 + ((i * NT + tid) & 7) * 8;
+      const uint4_t v = *(const uint4_t*)(x + (off >= 0 ? off : 0));
+      rsl[i] = off >= 0 ? v : uint4_t{0u, 0u, 0u, 0u};
+    }
+  };
+  auto store = [&]() {
+#pragma unroll
+    for (int i = 0; i < DZ_PER; ++i) {
+      const int e = i * NT + tid;
+      if (e < DZ_N) *(uint4_t*)(dzs + (e >> 3) * RS + (e & 7) * 16) = rdz[i];
+    }
+#pragma unroll
+    for (int i = 0; i < SL_PER; ++i) {
+      const int e = i * NT + tid;
+      if (e < SL_N) *(uint4_t*)(sls + (e >> 3) * RS + (e & 7) * 16) = rsl[i];
+    }
+  };
+  floatx4 acc[4][3];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+  int cofs[3];
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    const int cb = 3 * wave + j, ih = cb / 12, iw = (cb % 12) >> 2;
+    cofs[j] = (ih * Ls + iw) * RS + (cb & 3) * 32;
+  }
+  if (c_beg < c_end) {
+    load(c_beg);
+    store();
+  }
+  __syncthreads();
+  for (int c = c_beg; c < c_end; ++c) {
+    const bool more = c + 1 < c_end;
+    const int kmax = (R * g.Wo + 31) / 32;   // 32-slot steps that can hold valid slots
+    if (more) load(c + 1);
+#pragma unroll
+    for (int kk = 0; kk < 8; ++kk) {
+      if (kk < kmax) {
+        bf16x8 af[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const char* a = dzs + dz_off + 32 * kk * RS + i * 32;
+          af[i] = wr::frag_at(a, a + 4 * RS);
+        }
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+          const bf16x8 bf = wr::frag_at(sls + sl_off[kk][0] + cofs[j], sls + sl_off[kk][1] + cofs[j]);
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bf, acc[i][j], 0, 0, 0);
+        }
+      }
+    }
+    __syncthreads();
+    if (more) store();
+    __syncthreads();
+  }
+  float* o = out + (long)split * Cout * g.K;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      const int cb = 3 * wave + j, ih = cb / 12, iw = (cb % 12) >> 2;
+      const long col = ((long)(it * g.kh + ih) * g.kw + iw) * g.C + ct * 64 + (cb & 3) * 16 + (lane & 15);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int co = cot * 64 + 16 * i + 4 * (lane >> 4) + r;
+        o[(long)co * g.K + col] = acc[i][j][r];
+      }
+    }
+}
+
 // ---- forward (and stride-1 input gradient) of the k x k x 3 convolutions from input row slabs -------------------
 // z[m, co] = Σ_(it, ih) Σ_iw Σ_c x[in(m, it, ih) + iw, c] · W[co, (it, ih, iw), c].  The generic kernel gathers one
 // tap's 128 input rows per K-step; here a 256-row tile of M stages, per (it, ih, 64-channel slice), the input row
@@ -1336,13 +1479,38 @@ static int wgrad_splits(const Geom& g, int Cout, int& mlen) {
 // Row-slab weight-gradient plan (conv3d_wgrad_rows): kw = 3, whole output rows of <= 64 positions per chunk, the
 // chunk's input slab within MAXQ rows, Cout a multiple of 64.  Splits of the output-row chunks give ~2048 workgroups
 // (>= 4 chunks each); every split writes a full [Cout][K] partial (the kernel covers all K columns of its tiles).
-struct RowsPlan { int R, Ls, rows, cps, splits, cot, grp; };
+struct RowsPlan { int R, Ls, rows, cps, splits, cot, grp, cpf, nchunk; };
 static bool rows_plan(const Geom& g, int Cout, RowsPlan& p) {
   static const bool on = [] {
     const char* v = getenv("CMHAR_WGRAD_ROWS");
     return !(v && v[0] == '0');
   }();
   if (!on || g.kw != 3 || g.Wo > wr::SLOTS || Cout % 64 || g.C % 64) return false;
+  static const bool nine = [] {   // CMHAR_WGRAD_ROWS3=0: one-tap-row kernel for the Cout = 64 shapes too (A/B runs)
+    const char* v = getenv("CMHAR_WGRAD_ROWS3");
+    return !(v && v[0] == '0');
+  }();
+  if (nine && Cout == 64 && g.kh == 3 && g.sh == 1 && g.sw == 1) {
+    const int R3 = wr3::SLOTS / g.Wo;
+    const int Ls3 = g.Wo - 1 + g.kw;
+    if ((min(R3, g.Ho) + 2) * Ls3 <= wr3::SQ) {
+      p.grp = 9;
+      p.cot = 64;
+      p.R = min(R3, g.Ho);
+      p.Ls = Ls3;
+      p.cpf = (g.Ho + p.R - 1) / p.R;
+      p.nchunk = g.N * g.To * p.cpf;
+      const int tiles = g.kt * (g.C / 64);
+      // one 12-wave workgroup per CU: ~2 rounds, >= 4 chunks each, <= ~80 MB of split partials
+      int s = (512 + tiles - 1) / tiles;
+      s = min(s, (int)((80L << 20) / ((long)Cout * g.K * 4)));
+      s = max(1, min(s, p.nchunk / 4));
+      p.cps = (p.nchunk + s - 1) / s;
+      p.splits = (p.nchunk + p.cps - 1) / p.cps;
+      p.rows = g.N * g.To * g.Ho;
+      return true;
+    }
+  }
   p.R = wr::SLOTS / g.Wo;
   p.Ls = (g.Wo - 1) * g.sw + g.kw;
   if (p.R * p.Ls > wr::MAXQ) return false;
@@ -1382,8 +1550,19 @@ extern "C" int cmhar_conv3d_wgrad(const int* dims, int Cout, const void* x, cons
   RowsPlan rp;
   if (rows_plan(g, Cout, rp)) {
     if (rp.splits > 1 && !ws) return -2;
-    const int tiles = g.kt * (g.kh / rp.grp) * (g.C / 64) * (Cout / rp.cot);
     float* dst = rp.splits > 1 ? ws : dw;
+    if (rp.grp == 9) {
+      const dim3 grid3(g.kt * (g.C / 64), rp.splits);
+      conv3d_wgrad_rows3<<<grid3, wr3::NT, 0, stream>>>(g, Cout, rp.R, rp.Ls, rp.cpf, rp.nchunk, rp.cps,
+                                                        (const bf16*)x, (const bf16*)dz, dst);
+      if (rp.splits > 1) {
+        const long slab = (long)Cout * g.K, n4 = slab / 4;
+        conv3d_wgrad_reduce<<<grid_for(n4), 256, 0, stream>>>(n4, rp.splits, slab, ws, dw);
+      }
+      CMHAR_CHECK_LAUNCH();
+      return 0;
+    }
+    const int tiles = g.kt * (g.kh / rp.grp) * (g.C / 64) * (Cout / rp.cot);
     const dim3 grid(tiles, rp.splits);
 #define WR(COT, G, SQ, NW)                                                                                       \
   conv3d_wgrad_rows<COT, G, SQ, NW><<<grid, 64 * NW, 0, stream>>>(g, Cout, rp.R, rp.Ls, rp.rows, rp.cps,          \
