@@ -164,12 +164,14 @@ def _bn_fwd(z, bn, res, relu, training):
     return y, sm, sr
 
 
-def _bn_fwd_tiles(z, bn, res, relu, tstats):
+def _bn_fwd_tiles(z, bn, res, relu, tstats, ntile):
+    """Training BatchNorm3d of a conv output whose per-tile statistics the conv epilogue wrote into `tstats`
+    (`ntile` tiles, layout of cmhar_conv3d_fwd_stats_floats)."""
     M, Cc = z.shape
     y = torch.empty_like(z)
     sm = torch.empty(Cc, dtype=torch.float32, device=z.device)
     sr = torch.empty(Cc, dtype=torch.float32, device=z.device)
-    call('cmhar_bn_cl_fwd_tiles', M, Cc, ptr(tstats), ptr(z), ptr(res), ptr(y), ptr(bn.weight), ptr(bn.bias),
+    call('cmhar_bn_cl_fwd_tiles', M, Cc, ntile, ptr(tstats), ptr(z), ptr(res), ptr(y), ptr(bn.weight), ptr(bn.bias),
          ptr(bn.running_mean), ptr(bn.running_var), ptr(sm), ptr(sr),
          bn_momentum(bn, True), bn.eps, int(relu), ptr(bn.num_batches_tracked),
          L.stream(z.device))
@@ -203,11 +205,12 @@ def _unit_fwd(x, shape, conv, bn, relu, training, save, res=None, wp=None, keep_
     tstats = None
     if igemm:
         col = None
+        dims = _dims(shape, conv, Kp)
         if training and bn.track_running_stats:      # BN statistics from the conv epilogue (no statistics pass)
-            ntile = (M + 127) // 128
-            tstats = K.workspace(2 * (ntile + (ntile + 63) // 64) * conv.out_channels, x.device)
-        call('cmhar_conv3d_fwd', _dims(shape, conv, Kp), conv.out_channels, ptr(x), ptr(wp), None, ptr(z),
-             ptr(tstats), L.stream(x.device))
+            ntile = L.lib().cmhar_conv3d_fwd_tiles(dims, conv.out_channels)
+            tstats = K.workspace(L.lib().cmhar_conv3d_fwd_stats_floats(dims, conv.out_channels), x.device)
+        call('cmhar_conv3d_fwd', dims, conv.out_channels, ptr(x), ptr(wp), None, ptr(z), ptr(tstats),
+             L.stream(x.device))
     elif _pointwise(conv, shape, Kp, M, rows):
         col = x.reshape(M, Kp)
         K.gemm(0, col, wp, z)
@@ -215,7 +218,7 @@ def _unit_fwd(x, shape, conv, bn, relu, training, save, res=None, wp=None, keep_
         col = _im2col(x, shape, conv, Kp, rows)
         K.gemm(0, col[:M], wp, z)
     if tstats is not None:
-        y, sm, sr = _bn_fwd_tiles(z, bn, res, relu, tstats)
+        y, sm, sr = _bn_fwd_tiles(z, bn, res, relu, tstats, ntile)
     else:
         y, sm, sr = _bn_fwd(z, bn, res, relu, training)
     u = None

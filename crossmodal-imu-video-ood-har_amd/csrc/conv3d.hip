@@ -247,20 +247,24 @@ __global__ __launch_bounds__(256) void bn_cl_final(int mode, long M, int C, int 
   }
 }
 
-// Combine per-tile (mean_t, M2_t) over the ntile row tiles of 128 rows (the last one ragged) with Chan's formula,
-// in a fixed order: mean = Σ n_t·mean_t / M,  M2 = Σ M2_t + n_t·(mean_t − mean)².  16 tile slots x 16 channels per
-// block.  Then rstd and the running statistics as bn_cl_final.
-// Level 1: one thread per (group of 64 tiles, channel) merges its tiles' (n, mean, M2) sequentially (Chan's update)
-// into the group's (mean, M2); out: [2][ngroup][C].
-__global__ __launch_bounds__(256) void bn_tile_group(long M, int C, int ntile, const float* __restrict__ ts,
-                                                     float* __restrict__ out) {
+// Combine per-tile (n_t, mean_t, M2_t) over the ntile row tiles written by a conv epilogue (their row counts n_t in
+// `cnt`: 128-row tiles for the generic / 256-row kernels, whole-output-row tiles for the nine-tap forward) with Chan's
+// formula, in a fixed order: mean = Σ n_t·mean_t / M,  M2 = Σ M2_t + n_t·(mean_t − mean)².  Then rstd and the
+// running statistics as bn_cl_final.  Statistics buffer: [2][ntile][C] tile (mean, M2) | [2][ngroup][C] group
+// partials | [ntile] tile counts | [ngroup] group counts (ngroup = ⌈ntile / 64⌉).
+// Level 1: one thread per (group of 64 tiles, channel) merges its tiles sequentially (Chan's update) into the
+// group's (mean, M2); channel 0's thread also writes the group's row count.
+__global__ __launch_bounds__(256) void bn_tile_group(int C, int ntile, const float* __restrict__ ts,
+                                                     const float* __restrict__ cnt, float* __restrict__ out,
+                                                     float* __restrict__ gcnt) {
   const int ngroup = (ntile + 63) / 64;
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= (long)ngroup * C) return;
   const int g = (int)(i / C), c = (int)(i % C);
   float n = 0.f, mu = 0.f, m2 = 0.f;
   for (int t = g * 64; t < min(ntile, g * 64 + 64); ++t) {
-    const float nt = (float)min(128L, M - 128L * t), mt = ts[(long)t * C + c];
+    const float nt = cnt[t], mt = ts[(long)t * C + c];
+    if (nt <= 0.f) continue;
     const float d = mt - mu, n2 = n + nt;
     mu = fmaf(d, nt / n2, mu);
     m2 += ts[((long)ntile + t) * C + c] + d * d * (n * nt / n2);
@@ -268,21 +272,22 @@ __global__ __launch_bounds__(256) void bn_tile_group(long M, int C, int ntile, c
   }
   out[(long)g * C + c] = mu;
   out[((long)ngroup + g) * C + c] = m2;
+  if (c == 0) gcnt[g] = n;
 }
 
-// Level 2 over the groups (rows_per: rows a group covers, the last one ragged).
-__global__ __launch_bounds__(256) void bn_tile_final(long M, int C, int ntile, long rows_per, const float* __restrict__ ts,
-                                                     float* __restrict__ mean, float* __restrict__ rstd,
-                                                     float* __restrict__ rmean, float* __restrict__ rvar,
-                                                     long long* __restrict__ nbt, float momentum, float eps) {
+// Level 2 over the groups (their row counts in gcnt).
+__global__ __launch_bounds__(256) void bn_tile_final(long M, int C, int ngroup, const float* __restrict__ ts,
+                                                     const float* __restrict__ gcnt, float* __restrict__ mean,
+                                                     float* __restrict__ rstd, float* __restrict__ rmean,
+                                                     float* __restrict__ rvar, long long* __restrict__ nbt,
+                                                     float momentum, float eps) {
   __shared__ float sh[256];
   __shared__ float smu[16];
   const int tid = threadIdx.x, cl = tid & 15, slot = tid >> 4;
   const int c = blockIdx.x * 16 + cl;
-  auto nrows = [&](int t) { return (float)min(rows_per, M - rows_per * t); };
   float a = 0.f;
   if (c < C)
-    for (int t = slot; t < ntile; t += 16) a = fmaf(nrows(t), ts[(long)t * C + c], a);
+    for (int t = slot; t < ngroup; t += 16) a = fmaf(gcnt[t], ts[(long)t * C + c], a);
   sh[tid] = a;
   __syncthreads();
   if (slot == 0) {
@@ -294,9 +299,9 @@ __global__ __launch_bounds__(256) void bn_tile_final(long M, int C, int ntile, l
   const float mu = smu[cl];
   float q = 0.f;
   if (c < C)
-    for (int t = slot; t < ntile; t += 16) {
+    for (int t = slot; t < ngroup; t += 16) {
       const float d = ts[(long)t * C + c] - mu;
-      q += ts[((long)ntile + t) * C + c] + nrows(t) * d * d;
+      q += ts[((long)ngroup + t) * C + c] + gcnt[t] * d * d;
     }
   __syncthreads();
   sh[tid] = q;
@@ -312,6 +317,11 @@ __global__ __launch_bounds__(256) void bn_tile_final(long M, int C, int ntile, l
     rvar[c] = (1.f - momentum) * rvar[c] + momentum * var * ((float)M / (float)(M > 1 ? M - 1 : 1));
   }
   if (nbt && c == 0) *nbt += 1;
+}
+
+// Row counts of the tile statistics: where a conv epilogue writes n_t (after the tile and group partials)
+__device__ __forceinline__ float* tile_counts(float* ts, int ntile, int C) {
+  return ts + 2L * (ntile + (ntile + 63) / 64) * C;
 }
 
 __global__ void bn_cl_eval_stats(int C, const float* __restrict__ rmean, const float* __restrict__ rvar, float eps,
@@ -625,6 +635,7 @@ __global__ __launch_bounds__(256, JN == 2 ? 3 : 2) void conv3d_fwd_igemm(Geom g,
       tstats[(long)tm * Cout + bn + c] = mu;
       tstats[((long)ntm + tm) * Cout + bn + c] = m2;
     }
+    if (tid == 0 && bn == 0) tile_counts(tstats, ntm, Cout)[tm] = (float)rows;
   }
 }
 
@@ -1193,7 +1204,156 @@ __global__ __launch_bounds__(256, 2) void conv3d_fwd_rows(Geom g, int M, int Cou
       }
       tstats[(long)tm * Cout + bn + c] = mu;
       tstats[((long)ntm + tm) * Cout + bn + c] = m2;
+      if (c == 0 && bn == 0) tile_counts(tstats, ntm, Cout)[tm] = (float)rows;
     }
+  }
+}
+
+// Cout = 64, stride-1 H/W forward with all nine (ih, iw) taps per staged slab: a tile is up to R = ⌊256 / Wo⌋
+// consecutive output rows of one frame; per (it, 64-channel slice) it stages the R + 2 input row segments its
+// rows read under any ih once, then the three kh taps' weights one after another (slab kept), so each staged input
+// byte feeds 3·3 taps instead of 3 (the 256-row kernel restages per ih).  Same 4-wave 64-slot x 64-Cout layout,
+// LDS image and register prefetch as conv3d_fwd_rows<256>; BatchNorm statistics per tile (its row count written).
+namespace fr3 {
+constexpr int SQ = 352, TN = 64, NT = 256, RS = 144;
+constexpr int SLAB = SQ * RS, WB = 3 * TN * RS, ELD = TN + 4;
+constexpr int SL_PER = (SQ * 8 + NT - 1) / NT, W_PER = 3 * TN * 8 / NT;
+static_assert(256 * ELD * 4 <= SLAB + WB, "epilogue staging must fit the operand LDS");
+}  // namespace fr3
+
+__global__ __launch_bounds__(256, 2) void conv3d_fwd_rows3(Geom g, int R, int Ls, int cpf, const bf16* __restrict__ x,
+                                                           const bf16* __restrict__ Wt, const bf16* __restrict__ res,
+                                                           bf16* __restrict__ z, float* __restrict__ tstats) {
+  using namespace fr3;
+  __shared__ __attribute__((aligned(16))) char smem[SLAB + WB];
+  char* const slab = smem;
+  char* const wl = smem + SLAB;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int ntile = gridDim.x;
+  const int t = xcd_remap(blockIdx.x, ntile);
+  const int f = t / cpf, ho0 = (t - f * cpf) * R, nr = min(R, g.Ho - ho0);
+  const int to = f % g.To, n = f / g.To;
+  const int used = nr * g.Wo;
+  const long m0 = ((long)f * g.Ho + ho0) * g.Wo;
+  const int nq = (nr + 2) * Ls;
+  // block-invariant slab slots: input row u (0..nr+1) and position
+  int su[SL_PER], sp[SL_PER];
+#pragma unroll
+  for (int i = 0; i < SL_PER; ++i) {
+    const int q = (i * NT + tid) >> 3;
+    su[i] = q < nq ? q / Ls : -1;
+    sp[i] = q < nq ? q - su[i] * Ls - g.pw : 0;
+  }
+  int a_off[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int k = 64 * wave + 16 * i + (lane & 15);
+    a_off[i] = (k < used ? (k / g.Wo) * Ls + (k % g.Wo) : 0) * RS + (lane >> 4) * 16;
+  }
+  const int b_off = (lane & 15) * RS + (lane >> 4) * 16;
+  const int ncc = g.C / 64, nst = g.kt * ncc * 3;
+  uint4_t rsl[SL_PER], rw[W_PER];
+  // stage s = (it, cc, ih), ih fastest; the slab changes with (it, cc), i.e. at ih = 0
+  auto load = [&](int st) {
+    const int ih = st % 3, cc = (st / 3) % ncc, it = st / (3 * ncc);
+    if (ih == 0) {
+      const int ti = to * g.st - g.pt + it;
+      const bool tok = ti >= 0 && ti < g.T;
+#pragma unroll
+      for (int i = 0; i < SL_PER; ++i) {
+        const int hi = ho0 - g.ph + su[i], wi = sp[i];
+        long off = -1;
+        if (tok && su[i] >= 0 && hi >= 0 && hi < g.H && wi >= 0 && wi < g.W)
+          off = ((((long)n * g.T + ti) * g.H + hi) * g.W + wi) * g.C + cc * 64 + ((i * NT + tid) & 7) * 8;
+        const uint4_t v = *(const uint4_t*)(x + (off >= 0 ? off : 0));
+        rsl[i] = off >= 0 ? v : uint4_t{0u, 0u, 0u, 0u};
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < W_PER; ++i) {
+      const int e = i * NT + tid, iw = e >> 9, co = (e >> 3) & 63, ch = e & 7;
+      rw[i] = *(const uint4_t*)(Wt + (long)co * g.Kp + ((it * g.kh + ih) * g.kw + iw) * g.C + cc * 64 + ch * 8);
+    }
+  };
+  auto store = [&](int st) {
+    if (st % 3 == 0) {
+#pragma unroll
+      for (int i = 0; i < SL_PER; ++i) {
+        const int e = i * NT + tid;
+        if ((e >> 3) < SQ) *(uint4_t*)(slab + (e >> 3) * RS + (e & 7) * 16) = rsl[i];
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < W_PER; ++i) {
+      const int e = i * NT + tid;
+      *(uint4_t*)(wl + (e >> 3) * RS + (e & 7) * 16) = rw[i];
+    }
+  };
+  floatx4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+  load(0);
+  store(0);
+  __syncthreads();
+  for (int st = 0; st < nst; ++st) {
+    const bool more = st + 1 < nst;
+    if (more) load(st + 1);
+    const int rofs = (st % 3) * Ls * RS;             // input row r + ih
+#pragma unroll
+    for (int iw = 0; iw < 3; ++iw)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        bf16x8 af[4], bfr[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) af[i] = *(const bf16x8*)(slab + a_off[i] + rofs + iw * RS + kk * 64);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) bfr[j] = *(const bf16x8*)(wl + (iw * TN + 16 * j) * RS + b_off + kk * 64);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+      }
+    __syncthreads();
+    if (more) store(st + 1);
+    __syncthreads();
+  }
+  float* T = (float*)smem;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) T[(64 * wave + 16 * i + 4 * (lane >> 4) + r) * ELD + 16 * j + (lane & 15)] = acc[i][j][r];
+  __syncthreads();
+  const int cg = (tid & 7) * 8;
+  for (int rr = tid >> 3; rr < used; rr += NT / 8) {
+    const long m = m0 + rr;
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = T[rr * ELD + cg + j];
+    if (res) {
+      float q[8];
+      vload<bf16, 8>(res + m * TN + cg, q);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] += q[j];
+    }
+    vstore<bf16, 8>(z + m * TN + cg, v);
+  }
+  if (tstats && tid < TN) {
+    const int c = tid;
+    float sum = 0.f;
+    for (int r = 0; r < used; ++r) sum += (float)(bf16)T[r * ELD + c];
+    const float mu = sum / (float)used;
+    float m2 = 0.f;
+    for (int r = 0; r < used; ++r) {
+      const float d = (float)(bf16)T[r * ELD + c] - mu;
+      m2 = fmaf(d, d, m2);
+    }
+    tstats[(long)t * TN + c] = mu;
+    tstats[((long)ntile + t) * TN + c] = m2;
+    if (c == 0) tile_counts(tstats, ntile, TN)[t] = (float)used;
   }
 }
 
@@ -1329,16 +1489,18 @@ extern "C" int cmhar_bn_cl_fwd(int dtype, long M, int C, const void* x, const vo
   return 0;
 }
 
-extern "C" int cmhar_bn_cl_fwd_tiles(long M, int C, float* tile_stats, const void* x, const void* res, void* y,
-                                     const float* w, const float* b, float* rmean, float* rvar, float* smean,
-                                     float* srstd, float momentum, float eps, int relu, long long* num_batches_tracked,
-                                     hipStream_t stream) {
-  if (M <= 0 || !bn_channels_ok(C) || !tile_stats) return -1;
+extern "C" int cmhar_bn_cl_fwd_tiles(long M, int C, int ntile, float* tile_stats, const void* x, const void* res,
+                                     void* y, const float* w, const float* b, float* rmean, float* rvar,
+                                     float* smean, float* srstd, float momentum, float eps, int relu,
+                                     long long* num_batches_tracked, hipStream_t stream) {
+  if (M <= 0 || !bn_channels_ok(C) || !tile_stats || ntile <= 0) return -1;
   if (M >= (1L << 31) || M * C / 8 >= (1L << 31)) return -2;   // unsigned grid-stride loops never wrap
-  const int ntile = (int)((M + 127) / 128), ngroup = (ntile + 63) / 64;
+  const int ngroup = (ntile + 63) / 64;
   float* groups = (float*)tile_stats + 2L * ntile * C;
-  bn_tile_group<<<cdiv((long)ngroup * C, 256), 256, 0, stream>>>(M, C, ntile, tile_stats, groups);
-  bn_tile_final<<<(C + 15) / 16, 256, 0, stream>>>(M, C, ngroup, 128L * 64, groups, smean, srstd, rmean, rvar,
+  const float* cnt = (float*)tile_stats + 2L * (ntile + ngroup) * C;
+  float* gcnt = (float*)cnt + ntile;
+  bn_tile_group<<<cdiv((long)ngroup * C, 256), 256, 0, stream>>>(C, ntile, tile_stats, cnt, groups, gcnt);
+  bn_tile_final<<<(C + 15) / 16, 256, 0, stream>>>(M, C, ngroup, groups, gcnt, smean, srstd, rmean, rvar,
                                                    num_batches_tracked, momentum, eps);
   const unsigned nvec = (unsigned)(M * C / 8);
   bn_cl_apply<bf16><<<grid_for(nvec), 256, 0, stream>>>(nvec, C, (const bf16*)x, (const bf16*)res, smean, srstd, w,
@@ -1418,11 +1580,55 @@ static bool igemm_ok(const Geom& g, int Cout) {
          (long)g.N * g.To * g.Ho * g.Wo < (1L << 31);
 }
 
+// Statistics tiles the forward plan writes (see cmhar_conv3d_fwd; all its kernels use 128-row tiles) and the floats
+// the caller provides for them: tile and group partials plus their row counts.
+// Nine-tap forward (conv3d_fwd_rows3) plan: Cout = 64, 3x3 taps at unit H/W stride, R + 2 input rows of a tile in
+// the slab.  CMHAR_FWD_ROWS3=0 turns it off (A/B runs).
+struct Fwd3Plan { int R, Ls, cpf, ntile; };
+static bool fwd3_plan(const Geom& g, int Cout, Fwd3Plan& p) {
+  static const bool on = [] {
+    const char* v = getenv("CMHAR_FWD_ROWS3");
+    return !(v && v[0] == '0');
+  }();
+  if (!on || Cout != fr3::TN || g.kh != 3 || g.kw != 3 || g.sh != 1 || g.sw != 1 || g.C % 64 || g.Wo > 256 ||
+      (long)g.N * g.T * g.H * g.W >= (1L << 30))
+    return false;
+  p.R = min(256 / g.Wo, g.Ho);
+  p.Ls = g.Wo - 1 + g.kw;
+  if ((p.R + 2) * p.Ls > fr3::SQ) return false;
+  p.cpf = (g.Ho + p.R - 1) / p.R;
+  p.ntile = g.N * g.To * p.cpf;
+  return true;
+}
+static int fwd_stat_tiles(const Geom& g, int M, int Cout) {
+  Fwd3Plan p;
+  if (fwd3_plan(g, Cout, p)) return p.ntile;
+  return (M + 127) / 128;
+}
+extern "C" int cmhar_conv3d_fwd_tiles(const int* dims, int Cout) {
+  const Geom g = make_geom(dims);
+  if (!igemm_ok(g, Cout)) return -1;
+  return fwd_stat_tiles(g, g.N * g.To * g.Ho * g.Wo, Cout);
+}
+extern "C" long cmhar_conv3d_fwd_stats_floats(const int* dims, int Cout) {
+  const int nt = cmhar_conv3d_fwd_tiles(dims, Cout);
+  if (nt <= 0) return -1;
+  const int ng = (nt + 63) / 64;
+  return 2L * (nt + ng) * Cout + nt + ng;
+}
+
 extern "C" int cmhar_conv3d_fwd(const int* dims, int Cout, const void* x, const void* w, const void* res, void* z,
                                 float* tile_stats, hipStream_t stream) {
   const Geom g = make_geom(dims);
   if (!igemm_ok(g, Cout)) return -1;
   const int M = g.N * g.To * g.Ho * g.Wo;
+  Fwd3Plan p3;
+  if (fwd3_plan(g, Cout, p3)) {
+    conv3d_fwd_rows3<<<p3.ntile, 256, 0, stream>>>(g, p3.R, p3.Ls, p3.cpf, (const bf16*)x, (const bf16*)w,
+                                                   (const bf16*)res, (bf16*)z, tile_stats);
+    CMHAR_CHECK_LAUNCH();
+    return 0;
+  }
   // row-slab kernel: kw = 3, the input row segments of a 256-row tile's output rows within fr::SQ slab rows, whole
   // 64-wide Cout tiles (CMHAR_FWD_ROWS=0: the generic gather kernel, A/B runs)
   static const bool rows_on = [] {

@@ -227,10 +227,14 @@ int cmhar_conv3d_im2col(int in_dtype, int out_dtype, const int* dims, const void
  * dzᵀ · col(x), split over M into ws (cmhar_conv3d_wgrad_ws floats; 0 = no workspace), reduced in a fixed order. */
 int cmhar_conv3d_fwd(const int* dims, int Cout, const void* x, const void* w, const void* res, void* z,
                      float* tile_stats, hipStream_t stream);
-/* tile_stats (nullable): 2·ceil(M/128)·Cout floats — per 128-row tile and channel, the mean and Σ(v − mean)² of the
- * bf16 outputs, consumed by cmhar_bn_cl_fwd_tiles (training-mode BatchNorm3d of z without a statistics pass), which
- * needs 2·(ntile + ceil(ntile/64))·C floats there (its group partials follow the tile partials). */
-int cmhar_bn_cl_fwd_tiles(long M, int C, float* tile_stats, const void* x, const void* res, void* y,
+/* tile_stats (nullable): per row tile of z and channel, the mean and Σ(v − mean)² of the bf16 outputs and each
+ * tile's row count, consumed by cmhar_bn_cl_fwd_tiles (training-mode BatchNorm3d of z without a statistics pass).
+ * cmhar_conv3d_fwd_tiles gives the tile count ntile of the forward's plan (-1: not an implicit-GEMM conv) and
+ * cmhar_conv3d_fwd_stats_floats the buffer size: [2][ntile][Cout] tile partials | [2][ngroup][Cout] group partials
+ * | [ntile] tile row counts | [ngroup] group row counts, ngroup = ceil(ntile/64). */
+int cmhar_conv3d_fwd_tiles(const int* dims, int Cout);
+long cmhar_conv3d_fwd_stats_floats(const int* dims, int Cout);
+int cmhar_bn_cl_fwd_tiles(long M, int C, int ntile, float* tile_stats, const void* x, const void* res, void* y,
                           const float* w, const float* b, float* rmean, float* rvar, float* smean, float* srstd,
                           float momentum, float eps, int relu, long long* num_batches_tracked, hipStream_t stream);
 long cmhar_conv3d_wgrad_ws(const int* dims, int Cout);

@@ -257,8 +257,8 @@ def test_conv3d_implicit_gemm_fwd_wgrad(cin, cout, k, s, p, shape):
     M = math.prod(osh[:4])
     z = torch.empty(M, cout, dtype=torch.bfloat16, device=DEV)
     dims = r3d._dims(shp, conv, Kp)
-    ntm = (M + 127) // 128
-    ts = torch.empty(2 * (ntm + (ntm + 63) // 64) * cout, device=DEV)
+    ntm = L.lib().cmhar_conv3d_fwd_tiles(dims, cout)
+    ts = torch.empty(L.lib().cmhar_conv3d_fwd_stats_floats(dims, cout), device=DEV)
     L.call('cmhar_conv3d_fwd', dims, cout, xc.data_ptr(), wp.data_ptr(), None, z.data_ptr(), ts.data_ptr(),
            L.stream(xc.device))
     got = z.float().reshape(osh).permute(0, 4, 1, 2, 3).cpu()
@@ -267,7 +267,7 @@ def test_conv3d_implicit_gemm_fwd_wgrad(cin, cout, k, s, p, shape):
     bn_a, bn_b = torch.nn.BatchNorm3d(cout).to(DEV), torch.nn.BatchNorm3d(cout).to(DEV)
     if cout % 8 == 0 and 256 % (cout // 8) == 0:
         ya, sma, sra = r3d._bn_fwd(z, bn_a, None, True, True)
-        yb, smb, srb = r3d._bn_fwd_tiles(z, bn_b, None, True, ts)
+        yb, smb, srb = r3d._bn_fwd_tiles(z, bn_b, None, True, ts, ntm)
         assert rel(smb, sma) < 1e-5 and rel(srb, sra) < 1e-5
         assert rel(bn_b.running_var, bn_a.running_var) < 1e-5 and int(bn_b.num_batches_tracked) == 1
         assert rel(yb.float(), ya.float()) < 1e-2
