@@ -40,12 +40,14 @@ def pmc_traffic(label, path=TRAFFIC_JSON):
         return None, None
     base, args = label.split('<', 1)
     code = {'true': 'Lb1E', 'false': 'Lb0E', 'bf16': 'DF16b', 'float': 'f'}
-    mangled = base + 'I' + ''.join(code[a.strip()] for a in args.rstrip('>').split(','))
+    codes = ''.join(code[a.strip()] for a in args.rstrip('>').split(','))
+    # the GEMM kernels take the MFMA number format E (bf16 on this path) as their first template argument
+    mangled = (base + 'I' + codes, base + 'IDF16b' + codes)
     with open(path) as f:
         doc = json.load(f)
     ks = doc['kernels']
     demangled = base + '<' + ', '.join(a.strip() for a in args.rstrip('>').split(','))   # rocprof demangles some
-    hits = [v for k, v in ks.items() if mangled in k or demangled in k]
+    hits = [v for k, v in ks.items() if any(mg in k for mg in mangled) or demangled in k]
     src = {'file': os.path.relpath(path, REPO), 'commit': doc.get('commit'), 'cmd': doc.get('cmd')}
     if not hits:
         return None, src
