@@ -385,13 +385,16 @@ extern "C" int cmhar_layernorm_fwd(int dtype, int M, int N, const void* a, long 
 }
 
 // Sum `rows` fp32 partial rows [rows][N] into out (alpha/beta), via a second partial level when rows is large.
-constexpr int CS_ROWS = 128;
-static long reduce_rows_ws(int rows, int N) { return rows > 32 ? (long)cdiv(rows, CS_ROWS) * N : 0; }
+// Partial-row reduction of per-block partial sums (a few hundred rows of N or 2N columns): chunks of >= 8 rows, at
+// most 64 of them, so the partial pass has ~(N/256)·64 workgroups instead of a handful of long row loops (the LN
+// backward's 512 x 1536 partials: 21 -> ~5 us per call).
+static int rr_chunks(int rows) { return std::min(64, cdiv(rows, 8)); }
+static long reduce_rows_ws(int rows, int N) { return rows > 32 ? (long)rr_chunks(rows) * N : 0; }
 static void reduce_rows(const float* part, int rows, int N, float* out, float alpha, float beta, float* scratch,
                         hipStream_t st) {
   if (rows > 32) {
-    const int chunks = cdiv(rows, CS_ROWS);
-    colsum_partial_kernel<float><<<dim3(cdiv(N, 64 * CS_VEC), chunks), 256, 0, st>>>(rows, N, part, N, CS_ROWS,
+    const int chunks = rr_chunks(rows), rpc = cdiv(rows, chunks);
+    colsum_partial_kernel<float><<<dim3(cdiv(N, 64 * CS_VEC), chunks), 256, 0, st>>>(rows, N, part, N, rpc,
                                                                                      scratch);
     colsum_final_kernel<<<cdiv(N, 64), 256, 0, st>>>(chunks, N, scratch, out, alpha, beta);
   } else {
@@ -403,9 +406,9 @@ static void reduce_rows(const float* part, int rows, int N, float* out, float al
 static void reduce_rows_gb(const float* part, int rows, int N, float* dgamma, float* dbeta, float beta,
                            float* scratch, hipStream_t st) {
   if (rows > 32) {
-    const int chunks = cdiv(rows, CS_ROWS);
+    const int chunks = rr_chunks(rows), rpc = cdiv(rows, chunks);
     colsum_partial_kernel<float><<<dim3(cdiv(2 * N, 64 * CS_VEC), chunks), 256, 0, st>>>(rows, 2 * N, part, 2 * N,
-                                                                                         CS_ROWS, scratch);
+                                                                                         rpc, scratch);
     colsum_final2_kernel<<<cdiv(2 * N, 64), 256, 0, st>>>(chunks, N, scratch, dgamma, dbeta, beta);
   } else {
     colsum_final2_kernel<<<cdiv(2 * N, 64), 256, 0, st>>>(rows, N, part, dgamma, dbeta, beta);
@@ -544,23 +547,25 @@ extern "C" int cmhar_layernorm_bwd(int dtype, int M, int N, const void* dy, long
   return 0;
 }
 
-constexpr int CS_CHUNK = 256;
+// rows per partial chunk: 256, or fewer for short columns (the IMU / head bias gradients, M = 13·batch rows) so the
+// partial pass still has up to 64 chunks of rows in flight
+static int cs_rows(int M) { return M >= 64 * 256 ? 256 : std::max(8, cdiv(M, 64)); }
 extern "C" long cmhar_colsum_ws(int M, int N) {
-  const int chunks = cdiv(M, CS_CHUNK);
+  const int chunks = cdiv(M, cs_rows(M));
   return (long)chunks * N + reduce_rows_ws(chunks, N);
 }
 
 extern "C" int cmhar_colsum(int dtype, int M, int N, const void* X, long ldx, float* out, float alpha, float beta,
                             float* ws, long ws_floats, hipStream_t st) {
   if (N <= 0) return 0;
-  const int chunks = cdiv(M, CS_CHUNK);
+  const int rpc = cs_rows(M), chunks = cdiv(M, rpc);
   if ((long)chunks * N + reduce_rows_ws(chunks, N) > ws_floats) return -2;
   if (M > 0) {
     dim3 grid(cdiv(N, 64 * CS_VEC), chunks);
     if (dtype == CMHAR_BF16)
-      colsum_partial_kernel<bf16><<<grid, 256, 0, st>>>(M, N, (const bf16*)X, ldx, CS_CHUNK, ws);
+      colsum_partial_kernel<bf16><<<grid, 256, 0, st>>>(M, N, (const bf16*)X, ldx, rpc, ws);
     else
-      colsum_partial_kernel<float><<<grid, 256, 0, st>>>(M, N, (const float*)X, ldx, CS_CHUNK, ws);
+      colsum_partial_kernel<float><<<grid, 256, 0, st>>>(M, N, (const float*)X, ldx, rpc, ws);
   }
   reduce_rows(ws, M > 0 ? chunks : 0, N, out, alpha, beta, ws + (long)chunks * N, st);
   CMHAR_CHECK_LAUNCH();
