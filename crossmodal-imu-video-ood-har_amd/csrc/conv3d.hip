@@ -251,18 +251,19 @@ __global__ __launch_bounds__(256) void bn_cl_final(int mode, long M, int C, int 
 // `cnt`: 128-row tiles for the generic / 256-row kernels, whole-output-row tiles for the nine-tap forward) with Chan's
 // formula, in a fixed order: mean = Σ n_t·mean_t / M,  M2 = Σ M2_t + n_t·(mean_t − mean)².  Then rstd and the
 // running statistics as bn_cl_final.  Statistics buffer: [2][ntile][C] tile (mean, M2) | [2][ngroup][C] group
-// partials | [ntile] tile counts | [ngroup] group counts (ngroup = ⌈ntile / 64⌉).
-// Level 1: one thread per (group of 64 tiles, channel) merges its tiles sequentially (Chan's update) into the
+// partials | [ntile] tile counts | [ngroup] group counts (ngroup = ⌈ntile / BN_TG⌉).
+// Level 1: one thread per (group of BN_TG tiles, channel) merges its tiles sequentially (Chan's update) into the
 // group's (mean, M2); channel 0's thread also writes the group's row count.
+constexpr int BN_TG = 16;   // tiles per level-1 group: short sequential chains, enough threads (64 measured 35 us/call)
 __global__ __launch_bounds__(256) void bn_tile_group(int C, int ntile, const float* __restrict__ ts,
                                                      const float* __restrict__ cnt, float* __restrict__ out,
                                                      float* __restrict__ gcnt) {
-  const int ngroup = (ntile + 63) / 64;
+  const int ngroup = (ntile + BN_TG - 1) / BN_TG;
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= (long)ngroup * C) return;
   const int g = (int)(i / C), c = (int)(i % C);
   float n = 0.f, mu = 0.f, m2 = 0.f;
-  for (int t = g * 64; t < min(ntile, g * 64 + 64); ++t) {
+  for (int t = g * BN_TG; t < min(ntile, (g + 1) * BN_TG); ++t) {
     const float nt = cnt[t], mt = ts[(long)t * C + c];
     if (nt <= 0.f) continue;
     const float d = mt - mu, n2 = n + nt;
@@ -321,7 +322,7 @@ __global__ __launch_bounds__(256) void bn_tile_final(long M, int C, int ngroup, 
 
 // Row counts of the tile statistics: where a conv epilogue writes n_t (after the tile and group partials)
 __device__ __forceinline__ float* tile_counts(float* ts, int ntile, int C) {
-  return ts + 2L * (ntile + (ntile + 63) / 64) * C;
+  return ts + 2L * (ntile + (ntile + BN_TG - 1) / BN_TG) * C;
 }
 
 __global__ void bn_cl_eval_stats(int C, const float* __restrict__ rmean, const float* __restrict__ rvar, float eps,
@@ -1495,7 +1496,7 @@ extern "C" int cmhar_bn_cl_fwd_tiles(long M, int C, int ntile, float* tile_stats
                                      long long* num_batches_tracked, hipStream_t stream) {
   if (M <= 0 || !bn_channels_ok(C) || !tile_stats || ntile <= 0) return -1;
   if (M >= (1L << 31) || M * C / 8 >= (1L << 31)) return -2;   // unsigned grid-stride loops never wrap
-  const int ngroup = (ntile + 63) / 64;
+  const int ngroup = (ntile + BN_TG - 1) / BN_TG;
   float* groups = (float*)tile_stats + 2L * ntile * C;
   const float* cnt = (float*)tile_stats + 2L * (ntile + ngroup) * C;
   float* gcnt = (float*)cnt + ntile;
@@ -1613,7 +1614,7 @@ extern "C" int cmhar_conv3d_fwd_tiles(const int* dims, int Cout) {
 extern "C" long cmhar_conv3d_fwd_stats_floats(const int* dims, int Cout) {
   const int nt = cmhar_conv3d_fwd_tiles(dims, Cout);
   if (nt <= 0) return -1;
-  const int ng = (nt + 63) / 64;
+  const int ng = (nt + BN_TG - 1) / BN_TG;
   return 2L * (nt + ng) * Cout + nt + ng;
 }
 

@@ -231,7 +231,7 @@ int cmhar_conv3d_fwd(const int* dims, int Cout, const void* x, const void* w, co
  * tile's row count, consumed by cmhar_bn_cl_fwd_tiles (training-mode BatchNorm3d of z without a statistics pass).
  * cmhar_conv3d_fwd_tiles gives the tile count ntile of the forward's plan (-1: not an implicit-GEMM conv) and
  * cmhar_conv3d_fwd_stats_floats the buffer size: [2][ntile][Cout] tile partials | [2][ngroup][Cout] group partials
- * | [ntile] tile row counts | [ngroup] group row counts, ngroup = ceil(ntile/64). */
+ * | [ntile] tile row counts | [ngroup] group row counts, ngroup = ceil(ntile/16). */
 int cmhar_conv3d_fwd_tiles(const int* dims, int Cout);
 long cmhar_conv3d_fwd_stats_floats(const int* dims, int Cout);
 int cmhar_bn_cl_fwd_tiles(long M, int C, int ntile, float* tile_stats, const void* x, const void* res, void* y,
