@@ -23,7 +23,7 @@ import torch.nn as nn
 from . import _lib as L
 from . import kernels as K
 from ._lib import call, ptr
-from .r3d import _bn_fwd, _dgrad_igemm_ok, _pack, _unit_bwd, _unit_fwd
+from .r3d import _bn_fwd, _dgrad_igemm_ok, _pack, _stem_ok, _unit_bwd, _unit_fwd
 
 RELU, RELU6 = 1, 2
 
@@ -231,7 +231,9 @@ def _frames_nhwc(video, dt):
 def _unit(units, xin, shp, conv2d, bn, relu, training, save, res=None):
     conv = _As3d(conv2d)
     wf = None
-    if save and xin.dtype == torch.bfloat16 and _dgrad_igemm_ok(conv) and shp[4] % 64 == 0:
+    if _stem_ok(xin, shp, conv):
+        wp = None                                   # _unit_fwd packs the implicit stem's own layout
+    elif save and xin.dtype == torch.bfloat16 and _dgrad_igemm_ok(conv) and shp[4] % 64 == 0:
         wp, wf = _pack(conv, xin.dtype, flip=True)
     else:
         wp = _pack(conv, xin.dtype)

@@ -129,6 +129,31 @@ def _pack(conv, dt, flip=False):
     return (wp, wf) if flip else wp
 
 
+def _stem_ok(x, shape, conv):
+    """Implicit stem kernel (cmhar_conv3d_stem_*): bf16, <= 4 input channels, kw <= 8 taps at w-stride 2, 64 outputs
+    (R3D-18's 3x7x7 (1,2,2) stem, ResNet-18's 7x7/2 stem run as (1, 7, 7))."""
+    if x.dtype != torch.bfloat16 or shape[4] > 4 or conv.out_channels != 64 or conv.kernel_size[2] > 8 or \
+            conv.stride[2] != 2:
+        return False
+    return L.lib().cmhar_conv3d_stem_tiles(_dims(shape, conv, _stem_kp(conv)), 64) > 0
+
+
+def _stem_kp(conv):
+    kt, kh, _ = conv.kernel_size
+    return kt * kh * 32
+
+
+def _pack_stem(conv):
+    """[64, C, kt, kh, kw] fp32 master → [64, kt·kh·32] bf16, element iw·4 + c of each (it, ih) tap row."""
+    w = conv.weight.detach()
+    if not w.is_contiguous():
+        w = w.contiguous()
+    co, ci, kt, kh, kw = w.shape
+    w4 = torch.empty(co, kt * kh * 32, dtype=torch.bfloat16, device=w.device)
+    call('cmhar_conv_pack_stem', co, ci, kt, kh, kw, ptr(w), ptr(w4), L.stream(w.device))
+    return w4
+
+
 def _pack_flip(conv, dt):
     w = conv.weight.detach().contiguous()
     co, ci, kt, kh, kw = w.shape
@@ -181,7 +206,7 @@ def _bn_fwd_tiles(z, bn, res, relu, tstats, ntile):
 class _Unit:
     """Forward state of one conv+BN unit (input, pre-BN output, BN output, batch statistics)."""
     __slots__ = ('conv', 'bn', 'relu', 'shape', 'oshape', 'x', 'z', 'y', 'sm', 'sr', 'Kp', 'rows', 'wp', 'col',
-                 'igemm', 'wf')
+                 'igemm', 'wf', 'stem')
 
 
 def _pointwise(conv, shape, Kp, M, rows):
@@ -201,9 +226,19 @@ def _unit_fwd(x, shape, conv, bn, relu, training, save, res=None, wp=None, keep_
     Kp = _r8(conv.weight[0].numel())
     rows = _r8(M) if x.dtype == torch.bfloat16 else M
     z = torch.empty(M, conv.out_channels, dtype=x.dtype, device=x.device)
-    igemm = _igemm_ok(x, shape, conv, Kp)
+    stem = _stem_ok(x, shape, conv)
+    igemm = not stem and _igemm_ok(x, shape, conv, Kp)
     tstats = None
-    if igemm:
+    if stem:
+        # implicit stem: no column matrix; the packed [64, kt·kh·32] weight replaces the im2col-order pack
+        col = None
+        wp = _pack_stem(conv)
+        dims = _dims(shape, conv, _stem_kp(conv))
+        if training and bn.track_running_stats:
+            ntile = L.lib().cmhar_conv3d_stem_tiles(dims, 64)
+            tstats = K.workspace(L.lib().cmhar_conv3d_stem_stats_floats(dims, 64), x.device)
+        call('cmhar_conv3d_stem_fwd', dims, 64, ptr(x), ptr(wp), ptr(z), ptr(tstats), L.stream(x.device))
+    elif igemm:
         col = None
         dims = _dims(shape, conv, Kp)
         if training and bn.track_running_stats:      # BN statistics from the conv epilogue (no statistics pass)
@@ -229,6 +264,7 @@ def _unit_fwd(x, shape, conv, bn, relu, training, save, res=None, wp=None, keep_
         u.col = col if keep_col else None
         u.igemm = igemm
         u.wf = wf
+        u.stem = stem
     return y, oshape, u
 
 
@@ -269,6 +305,22 @@ def _unit_bwd(u, dy, grads, training, need_dx, want_dres, dx_acc=None):
          L.stream(dy.device))
     grads[u.bn.weight] = dw_bn
     grads[u.bn.bias] = db_bn
+    w = u.conv.weight
+    if u.stem:
+        dims = _dims(u.shape, u.conv, _stem_kp(u.conv))
+        dw4 = torch.empty(Cc, _stem_kp(u.conv), dtype=torch.float32, device=dy.device)
+        ws = K.workspace(L.lib().cmhar_conv3d_stem_wgrad_ws(dims, Cc), dy.device)
+        call('cmhar_conv3d_stem_wgrad', dims, Cc, ptr(u.x), ptr(dz), ptr(dw4), ptr(ws), L.stream(dy.device))
+        _, ci, kt, kh, kw = w.shape
+        g5 = dw4.view(Cc, kt, kh, 8, 4)[:, :, :, :kw, :ci].permute(0, 4, 1, 2, 3)
+        p = getattr(u.conv, 'param', None)
+        if p is None:
+            grads[w] = g5
+        else:
+            grads[p] = g5.reshape(p.shape)
+        if need_dx:
+            raise RuntimeError('the implicit stem has no input gradient (its input is the video)')
+        return None, dres
     dwp = torch.empty(Cc, u.Kp, dtype=torch.float32, device=dy.device)
     if u.igemm:
         dims = _dims(u.shape, u.conv, u.Kp)
@@ -332,7 +384,9 @@ def _forward_impl(m: R3D18, video, training, save):
     def unit(xin, shp, seq, relu, res=None):
         conv, bn = seq[0], seq[1]
         wf = None
-        if save and dt == torch.bfloat16 and _dgrad_igemm_ok(conv) and shp[4] % 64 == 0:
+        if _stem_ok(xin, shp, conv):
+            wp = None                                # _unit_fwd packs the stem's own layout
+        elif save and dt == torch.bfloat16 and _dgrad_igemm_ok(conv) and shp[4] % 64 == 0:
             wp, wf = _pack(conv, dt, flip=True)      # the backward's flipped weight from the same pass
         else:
             wp = _pack(conv, dt)

@@ -1358,6 +1358,199 @@ __global__ __launch_bounds__(256, 2) void conv3d_fwd_rows3(Geom g, int R, int Ls
   }
 }
 
+// ---- implicit stem: few input channels (C <= 4), kw <= 8 taps at w-stride 2 (R3D-18's 3->64, 3x7x7, (1,2,2)) ----
+// The generic path materialises a 448-wide bf16 column matrix (1.44 GB at B = 32) and multiplies it.  Here each
+// (it, ih) tap row is ONE 32-wide K-step: an input row is staged in LDS as [position][4 channels] (8 B per position,
+// channel 3 and the row padding zero), so the kw·4 window of output column wo starts at byte 16·wo — a 16-B
+// aligned MFMA fragment read straight from the row (windows of neighbouring outputs overlap in LDS, no copy) — and
+// the weights are packed [co][(it, ih)][iw·4 + c] with zeros at c >= C and iw >= kw (so the fragment's k beyond the
+// window multiplies zero).  Tiles are up to R = ⌊256 / Wo⌋ output rows of one frame; per it the tile stages the
+// (R−1)·sh + kh input rows its (row, ih) pairs read.  Forward and weight gradient; BatchNorm tile statistics as the
+// row-slab kernels.
+namespace stm {
+constexpr int RB = 16 * 64 + 16;      // LDS bytes per staged input row (<= 127 positions x 8 B, + pad)
+constexpr int UMAX = 13, KHMAX = 8, WCO = 80;   // staged rows per tile, kh taps, weight row stride (64 B + pad)
+constexpr int ROWS_B = UMAX * RB, W_B = KHMAX * 64 * WCO, ELD = 68;
+constexpr int FWD_LDS = (ROWS_B + W_B) > 256 * ELD * 4 ? (ROWS_B + W_B) : 256 * ELD * 4;
+__device__ __forceinline__ bool ok(const Geom& g) { return g.C <= 4 && g.kw <= 8 && g.sw == 2 && g.kh <= KHMAX; }
+}  // namespace stm
+
+// Stage the tile's input rows for tap plane it: row u = input row ho0·sh − ph + u, positions p = 0..Lrow−1 ↔ input
+// column p − pw, 4 channels (zero past C and outside the image).  One position (8 B) per thread per step.
+__device__ __forceinline__ void stem_rows(const Geom& g, const bf16* __restrict__ x, int n, int ti, int ho0, int U,
+                                          int Lrow, char* lds, int tid, int nt) {
+  const bool tok = ti >= 0 && ti < g.T;
+  for (int e = tid; e < U * Lrow; e += nt) {
+    const int u = e / Lrow, pp = e - u * Lrow, hi = ho0 * g.sh - g.ph + u, wi = pp - g.pw;
+    short v[4] = {0, 0, 0, 0};
+    if (tok && hi >= 0 && hi < g.H && wi >= 0 && wi < g.W) {
+      const short* src = (const short*)(x + ((((long)n * g.T + ti) * g.H + hi) * g.W + wi) * g.C);
+      for (int c = 0; c < g.C; ++c) v[c] = src[c];
+    }
+    *(short4_t*)(lds + u * stm::RB + pp * 8) = short4_t{v[0], v[1], v[2], v[3]};
+  }
+}
+
+__global__ __launch_bounds__(256, 2) void conv3d_stem_fwd(Geom g, int R, int cpf, const bf16* __restrict__ x,
+                                                          const bf16* __restrict__ W4, bf16* __restrict__ z,
+                                                          float* __restrict__ tstats) {
+  using namespace stm;
+  __shared__ __attribute__((aligned(16))) char smem[FWD_LDS];
+  char* const rows = smem;
+  char* const wl = smem + ROWS_B;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int ntile = gridDim.x;
+  const int t = xcd_remap(blockIdx.x, ntile);
+  const int f = t / cpf, ho0 = (t - f * cpf) * R, nr = min(R, g.Ho - ho0);
+  const int to = f % g.To, n = f / g.To;
+  const int used = nr * g.Wo, U = (nr - 1) * g.sh + g.kh, Lrow = (g.Wo - 1) * g.sw + 8;
+  const long m0 = ((long)f * g.Ho + ho0) * g.Wo;
+  const int G = g.kh * 32;   // weight elements per (co, it)
+  int a_off[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int k = 64 * wave + 16 * i + (lane & 15);
+    a_off[i] = (k < used ? (k / g.Wo) * g.sh * RB + (k % g.Wo) * 16 : 0) + (lane >> 4) * 16;
+  }
+  const int b_off = (lane & 15) * WCO + (lane >> 4) * 16;
+  floatx4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+  for (int it = 0; it < g.kt; ++it) {
+    if (it) __syncthreads();      // the previous plane's reads are done
+    stem_rows(g, x, n, to * g.st - g.pt + it, ho0, U, Lrow, rows, tid, 256);
+    for (int e = tid; e < g.kh * 64 * 4; e += 256) {       // [ih][co][4 x 16 B]
+      const int ih = e >> 8, co = (e >> 2) & 63, q = e & 3;
+      *(uint4_t*)(wl + (ih * 64 + co) * WCO + q * 16) = *(const uint4_t*)(W4 + (long)co * g.kt * G + it * G + ih * 32 + q * 8);
+    }
+    __syncthreads();
+    for (int ih = 0; ih < g.kh; ++ih) {
+      bf16x8 af[4], bfr[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) af[i] = *(const bf16x8*)(rows + a_off[i] + ih * RB);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bfr[j] = *(const bf16x8*)(wl + (ih * 64 + 16 * j) * WCO + b_off);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+  }
+  __syncthreads();
+  float* T = (float*)smem;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) T[(64 * wave + 16 * i + 4 * (lane >> 4) + r) * ELD + 16 * j + (lane & 15)] = acc[i][j][r];
+  __syncthreads();
+  const int cg = (tid & 7) * 8;
+  for (int rr = tid >> 3; rr < used; rr += 32) {
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = T[rr * ELD + cg + j];
+    vstore<bf16, 8>(z + (m0 + rr) * 64 + cg, v);
+  }
+  if (tstats && tid < 64) {
+    const int c = tid;
+    float sum = 0.f;
+    for (int r = 0; r < used; ++r) sum += (float)(bf16)T[r * ELD + c];
+    const float mu = sum / (float)used;
+    float m2 = 0.f;
+    for (int r = 0; r < used; ++r) {
+      const float d = (float)(bf16)T[r * ELD + c] - mu;
+      m2 = fmaf(d, d, m2);
+    }
+    tstats[(long)t * 64 + c] = mu;
+    tstats[((long)ntile + t) * 64 + c] = m2;
+    if (c == 0) tile_counts(tstats, ntile, 64)[t] = (float)used;
+  }
+}
+
+// Weight gradient dW4[co][it][ih][iw·4 + c] = Σ_slots dz[slot][co] · window(slot, it, ih)[iw·4 + c]: workgroup =
+// (it, split of the tiles), wave = ih (2 column blocks of 16 x 4 Cout blocks); per tile it stages dz [256 slots][64]
+// and the tile's input rows for plane it, and reads the window columns transposed (rows = slots, 16 B apart).
+constexpr int STW_DZ = 256 * 144;
+__global__ __launch_bounds__(512, 1) void conv3d_stem_wgrad(Geom g, int R, int cpf, int ntile, int tiles_per_split,
+                                                            const bf16* __restrict__ x, const bf16* __restrict__ dz,
+                                                            float* __restrict__ out) {
+  using namespace stm;
+  __shared__ __attribute__((aligned(16))) char smem[STW_DZ + ROWS_B];
+  char* const dzs = smem;
+  char* const rows = smem + STW_DZ;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nt = blockDim.x;
+  const int it = blockIdx.x, split = blockIdx.y;
+  const int t_beg = split * tiles_per_split, t_end = min(ntile, t_beg + tiles_per_split);
+  const int Lrow = (g.Wo - 1) * g.sw + 8, G = g.kh * 32;
+  const int gq = lane >> 4, q4 = (lane & 15) >> 2, p = lane & 3;
+  const int lane_col = (p >> 1) * 16 + (p & 1) * 8;
+  const bool active = wave < g.kh;
+  floatx4 acc[4][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+  for (int t = t_beg; t < t_end; ++t) {
+    const int f = t / cpf, ho0 = (t - f * cpf) * R, nr = min(R, g.Ho - ho0);
+    const int to = f % g.To, n = f / g.To;
+    const int used = nr * g.Wo, U = (nr - 1) * g.sh + g.kh;
+    const long m0 = ((long)f * g.Ho + ho0) * g.Wo;
+    if (t > t_beg) __syncthreads();
+    for (int e = tid; e < 256 * 8; e += nt) {
+      const int j = e >> 3, ch = e & 7;
+      const bool okr = j < used;
+      const uint4_t v = *(const uint4_t*)(dz + (okr ? (m0 + j) * 64 : 0) + ch * 8);
+      *(uint4_t*)(dzs + j * 144 + ch * 16) = okr ? v : uint4_t{0u, 0u, 0u, 0u};
+    }
+    stem_rows(g, x, n, to * g.st - g.pt + it, ho0, U, Lrow, rows, tid, nt);
+    __syncthreads();
+    if (active) {
+      const int kmax = (used + 31) / 32;
+      for (int kk = 0; kk < kmax; ++kk) {
+        const int k_lo = 32 * kk + 8 * gq + q4, k_hi = k_lo + 4;
+        const int r_lo = k_lo < used ? (k_lo / g.Wo) * g.sh * RB + (k_lo % g.Wo) * 16 : 0;
+        const int r_hi = k_hi < used ? (k_hi / g.Wo) * g.sh * RB + (k_hi % g.Wo) * 16 : 0;
+        bf16x8 af[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const char* a = dzs + (32 * kk + 8 * gq + q4) * 144 + lane_col + i * 32;
+          af[i] = wr::frag_at(a, a + 4 * 144);
+        }
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const char* b = rows + wave * RB + lane_col + 32 * j;
+          const bf16x8 bf = wr::frag_at(b + r_lo, b + r_hi);
+#pragma unroll
+          for (int i = 0; i < 4; ++i) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bf, acc[i][j], 0, 0, 0);
+        }
+      }
+    }
+  }
+  if (!active) return;
+  float* o = out + (long)split * 64 * g.kt * G;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int co = 16 * i + 4 * (lane >> 4) + r;
+        o[(long)co * g.kt * G + it * G + wave * 32 + 16 * j + (lane & 15)] = acc[i][j][r];
+      }
+}
+
+// [Cout][C][kt][kh][kw] fp32 → [Cout][kt][kh][32] bf16 with element iw·4 + c (zero past kw / C)
+__global__ void stem_pack_kernel(int Cout, int C, int kt, int kh, int kw, const float* __restrict__ w,
+                                 bf16* __restrict__ out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x, G = kh * 32;
+  if (i >= Cout * kt * G) return;
+  const int co = i / (kt * G), r = i % (kt * G), it = r / G, ih = (r % G) / 32, e = r % 32, iw = e >> 2, c = e & 3;
+  out[i] = (iw < kw && c < C) ? (bf16)w[((((long)co * C + c) * kt + it) * kh + ih) * kw + iw] : (bf16)0.f;
+}
+
 // dW = Σ_z ws[z] in a fixed order (deterministic), 4 floats per thread.
 __global__ __launch_bounds__(256) void conv3d_wgrad_reduce(long n4, int splits, long slab, const float* __restrict__ ws,
                                                            float* __restrict__ dw) {
@@ -1665,6 +1858,75 @@ extern "C" int cmhar_conv3d_fwd(const int* dims, int Cout, const void* x, const 
     conv3d_fwd_igemm<4><<<tiles, 256, 0, stream>>>(g, M, Cout, (const bf16*)x, (const bf16*)w, (const bf16*)res,
                                                    (bf16*)z, tile_stats);
   }
+  CMHAR_CHECK_LAUNCH();
+  return 0;
+}
+
+// ---- implicit stem entry points (bf16, C <= 4, kw <= 8, w-stride 2, Cout = 64) ----
+struct StemPlan { int R, cpf, ntile; };
+static bool stem_plan(const Geom& g, int Cout, StemPlan& p) {
+  if (!geom_ok(g) || !(g.C <= 4 && g.kw <= 8 && g.sw == 2 && g.kh <= stm::KHMAX) || Cout != 64) return false;
+  // staged positions: every window column a fragment reads, iw = 0..7 (weights zero past kw), all written (zeros)
+  if ((g.Wo - 1) * g.sw + 8 > (stm::RB - 16) / 8 || g.Wo > 256) return false;
+  if ((long)g.N * g.T * g.H * g.W * g.C >= (1L << 31)) return false;
+  p.R = min(256 / g.Wo, g.Ho);
+  while (p.R > 1 && (p.R - 1) * g.sh + g.kh > stm::UMAX) --p.R;
+  if ((p.R - 1) * g.sh + g.kh > stm::UMAX) return false;
+  p.cpf = (g.Ho + p.R - 1) / p.R;
+  p.ntile = g.N * g.To * p.cpf;
+  return true;
+}
+extern "C" int cmhar_conv3d_stem_tiles(const int* dims, int Cout) {
+  StemPlan p;
+  return stem_plan(make_geom(dims), Cout, p) ? p.ntile : -1;
+}
+extern "C" long cmhar_conv3d_stem_stats_floats(const int* dims, int Cout) {
+  const int nt = cmhar_conv3d_stem_tiles(dims, Cout);
+  if (nt <= 0) return -1;
+  const int ng = (nt + BN_TG - 1) / BN_TG;
+  return 2L * (nt + ng) * Cout + nt + ng;
+}
+extern "C" int cmhar_conv_pack_stem(int Cout, int C, int kt, int kh, int kw, const float* w, void* out,
+                                    hipStream_t stream) {
+  if (Cout <= 0 || C <= 0 || C > 4 || kt <= 0 || kh <= 0 || kw <= 0 || kw > 8 || !w || !out) return -1;
+  const int n = Cout * kt * kh * 32;
+  stem_pack_kernel<<<cdiv(n, 256), 256, 0, stream>>>(Cout, C, kt, kh, kw, w, (bf16*)out);
+  CMHAR_CHECK_LAUNCH();
+  return 0;
+}
+extern "C" int cmhar_conv3d_stem_fwd(const int* dims, int Cout, const void* x, const void* w4, void* z,
+                                     float* tile_stats, hipStream_t stream) {
+  const Geom g = make_geom(dims);
+  StemPlan p;
+  if (!stem_plan(g, Cout, p)) return -1;
+  conv3d_stem_fwd<<<p.ntile, 256, 0, stream>>>(g, p.R, p.cpf, (const bf16*)x, (const bf16*)w4, (bf16*)z, tile_stats);
+  CMHAR_CHECK_LAUNCH();
+  return 0;
+}
+static int stem_splits(const Geom& g, const StemPlan& p, int& tps) {
+  int s = max(1, min((512 + g.kt - 1) / g.kt, p.ntile / 8));
+  tps = (p.ntile + s - 1) / s;
+  return (p.ntile + tps - 1) / tps;
+}
+extern "C" long cmhar_conv3d_stem_wgrad_ws(const int* dims, int Cout) {
+  const Geom g = make_geom(dims);
+  StemPlan p;
+  if (!stem_plan(g, Cout, p)) return -1;
+  int tps;
+  const int s = stem_splits(g, p, tps);
+  return (long)s * Cout * g.kt * g.kh * 32;
+}
+extern "C" int cmhar_conv3d_stem_wgrad(const int* dims, int Cout, const void* x, const void* dz, float* dw4, float* ws,
+                                       hipStream_t stream) {
+  const Geom g = make_geom(dims);
+  StemPlan p;
+  if (!stem_plan(g, Cout, p) || !ws || !dw4) return -1;
+  int tps;
+  const int s = stem_splits(g, p, tps);
+  conv3d_stem_wgrad<<<dim3(g.kt, s), 64 * stm::KHMAX, 0, stream>>>(g, p.R, p.cpf, p.ntile, tps, (const bf16*)x,
+                                                                  (const bf16*)dz, ws);
+  const long slab = (long)Cout * g.kt * g.kh * 32, n4 = slab / 4;
+  conv3d_wgrad_reduce<<<grid_for(n4), 256, 0, stream>>>(n4, s, slab, ws, dw4);
   CMHAR_CHECK_LAUNCH();
   return 0;
 }

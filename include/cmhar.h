@@ -237,6 +237,21 @@ long cmhar_conv3d_fwd_stats_floats(const int* dims, int Cout);
 int cmhar_bn_cl_fwd_tiles(long M, int C, int ntile, float* tile_stats, const void* x, const void* res, void* y,
                           const float* w, const float* b, float* rmean, float* rvar, float* smean, float* srstd,
                           float momentum, float eps, int relu, long long* num_batches_tracked, hipStream_t stream);
+/* Implicit stem convolution for few input channels (C <= 4), kw <= 8 at w-stride 2, Cout = 64 — R3D-18's BasicStem
+ * Conv3d(3, 64, (3,7,7), (1,2,2), (1,3,3)) and ResNet-18's 7x7/2 stem, replacing their im2col + GEMM (replaces: the
+ * stem nn.Conv3d / nn.Conv2d of torchvision r3d_18 / resnet18, models.py:160-216).  Weights packed by
+ * cmhar_conv_pack_stem as [Cout][kt][kh][32] bf16, element iw·4 + c (zero past kw / C); z = [M][64] bf16 with
+ * tile statistics as cmhar_conv3d_fwd's (sized by cmhar_conv3d_stem_tiles / cmhar_conv3d_stem_stats_floats; -1:
+ * geometry not supported); the weight gradient is written fp32 in the packed layout, with ws =
+ * cmhar_conv3d_stem_wgrad_ws floats. */
+int cmhar_conv3d_stem_tiles(const int* dims, int Cout);
+long cmhar_conv3d_stem_stats_floats(const int* dims, int Cout);
+int cmhar_conv_pack_stem(int Cout, int C, int kt, int kh, int kw, const float* w, void* out, hipStream_t stream);
+int cmhar_conv3d_stem_fwd(const int* dims, int Cout, const void* x, const void* w4, void* z, float* tile_stats,
+                          hipStream_t stream);
+long cmhar_conv3d_stem_wgrad_ws(const int* dims, int Cout);
+int cmhar_conv3d_stem_wgrad(const int* dims, int Cout, const void* x, const void* dz, float* dw4, float* ws,
+                            hipStream_t stream);
 long cmhar_conv3d_wgrad_ws(const int* dims, int Cout);
 int cmhar_conv3d_wgrad(const int* dims, int Cout, const void* x, const void* dz, float* dw, float* ws,
                        hipStream_t stream);

@@ -282,6 +282,60 @@ def test_conv3d_implicit_gemm_fwd_wgrad(cin, cout, k, s, p, shape):
     assert rel(dw, wq.grad) < 1e-4
 
 
+@pytest.mark.parametrize('cin,k,s,p,shape', [(3, (3, 7, 7), (1, 2, 2), (1, 3, 3), (1, 4, 112, 112)),
+                                             (3, (3, 7, 7), (1, 2, 2), (1, 3, 3), (2, 3, 30, 34)),
+                                             (3, (1, 7, 7), (1, 2, 2), (0, 3, 3), (2, 2, 40, 36)),
+                                             (2, (3, 5, 5), (2, 1, 2), (1, 2, 2), (1, 5, 20, 24)),
+                                             (4, (2, 3, 8), (1, 2, 2), (0, 1, 3), (2, 3, 11, 120))])
+def test_conv3d_implicit_stem_fwd_wgrad(cin, k, s, p, shape):
+    """Implicit stem (cmhar_conv3d_stem_*: C <= 4, kw <= 8 at w-stride 2, Cout = 64 — R3D-18's 3x7x7 (1,2,2) stem at
+    the production 112² frame, ragged row tiles, ResNet-18's 7x7/2 stem as (1,7,7), h-stride 1, kw = 8 at the widest
+    staged row) vs F.conv3d in fp32 on the same bf16-rounded operands: forward ≤ 5e-3 rel (bf16 output), epilogue
+    BatchNorm statistics ≤ 1e-5 vs the two-pass kernel, weight gradient ≤ 1e-4 rel (fp32 output)."""
+    from cmhar import _lib as L
+    from cmhar import kernels as K
+    from cmhar import r3d
+    torch.manual_seed(6)
+    N, T, H, W = shape
+    conv = torch.nn.Conv3d(cin, 64, k, s, p, bias=False)
+    x = torch.randn(N, cin, T, H, W).bfloat16().float().requires_grad_(True)
+    wq = conv.weight.detach().bfloat16().float().requires_grad_(True)
+    ref = F.conv3d(x, wq, stride=s, padding=p)
+    dz = torch.randn_like(ref).bfloat16().float()
+    ref.backward(dz)
+    conv = conv.to(DEV)
+    xc = x.detach().permute(0, 2, 3, 4, 1).contiguous().to(DEV).bfloat16()
+    shp = tuple(xc.shape)
+    assert r3d._stem_ok(xc, shp, conv)
+    w4 = r3d._pack_stem(conv)
+    osh = r3d._out_shape(shp, conv)
+    M = math.prod(osh[:4])
+    dims = r3d._dims(shp, conv, r3d._stem_kp(conv))
+    ntile = L.lib().cmhar_conv3d_stem_tiles(dims, 64)
+    ts = torch.empty(L.lib().cmhar_conv3d_stem_stats_floats(dims, 64), device=DEV)
+    z = torch.empty(M, 64, dtype=torch.bfloat16, device=DEV)
+    L.call('cmhar_conv3d_stem_fwd', dims, 64, xc.data_ptr(), w4.data_ptr(), z.data_ptr(), ts.data_ptr(),
+           L.stream(xc.device))
+    got = z.float().reshape(osh).permute(0, 4, 1, 2, 3).cpu()
+    assert rel(got, ref) < 5e-3
+    bn_a, bn_b = torch.nn.BatchNorm3d(64).to(DEV), torch.nn.BatchNorm3d(64).to(DEV)
+    ya, sma, sra = r3d._bn_fwd(z, bn_a, None, True, True)
+    yb, smb, srb = r3d._bn_fwd_tiles(z, bn_b, None, True, ts, ntile)
+    assert rel(smb, sma) < 1e-5 and rel(srb, sra) < 1e-5
+    assert rel(yb.float(), ya.float()) < 1e-2
+    dzc = dz.permute(0, 2, 3, 4, 1).reshape(M, 64).contiguous().to(DEV).bfloat16()
+    dw4 = torch.empty(64, r3d._stem_kp(conv), device=DEV)
+    ws = K.workspace(L.lib().cmhar_conv3d_stem_wgrad_ws(dims, 64), xc.device)
+    L.call('cmhar_conv3d_stem_wgrad', dims, 64, xc.data_ptr(), dzc.data_ptr(), dw4.data_ptr(), ws.data_ptr(),
+           L.stream(xc.device))
+    kt, kh, kw = k
+    dw = dw4.view(64, kt, kh, 8, 4)[:, :, :, :kw, :cin].permute(0, 4, 1, 2, 3).cpu()
+    assert rel(dw, wq.grad) < 1e-4
+    # the zero padding of the packed layout (iw >= kw, c >= C) carries no gradient into the parameter view
+    assert torch.equal(w4.view(64, kt, kh, 8, 4)[:, :, :, kw:, :].float().cpu(),
+                       torch.zeros(64, kt, kh, 8 - kw, 4))
+
+
 @pytest.mark.parametrize('cin,cout,shape,acc', [(64, 64, (2, 4, 9, 7), True), (128, 192, (1, 3, 5, 6), False)])
 def test_conv3d_implicit_gemm_dgrad(cin, cout, shape, acc):
     """Stride-1 input gradient as the flipped-weight implicit GEMM (+ the residual-branch gradient in its epilogue)
