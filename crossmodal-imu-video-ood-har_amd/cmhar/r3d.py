@@ -289,6 +289,17 @@ def _dgrad_igemm(dz, conv, oshape, x, dx_acc=None, wf=None):
     return dx
 
 
+def _store_wgrad(conv, src, rs, cs, grads):
+    """Packed fp32 weight gradient [Cout, Kp] → a contiguous gradient in the parameter's own layout (one HIP pass;
+    a strided view here would make autograd's gradient accumulation copy it with a torch kernel)."""
+    w = conv.weight
+    co, ci, kt, kh, kw = w.shape
+    p = getattr(conv, 'param', None)          # a 2-D conv run as (1, kh, kw): gradient in the parameter's shape
+    g = torch.empty(w.shape if p is None else p.shape, dtype=torch.float32, device=src.device)
+    call('cmhar_conv_grad_unpack', co, ci, kt * kh, kw, src.shape[1], rs, cs, ptr(src), ptr(g), L.stream(src.device))
+    grads[w if p is None else p] = g
+
+
 def _unit_bwd(u, dy, grads, training, need_dx, want_dres, dx_acc=None):
     """Returns (dx or None, dres or None); dx accumulates into dx_acc when given."""
     M, Cc = u.z.shape
@@ -311,13 +322,7 @@ def _unit_bwd(u, dy, grads, training, need_dx, want_dres, dx_acc=None):
         dw4 = torch.empty(Cc, _stem_kp(u.conv), dtype=torch.float32, device=dy.device)
         ws = K.workspace(L.lib().cmhar_conv3d_stem_wgrad_ws(dims, Cc), dy.device)
         call('cmhar_conv3d_stem_wgrad', dims, Cc, ptr(u.x), ptr(dz), ptr(dw4), ptr(ws), L.stream(dy.device))
-        _, ci, kt, kh, kw = w.shape
-        g5 = dw4.view(Cc, kt, kh, 8, 4)[:, :, :, :kw, :ci].permute(0, 4, 1, 2, 3)
-        p = getattr(u.conv, 'param', None)
-        if p is None:
-            grads[w] = g5
-        else:
-            grads[p] = g5.reshape(p.shape)
+        _store_wgrad(u.conv, dw4, 32, 4, grads)
         if need_dx:
             raise RuntimeError('the implicit stem has no input gradient (its input is the video)')
         return None, dres
@@ -338,14 +343,7 @@ def _unit_bwd(u, dy, grads, training, need_dx, want_dres, dx_acc=None):
             splits = max(1, min(1024 // tiles, u.rows // 4096))
         K.gemm(2, dz, col, dwp, splits=splits)
         del col
-    w = u.conv.weight
-    k = w[0].numel()
-    g5 = dwp[:, :k].reshape(Cc, w.shape[2], w.shape[3], w.shape[4], w.shape[1]).permute(0, 4, 1, 2, 3)
-    p = getattr(u.conv, 'param', None)          # a 2-D conv run as (1, kh, kw): gradient in the parameter's shape
-    if p is None:
-        grads[w] = g5
-    else:
-        grads[p] = g5.reshape(p.shape)
+    _store_wgrad(u.conv, dwp, w.shape[4] * w.shape[1], w.shape[1], grads)
     dx = None
     if need_dx and u.igemm and _dgrad_igemm_ok(u.conv):
         dx = _dgrad_igemm(dz, u.conv, u.oshape, u.x, dx_acc, u.wf)

@@ -284,22 +284,32 @@ inline int dw_chunks(long M) {   // ≤ 2048 chunks of ≥ 256 rows (≥ 8 block
 // contiguous run of CI_T·taps floats), then writes ci-contiguous segments of `out` and co-contiguous segments of
 // `outf` from it.
 constexpr int PACK_CO = 32, PACK_LDS = 12288;     // floats (48 KiB)
+// i / d for 0 <= i, i·d < 2^32 as one multiply-high (m = ⌈2^32 / d⌉, exact under that bound); the pack's index maps
+// had four runtime integer divisions per element and ran the step's 19 packs at ~0.5 TB/s.
+struct PackDiv {
+  unsigned d, m;
+  __device__ __forceinline__ int q(int i) const { return d == 1 ? i : (int)__umulhi((unsigned)i, m); }
+};
+inline PackDiv pack_div(int d) { return PackDiv{(unsigned)d, d == 1 ? 0u : (unsigned)((0x100000000ull + d - 1) / d)}; }
 template <typename T>
-__global__ __launch_bounds__(256) void conv_pack_kernel(int Cout, int Cin, int taps, int Kp, int ci_t,
+__global__ __launch_bounds__(256) void conv_pack_kernel(int Cout, int Cin, int taps, int Kp, int ci_t, PackDiv d_taps,
                                                         const float* __restrict__ w, T* __restrict__ out,
                                                         T* __restrict__ outf) {
   __shared__ float brick[PACK_LDS];
   const int co0 = blockIdx.x * PACK_CO, ci0 = blockIdx.y * ci_t;
   const int nco = min(PACK_CO, Cout - co0), nci = min(ci_t, Cin - ci0);
   const int run = nci * taps;                      // contiguous floats per co
+  const PackDiv d_run{(unsigned)run, run == 1 ? 0u : (unsigned)((0x100000000ull + run - 1) / run)};
+  const PackDiv d_nci{(unsigned)nci, nci == 1 ? 0u : (unsigned)((0x100000000ull + nci - 1) / nci)};
+  const PackDiv d_nco{(unsigned)nco, nco == 1 ? 0u : (unsigned)((0x100000000ull + nco - 1) / nco)};
   for (int i = threadIdx.x; i < nco * run; i += 256) {
-    const int c = i / run, e = i % run;
+    const int c = d_run.q(i), e = i - c * run;
     brick[c * run + e] = w[((long)(co0 + c) * Cin + ci0) * taps + e];
   }
   __syncthreads();
   if (out) {
     for (int i = threadIdx.x; i < nco * taps * nci; i += 256) {      // ci fastest
-      const int ci = i % nci, r = i / nci, tap = r % taps, c = r / taps;
+      const int r = d_nci.q(i), ci = i - r * nci, c = d_taps.q(r), tap = r - c * taps;
       out[(long)(co0 + c) * Kp + (long)tap * Cin + ci0 + ci] = from_f<T>(brick[c * run + ci * taps + tap]);
     }
     if (blockIdx.y == 0) {                          // zero padding k in [K, Kp)
@@ -310,10 +320,24 @@ __global__ __launch_bounds__(256) void conv_pack_kernel(int Cout, int Cin, int t
   }
   if (outf) {
     for (int i = threadIdx.x; i < nci * taps * nco; i += 256) {      // co fastest
-      const int c = i % nco, r = i / nco, tap = r % taps, ci = r / taps;
+      const int r = d_nco.q(i), c = i - r * nco, ci = d_taps.q(r), tap = r - ci * taps;
       outf[(long)(ci0 + ci) * taps * Cout + (long)(taps - 1 - tap) * Cout + co0 + c] =
           from_f<T>(brick[c * run + ci * taps + tap]);
     }
+  }
+}
+
+// Weight gradient [Cout][Kp] fp32 in a packed k order → the parameter layout [Cout][Cin][R][kw] (R = kt·kh tap rows):
+// source offset co·Kp + r·rs + iw·cs + ci (im2col order: rs = kw·Cin, cs = Cin; implicit stem: rs = 32, cs = 4).  One
+// thread per destination element, coalesced writes (replaces the strided-view copy torch's gradient accumulation made).
+__global__ __launch_bounds__(256) void conv_grad_unpack_kernel(unsigned n, int Cin, int R, int kw, int Kp, int rs,
+                                                               int cs, PackDiv d_kw, PackDiv d_R, PackDiv d_ci,
+                                                               const float* __restrict__ src, float* __restrict__ dst) {
+  for (unsigned i = blockIdx.x * 256u + threadIdx.x; i < n; i += gridDim.x * 256u) {
+    const int t = d_kw.q((int)i), iw = (int)i - t * kw;
+    const int t2 = d_R.q(t), r = t - t2 * R;
+    const int co = d_ci.q(t2), ci = t2 - co * Cin;
+    dst[i] = src[(long)co * Kp + (long)r * rs + iw * cs + ci];
   }
 }
 
@@ -423,9 +447,22 @@ extern "C" int cmhar_conv_pack_weight(int out_dtype, int Cout, int Cin, int kt, 
   if (PACK_CO * taps > PACK_LDS) return -1;
   const int ci_t = max(1, min(Cin, min(32, PACK_LDS / (PACK_CO * taps))));
   dim3 grid(cdiv(Cout, PACK_CO), cdiv(Cin, ci_t));
-#define F(T) conv_pack_kernel<T><<<grid, 256, 0, stream>>>(Cout, Cin, taps, Kp, ci_t, w, (T*)out, (T*)out_flip)
+#define F(T) conv_pack_kernel<T><<<grid, 256, 0, stream>>>(Cout, Cin, taps, Kp, ci_t, pack_div(taps), w, (T*)out, (T*)out_flip)
   DT_SWITCH(out_dtype, F);
 #undef F
+  CMHAR_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int cmhar_conv_grad_unpack(int Cout, int Cin, int R, int kw, int Kp, int rs, int cs, const float* src,
+                                      float* dst, hipStream_t stream) {
+  if (Cout <= 0 || Cin <= 0 || R <= 0 || kw <= 0 || rs <= 0 || cs <= 0 || !src || !dst) return -1;
+  if ((long)(R - 1) * rs + (long)(kw - 1) * cs + Cin > Kp) return -1;
+  const long n = (long)Cout * Cin * R * kw;
+  const long dmax = max(kw, max(R, Cin));
+  if (n * dmax >= (1L << 32)) return -2;       // PackDiv exactness bound
+  conv_grad_unpack_kernel<<<grid_for(n), 256, 0, stream>>>((unsigned)n, Cin, R, kw, Kp, rs, cs, pack_div(kw),
+                                                           pack_div(R), pack_div(Cin), src, dst);
   CMHAR_CHECK_LAUNCH();
   return 0;
 }

@@ -176,14 +176,7 @@ __global__ __launch_bounds__(256) void bn_cl_partial(int mode, int M, int C, int
     rs[j] = mode == 2 ? rstd[c0 + j] : 0.f;
     a0[j] = a1[j] = 0.f;
   }
-  for (int r = rs0; r < r1; r += RPI) {
-    const long off = (long)r * C + c0;
-    float v[8], gv[8], yv[8];
-    Vec8<T>::load(x + off, v);
-    if (mode == 2) {
-      Vec8<T>::load(dy + off, gv);
-      if (relu) Vec8<T>::load(y + off, yv);
-    }
+  auto accum = [&](const float* v, const float* gv, const float* yv) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       if (mode == 0) {
@@ -197,6 +190,34 @@ __global__ __launch_bounds__(256) void bn_cl_partial(int mode, int M, int C, int
         a1[j] = fmaf(gj, (v[j] - mu[j]) * rs[j], a1[j]);
       }
     }
+  };
+  // four row slots' loads in flight per thread (with 2–3 waves per SIMD one 16-B load per tensor left the kernel at
+  // ~1.5 TB/s), accumulated in the same sequential row order as the one-row tail loop
+  constexpr int UR = 4;
+  int r = rs0;
+  for (; r + (UR - 1) * RPI < r1; r += UR * RPI) {
+    float v[UR][8], gv[UR][8], yv[UR][8];
+#pragma unroll
+    for (int u = 0; u < UR; ++u) {
+      const long off = (long)(r + u * RPI) * C + c0;
+      Vec8<T>::load(x + off, v[u]);
+      if (mode == 2) {
+        Vec8<T>::load(dy + off, gv[u]);
+        if (relu) Vec8<T>::load(y + off, yv[u]);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < UR; ++u) accum(v[u], gv[u], yv[u]);
+  }
+  for (; r < r1; r += RPI) {
+    const long off = (long)r * C + c0;
+    float v[8], gv[8], yv[8];
+    Vec8<T>::load(x + off, v);
+    if (mode == 2) {
+      Vec8<T>::load(dy + off, gv);
+      if (relu) Vec8<T>::load(y + off, yv);
+    }
+    accum(v, gv, yv);
   }
 #pragma unroll
   for (int j = 0; j < 8; ++j) { s0[tid][j] = a0[j]; s1[tid][j] = a1[j]; }
@@ -209,19 +230,20 @@ __global__ __launch_bounds__(256) void bn_cl_partial(int mode, int M, int C, int
   }
 }
 
-// Combine the chunk partials (64 columns per block, 4 chunk slots, fixed order) and finish the statistic.
+// Combine the chunk partials (BN_FC columns per block, 256 / BN_FC chunk slots, fixed order) and finish the statistic.
 // mode 0: mean;  mode 1: rstd (+ running stats, num_batches_tracked);  mode 2: db = Σg, dw = Σg·x̂.
+constexpr int BN_FC = 8, BN_FS = 256 / BN_FC;
 __global__ __launch_bounds__(256) void bn_cl_final(int mode, long M, int C, int nchunk, const float* __restrict__ part,
                                                    float* __restrict__ mean, float* __restrict__ rstd,
                                                    float* __restrict__ rmean, float* __restrict__ rvar,
                                                    long long* __restrict__ nbt, float momentum, float eps,
                                                    float* __restrict__ dw, float* __restrict__ db) {
   __shared__ float s0[256], s1[256];
-  const int tid = threadIdx.x, cl = tid & 63, slot = tid >> 6;
-  const int c = blockIdx.x * 64 + cl;
+  const int tid = threadIdx.x, cl = tid % BN_FC, slot = tid / BN_FC;
+  const int c = blockIdx.x * BN_FC + cl;
   float a0 = 0.f, a1 = 0.f;
   if (c < C)
-    for (int k = slot; k < nchunk; k += 4) {
+    for (int k = slot; k < nchunk; k += BN_FS) {
       a0 += part[(long)k * C + c];
       if (mode == 2) a1 += part[((long)nchunk + k) * C + c];
     }
@@ -229,8 +251,11 @@ __global__ __launch_bounds__(256) void bn_cl_final(int mode, long M, int C, int 
   s1[tid] = a1;
   __syncthreads();
   if (slot || c >= C) return;
-  const float b0 = s0[cl] + s0[64 + cl] + s0[128 + cl] + s0[192 + cl];
-  const float b1 = s1[cl] + s1[64 + cl] + s1[128 + cl] + s1[192 + cl];
+  float b0 = 0.f, b1 = 0.f;
+  for (int s = 0; s < BN_FS; ++s) {
+    b0 += s0[s * BN_FC + cl];
+    b1 += s1[s * BN_FC + cl];
+  }
   if (mode == 0) {
     mean[c] = b0 / (float)M;
   } else if (mode == 1) {
@@ -1568,9 +1593,11 @@ inline int grid_for(long work) {
 
 inline bool bn_channels_ok(int C) { return C >= 8 && C % 8 == 0 && C <= 2048; }
 
-inline int bn_chunks(long M) {   // ≤ 512 chunks of ≥ 512 rows: enough blocks to stream M·C, few partials to combine
-  const long c = (M + 511) / 512;
-  return (int)(c < 512 ? (c > 0 ? c : 1) : 512);
+// ≤ 1024 chunks of ≥ 16 K elements per tensor: four blocks per CU stream the big R3D-18 layers (M·C = 103 M at
+// 16×56², where ≤ 512 chunks of ≥ 512 rows ran 1.5 TB/s), a few blocks the 7² layer-4 maps; few partials to combine
+inline int bn_chunks(long M, int C) {
+  const long c = (M * C + 16383) / 16384;
+  return (int)(c < 1024 ? (c > 0 ? c : 1) : 1024);
 }
 
 Geom make_geom(const int* dims) {
@@ -1645,7 +1672,7 @@ extern "C" int cmhar_conv3d_col2im(int dtype, const int* dims, const void* dcol,
   return 0;
 }
 
-extern "C" long cmhar_bn_cl_ws(long M, int C) { return 2L * bn_chunks(M) * C; }
+extern "C" long cmhar_bn_cl_ws(long M, int C) { return 2L * bn_chunks(M, C) * C; }
 
 extern "C" int cmhar_bn_cl_fwd(int dtype, long M, int C, const void* x, const void* res, void* y, const float* w,
                                const float* b, float* rmean, float* rvar, float* smean, float* srstd, int training,
@@ -1653,9 +1680,9 @@ extern "C" int cmhar_bn_cl_fwd(int dtype, long M, int C, const void* x, const vo
                                hipStream_t stream) {
   if (M <= 0 || !bn_channels_ok(C) || !ws) return -1;
   if (M >= (1L << 31) || M * C / 8 >= (1L << 31)) return -2;   // unsigned grid-stride loops never wrap
-  const int nch = bn_chunks(M);
+  const int nch = bn_chunks(M, C);
   const int rpc = (int)((M + nch - 1) / nch);
-  const int fgrid = (C + 63) / 64;
+  const int fgrid = (C + BN_FC - 1) / BN_FC;
   if (training) {
     for (int mode = 0; mode < 2; ++mode) {
       if (dtype == CMHAR_BF16)
@@ -1708,7 +1735,7 @@ extern "C" int cmhar_bn_cl_bwd(int dtype, long M, int C, const void* x, const vo
                                float* dw, float* db, int training, int relu, float* ws, hipStream_t stream) {
   if (M <= 0 || !bn_channels_ok(C) || !ws || !dw || !db) return -1;
   if (M >= (1L << 31) || M * C / 8 >= (1L << 31)) return -2;   // unsigned grid-stride loops never wrap
-  const int nch = bn_chunks(M);
+  const int nch = bn_chunks(M, C);
   const int rpc = (int)((M + nch - 1) / nch);
   if (dtype == CMHAR_BF16)
     bn_cl_partial<bf16><<<nch, 256, 0, stream>>>(2, (int)M, C, rpc, (const bf16*)x, (const bf16*)y, (const bf16*)dy,
@@ -1717,7 +1744,7 @@ extern "C" int cmhar_bn_cl_bwd(int dtype, long M, int C, const void* x, const vo
     bn_cl_partial<float><<<nch, 256, 0, stream>>>(2, (int)M, C, rpc, (const float*)x, (const float*)y, (const float*)dy,
                                                   smean, srstd, relu, ws);
   else return -1;
-  bn_cl_final<<<(C + 63) / 64, 256, 0, stream>>>(2, M, C, nch, ws, nullptr, nullptr, nullptr, nullptr, nullptr, 0.f,
+  bn_cl_final<<<(C + BN_FC - 1) / BN_FC, 256, 0, stream>>>(2, M, C, nch, ws, nullptr, nullptr, nullptr, nullptr, nullptr, 0.f,
                                                  0.f, dw, db);
   const unsigned nvec = (unsigned)(M * C / 8);
   if (dtype == CMHAR_BF16)

@@ -277,6 +277,12 @@ int cmhar_avgpool_cl_bwd(int dtype, int N, long S, int C, const float* dout, voi
  * gradient convolves dz with.  taps = kt·kh·kw ≤ 384. */
 int cmhar_conv_pack_weight(int out_dtype, int Cout, int Cin, int kt, int kh, int kw, int Kp, const float* w,
                            void* out, void* out_flip, hipStream_t stream);
+/* Weight gradient from a packed k order back to the parameter layout (replaces the strided-view copy autograd's
+ * gradient accumulation made of the conv weight gradient, torchvision conv weights [Cout, Cin, kt, kh, kw]):
+ * dst [Cout, Cin, R, kw] fp32 (R = kt·kh) from src [Cout, Kp] fp32 at co·Kp + r·rs + iw·cs + ci — im2col order
+ * rs = kw·Cin, cs = Cin; implicit stem rs = 32, cs = 4.  -2: Cout·Cin·R·kw too large. */
+int cmhar_conv_grad_unpack(int Cout, int Cin, int R, int kw, int Kp, int rs, int cs, const float* src, float* dst,
+                           hipStream_t stream);
 
 /* ---- per-frame 2-D CNN video backbones (replaces: torchvision resnet18 children[:-2] / mobilenet_v2 .features under
  * VideoEncoder, models.py:163-173,208-216).  Dense Conv2d = the conv3d entry points above with kt = 1; BatchNorm2d =
