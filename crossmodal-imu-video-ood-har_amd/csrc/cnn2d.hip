@@ -291,7 +291,9 @@ struct PackDiv {
   __device__ __forceinline__ int q(int i) const { return d == 1 ? i : (int)__umulhi((unsigned)i, m); }
 };
 inline PackDiv pack_div(int d) { return PackDiv{(unsigned)d, d == 1 ? 0u : (unsigned)((0x100000000ull + d - 1) / d)}; }
-template <typename T>
+// V8 (Cin, Cout, Kp and ci_t multiples of 8): each thread gathers 8 channels from the brick and writes them as one
+// 16-B vector (2-B scalar stores left the kernel store-issue bound).
+template <typename T, bool V8>
 __global__ __launch_bounds__(256) void conv_pack_kernel(int Cout, int Cin, int taps, int Kp, int ci_t, PackDiv d_taps,
                                                         const float* __restrict__ w, T* __restrict__ out,
                                                         T* __restrict__ outf) {
@@ -307,18 +309,42 @@ __global__ __launch_bounds__(256) void conv_pack_kernel(int Cout, int Cin, int t
     brick[c * run + e] = w[((long)(co0 + c) * Cin + ci0) * taps + e];
   }
   __syncthreads();
-  if (out) {
+  if (out && V8) {
+    const int n8 = nci >> 3;
+    const PackDiv d_n8{(unsigned)n8, n8 == 1 ? 0u : (unsigned)((0x100000000ull + n8 - 1) / n8)};
+    for (int i = threadIdx.x; i < nco * taps * n8; i += 256) {       // 8-channel groups, ci fastest
+      const int r = d_n8.q(i), g = i - r * n8, c = d_taps.q(r), tap = r - c * taps;
+      const float* src = brick + c * run + 8 * g * taps + tap;
+      float v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = src[j * taps];
+      Vec8<T>::store(out + (long)(co0 + c) * Kp + (long)tap * Cin + ci0 + 8 * g, v);
+    }
+  } else if (out) {
     for (int i = threadIdx.x; i < nco * taps * nci; i += 256) {      // ci fastest
       const int r = d_nci.q(i), ci = i - r * nci, c = d_taps.q(r), tap = r - c * taps;
       out[(long)(co0 + c) * Kp + (long)tap * Cin + ci0 + ci] = from_f<T>(brick[c * run + ci * taps + tap]);
     }
+  }
+  if (out) {
     if (blockIdx.y == 0) {                          // zero padding k in [K, Kp)
       const int K = taps * Cin, pad = Kp - K;
       for (int i = threadIdx.x; i < nco * pad; i += 256)
         out[(long)(co0 + i / pad) * Kp + K + i % pad] = from_f<T>(0.f);
     }
   }
-  if (outf) {
+  if (outf && V8) {
+    const int n8 = nco >> 3;
+    const PackDiv d_n8{(unsigned)n8, n8 == 1 ? 0u : (unsigned)((0x100000000ull + n8 - 1) / n8)};
+    for (int i = threadIdx.x; i < nci * taps * n8; i += 256) {       // 8-output groups, co fastest
+      const int r = d_n8.q(i), g = i - r * n8, ci = d_taps.q(r), tap = r - ci * taps;
+      const float* src = brick + 8 * g * run + ci * taps + tap;
+      float v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = src[j * run];
+      Vec8<T>::store(outf + (long)(ci0 + ci) * taps * Cout + (long)(taps - 1 - tap) * Cout + co0 + 8 * g, v);
+    }
+  } else if (outf) {
     for (int i = threadIdx.x; i < nci * taps * nco; i += 256) {      // co fastest
       const int r = d_nco.q(i), c = i - r * nco, ci = d_taps.q(r), tap = r - ci * taps;
       outf[(long)(ci0 + ci) * taps * Cout + (long)(taps - 1 - tap) * Cout + co0 + c] =
@@ -445,9 +471,17 @@ extern "C" int cmhar_conv_pack_weight(int out_dtype, int Cout, int Cin, int kt, 
   const int taps = kt * kh * kw;
   if (out && Kp < taps * Cin) return -1;
   if (PACK_CO * taps > PACK_LDS) return -1;
-  const int ci_t = max(1, min(Cin, min(32, PACK_LDS / (PACK_CO * taps))));
+  int ci_t = max(1, min(Cin, min(32, PACK_LDS / (PACK_CO * taps))));
+  const bool v8 = Cin % 8 == 0 && Cout % 8 == 0 && (!out || Kp % 8 == 0) && ci_t >= 8;
+  if (v8) ci_t &= ~7;
   dim3 grid(cdiv(Cout, PACK_CO), cdiv(Cin, ci_t));
-#define F(T) conv_pack_kernel<T><<<grid, 256, 0, stream>>>(Cout, Cin, taps, Kp, ci_t, pack_div(taps), w, (T*)out, (T*)out_flip)
+#define F(T)                                                                                                       \
+  if (v8)                                                                                                          \
+    conv_pack_kernel<T, true><<<grid, 256, 0, stream>>>(Cout, Cin, taps, Kp, ci_t, pack_div(taps), w, (T*)out,     \
+                                                        (T*)out_flip);                                             \
+  else                                                                                                             \
+    conv_pack_kernel<T, false><<<grid, 256, 0, stream>>>(Cout, Cin, taps, Kp, ci_t, pack_div(taps), w, (T*)out,    \
+                                                         (T*)out_flip)
   DT_SWITCH(out_dtype, F);
 #undef F
   CMHAR_CHECK_LAUNCH();

@@ -1,6 +1,6 @@
 """How much of the bench step the IMU branch costs: step time with the IMU branch on its side stream (product),
 on the main stream, and replaced by a zero-cost stub (a learnable (B, 128) feature; the video branch unchanged).
-    python tools/debug/imu_cost.py"""
+    python tools/debug/imu_cost.py [r3d_18]     (r3d_18: the config-2 step, R3D-18 at 16x112^2)"""
 import os
 import sys
 import time
@@ -20,14 +20,21 @@ def main():
     dev = torch.device('cuda')
     cfg = Config()
     cfg.model.allow_random_init = True
+    r3d = 'r3d_18' in sys.argv[1:]
+    S = 224
+    if r3d:
+        cfg.model.video_backbone = 'r3d_18'
+        cfg.data.video_resize = (112, 112)
+        S = 112
     torch.manual_seed(0)
     with warnings.catch_warnings():
         warnings.simplefilter('ignore')
         model = CrossModalModel(cfg).to(dev).train()
     lf = SigmoidContrastiveLoss().to(dev)
-    opt = FusedAdamW(model.parameters(), lr=1e-5, weight_decay=0.01, shadow_sources=[model.video_encoder.backbone])
+    opt = FusedAdamW(model.parameters(), lr=1e-5, weight_decay=0.01,
+                     shadow_sources=[] if r3d else [model.video_encoder.backbone])
     B = 32
-    video = torch.randn(B, 16, 3, 224, 224, device=dev)
+    video = torch.randn(B, 16, 3, S, S, device=dev)
     imu = torch.randn(B, 6, 200, device=dev)
     params = list(model.parameters())
     stub = torch.nn.Parameter(torch.randn(B, 128, device=dev))
