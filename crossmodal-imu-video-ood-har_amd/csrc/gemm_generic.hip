@@ -17,8 +17,9 @@ constexpr int TM = 64, TN = 64, TK = 32, NTH = 256;   // default tile; T = 32 fo
 // The GEMMs this kernel serves are small (tens of blocks) with K up to a few thousand, so a K-step is bounded by
 // memory LATENCY, not bandwidth: tile k+1 is loaded into registers while tile k is consumed from LDS (double-
 // buffered LDS, one barrier per K-step), so each step pays compute + one overlapped fetch.
-template <typename TIn, int T>
+template <typename TIn, int T, int KT = TK>
 struct GenStage {
+  static constexpr int TK = KT;
   static constexpr int PER = T * TK / NTH;      // A and B elements staged per thread per K-tile
   float a[PER], b[PER];
   __device__ __forceinline__ void load(const TIn* __restrict__ A, long sam, long sak, const TIn* __restrict__ B,
@@ -53,11 +54,13 @@ struct GenStage {
 // T x T output tile, 16 x 16 threads with (T/16)² outputs each.  Every output is one fmaf chain over k = 0..K-1 in
 // order whatever T is, so the two tile sizes give bit-identical results (T = 32 quadruples the workgroups of the
 // IMU encoder's few-tile GEMMs and quarters each one's K-loop FMA count).
-template <typename TIn, typename TOut, int T = TM>
+// KT: K-tile.  The IMU encoder's few-tile GEMMs (T = 32) take KT = 128 when K >= 128: their K-steps are bound by
+// the global-load latency, so four times the k per step quarters the exposed latencies (same per-output fmaf chain).
+template <typename TIn, typename TOut, int T = TM, int KT = TK>
 __global__ __launch_bounds__(NTH) void gemm_generic_kernel(
     int M, int N, int K, const TIn* __restrict__ A, long sam, long sak, long sAb, const TIn* __restrict__ B,
     long sbk, long sbn, long sBb, TOut* __restrict__ C, long ldc, long sCb, Epilogue e) {
-  constexpr int R = T / 16;
+  constexpr int R = T / 16, TK = KT;
   __shared__ float As[2][TK][T + 4];
   __shared__ float Bs[2][TK][T + 4];
   const int tid = threadIdx.x;
@@ -68,7 +71,7 @@ __global__ __launch_bounds__(NTH) void gemm_generic_kernel(
   const int tr = tid / 16, tc = tid % 16;   // 16x16 threads, R x R outputs each
   float acc[R][R] = {};
   const int nk = (K + TK - 1) / TK;
-  GenStage<TIn, T> st;
+  GenStage<TIn, T, KT> st;
   st.load(A, sam, sak, B, sbk, sbn, M, N, K, bm, bn, 0, tid);
   st.store(As[0], Bs[0], sak, sbn, tid);
   __syncthreads();
@@ -357,7 +360,10 @@ extern "C" int cmhar_gemm_generic(int in_dtype, int out_dtype, int M, int N, int
   dim3 grid(cdiv(N, TN), cdiv(M, TM), batch), grid32(cdiv(N, 32), cdiv(M, 32), batch);
 #define LAUNCH(TI, TO)                                                                                          \
   do {                                                                                                          \
-    if (small)                                                                                                  \
+    if (small && K >= 128)                                                                                      \
+      gemm_generic_kernel<TI, TO, 32, 128><<<grid32, 256, 0, stream>>>(M, N, K, (const TI*)A, sam, sak, sAb,   \
+                                                                       (const TI*)B, sbk, sbn, sBb, (TO*)C, ldc, sCb, e); \
+    else if (small)                                                                                             \
       gemm_generic_kernel<TI, TO, 32><<<grid32, 256, 0, stream>>>(M, N, K, (const TI*)A, sam, sak, sAb,        \
                                                                   (const TI*)B, sbk, sbn, sBb, (TO*)C, ldc, sCb, e); \
     else                                                                                                        \

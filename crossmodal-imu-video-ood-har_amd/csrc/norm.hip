@@ -123,7 +123,7 @@ __global__ __launch_bounds__(256) void ln_fwd_vec_kernel(int M, const T* __restr
 // dh = LN_bwd(dy) (+ dres); db_out (optional) = dh * dropmask(b); dgamma/dbeta partial slabs per block.
 // Each block: 4 waves x ROWS_PER_WAVE rows.
 constexpr int LN_BWD_ROWS = 16;
-template <typename T>
+template <typename T, int MP = MAXPER>   // MP: columns per lane (N <= 64·MP)
 __global__ __launch_bounds__(256) void ln_bwd_kernel(int M, int N, const T* __restrict__ dy, long lddy,
                                                      const T* __restrict__ h, long ldh, const float* __restrict__ gamma,
                                                      const float* __restrict__ mean, const float* __restrict__ rstd,
@@ -133,23 +133,45 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(int M, int N, const T* __re
                                                      float* __restrict__ pbeta) {
   __shared__ float red[2][4][1024];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  float ag[MAXPER], ab[MAXPER];
+  float ag[MP], ab[MP];
 #pragma unroll
-  for (int i = 0; i < MAXPER; ++i) { ag[i] = 0.f; ab[i] = 0.f; }
-  for (int rr = 0; rr < LN_BWD_ROWS; ++rr) {
-    const long row = ((long)blockIdx.x * 4 + wave) * LN_BWD_ROWS + rr;
+  for (int i = 0; i < MP; ++i) { ag[i] = 0.f; ab[i] = 0.f; }
+  // rows in groups of LN_BWD_PF whose dy / h / statistics loads are all issued before the first row's reductions
+  // (one row at a time, each row's loads waited on the previous row's cross-lane sums: the M = 416 IMU LayerNorms
+  // ran ~16 exposed load latencies per wave); per-row arithmetic and accumulation order unchanged
+  constexpr int LN_BWD_PF = 4;
+  const long row0 = ((long)blockIdx.x * 4 + wave) * LN_BWD_ROWS;
+  for (int rg = 0; rg < LN_BWD_ROWS; rg += LN_BWD_PF) {
+    if (row0 + rg >= M) break;
+    float pd[LN_BWD_PF][MP], ph[LN_BWD_PF][MP], pmu[LN_BWD_PF], prs[LN_BWD_PF];
+#pragma unroll
+    for (int u = 0; u < LN_BWD_PF; ++u) {
+      const long row = row0 + rg + u;
+      const bool ok = row < M;
+      pmu[u] = ok ? mean[row] : 0.f;
+      prs[u] = ok ? rstd[row] : 0.f;
+#pragma unroll
+      for (int i = 0; i < MP; ++i) {
+        const int c = lane + 64 * i;
+        pd[u][i] = ok && c < N ? to_f<T>(dy[row * lddy + c]) : 0.f;
+        ph[u][i] = ok && c < N ? to_f<T>(h[row * ldh + c]) : 0.f;
+      }
+    }
+#pragma unroll
+  for (int u = 0; u < LN_BWD_PF; ++u) {
+    const long row = row0 + rg + u;
     if (row >= M) break;
-    const float mu = mean[row], r = rstd[row];
-    float xh[MAXPER], g[MAXPER];
+    const float mu = pmu[u], r = prs[u];
+    float xh[MP], g[MP];
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
-    for (int i = 0; i < MAXPER; ++i) {
+    for (int i = 0; i < MP; ++i) {
       const int c = lane + 64 * i;
       xh[i] = 0.f;
       g[i] = 0.f;
       if (c < N) {
-        const float d = to_f<T>(dy[row * lddy + c]);
-        xh[i] = (to_f<T>(h[row * ldh + c]) - mu) * r;
+        const float d = pd[u][i];
+        xh[i] = (ph[u][i] - mu) * r;
         g[i] = d * gamma[c];
         ag[i] += d * xh[i];
         ab[i] += d;
@@ -160,7 +182,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(int M, int N, const T* __re
     s1 = wave_sum(s1) / N;
     s2 = wave_sum(s2) / N;
 #pragma unroll
-    for (int i = 0; i < MAXPER; ++i) {
+    for (int i = 0; i < MP; ++i) {
       const int c = lane + 64 * i;
       if (c < N) {
         float v = r * (g[i] - s1 - xh[i] * s2);
@@ -170,8 +192,9 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(int M, int N, const T* __re
       }
     }
   }
+  }
 #pragma unroll
-  for (int i = 0; i < MAXPER; ++i) {
+  for (int i = 0; i < MP; ++i) {
     const int c = lane + 64 * i;
     if (c < N) { red[0][wave][c] = ag[i]; red[1][wave][c] = ab[i]; }
   }
@@ -537,9 +560,14 @@ extern "C" int cmhar_layernorm_bwd(int dtype, int M, int N, const void* dy, long
                                                 (const bf16*)dres, ldres, (bf16*)dh, lddh, (bf16*)db_out, lddb, pdrop,
                                                 seed, pg, pb);
   } else {
-    ln_bwd_kernel<float><<<blocks, 256, 0, st>>>(M, N, (const float*)dy, lddy, (const float*)h, ldh, gamma, mean,
-                                                 rstd, (const float*)dres, ldres, (float*)dh, lddh, (float*)db_out,
-                                                 lddb, pdrop, seed, pg, pb);
+    if (N <= 128)   // the IMU encoder / fusion LayerNorms (d = 128): two columns per lane, small prefetch set
+      ln_bwd_kernel<float, 2><<<blocks, 256, 0, st>>>(M, N, (const float*)dy, lddy, (const float*)h, ldh, gamma,
+                                                      mean, rstd, (const float*)dres, ldres, (float*)dh, lddh,
+                                                      (float*)db_out, lddb, pdrop, seed, pg, pb);
+    else
+      ln_bwd_kernel<float><<<blocks, 256, 0, st>>>(M, N, (const float*)dy, lddy, (const float*)h, ldh, gamma, mean,
+                                                   rstd, (const float*)dres, ldres, (float*)dh, lddh, (float*)db_out,
+                                                   lddb, pdrop, seed, pg, pb);
   }
   CMHAR_CHECK_LAUNCH();
   reduce_rows_gb(pg, blocks, N, dgamma, dbeta, beta_acc, scr, st);
