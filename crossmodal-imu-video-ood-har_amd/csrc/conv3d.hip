@@ -350,6 +350,37 @@ __device__ __forceinline__ float* tile_counts(float* ts, int ntile, int C) {
   return ts + 2L * (ntile + (ntile + BN_TG - 1) / BN_TG) * C;
 }
 
+// Per-column BatchNorm statistics (mean, Σ(v − mean)²) of the bf16-rounded values of a conv tile's fp32 LDS staging
+// image, by ALL NT threads of the block: ncols (dividing NT) columns, P = NT / ncols row partitions per column (rows
+// p, p + P, …), partials combined in a fixed order through `scr` (2·NT floats of LDS outside the image).  One thread
+// per column walking up to 256 rows twice left each tile a long single-wave tail (the other waves idle, the CU's
+// workgroup slot held).  Every thread of the block must call it (two barriers).  val(c, r): image value of column c,
+// row r; nrows(c): valid rows of column c (≤ 0: none); out(c, mean, m2) runs on one thread per column.
+template <int NT, typename V, typename NR, typename OUT>
+__device__ __forceinline__ void tile_col_stats(int ncols, float* scr, int tid, V val, NR nrows, OUT out) {
+  const int P = NT / ncols, c = tid % ncols, p = tid / ncols;
+  const int rows = nrows(c);
+  float s = 0.f;
+  for (int r = p; r < rows; r += P) s += (float)(bf16)val(c, r);
+  scr[tid] = s;
+  __syncthreads();
+  float mu = 0.f;
+  for (int q = 0; q < P; ++q) mu += scr[q * ncols + c];
+  mu = rows > 0 ? mu / (float)rows : 0.f;
+  float m2 = 0.f;
+  for (int r = p; r < rows; r += P) {
+    const float d = (float)(bf16)val(c, r) - mu;
+    m2 = fmaf(d, d, m2);
+  }
+  scr[NT + tid] = m2;
+  __syncthreads();
+  if (p == 0 && rows > 0) {
+    float t = 0.f;
+    for (int q = 0; q < P; ++q) t += scr[NT + q * ncols + c];
+    out(c, mu, t);
+  }
+}
+
 __global__ void bn_cl_eval_stats(int C, const float* __restrict__ rmean, const float* __restrict__ rvar, float eps,
                                  float* __restrict__ mean, float* __restrict__ rstd) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
@@ -575,7 +606,7 @@ __device__ __forceinline__ void store_tile(char* smem, const floatx4 (&acc)[4][J
 template <int JN> struct FwdLds {
   static constexpr int B0 = 32768, BSTAGE = JN * 4096;
   static constexpr int OPS = B0 + 2 * BSTAGE, EPI = 128 * (JN * 32 + 4) * 4;
-  static constexpr int BYTES = OPS > EPI ? OPS : EPI;
+  static constexpr int BYTES = OPS > EPI + 2048 ? OPS : EPI + 2048;   // + tile_col_stats scratch past the image
 };
 
 template <int JN>
@@ -648,19 +679,13 @@ __global__ __launch_bounds__(256, JN == 2 ? 3 : 2) void conv3d_fwd_igemm(Geom g,
     // valid rows, from the fp32 staging image still in LDS (combined across tiles by bn_tile_final, Chan's formula)
     const float* T = (const float*)smem;
     const int rows = min(BM, M - bm), tm = bm / BM, ntm = gridDim.x / ((Cout + TN - 1) / TN);
-    for (int c = tid; c < TN; c += NT) {
-      if (bn + c >= Cout) break;
-      float sum = 0.f;
-      for (int r = 0; r < rows; ++r) sum += (float)(bf16)T[r * (TN + 4) + c];
-      const float mu = sum / (float)rows;
-      float m2 = 0.f;
-      for (int r = 0; r < rows; ++r) {
-        const float d = (float)(bf16)T[r * (TN + 4) + c] - mu;
-        m2 = fmaf(d, d, m2);
-      }
-      tstats[(long)tm * Cout + bn + c] = mu;
-      tstats[((long)ntm + tm) * Cout + bn + c] = m2;
-    }
+    tile_col_stats<NT>(TN, (float*)(smem + Lds::EPI), tid, [&](int c, int r) { return T[r * (TN + 4) + c]; },
+                       [&](int) { return rows; }, [&](int c, float mu, float m2) {
+                         if (bn + c < Cout) {
+                           tstats[(long)tm * Cout + bn + c] = mu;
+                           tstats[((long)ntm + tm) * Cout + bn + c] = m2;
+                         }
+                       });
     if (tid == 0 && bn == 0) tile_counts(tstats, ntm, Cout)[tm] = (float)rows;
   }
 }
@@ -1073,7 +1098,7 @@ template <int TM> struct Cfg {
   static constexpr int SLAB = SQ * RS, WB = 3 * TN * RS;
   static constexpr int SL_PER = (SQ * 8 + NT - 1) / NT, W_PER = 3 * TN * 8 / NT, ELD = TN + 4;
   static constexpr int LDS = SLAB + WB + 2 * 64 * 4;   // + per-output-row table
-  static_assert(TM * ELD * 4 <= SLAB + WB, "epilogue staging must fit the operand LDS");
+  static_assert(TM * ELD * 4 + 2048 <= SLAB + WB, "epilogue staging + statistics scratch must fit the operand LDS");
 };
 }  // namespace fr
 
@@ -1215,23 +1240,18 @@ __global__ __launch_bounds__(256, 2) void conv3d_fwd_rows(Geom g, int M, int Cou
     vstore<bf16, 8>(z + (long)m * Cout + bn + cg, v);
   }
   if (tstats) {
+    // one statistics column per (128-row half, Cout column)
     const int ntm = (M + 127) / 128;
-    for (int w = tid; w < (TM / 128) * TN; w += NT) {
-      const int half = w / TN, c = w % TN, r0 = half * 128, tm = bm / 128 + half;
-      const int rows = min(128, M - (bm + r0));
-      if (rows <= 0) continue;
-      float sum = 0.f;
-      for (int r = 0; r < rows; ++r) sum += (float)(bf16)T[(r0 + r) * ELD + c];
-      const float mu = sum / (float)rows;
-      float m2 = 0.f;
-      for (int r = 0; r < rows; ++r) {
-        const float d = (float)(bf16)T[(r0 + r) * ELD + c] - mu;
-        m2 = fmaf(d, d, m2);
-      }
-      tstats[(long)tm * Cout + bn + c] = mu;
-      tstats[((long)ntm + tm) * Cout + bn + c] = m2;
-      if (c == 0 && bn == 0) tile_counts(tstats, ntm, Cout)[tm] = (float)rows;
-    }
+    tile_col_stats<NT>(
+        (TM / 128) * TN, (float*)(smem + TM * ELD * 4), tid,
+        [&](int w, int r) { return T[((w / TN) * 128 + r) * ELD + w % TN]; },
+        [&](int w) { return min(128, M - (bm + (w / TN) * 128)); },
+        [&](int w, float mu, float m2) {
+          const int half = w / TN, c = w % TN, tm = bm / 128 + half;
+          tstats[(long)tm * Cout + bn + c] = mu;
+          tstats[((long)ntm + tm) * Cout + bn + c] = m2;
+          if (c == 0 && bn == 0) tile_counts(tstats, ntm, Cout)[tm] = (float)min(128, M - (bm + half * 128));
+        });
   }
 }
 
@@ -1244,7 +1264,7 @@ namespace fr3 {
 constexpr int SQ = 352, TN = 64, NT = 256, RS = 144;
 constexpr int SLAB = SQ * RS, WB = 3 * TN * RS, ELD = TN + 4;
 constexpr int SL_PER = (SQ * 8 + NT - 1) / NT, W_PER = 3 * TN * 8 / NT;
-static_assert(256 * ELD * 4 <= SLAB + WB, "epilogue staging must fit the operand LDS");
+static_assert(256 * ELD * 4 + 2048 <= SLAB + WB, "epilogue staging + statistics scratch must fit the operand LDS");
 }  // namespace fr3
 
 __global__ __launch_bounds__(256, 2) void conv3d_fwd_rows3(Geom g, int R, int Ls, int cpf, const bf16* __restrict__ x,
@@ -1367,20 +1387,13 @@ __global__ __launch_bounds__(256, 2) void conv3d_fwd_rows3(Geom g, int R, int Ls
     }
     vstore<bf16, 8>(z + m * TN + cg, v);
   }
-  if (tstats && tid < TN) {
-    const int c = tid;
-    float sum = 0.f;
-    for (int r = 0; r < used; ++r) sum += (float)(bf16)T[r * ELD + c];
-    const float mu = sum / (float)used;
-    float m2 = 0.f;
-    for (int r = 0; r < used; ++r) {
-      const float d = (float)(bf16)T[r * ELD + c] - mu;
-      m2 = fmaf(d, d, m2);
-    }
-    tstats[(long)t * TN + c] = mu;
-    tstats[((long)ntile + t) * TN + c] = m2;
-    if (c == 0) tile_counts(tstats, ntile, TN)[t] = (float)used;
-  }
+  if (tstats)
+    tile_col_stats<NT>(TN, (float*)(smem + 256 * ELD * 4), tid, [&](int c, int r) { return T[r * ELD + c]; },
+                       [&](int) { return used; }, [&](int c, float mu, float m2) {
+                         tstats[(long)t * TN + c] = mu;
+                         tstats[((long)ntile + t) * TN + c] = m2;
+                         if (c == 0) tile_counts(tstats, ntile, TN)[t] = (float)used;
+                       });
 }
 
 // ---- implicit stem: few input channels (C <= 4), kw <= 8 taps at w-stride 2 (R3D-18's 3->64, 3x7x7, (1,2,2)) ----
@@ -1396,7 +1409,7 @@ namespace stm {
 constexpr int RB = 16 * 64 + 16;      // LDS bytes per staged input row (<= 127 positions x 8 B, + pad)
 constexpr int UMAX = 13, KHMAX = 8, WCO = 80;   // staged rows per tile, kh taps, weight row stride (64 B + pad)
 constexpr int ROWS_B = UMAX * RB, W_B = KHMAX * 64 * WCO, ELD = 68;
-constexpr int FWD_LDS = (ROWS_B + W_B) > 256 * ELD * 4 ? (ROWS_B + W_B) : 256 * ELD * 4;
+constexpr int FWD_LDS = (ROWS_B + W_B) > 256 * ELD * 4 + 2048 ? (ROWS_B + W_B) : 256 * ELD * 4 + 2048;
 __device__ __forceinline__ bool ok(const Geom& g) { return g.C <= 4 && g.kw <= 8 && g.sw == 2 && g.kh <= KHMAX; }
 }  // namespace stm
 
@@ -1479,20 +1492,13 @@ __global__ __launch_bounds__(256, 2) void conv3d_stem_fwd(Geom g, int R, int cpf
     for (int j = 0; j < 8; ++j) v[j] = T[rr * ELD + cg + j];
     vstore<bf16, 8>(z + (m0 + rr) * 64 + cg, v);
   }
-  if (tstats && tid < 64) {
-    const int c = tid;
-    float sum = 0.f;
-    for (int r = 0; r < used; ++r) sum += (float)(bf16)T[r * ELD + c];
-    const float mu = sum / (float)used;
-    float m2 = 0.f;
-    for (int r = 0; r < used; ++r) {
-      const float d = (float)(bf16)T[r * ELD + c] - mu;
-      m2 = fmaf(d, d, m2);
-    }
-    tstats[(long)t * 64 + c] = mu;
-    tstats[((long)ntile + t) * 64 + c] = m2;
-    if (c == 0) tile_counts(tstats, ntile, 64)[t] = (float)used;
-  }
+  if (tstats)
+    tile_col_stats<256>(64, (float*)(smem + 256 * ELD * 4), tid, [&](int c, int r) { return T[r * ELD + c]; },
+                        [&](int) { return used; }, [&](int c, float mu, float m2) {
+                          tstats[(long)t * 64 + c] = mu;
+                          tstats[((long)ntile + t) * 64 + c] = m2;
+                          if (c == 0) tile_counts(tstats, ntile, 64)[t] = (float)used;
+                        });
 }
 
 // Weight gradient dW4[co][it][ih][iw·4 + c] = Σ_slots dz[slot][co] · window(slot, it, ih)[iw·4 + c]: workgroup =

@@ -194,6 +194,49 @@ def test_r3d_stem_weight_gradient_split_k_production_rows():
     assert r3d._r8(3 * 3 * 7 * 7) == Kp                      # the stem's padded K
 
 
+def test_r3d_implicit_stem_production_geometry():
+    """The implicit stem kernels at the bench geometry (32 clips of 16 × 112² → 7168 row tiles, ~171-way split weight
+    gradient) against fp32 products of the same bf16 operands on the device: the column matrix is built by
+    cmhar_conv3d_im2col (itself checked against F.conv3d above), z_ref = col · Wᵀ (≤ 5e-3 rel, bf16 output) and
+    dW_ref = dzᵀ · col (≤ 1e-4 rel, fp32 output), plus the epilogue BatchNorm statistics vs the two-pass kernel."""
+    from cmhar import _lib as L
+    from cmhar import kernels as K
+    from cmhar import r3d
+    torch.manual_seed(8)
+    conv = torch.nn.Conv3d(3, 64, (3, 7, 7), (1, 2, 2), (1, 3, 3), bias=False).to(DEV)
+    x = torch.randn(32, 16, 112, 112, 3, device=DEV).bfloat16()
+    shp = tuple(x.shape)
+    assert r3d._stem_ok(x, shp, conv)
+    osh = r3d._out_shape(shp, conv)
+    M = math.prod(osh[:4])
+    Kp = r3d._r8(conv.weight[0].numel())
+    col = r3d._im2col(x, shp, conv, Kp, M)                           # [M, 448] bf16, k = ((it·7 + ih)·7 + iw)·3 + c
+    wq = conv.weight.detach().bfloat16().float()                      # the bf16 operand the kernel multiplies
+    wk = wq.permute(0, 2, 3, 4, 1).reshape(64, -1)                    # im2col k order
+    w4 = r3d._pack_stem(conv)
+    dims = r3d._dims(shp, conv, r3d._stem_kp(conv))
+    ntile = L.lib().cmhar_conv3d_stem_tiles(dims, 64)
+    assert ntile == 32 * 16 * 14
+    ts = torch.empty(L.lib().cmhar_conv3d_stem_stats_floats(dims, 64), device=DEV)
+    z = torch.empty(M, 64, dtype=torch.bfloat16, device=DEV)
+    L.call('cmhar_conv3d_stem_fwd', dims, 64, x.data_ptr(), w4.data_ptr(), z.data_ptr(), ts.data_ptr(),
+           L.stream(x.device))
+    z_ref = col[:, :wk.shape[1]].float() @ wk.T
+    assert rel(z.float(), z_ref) < 5e-3
+    bn_a, bn_b = torch.nn.BatchNorm3d(64).to(DEV), torch.nn.BatchNorm3d(64).to(DEV)
+    _, sma, sra = r3d._bn_fwd(z, bn_a, None, True, True)
+    _, smb, srb = r3d._bn_fwd_tiles(z, bn_b, None, True, ts, ntile)
+    assert rel(smb, sma) < 1e-5 and rel(srb, sra) < 1e-5
+    dz = torch.randn(M, 64, device=DEV).bfloat16()
+    dw4 = torch.empty(64, r3d._stem_kp(conv), device=DEV)
+    ws = K.workspace(L.lib().cmhar_conv3d_stem_wgrad_ws(dims, 64), x.device)
+    L.call('cmhar_conv3d_stem_wgrad', dims, 64, x.data_ptr(), dz.data_ptr(), dw4.data_ptr(), ws.data_ptr(),
+           L.stream(x.device))
+    dw = dw4.view(64, 3, 7, 8, 4)[:, :, :, :7, :3].reshape(64, -1)
+    dw_ref = dz.float().T @ col[:, :wk.shape[1]].float()
+    assert rel(dw, dw_ref) < 1e-4
+
+
 def test_r3d18_eval_running_stats():
     from cmhar.r3d import run_r3d
     from oracle.r3d_cpu import r3d18_features
