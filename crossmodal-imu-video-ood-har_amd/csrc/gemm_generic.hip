@@ -13,6 +13,9 @@
 namespace {
 
 constexpr int TM = 64, TN = 64, TK = 32, NTH = 256;   // default tile; T = 32 for grids of few 64² tiles
+#ifndef CMHAR_SMALL_KT
+#define CMHAR_SMALL_KT 64    // K-tile of the few-tile (T = 32) kernel when K >= it (A/B: tools/debug/imu_kt_ab.sh)
+#endif
 
 // The GEMMs this kernel serves are small (tens of blocks) with K up to a few thousand, so a K-step is bounded by
 // memory LATENCY, not bandwidth: tile k+1 is loaded into registers while tile k is consumed from LDS (double-
@@ -54,8 +57,11 @@ struct GenStage {
 // T x T output tile, 16 x 16 threads with (T/16)² outputs each.  Every output is one fmaf chain over k = 0..K-1 in
 // order whatever T is, so the two tile sizes give bit-identical results (T = 32 quadruples the workgroups of the
 // IMU encoder's few-tile GEMMs and quarters each one's K-loop FMA count).
-// KT: K-tile.  The IMU encoder's few-tile GEMMs (T = 32) take KT = 128 when K >= 128: their K-steps are bound by
-// the global-load latency, so four times the k per step quarters the exposed latencies (same per-output fmaf chain).
+// KT: K-tile.  The IMU encoder's few-tile GEMMs (T = 32) take KT = CMHAR_SMALL_KT = 64 when K >= 64: their K-steps
+// are bound by the global-load latency, so more k per step exposes fewer latencies (same per-output fmaf chain).
+// Measured (tools/debug/imu_kt_ab.sh, one box): standalone KT 32 → 128 cut the GEMMs 21.5 → 15.9 µs, but inside the
+// bench step, where these workgroups only fill gaps beside the video kernels, KT = 64 gives the least IMU GEMM time
+// (2.7 ms/step vs 3.2 at 32 and 3.9 at 128); the step's wall time is the same for all three.
 template <typename TIn, typename TOut, int T = TM, int KT = TK>
 __global__ __launch_bounds__(NTH) void gemm_generic_kernel(
     int M, int N, int K, const TIn* __restrict__ A, long sam, long sak, long sAb, const TIn* __restrict__ B,
@@ -360,8 +366,8 @@ extern "C" int cmhar_gemm_generic(int in_dtype, int out_dtype, int M, int N, int
   dim3 grid(cdiv(N, TN), cdiv(M, TM), batch), grid32(cdiv(N, 32), cdiv(M, 32), batch);
 #define LAUNCH(TI, TO)                                                                                          \
   do {                                                                                                          \
-    if (small && K >= 128)                                                                                      \
-      gemm_generic_kernel<TI, TO, 32, 128><<<grid32, 256, 0, stream>>>(M, N, K, (const TI*)A, sam, sak, sAb,   \
+    if (small && K >= CMHAR_SMALL_KT)                                                                           \
+      gemm_generic_kernel<TI, TO, 32, CMHAR_SMALL_KT><<<grid32, 256, 0, stream>>>(M, N, K, (const TI*)A, sam, sak, sAb, \
                                                                        (const TI*)B, sbk, sbn, sBb, (TO*)C, ldc, sCb, e); \
     else if (small)                                                                                             \
       gemm_generic_kernel<TI, TO, 32><<<grid32, 256, 0, stream>>>(M, N, K, (const TI*)A, sam, sak, sAb,        \
