@@ -36,10 +36,14 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--batch', type=int, default=32)
     ap.add_argument('--reps', type=int, default=10)
+    ap.add_argument('--layers', default='', help='comma-separated layer names (default: all)')
     a = ap.parse_args()
     dev = torch.device('cuda')
     st = L.stream(dev)
+    keep = set(a.layers.split(',')) if a.layers else None
     for name, T, H, C, Co, s in LAYERS:
+        if keep is not None and name not in keep:
+            continue
         N = a.batch
         To, Ho = (T - 1) // s + 1, (H - 1) // s + 1
         Kd = 27 * C
