@@ -24,7 +24,7 @@ class Epilogue(C.Structure):
     _fields_ = [('bias', vp), ('residual', vp), ('ldr', i64), ('aux_in', vp), ('lda', i64), ('aux_out', vp),
                 ('ldo', i64), ('rowadd', vp), ('rowadd_mod', i32), ('rowadd_ld', i32), ('act', i32),
                 ('alpha', f32), ('beta', f32), ('pdrop', f32), ('pad_', i32), ('seed', u64), ('rowsum', vp),
-                ('rowsum_beta', f32), ('pad2_', i32)]
+                ('rowsum_beta', f32), ('colscale_lo', i32), ('colscale_hi', i32), ('colscale', f32)]
 
 
 _SIGS = {
@@ -43,6 +43,8 @@ _SIGS = {
                                   vp]),
     'cmhar_attention_bwd': (i32, [i32, i32, i32, i32, i32, i32, vp, i64, vp, i64, vp, i64, vp, i64, vp, i64, vp, vp,
                                   vp, i64, vp, i64, vp, i64, f32, f32, u64, vp]),
+    'cmhar_attention_bwd_prescaled': (i32, [i32, i32, i32, i32, vp, i64, vp, i64, vp, i64, vp, i64, vp, i64, vp, vp,
+                                            vp, i64, vp, i64, vp, i64, f32, vp]),
     'cmhar_layernorm_fwd': (i32, [i32, i32, i32, vp, i64, vp, i64, f32, u64, vp, i64, vp, i64, vp, vp, vp, vp, f32,
                                   vp]),
     'cmhar_layernorm_bwd_ws': (i64, [i32, i32]),
@@ -151,8 +153,11 @@ def dtype_code(dt):
 
 
 def epilogue(bias=None, residual=None, aux_in=None, aux_out=None, rowadd=None, rowadd_mod=1, act=ACT_NONE,
-             alpha=1.0, beta=0.0, pdrop=0.0, seed=0, rowsum=None, rowsum_beta=0.0):
+             alpha=1.0, beta=0.0, pdrop=0.0, seed=0, rowsum=None, rowsum_beta=0.0, colscale=None):
+    """colscale: (lo, hi, s) — columns [lo, hi) multiplied by s before the activation."""
     e = Epilogue()
+    if colscale is not None:
+        e.colscale_lo, e.colscale_hi, e.colscale = int(colscale[0]), int(colscale[1]), float(colscale[2])
     e.rowsum = ptr(rowsum)
     e.rowsum_beta = rowsum_beta
     e.bias = ptr(bias)

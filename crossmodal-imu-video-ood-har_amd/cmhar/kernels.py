@@ -160,9 +160,10 @@ def _tail_ws(M, N, K):
 # ------------------------------------------------------------------------------------------------------------
 def gemm(layout: int, a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, *, bias=None, residual=None,
          aux_in=None, aux_out=None, rowadd=None, rowadd_mod=1, act=L.ACT_NONE, alpha=1.0, beta=0.0, splits=None,
-         pdrop=0.0, seed=0, rowsum=None, rowsum_beta=0.0):
+         pdrop=0.0, seed=0, rowsum=None, rowsum_beta=0.0, colscale=None):
     """layout 0: out[M,N] = a[M,K]·b[N,K]ᵀ;  1: a[M,K]·b[K,N];  2: a[K,M]ᵀ·b[K,N].
-    rowsum (layout 2, bf16, 256-tile shapes): rowsum[m] = Σ_k a[k,m] + rowsum_beta·rowsum[m] (bias gradient)."""
+    rowsum (layout 2, bf16, 256-tile shapes): rowsum[m] = Σ_k a[k,m] + rowsum_beta·rowsum[m] (bias gradient).
+    colscale (lo, hi, s): columns [lo, hi) (multiples of 8) of the product + bias scaled by s before the activation."""
     for t, n in ((a, 'A'), (b, 'B'), (out, 'C')):
         _check_2d(t, n)
     if layout == 0:
@@ -202,8 +203,10 @@ def gemm(layout: int, a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, *, bi
             raise ValueError('rowsum needs the bf16 256-tile weight-gradient path')
         if rowsum.dtype != torch.float32 or rowsum.numel() != M or not rowsum.is_contiguous():
             raise ValueError(f'rowsum must be a contiguous fp32 [{M}] tensor')
+    if colscale is not None and (colscale[0] % 8 or colscale[1] % 8 or not 0 <= colscale[0] <= colscale[1] <= N):
+        raise ValueError('colscale columns must be a multiple-of-8 range inside [0, N]')
     epi = L.epilogue(bias, residual, aux_in, aux_out, rowadd, rowadd_mod, act, alpha, beta, pdrop, seed, rowsum,
-                     rowsum_beta)
+                     rowsum_beta, colscale)
     st = L.stream(out.device)
     if a.dtype == torch.float16:
         # fp16 inference path (BASELINE config 5): the bf16 kernels on the fp16 MFMA, forward layout only
@@ -275,13 +278,13 @@ def gemm(layout: int, a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, *, bi
 
 
 def linear(x, w, bias=None, *, residual=None, act=L.ACT_NONE, aux_out=None, rowadd=None, rowadd_mod=1,
-           out=None, out_dtype=None, pdrop=0.0, seed=0):
+           out=None, out_dtype=None, pdrop=0.0, seed=0, colscale=None):
     """y = dropout(act(x·wᵀ + bias [+ rowadd])) [+ residual]  — nn.Linear forward (+ fused activation)."""
     M, N = x.shape[0], w.shape[0]
     if out is None:
         out = torch.empty(M, N, dtype=out_dtype or x.dtype, device=x.device)
     return gemm(0, x, w, out, bias=bias, residual=residual, act=act, aux_out=aux_out, rowadd=rowadd,
-                rowadd_mod=rowadd_mod, pdrop=pdrop, seed=seed)
+                rowadd_mod=rowadd_mod, pdrop=pdrop, seed=seed, colscale=colscale)
 
 
 def linear_dgrad(dy, w, *, act=L.ACT_NONE, aux_in=None, residual=None, out=None, beta=0.0, pdrop=0.0, seed=0):
@@ -367,6 +370,26 @@ def attention_bwd(q, k, v, o, do, lse, dq, dk, dv, *, B, H, Lq, Lk, D, scale, pd
     call('cmhar_attention_bwd', dt, B, H, Lq, Lk, D, ptr(q), q.stride(0), ptr(k), k.stride(0), ptr(v), v.stride(0),
          ptr(o), o.stride(0), ptr(do), do.stride(0), ptr(lse), ptr(delta), ptr(dq), dq.stride(0), ptr(dk),
          dk.stride(0), ptr(dv), dv.stride(0), scale, pdrop, seed, L.stream(q.device))
+    TRACE.end(ev, 'attn_bwd_bf16(dq+delta,dkdv)', 14 * B * H * Lq * Lk * D, 2 * (6 * B * Lq + 4 * B * Lk) * H * D)
+
+
+LOG2E = 1.4426950408889634
+
+
+def attention_bwd_prescaled(q, k, v, o, do, lse, dq, dk, dv, *, B, H, Lq, Lk, D, scale):
+    """Backward of bf16 flash attention whose keys were written pre-scaled by scale·log2(e) (linear(..., colscale))
+    and whose forward ran with scale = 1/log2(e): dq, dv and dk (gradient of the UNSCALED key) for the true `scale`."""
+    for t, n, Lx in ((q, 'q', Lq), (k, 'k', Lk), (v, 'v', Lk), (o, 'o', Lq), (do, 'do', Lq), (dq, 'dq', Lq),
+                     (dk, 'dk', Lk), (dv, 'dv', Lk)):
+        _head_view_ok(t, B, Lx, H, D, n)
+        _check_bf16_operand(t, n)
+    if q.dtype != torch.bfloat16 or D != 64:
+        raise ValueError('pre-scaled attention backward: bf16, head dim 64')
+    delta = workspace(B * H * Lq, q.device)
+    ev = TRACE.begin('attn_bwd_bf16(dq+delta,dkdv)')
+    call('cmhar_attention_bwd_prescaled', B, H, Lq, Lk, ptr(q), q.stride(0), ptr(k), k.stride(0), ptr(v), v.stride(0),
+         ptr(o), o.stride(0), ptr(do), do.stride(0), ptr(lse), ptr(delta), ptr(dq), dq.stride(0), ptr(dk),
+         dk.stride(0), ptr(dv), dv.stride(0), scale, L.stream(q.device))
     TRACE.end(ev, 'attn_bwd_bf16(dq+delta,dkdv)', 14 * B * H * Lq * Lk * D, 2 * (6 * B * Lq + 4 * B * Lk) * H * D)
 
 

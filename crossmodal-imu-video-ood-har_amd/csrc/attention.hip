@@ -354,13 +354,19 @@ __global__ __launch_bounds__(256, CMHAR_ATTN_FWD_PERKB ? 3 : 2) void attn_fwd_bf
 #ifndef CMHAR_DKDV_OCC
 #define CMHAR_DKDV_OCC 3
 #endif
+// PS (pre-scaled keys): K holds bf16(scale·log2e·K) written by the QKV GEMM's epilogue (CmharEpilogue.colscale) and
+// the launch passes scale = 1/log2e, so c = 1 and p = exp2(acc) needs no multiply per score (−6 % backward time:
+// the kernels are VALU-issue bound beside their MFMAs); kscale is the dK output factor (the true softmax scale, so
+// dK is the gradient of the unscaled key and the QKV backward is unchanged).
+template <bool PS = false>
 __global__ __launch_bounds__(256, CMHAR_DKDV_OCC) void attn_bwd_dkdv_bf16(int H, int Lq, int Lk, const bf16* __restrict__ Q,
                                                              long ldq, const bf16* __restrict__ K, long ldk,
                                                              const bf16* __restrict__ V, long ldv,
                                                              const bf16* __restrict__ dO, long lddo,
                                                              const float* __restrict__ lse,
                                                              const float* __restrict__ delta, bf16* __restrict__ dK,
-                                                             long lddk, bf16* __restrict__ dV, long lddv, float scale) {
+                                                             long lddk, bf16* __restrict__ dV, long lddv, float scale,
+                                                             float kscale) {
   __shared__ __attribute__((aligned(16))) char smem[4 * 8192 + 2 * 2 * 64 * 4];
 #define Qs(buf) (smem + 8192 * (buf))
 #define Gs(buf) (smem + 16384 + 8192 * (buf))
@@ -443,7 +449,7 @@ __global__ __launch_bounds__(256, CMHAR_DKDV_OCC) void attn_bwd_dkdv_bf16(int H,
       bf16x8 pbv[2], dbv[2];
 #pragma unroll
       for (int r = 0; r < 16; r += 2) {
-        const float2_t pv = {fexp2(s[r] * c), fexp2(s[r + 1] * c)};
+        const float2_t pv = PS ? float2_t{fexp2(s[r]), fexp2(s[r + 1])} : float2_t{fexp2(s[r] * c), fexp2(s[r + 1] * c)};
         const float2_t dv2 = pv * float2_t{dp[r], dp[r + 1]};
         const bf16x2_t pp = __builtin_convertvector(pv, bf16x2_t);
         const bf16x2_t dd = __builtin_convertvector(dv2, bf16x2_t);
@@ -482,7 +488,7 @@ __global__ __launch_bounds__(256, CMHAR_DKDV_OCC) void attn_bwd_dkdv_bf16(int H,
       for (int g = 0; g < 4; ++g) {
         bf16x4 a, v;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) { a[j] = (bf16)(dk[d][4 * g + j] * scale); v[j] = (bf16)dv[d][4 * g + j]; }
+        for (int j = 0; j < 4; ++j) { a[j] = (bf16)(dk[d][4 * g + j] * kscale); v[j] = (bf16)dv[d][4 * g + j]; }
         *(bf16x4*)(krow + d * 32 + 8 * g + 4 * h) = a;
         *(bf16x4*)(vrow + d * 32 + 8 * g + 4 * h) = v;
       }
@@ -500,7 +506,7 @@ __global__ __launch_bounds__(256, CMHAR_DKDV_OCC) void attn_bwd_dkdv_bf16(int H,
 #ifndef CMHAR_DQ_OCC
 #define CMHAR_DQ_OCC 3
 #endif
-template <int QB>
+template <int QB, bool PS = false>
 __global__ __launch_bounds__(256, QB == 1 ? CMHAR_DQ_OCC : 2) void attn_bwd_dq_bf16(int H, int Lq, int Lk, int q_base,
                                                            const bf16* __restrict__ Q, long ldq,
                                                            const bf16* __restrict__ K, long ldk,
@@ -598,7 +604,8 @@ __global__ __launch_bounds__(256, QB == 1 ? CMHAR_DQ_OCC : 2) void attn_bwd_dq_b
       for (int j = 0; j < QB; ++j) {
 #pragma unroll
         for (int r = 0; r < 16; r += 2) {   // aligned pairs: one v_pk_mul_f32 + one v_cvt_pk_bf16_f32 each
-          const float2_t pv = {fexp2(s[j][r] * c), fexp2(s[j][r + 1] * c)};
+          const float2_t pv = PS ? float2_t{fexp2(s[j][r]), fexp2(s[j][r + 1])}
+                                 : float2_t{fexp2(s[j][r] * c), fexp2(s[j][r + 1] * c)};
           const bf16x2_t dd = __builtin_convertvector(pv * float2_t{dp[j][r], dp[j][r + 1]}, bf16x2_t);
           db[j][r >> 3][r & 7] = dd[0];
           db[j][r >> 3][(r & 7) + 1] = dd[1];
@@ -884,6 +891,43 @@ extern "C" int cmhar_attention_fwd(int dtype, int B, int H, int Lq, int Lk, int 
 }
 
 // Backward.  delta: fp32 [B*H*Lq] workspace (written here).
+// bf16 flash backward; PS: pre-scaled keys (see attn_bwd_dkdv_bf16), `scale` then the true softmax scale
+template <bool PS>
+static void flash_bwd_bf16(int B, int H, int Lq, int Lk, const void* Q, long ldq, const void* K, long ldk,
+                           const void* V, long ldv, const void* O, long ldo, const void* dO, long lddo,
+                           const float* lse, float* delta, void* dQ, long lddq, void* dK, long lddk, void* dV,
+                           long lddv, float scale, hipStream_t st) {
+  const float s_in = PS ? 1.f / LOG2E : scale;   // c = s_in·log2e (1 when PS) and the dQ output factor
+  // 256-query workgroups (QB = 2) over the bulk, 128-query workgroups for the rest (as the forward)
+  const int bulk = CMHAR_ATTN_DQ_QB == 2 ? (Lq / 256) * 256 : 0;
+  if (bulk > 0)
+    attn_bwd_dq_bf16<2, PS><<<dim3(bulk / 256, H, B), 256, 0, st>>>(H, Lq, Lk, 0, (const bf16*)Q, ldq, (const bf16*)K,
+                                                                    ldk, (const bf16*)V, ldv, (const bf16*)O, ldo,
+                                                                    (const bf16*)dO, lddo, lse, delta, (bf16*)dQ,
+                                                                    lddq, s_in);
+  if (Lq > bulk)
+    attn_bwd_dq_bf16<1, PS><<<dim3(cdiv(Lq - bulk, 128), H, B), 256, 0, st>>>(
+        H, Lq, Lk, bulk, (const bf16*)Q, ldq, (const bf16*)K, ldk, (const bf16*)V, ldv, (const bf16*)O, ldo,
+        (const bf16*)dO, lddo, lse, delta, (bf16*)dQ, lddq, s_in);
+  attn_bwd_dkdv_bf16<PS><<<dim3(cdiv(Lk, 128), H, B), 256, 0, st>>>(H, Lq, Lk, (const bf16*)Q, ldq, (const bf16*)K,
+                                                                    ldk, (const bf16*)V, ldv, (const bf16*)dO, lddo,
+                                                                    lse, delta, (bf16*)dK, lddk, (bf16*)dV, lddv, s_in,
+                                                                    scale);
+}
+
+extern "C" int cmhar_attention_bwd_prescaled(int B, int H, int Lq, int Lk, const void* Q, long ldq, const void* K,
+                                             long ldk, const void* V, long ldv, const void* O, long ldo,
+                                             const void* dO, long lddo, const float* lse, float* delta, void* dQ,
+                                             long lddq, void* dK, long lddk, void* dV, long lddv, float scale,
+                                             hipStream_t st) {
+  if (B <= 0 || Lq <= 0) return 0;
+  if (Lk <= 0 || !Q || !K || !V || !O || !dO || !lse || !delta || !dQ || !dK || !dV) return -1;
+  flash_bwd_bf16<true>(B, H, Lq, Lk, Q, ldq, K, ldk, V, ldv, O, ldo, dO, lddo, lse, delta, dQ, lddq, dK, lddk, dV, lddv,
+                       scale, st);
+  CMHAR_CHECK_LAUNCH();
+  return 0;
+}
+
 extern "C" int cmhar_attention_bwd(int dtype, int B, int H, int Lq, int Lk, int D, const void* Q, long ldq,
                                    const void* K, long ldk, const void* V, long ldv, const void* O, long ldo,
                                    const void* dO, long lddo, const float* lse, float* delta, void* dQ, long lddq,
@@ -892,21 +936,8 @@ extern "C" int cmhar_attention_bwd(int dtype, int B, int H, int Lq, int Lk, int 
   if (B <= 0 || Lq <= 0) return 0;
   if (dtype == CMHAR_F16) return -1;   // fp16 is the inference-only path
   if (dtype == CMHAR_BF16 && D == 64 && pdrop == 0.f) {
-    // 256-query workgroups (QB = 2) over the bulk, 128-query workgroups for the rest (as the forward)
-    const int bulk = CMHAR_ATTN_DQ_QB == 2 ? (Lq / 256) * 256 : 0;
-    if (bulk > 0)
-      attn_bwd_dq_bf16<2><<<dim3(bulk / 256, H, B), 256, 0, st>>>(H, Lq, Lk, 0, (const bf16*)Q, ldq, (const bf16*)K,
-                                                                  ldk, (const bf16*)V, ldv, (const bf16*)O, ldo,
-                                                                  (const bf16*)dO, lddo, lse, delta, (bf16*)dQ, lddq,
-                                                                  scale);
-    if (Lq > bulk)
-      attn_bwd_dq_bf16<1><<<dim3(cdiv(Lq - bulk, 128), H, B), 256, 0, st>>>(H, Lq, Lk, bulk, (const bf16*)Q, ldq,
-                                                                            (const bf16*)K, ldk, (const bf16*)V, ldv,
-                                                                            (const bf16*)O, ldo, (const bf16*)dO, lddo,
-                                                                            lse, delta, (bf16*)dQ, lddq, scale);
-    attn_bwd_dkdv_bf16<<<dim3(cdiv(Lk, 128), H, B), 256, 0, st>>>(H, Lq, Lk, (const bf16*)Q, ldq, (const bf16*)K, ldk,
-                                                                  (const bf16*)V, ldv, (const bf16*)dO, lddo, lse,
-                                                                  delta, (bf16*)dK, lddk, (bf16*)dV, lddv, scale);
+    flash_bwd_bf16<false>(B, H, Lq, Lk, Q, ldq, K, ldk, V, ldv, O, ldo, dO, lddo, lse, delta, dQ, lddq, dK, lddk, dV,
+                          lddv, scale, st);
   } else if (f32m_ok(dtype, D, pdrop, {{Q, ldq}, {K, ldk}, {V, ldv}, {O, ldo}, {dO, lddo}, {dQ, lddq}, {dK, lddk},
                                        {dV, lddv}})) {
     cmhar_attn_f32m_bwd(B, H, Lq, Lk, (const float*)Q, ldq, (const float*)K, ldk, (const float*)V, ldv,

@@ -122,6 +122,7 @@ __device__ __forceinline__ void epilogue_store(const Epilogue& e, OutT* __restri
   float v = e.alpha * acc;
   if (e.bias) v += e.bias[n];
   if (e.rowadd) v += e.rowadd[(long)(m % e.rowadd_mod) * e.rowadd_ld + n];
+  if (n >= e.colscale_lo && n < e.colscale_hi) v *= e.colscale;
   switch (e.act) {
     case ACT_GELU:
       if (e.aux_out) ((OutT*)e.aux_out)[(long)m * e.ldo + n] = from_f<OutT>(v);

@@ -132,6 +132,10 @@ __device__ __forceinline__ void epilogue_store8(const Epilogue& e, OutT* __restr
 #pragma unroll
     for (int j = 0; j < 4; ++j) { x[j] += r0[j]; x[4 + j] += r1[j]; }
   }
+  if (n0 >= e.colscale_lo && n0 < e.colscale_hi) {    // the range is a multiple of 8 columns (host-checked)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) x[j] *= e.colscale;
+  }
   if (e.act == ACT_GELU) {
     if (e.aux_out) store8<OutT>((OutT*)e.aux_out + (long)m * e.ldo + n0, x);
 #pragma unroll
@@ -972,6 +976,7 @@ extern "C" int cmhar_gemm_bf16_phased(int layout, int out_dtype, int M, int N, i
   Epilogue plain{};
   plain.alpha = 1.f;
   const Epilogue& e = epi ? *epi : plain;             // NULL = the plain product
+  if ((e.colscale_lo | e.colscale_hi) & 7) return -1;  // whole 8-column epilogue groups
 #define DISPATCH(AK, BKc)                                                                                     \
   return out_dtype == CMHAR_BF16                                                                              \
              ? launch<bf16, AK, BKc, bf16>(M, N, K, a, lda, b, ldb, (bf16*)C, ldc, e, splits, w, stream, phases)    \
@@ -1004,6 +1009,7 @@ extern "C" int cmhar_gemm_f16(int layout, int out_dtype, int M, int N, int K, co
   plain.alpha = 1.f;
   const Epilogue& e = epi ? *epi : plain;
   if (e.rowsum) return -3;
+  if ((e.colscale_lo | e.colscale_hi) & 7) return -1;
   const bf16* a = (const bf16*)A;
   const bf16* b = (const bf16*)B;
   return out_dtype == CMHAR_F16

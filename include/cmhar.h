@@ -43,7 +43,9 @@ typedef struct CmharEpilogue {
   float* rowsum;          /* layout 2 (weight gradient) only: rowsum[m] = Σ_k A(m,k) + rowsum_beta·rowsum[m] —
                              the bias gradient Σ_tokens dY, taken from the same MFMA operand tiles; or NULL */
   float rowsum_beta;
-  int pad2_;
+  int colscale_lo;        /* columns [colscale_lo, colscale_hi) (multiples of 8) of alpha·acc + bias + rowadd are */
+  int colscale_hi;        /* multiplied by colscale before the activation (the pre-scaled attention keys of the  */
+  float colscale;         /* QKV projection); lo == hi: none */
 } CmharEpilogue;
 
 int cmhar_version(void);
@@ -100,6 +102,15 @@ int cmhar_attention_bwd(int dtype, int B, int H, int Lq, int Lk, int D, const vo
                         long ldk, const void* V, long ldv, const void* O, long ldo, const void* dO, long lddo,
                         const float* lse, float* delta, void* dQ, long lddq, void* dK, long lddk, void* dV, long lddv,
                         float scale, float pdrop, unsigned long long seed, hipStream_t stream);
+/* bf16, D = 64 flash backward for PRE-SCALED keys (the VideoMAE training path): K holds bf16(scale·log2(e)·K),
+ * written by the QKV GEMM's epilogue (CmharEpilogue.colscale over the key columns), and the forward was run with
+ * scale = 1/log2(e) — so the recomputed scores are already in the exp2 domain and the per-score multiply is gone.
+ * `scale` is the true softmax scale; dQ, dV and dK are the gradients of Q, V and the UNSCALED key (the QKV backward
+ * is unchanged).  (replaces: the same VideoMAESelfAttention backward as cmhar_attention_bwd) */
+int cmhar_attention_bwd_prescaled(int B, int H, int Lq, int Lk, const void* Q, long ldq, const void* K, long ldk,
+                                  const void* V, long ldv, const void* O, long ldo, const void* dO, long lddo,
+                                  const float* lse, float* delta, void* dQ, long lddq, void* dK, long lddk, void* dV,
+                                  long lddv, float scale, hipStream_t stream);
 
 /* y = LayerNorm(a + dropout(b)) (b nullable); h_out (nullable) receives a + dropout(b)
  * (replaces: VideoMAE layernorm_before/after modeling_videomae.py:337-350, IMU post-LN norm1/norm2 and

@@ -273,6 +273,41 @@ def test_flash_attention_bf16_fwd_bwd(L_):
     assert rel(dqkv[:, 2 * H * D:], gv) < 2e-2
 
 
+@pytest.mark.parametrize('L_', [200, 1568])
+def test_flash_attention_prescaled_keys(L_):
+    """The VideoMAE bf16 training form: the QKV GEMM's epilogue writes K pre-scaled by scale·log2(e) (colscale), the
+    forward runs with scale = 1/log2(e) and cmhar_attention_bwd_prescaled returns dQ, dV and the gradient of the
+    UNSCALED key — vs torch fp32 autograd on the unscaled operands, at the plain flash kernels' bounds; and the
+    colscale epilogue itself against the unscaled GEMM (same fp32 product, one rounding)."""
+    torch.manual_seed(12)
+    B, H, D = 2, 3, 64
+    Hd, scale = H * D, D ** -0.5
+    c = scale * K().LOG2E
+    x = torch.randn(B * L_, 256, device=DEV).bfloat16()
+    w = (torch.randn(3 * Hd, 256, device=DEV) * 0.1).bfloat16()
+    bias = torch.randn(3 * Hd, device=DEV) * 0.1
+    qkv = K().linear(x, w, bias, colscale=(Hd, 2 * Hd, c))
+    plain = (x.float() @ w.float().T + bias)
+    assert rel(qkv[:, :Hd], plain[:, :Hd]) < 5e-3 and rel(qkv[:, 2 * Hd:], plain[:, 2 * Hd:]) < 5e-3
+    assert rel(qkv[:, Hd:2 * Hd], c * plain[:, Hd:2 * Hd]) < 5e-3
+    q, kp, v = qkv[:, :Hd], qkv[:, Hd:2 * Hd], qkv[:, 2 * Hd:]
+    o = torch.empty(B * L_, Hd, dtype=torch.bfloat16, device=DEV)
+    lse = torch.empty(B * H * L_, device=DEV)
+    K().attention_fwd(q, kp, v, o, lse, B=B, H=H, Lq=L_, Lk=L_, D=D, scale=1.0 / K().LOG2E)
+    qr, vr = q.float().clone().requires_grad_(True), v.float().clone().requires_grad_(True)
+    kr = (kp.float() / c).requires_grad_(True)                # the unscaled key the model means
+    ref = _attn_ref(qr, kr, vr, B, H, L_, L_, D, scale)
+    assert rel(o, ref) < 1e-2
+    do = torch.randn(B * L_, Hd, device=DEV).bfloat16()
+    gq, gk, gv = torch.autograd.grad(ref, (qr, kr, vr), do.float())
+    dqkv = torch.empty_like(qkv)
+    K().attention_bwd_prescaled(q, kp, v, o, do, lse, dqkv[:, :Hd], dqkv[:, Hd:2 * Hd], dqkv[:, 2 * Hd:],
+                                B=B, H=H, Lq=L_, Lk=L_, D=D, scale=scale)
+    assert rel(dqkv[:, :Hd], gq) < 2e-2
+    assert rel(dqkv[:, Hd:2 * Hd], gk) < 2e-2
+    assert rel(dqkv[:, 2 * Hd:], gv) < 2e-2
+
+
 @pytest.mark.parametrize('D', [16, 64])
 def test_attention_fp32_exact(D):
     torch.manual_seed(3)
