@@ -3,6 +3,8 @@ median per variant), so device/clock differences between boxes do not enter the 
 
     python tools/debug/gemm_ab.py libA.so libB.so [libC.so ...] [--rounds R] [--dtype bf16|fp32] [--tokens T]
               [--torch]     (--torch: also time torch.matmul on the same operands, as variant 'T')
+              [--epi]       (--epi: the bench step's epilogues — QKV bias + key colscale, out-proj / FC2 bias +
+                             residual, FC1 bias + GELU with GELU' saved, FC2 dgrad × GELU'; bf16 only)
 """
 import ctypes as C
 import os
@@ -55,6 +57,9 @@ def main():
     if '--torch' in args:
         args.remove('--torch')
         with_torch = True
+    epi = '--epi' in args
+    if epi:
+        args.remove('--epi')
     libs = [load(a) for a in args]
     if with_torch:
         libs.append(None)
@@ -69,8 +74,21 @@ def main():
         dx = torch.empty(T, n_in, device='cuda', dtype=dt)
         dw = torch.empty(n_out, n_in, device='cuda', dtype=torch.float32)
         fl = 2 * T * n_out * n_in
-        cases = [('fwd', lambda: K.gemm(0, x, w, y), lambda: torch.matmul(x, w.t(), out=y)),
-                 ('dgrad', lambda: K.gemm(1, dy, w, dx), lambda: torch.matmul(dy, w, out=dx)),
+        fkw, dkw = {}, {}
+        if epi:
+            b = torch.randn(n_out, device='cuda') * 0.1
+            fkw = {'bias': b}
+            if name == 'qkv':
+                fkw['colscale'] = (768, 1536, 0.125 * K.LOG2E)
+            if name in ('out', 'fc2'):
+                fkw['residual'] = torch.randn(T, n_out, device='cuda').to(dt)
+            if name == 'fc1':
+                fkw['act'] = _lib.ACT_GELU_SAVEGRAD
+                fkw['aux_out'] = torch.empty(T, n_out, device='cuda', dtype=dt)
+            if name == 'fc2':
+                dkw = {'act': _lib.ACT_MULAUX, 'aux_in': torch.rand(T, n_in, device='cuda').to(dt)}
+        cases = [('fwd', lambda: K.gemm(0, x, w, y, **fkw), lambda: torch.matmul(x, w.t(), out=y)),
+                 ('dgrad', lambda: K.gemm(1, dy, w, dx, **dkw), lambda: torch.matmul(dy, w, out=dx)),
                  ('wgrad', lambda: K.gemm(2, dy, x, dw), lambda: torch.matmul(dy.t(), x, out=dw) if dt == torch.float32
                   else dw.copy_(dy.t() @ x))]
         for tag, fn0, tfn in cases:
