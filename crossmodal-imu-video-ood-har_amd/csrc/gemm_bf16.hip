@@ -139,21 +139,21 @@ __device__ __forceinline__ void epilogue_store8(const Epilogue& e, OutT* __restr
   if (e.act == ACT_GELU) {
     if (e.aux_out) store8<OutT>((OutT*)e.aux_out + (long)m * e.ldo + n0, x);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) x[j] = gelu_erf(x[j]);
+    for (int j = 0; j < 8; ++j) x[j] = gelu_for<OutT>(x[j]);
   } else if (e.act == ACT_RELU) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) x[j] = fmaxf(x[j], 0.f);
   } else if (e.act == ACT_DGELU) {
     load8<OutT>((const OutT*)e.aux_in + (long)m * e.lda + n0, t);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) x[j] *= gelu_erf_grad(t[j]);
+    for (int j = 0; j < 8; ++j) x[j] *= gelu_grad_for<OutT>(t[j]);
   } else if (e.act == ACT_DRELU) {
     load8<OutT>((const OutT*)e.aux_in + (long)m * e.lda + n0, t);
 #pragma unroll
     for (int j = 0; j < 8; ++j) x[j] = t[j] > 0.f ? x[j] : 0.f;
   } else if (e.act == ACT_GELU_SAVEGRAD) {
 #pragma unroll
-    for (int j = 0; j < 8; ++j) gelu_pair(x[j], x[j], t[j]);
+    for (int j = 0; j < 8; ++j) gelu_pair_for<OutT>(x[j], x[j], t[j]);
     if (e.aux_out) store8<OutT>((OutT*)e.aux_out + (long)m * e.ldo + n0, t);
   } else if (e.act == ACT_MULAUX) {
     load8<OutT>((const OutT*)e.aux_in + (long)m * e.lda + n0, t);
