@@ -27,6 +27,21 @@ class Epilogue(C.Structure):
                 ('rowsum_beta', f32), ('colscale_lo', i32), ('colscale_hi', i32), ('colscale', f32)]
 
 
+class IMULayer(C.Structure):
+    """CmharIMULayer (include/cmhar.h): one post-LN encoder layer's parameters and saved activations."""
+    _fields_ = ([(n, vp) for n in ('w_qkv', 'b_qkv', 'w_out', 'b_out', 'ln1_g', 'ln1_b', 'w_ff1', 'b_ff1', 'w_ff2',
+                                   'b_ff2', 'ln2_g', 'ln2_b')] + [('eps1', f32), ('eps2', f32)] +
+                [(n, vp) for n in ('qkv', 'o', 'lse', 's1', 'mu1', 'rs1', 'h1', 'fd', 's2', 'mu2', 'rs2', 'h2')])
+
+
+class IMULayerGrad(C.Structure):
+    """CmharIMULayerGrad (include/cmhar.h): one layer's token-gradient scratch and parameter gradients."""
+    _fields_ = [(n, vp) for n in ('dqkv', 'da', 'dpre', 'df2', 'gln1', 'gln2', 'dw_qkv', 'db_qkv', 'dw_out', 'db_out',
+                                  'dln1_g', 'dln1_b', 'dw_ff1', 'db_ff1', 'dw_ff2', 'db_ff2', 'dln2_g', 'dln2_b')]
+
+
+IMU_MAX_LAYERS = 8
+
 _SIGS = {
     'cmhar_version': (i32, []),
     'cmhar_gemm_bf16': (i32, [i32, i32, i32, i32, i32, vp, i64, vp, i64, vp, i64, C.POINTER(Epilogue), i32, vp, vp]),
@@ -63,6 +78,10 @@ _SIGS = {
                                   vp, vp]),
     'cmhar_imu_embed_bwd': (i32, [i32, i32, i32, i32, i32, i32, i32, i32, i32, vp, vp, vp, vp, C.POINTER(vp),
                                   C.POINTER(vp), vp]),
+    'cmhar_imu_encoder_fwd': (i32, [i32, i32, i32, i32, i32, i32, vp, C.POINTER(IMULayer), vp, vp, f32, vp, vp, vp,
+                                    f32, f32, u64, vp]),
+    'cmhar_imu_encoder_bwd': (i32, [i32, i32, i32, i32, i32, i32, vp, C.POINTER(IMULayer), C.POINTER(IMULayerGrad),
+                                    vp, vp, vp, vp, vp, vp, vp, f32, f32, u64, vp]),
     'cmhar_copy2d': (i32, [i32, i32, i32, i32, vp, i64, vp, i64, f32, f32, f32, u64, vp]),
     'cmhar_logits_energy': (i32, [i32, i32, i32, vp, i64, f32, vp, vp, vp, vp]),
     'cmhar_cross_entropy_ws': (i64, [i32]),

@@ -17,6 +17,7 @@ from __future__ import annotations
 
 import ctypes
 import math
+import os
 
 import torch
 import torch.nn as nn
@@ -115,6 +116,8 @@ def _imu_forward(m: IMUEncoder, x, p, seed, save):
     nh = m.nhead
     dh = D // nh
     scale = 1.0 / math.sqrt(dh)
+    if _fused_ok(m, T):
+        return _imu_forward_fused(m, emb, p, seed, (B, Cc, Lx, N, T, M, D, nh, dh, scale))
     h = emb
     saved = []
     for i in range(len(m.transformer.layers)):
@@ -142,7 +145,119 @@ def _imu_forward(m: IMUEncoder, x, p, seed, save):
     return enc.view(B, T, D), st
 
 
+# The whole transformer stack + final norm as ONE launch (cmhar_imu_encoder_fwd, bit-identical to the per-op chain
+# above) at the reference geometry: d_model 128, 8 heads, FF 512, T <= 32 tokens.  CMHAR_IMU_FUSED=0 keeps the
+# per-op launches (A/B tests).
+_FUSED = os.environ.get('CMHAR_IMU_FUSED', '1') != '0'
+
+
+def _fused_ok(m, T):
+    if not _FUSED or m.d_model != 128 or m.nhead != 8 or not 1 <= T <= 32:
+        return False
+    layers = m.transformer.layers
+    if not 1 <= len(layers) <= L.IMU_MAX_LAYERS:
+        return False
+    for lay in layers:
+        if lay.linear1.out_features != 512 or lay.norm_first or lay.activation_relu_or_gelu != 1:
+            return False
+    return all(q.dtype == torch.float32 and q.is_contiguous() for q in m.parameters())
+
+
+def _imu_forward_fused(m, emb, p, seed, geom):
+    B, Cc, Lx, N, T, M, D, nh, dh, scale = geom
+    nl = len(m.transformer.layers)
+    # one arena per call: per layer qkv | o | s1 | h1 | fd | s2 | h2 (M rows each) | lse | mu1 | rs1 | mu2 | rs2
+    per = M * 12 * D + B * nh * T + 4 * M
+    arena = torch.empty(nl * per + 2 * M, dtype=torch.float32, device=emb.device)
+    arr = (L.IMULayer * nl)()
+    saved = []
+    h = emb
+    for i in range(nl):
+        lay = _layer(m, i)
+        base = i * per
+        views = {}
+        off = base
+        for name, w in (('qkv', 3 * D), ('o', D), ('s1', D), ('h1', D), ('fd', 4 * D), ('s2', D), ('h2', D)):
+            views[name] = arena[off:off + M * w].view(M, w)
+            off += M * w
+        views['lse'] = arena[off:off + B * nh * T]
+        off += B * nh * T
+        for name in ('mu1', 'rs1', 'mu2', 'rs2'):
+            views[name] = arena[off:off + M]
+            off += M
+        e = arr[i]
+        sa = lay.self_attn
+        for f, t in (('w_qkv', sa.in_proj_weight), ('b_qkv', sa.in_proj_bias), ('w_out', sa.out_proj.weight),
+                     ('b_out', sa.out_proj.bias), ('ln1_g', lay.norm1.weight), ('ln1_b', lay.norm1.bias),
+                     ('w_ff1', lay.linear1.weight), ('b_ff1', lay.linear1.bias), ('w_ff2', lay.linear2.weight),
+                     ('b_ff2', lay.linear2.bias), ('ln2_g', lay.norm2.weight), ('ln2_b', lay.norm2.bias)):
+            setattr(e, f, t.data_ptr())
+        e.eps1, e.eps2 = lay.norm1.eps, lay.norm2.eps
+        for name, t in views.items():
+            setattr(e, name, t.data_ptr())
+        saved.append((h, views['qkv'], views['o'], views['lse'], views['s1'], views['mu1'], views['rs1'], views['h1'],
+                      views['fd'], views['s2'], views['mu2'], views['rs2']))
+        h = views['h2']
+    muf = arena[nl * per:nl * per + M]
+    rsf = arena[nl * per + M:]
+    enc = torch.empty(M, D, dtype=torch.float32, device=emb.device)   # the module output: not an arena view
+    L.call('cmhar_imu_encoder_fwd', B, T, D, nh, 4 * D, nl, emb.data_ptr(), arr, m.norm.weight.data_ptr(),
+           m.norm.bias.data_ptr(), m.norm.eps, enc.data_ptr(), muf.data_ptr(), rsf.data_ptr(), scale, p, seed,
+           L.stream(emb.device))
+    st = dict(geom=geom, saved=saved, final=(h, muf, rsf), p=p, seed=seed, fused=(arr, emb))
+    return enc.view(B, T, D), st
+
+
+def _imu_backward_fused(m, x, st, d_enc):
+    """Two launches for the whole stack (cmhar_imu_encoder_bwd), then the embedding backward."""
+    B, Cc, Lx, N, T, M, D, nh, dh, scale = st['geom']
+    arr, emb = st['fused']
+    nl = len(m.transformer.layers)
+    dev = d_enc.device
+    layers = [_layer(m, i) for i in range(nl)]
+    # one arena: per layer the token-gradient scratch, then every parameter gradient, then dx
+    tok = M * (3 * D + D + 4 * D + D + D + D)
+    pshapes = []
+    for lay in layers:
+        sa = lay.self_attn
+        pshapes.append([(f, t) for f, t in (('dw_qkv', sa.in_proj_weight), ('db_qkv', sa.in_proj_bias),
+                                            ('dw_out', sa.out_proj.weight), ('db_out', sa.out_proj.bias),
+                                            ('dln1_g', lay.norm1.weight), ('dln1_b', lay.norm1.bias),
+                                            ('dw_ff1', lay.linear1.weight), ('db_ff1', lay.linear1.bias),
+                                            ('dw_ff2', lay.linear2.weight), ('db_ff2', lay.linear2.bias),
+                                            ('dln2_g', lay.norm2.weight), ('dln2_b', lay.norm2.bias))])
+    # parameter gradients start on 16-B boundaries (4 floats) so every view is vector-aligned
+    psize = sum(((t.numel() + 3) // 4) * 4 for ps in pshapes for _, t in ps)
+    arena = torch.empty(nl * tok + psize + 2 * D + M * D, dtype=torch.float32, device=dev)
+    garr = (L.IMULayerGrad * nl)()
+    grads = {}
+    off = 0
+    for i in range(nl):
+        g = garr[i]
+        for name, w in (('dqkv', 3 * D), ('da', D), ('dpre', 4 * D), ('df2', D), ('gln1', D), ('gln2', D)):
+            setattr(g, name, arena[off:off + M * w].data_ptr())
+            off += M * w
+    for i in range(nl):
+        for name, t in pshapes[i]:
+            v = arena[off:off + t.numel()].view(t.shape)
+            off += ((t.numel() + 3) // 4) * 4
+            setattr(garr[i], name, v.data_ptr())
+            grads[t] = v
+    dgf, dbf = arena[off:off + D], arena[off + D:off + 2 * D]
+    off += 2 * D
+    dx = arena[off:off + M * D].view(M, D)
+    h, muf, rsf = st['final']
+    L.call('cmhar_imu_encoder_bwd', B, T, D, nh, 4 * D, nl, emb.data_ptr(), arr, garr, m.norm.weight.data_ptr(),
+           muf.data_ptr(), rsf.data_ptr(), d_enc.data_ptr(), dgf.data_ptr(), dbf.data_ptr(), dx.data_ptr(), scale,
+           st['p'], st['seed'], L.stream(dev))
+    grads[m.norm.weight], grads[m.norm.bias] = dgf, dbf
+    _embed_backward(m, x, st, dx, grads)
+    return grads
+
+
 def _imu_backward(m: IMUEncoder, x, st, d_enc):
+    if 'fused' in st:
+        return _imu_backward_fused(m, x, st, d_enc)
     B, Cc, Lx, N, T, M, D, nh, dh, scale = st['geom']
     p, seed = st['p'], st['seed']
     dev = d_enc.device
@@ -185,7 +300,17 @@ def _imu_backward(m: IMUEncoder, x, st, d_enc):
         dh_ = K.linear_dgrad(dqkv, lay.self_attn.in_proj_weight, residual=ds1)
         grads[lay.self_attn.in_proj_weight] = K.linear_wgrad(dqkv, hin)
         grads[lay.self_attn.in_proj_bias] = K.colsum(dqkv)
-    # embedding
+    _embed_backward(m, x, st, dh_, grads)
+    return grads
+
+
+def _embed_backward(m, x, st, dh_, grads):
+    B, Cc, Lx, N, T, M, D, nh, dh, scale = st['geom']
+    dev = dh_.device
+
+    def g32(t):
+        return torch.empty(t.shape, dtype=torch.float32, device=dev)
+
     dcls = g32(m.cls_token)
     dpos = g32(m.pos_encoding)
     dws = [g32(lin.weight) for lin in m.patch_embed.projections]
@@ -195,7 +320,6 @@ def _imu_backward(m: IMUEncoder, x, st, d_enc):
     grads[m.cls_token], grads[m.pos_encoding] = dcls, dpos
     for lin, dw, db in zip(m.patch_embed.projections, dws, dbs):
         grads[lin.weight], grads[lin.bias] = dw, db
-    return grads
 
 
 class _IMUFn(torch.autograd.Function):
@@ -216,7 +340,7 @@ class _IMUFn(torch.autograd.Function):
         B, Cc, Lx, N, T, M, D = st['geom'][:7]
         d = torch.zeros(M, D, dtype=torch.float32, device=x.device)
         if denc is not None:
-            K.copy2d(denc.reshape(M, D), d)
+            K.copy2d(denc.reshape(M, D).contiguous(), d)   # (an expanded gradient, e.g. of enc.sum(), has stride 0)
         if dcls is not None:
             K.copy2d(dcls.contiguous(), d.view(B, T * D)[:, :D], beta=1.0)
         grads = _imu_backward(ctx.module, x, st, d)

@@ -12,6 +12,7 @@
 // fp32 path (any head dim <= 64): exact-f32 scalar kernels with the same algorithm, used by the fp32 parity mode
 // and the tiny IMU attention (L = 13, d = 16), including counter-hash dropout regenerated in backward.
 #include "common.h"
+#include "rowops.h"
 
 #include <initializer_list>
 #include <type_traits>
@@ -651,19 +652,6 @@ __global__ __launch_bounds__(256, QB == 1 ? CMHAR_DQ_OCC : 2) void attn_bwd_dq_b
 // ---------------------------------------------------------------------------------------------------------------
 // exact fp32 path (any head dim <= 64), with optional attention-prob dropout (nn.MultiheadAttention semantics)
 // ---------------------------------------------------------------------------------------------------------------
-__device__ __forceinline__ unsigned hash4(unsigned long long seed, unsigned a, unsigned b, unsigned c) {
-  unsigned long long x = seed ^ (0x9E3779B97F4A7C15ull * (a + 1)) ^ (0xC2B2AE3D27D4EB4Full * (b + 1)) ^
-                         (0x165667B19E3779F9ull * (c + 1));
-  x ^= x >> 33; x *= 0xff51afd7ed558ccdull; x ^= x >> 33; x *= 0xc4ceb9fe1a85ec53ull; x ^= x >> 33;
-  return (unsigned)x;
-}
-// keep-mask for attention prob (bh, q, k): keep iff hash >= p * 2^32
-__device__ __forceinline__ float drop_scale(unsigned long long seed, float p, unsigned bh, unsigned q, unsigned k) {
-  if (p <= 0.f) return 1.f;
-  const float u = (float)hash4(seed, bh, q, k) * 2.3283064365386963e-10f;
-  return u >= p ? 1.f / (1.f - p) : 0.f;
-}
-
 template <typename T, int D>
 __global__ __launch_bounds__(64) void attn_fwd_f32(int H, int Lq, int Lk, const T* __restrict__ Q, long ldq, const T* __restrict__ K,
                              long ldk, const T* __restrict__ V, long ldv, T* __restrict__ O, long ldo,
@@ -687,20 +675,7 @@ __global__ __launch_bounds__(64) void attn_fwd_f32(int H, int Lq, int Lk, const 
       sV[kk][d] = ok ? to_f<T>(V[((long)b * Lk + k0 + kk) * ldv + hd * D + d]) : 0.f;
     }
     __syncthreads();
-    const int kn = min(64, Lk - k0);
-    for (int kk = 0; kk < kn; ++kk) {
-      float s = 0.f;
-#pragma unroll
-      for (int d = 0; d < D; ++d) s = fmaf(qv[d], sK[kk][d], s);
-      const float mn = fmaxf(m, s);
-      const float alpha = __expf(m - mn);
-      const float p = __expf(s - mn);
-      l = l * alpha + p;
-      const float pd = p * drop_scale(seed, pdrop, bh, qq, k0 + kk);
-#pragma unroll
-      for (int d = 0; d < D; ++d) o[d] = o[d] * alpha + pd * sV[kk][d];
-      m = mn;
-    }
+    attn_row_f32<D>(qv, o, m, l, &sK[0][0], D, &sV[0][0], D, min(64, Lk - k0), seed, pdrop, bh, qq, k0);
   }
   if (active) {
 #pragma unroll
@@ -727,7 +702,7 @@ __global__ __launch_bounds__(64) void attn_bwd_dq_f32(int H, int Lq, int Lk, con
   for (int d = 0; d < D; ++d) {
     qv[d] = to_f<T>(Q[((long)b * Lq + qq) * ldq + hd * D + d]) * scale;
     g[d] = to_f<T>(dO[((long)b * Lq + qq) * lddo + hd * D + d]);
-    delta += g[d] * to_f<T>(O[((long)b * Lq + qq) * ldo + hd * D + d]);
+    delta = fmaf(g[d], to_f<T>(O[((long)b * Lq + qq) * ldo + hd * D + d]), delta);   // explicit: as the fused IMU kernel
     dq[d] = 0.f;
   }
   const float L = lse[(long)bh * Lq + qq];
@@ -740,16 +715,7 @@ __global__ __launch_bounds__(64) void attn_bwd_dq_f32(int H, int Lq, int Lk, con
       sV[kk][d] = ok ? to_f<T>(V[((long)b * Lk + k0 + kk) * ldv + hd * D + d]) : 0.f;
     }
     __syncthreads();
-    const int kn = min(64, Lk - k0);
-    for (int kk = 0; kk < kn; ++kk) {
-      float s = 0.f, dp = 0.f;
-#pragma unroll
-      for (int d = 0; d < D; ++d) { s = fmaf(qv[d], sK[kk][d], s); dp = fmaf(g[d], sV[kk][d], dp); }
-      const float p = __expf(s - L);
-      const float ds = p * (dp * drop_scale(seed, pdrop, bh, qq, k0 + kk) - delta);
-#pragma unroll
-      for (int d = 0; d < D; ++d) dq[d] = fmaf(ds, sK[kk][d], dq[d]);
-    }
+    attn_row_dq_f32<D>(qv, g, L, delta, dq, &sK[0][0], D, &sV[0][0], D, min(64, Lk - k0), seed, pdrop, bh, qq, k0);
   }
   if (active) {
 #pragma unroll
@@ -793,20 +759,9 @@ __global__ __launch_bounds__(64) void attn_bwd_dkdv_f32(int H, int Lq, int Lk, c
       Ds[i] = ok ? delta[(long)bh * Lq + q0 + i] : 0.f;
     }
     __syncthreads();
-    const int qn = min(64, Lq - q0);
-    for (int qi = 0; qi < qn; ++qi) {
-      float s = 0.f, dp = 0.f;
-#pragma unroll
-      for (int d = 0; d < D; ++d) { s = fmaf(sQ[qi][d], kv[d], s); dp = fmaf(sG[qi][d], vv[d], dp); }
-      const float p = __expf(s - Ls[qi]);
-      const float ms = drop_scale(seed, pdrop, bh, q0 + qi, kk);
-      const float ds = p * (dp * ms - Ds[qi]);
-#pragma unroll
-      for (int d = 0; d < D; ++d) {
-        dv[d] = fmaf(p * ms, sG[qi][d], dv[d]);
-        dk[d] = fmaf(ds, sQ[qi][d], dk[d]);     // Qs already carries the scale
-      }
-    }
+    // sQ already carries the scale (qs = 1)
+    attn_row_dkdv_f32<D>(kv, vv, dk, dv, &sQ[0][0], D, 1.f, &sG[0][0], D, Ls, Ds, min(64, Lq - q0), seed, pdrop, bh,
+                         q0, kk);
   }
   if (active) {
 #pragma unroll

@@ -6,15 +6,10 @@
 //   L2 normalise       — F.normalize(dim=1, eps=1e-12) (models.py:288-289).
 //   column sums        — bias gradients and slab reductions.
 #include "common.h"
+#include "rowops.h"
 #include <algorithm>
 
 namespace {
-
-__device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
-  return v;
-}
 
 // Two independent wave sums with their shuffle chains interleaved (half the dependent latency of two calls).
 __device__ __forceinline__ void wave_sum2(float& a, float& b) {
@@ -48,35 +43,9 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(int M, int N, const T* __re
   const int lane = threadIdx.x & 63;
   const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= M) return;
-  float v[MAXPER];
-  float s = 0.f;
-#pragma unroll
-  for (int i = 0; i < MAXPER; ++i) {
-    const int c = lane + 64 * i;
-    v[i] = 0.f;
-    if (c < N) {
-      float x = to_f<T>(a[row * lda + c]);
-      if (b) x += to_f<T>(b[row * ldb + c]) * elem_drop(seed, pdrop, row, c);
-      v[i] = x;
-      s += x;
-    }
-  }
-  const float mu = wave_sum(s) / N;
-  float q = 0.f;
-#pragma unroll
-  for (int i = 0; i < MAXPER; ++i) {
-    const int c = lane + 64 * i;
-    if (c < N) { const float d = v[i] - mu; q += d * d; }
-  }
-  const float r = rsqrtf(wave_sum(q) / N + eps);
-#pragma unroll
-  for (int i = 0; i < MAXPER; ++i) {
-    const int c = lane + 64 * i;
-    if (c < N) {
-      if (h_out) h_out[row * ldh + c] = from_f<T>(v[i]);
-      y[row * ldy + c] = from_f<T>((v[i] - mu) * r * gamma[c] + beta[c]);
-    }
-  }
+  float mu, r;
+  ln_row_fwd<T>(lane, row, N, a + row * lda, b ? b + row * ldb : nullptr, pdrop, seed, h_out ? h_out + row * ldh : nullptr,
+                y + row * ldy, gamma, beta, eps, mu, r);
   if (lane == 0) { mean[row] = mu; rstd[row] = r; }
 }
 
@@ -161,31 +130,13 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(int M, int N, const T* __re
   for (int u = 0; u < LN_BWD_PF; ++u) {
     const long row = row0 + rg + u;
     if (row >= M) break;
-    const float mu = pmu[u], r = prs[u];
-    float xh[MP], g[MP];
-    float s1 = 0.f, s2 = 0.f;
-#pragma unroll
-    for (int i = 0; i < MP; ++i) {
-      const int c = lane + 64 * i;
-      xh[i] = 0.f;
-      g[i] = 0.f;
-      if (c < N) {
-        const float d = pd[u][i];
-        xh[i] = (ph[u][i] - mu) * r;
-        g[i] = d * gamma[c];
-        ag[i] += d * xh[i];
-        ab[i] += d;
-        s1 += g[i];
-        s2 += g[i] * xh[i];
-      }
-    }
-    s1 = wave_sum(s1) / N;
-    s2 = wave_sum(s2) / N;
+    float gx[MP];
+    ln_row_bwd<MP>(lane, N, pd[u], ph[u], pmu[u], prs[u], gamma, ag, ab, gx);
 #pragma unroll
     for (int i = 0; i < MP; ++i) {
       const int c = lane + 64 * i;
       if (c < N) {
-        float v = r * (g[i] - s1 - xh[i] * s2);
+        float v = gx[i];
         if (dres) v += to_f<T>(dres[row * ldres + c]);
         dh[row * lddh + c] = from_f<T>(v);
         if (db_out) db_out[row * lddb + c] = from_f<T>(v * elem_drop(seed, pdrop, row, c));

@@ -163,6 +163,44 @@ int cmhar_imu_embed_bwd(int B, int C, int L, int N, int P, int S, int D, int T, 
                         const float* dout, float* dcls, float* dpos, float* const* dw, float* const* db,
                         hipStream_t stream);
 
+/* One post-LN nn.TransformerEncoderLayer of the IMU encoder (models.py:85-95 with d_model 128, 8 heads, FF 512):
+ * parameters (fp32, torch layouts: in_proj [384,128], out_proj [128,128], linear1 [512,128], linear2 [128,512]) and
+ * the activations the backward reads, written as [B*T, width] rows: qkv [.,384], o [.,128], lse [B*8*T], s1 = h +
+ * drop(attn), mu1 / rs1 [B*T], h1 = LN1(s1), fd = drop(relu(linear1(h1))) [.,512], s2 = h1 + drop(linear2(fd)),
+ * mu2 / rs2, h2 = LN2(s2). */
+#define CMHAR_IMU_MAX_LAYERS 8
+typedef struct CmharIMULayer {
+  const float *w_qkv, *b_qkv, *w_out, *b_out, *ln1_g, *ln1_b, *w_ff1, *b_ff1, *w_ff2, *b_ff2, *ln2_g, *ln2_b;
+  float eps1, eps2;
+  float *qkv, *o, *lse, *s1, *mu1, *rs1, *h1, *fd, *s2, *mu2, *rs2, *h2;
+} CmharIMULayer;
+/* The IMU encoder's transformer stack + final LayerNorm in ONE launch (replaces: IMUEncoder.forward's
+ * self.transformer(x) and self.norm(x), models.py:125-130): one workgroup per window keeps its T <= 32 token rows in
+ * LDS through all `nlayers` (<= CMHAR_IMU_MAX_LAYERS) layers.  x: [B*T, 128] embedded tokens; layers: HOST array;
+ * enc = norm(h2 of the last layer) with its mean / rstd.  Dropout (pdrop, layer i's streams from seed + 7919(i+1))
+ * as the separate kernels; every output is bit-identical to the per-op launches (cmhar_gemm_generic,
+ * cmhar_attention_fwd, cmhar_layernorm_fwd).  Returns -1 for other geometries (D != 128, H != 8, FF != 512, T > 32). */
+int cmhar_imu_encoder_fwd(int B, int T, int D, int H, int FF, int nlayers, const float* x, const CmharIMULayer* layers,
+                          const float* norm_g, const float* norm_b, float norm_eps, float* enc, float* norm_mu,
+                          float* norm_rs, float scale, float pdrop, unsigned long long seed, hipStream_t stream);
+/* Per-layer outputs of the fused backward: token-gradient scratch [B*T, width] (dqkv 384, da 128, dpre 512, df2 128,
+ * gln1 / gln2 = the incoming gradients of norm1 / norm2, 128) and the parameter gradients (parameter shapes). */
+typedef struct CmharIMULayerGrad {
+  float *dqkv, *da, *dpre, *df2, *gln1, *gln2;
+  float *dw_qkv, *db_qkv, *dw_out, *db_out, *dln1_g, *dln1_b, *dw_ff1, *db_ff1, *dw_ff2, *db_ff2, *dln2_g, *dln2_b;
+} CmharIMULayerGrad;
+/* Backward of cmhar_imu_encoder_fwd (replaces: autograd through models.py:125-130) from the tensors it saved
+ * (layers: the same array; x: its input) and d_enc = dL/d(encoded tokens) [B*T, 128]: dx [B*T, 128] for the
+ * embedding backward, every layer's parameter gradients (grads, nlayers entries) and the final norm's (dnorm_g,
+ * dnorm_b).  Two launches: one workgroup per window runs the token-gradient chain through all layers (dgrads and
+ * attention backward bit-identical to the per-op launches); one grouped launch forms every weight gradient (the
+ * same token-ordered chain as the weight-gradient GEMM) and the bias / affine column sums (sequential over tokens;
+ * the per-op path sums in two levels, so these differ from it by rounding only). */
+int cmhar_imu_encoder_bwd(int B, int T, int D, int H, int FF, int nlayers, const float* x, const CmharIMULayer* layers,
+                          const CmharIMULayerGrad* grads, const float* norm_g, const float* norm_mu,
+                          const float* norm_rs, const float* d_enc, float* dnorm_g, float* dnorm_b, float* dx,
+                          float scale, float pdrop, unsigned long long seed, hipStream_t stream);
+
 /* dst[r, c] = alpha * src[r, c] * dropmask(seed, pdrop, r, c) + beta * dst[r, c], with dtype conversion
  * (token-0 gather, casts, gradient adds, nn.Dropout forward/backward, models.py:85-95, 311-322). */
 int cmhar_copy2d(int in_dtype, int out_dtype, int rows, int cols, const void* src, long lds, void* dst, long ldd,

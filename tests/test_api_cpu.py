@@ -31,8 +31,9 @@ def test_library_exports_every_declared_symbol():
     assert lib.cmhar_version() == 1
 
 
-def test_epilogue_struct_layout_matches_header(tmp_path):
-    """ctypes mirror vs the C compiler's view of CmharEpilogue (offsetof every field, sizeof)."""
+@pytest.mark.parametrize('cname,pyname', [('CmharEpilogue', 'Epilogue'), ('CmharIMULayer', 'IMULayer')])
+def test_struct_layout_matches_header(tmp_path, cname, pyname):
+    """ctypes mirrors vs the C compiler's view of the ABI structs (offsetof every field, sizeof)."""
     import ctypes
     import shutil
     import subprocess
@@ -40,15 +41,16 @@ def test_epilogue_struct_layout_matches_header(tmp_path):
     cc = shutil.which('gcc')
     if cc is None:
         pytest.skip('gcc not available')
-    fields = [f for f, _ in _lib.Epilogue._fields_]
+    cls = getattr(_lib, pyname)
+    fields = [f for f, _ in cls._fields_]
     src = tmp_path / 'probe.c'      # plain C: the header must be consumable by a C / cgo / FFI binding
-    src.write_text('#include "cmhar.h"\n#include <stdio.h>\n#include <stddef.h>\nint main(){printf("%zu", sizeof(CmharEpilogue));'
-                   + ''.join(f'printf(" %zu", offsetof(CmharEpilogue, {f}));' for f in fields) + 'return 0;}\n')
+    src.write_text(f'#include "cmhar.h"\n#include <stdio.h>\n#include <stddef.h>\nint main(){{printf("%zu", sizeof({cname}));'
+                   + ''.join(f'printf(" %zu", offsetof({cname}, {f}));' for f in fields) + 'return 0;}\n')
     exe = tmp_path / 'probe'
     subprocess.run([cc, '-D__HIP_PLATFORM_AMD__', '-I/opt/rocm/include', f'-I{REPO}/include', str(src), '-o',
                     str(exe)], check=True, capture_output=True)
     got = [int(v) for v in subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split()]
-    want = [ctypes.sizeof(_lib.Epilogue)] + [getattr(_lib.Epilogue, f).offset for f in fields]
+    want = [ctypes.sizeof(cls)] + [getattr(cls, f).offset for f in fields]
     assert got == want
 
 
