@@ -17,6 +17,9 @@
 namespace {
 
 constexpr int ID = 128, IH = 8, IDH = 16, IFF = 512, NT = 512;
+#ifndef CMHAR_IMU_KCX
+#define CMHAR_IMU_KCX 2   // chunk-size multiplier of the 128-wide weights (A/B builds)
+#endif
 
 struct IMULayerPack { CmharIMULayer l[CMHAR_IMU_MAX_LAYERS]; };
 
@@ -27,6 +30,9 @@ template <int RM> struct IMUCfg {
   static constexpr int LDD = ID + 4, LDF = IFF + 4, LDW = KC + 4;
   static constexpr int HS = 0, BG = HS + RM * LDD, OS = BG + RM * LDF, H1 = OS + RM * LDD, WS = H1 + RM * LDD;
   static constexpr int FLOATS = WS + IFF * LDW;
+  // the N = 128 GEMMs (out-proj, FC2) take 2× the k per chunk in the same buffer: a chunk's L2 latency is exposed
+  // once per chunk, and their chunks carry a quarter of the FMAs of the N = 512 ones
+  static constexpr int kc_for(int N) { return N == ID ? CMHAR_IMU_KCX * KC : KC; }
 };
 
 // acc[i][j] = Σ_k X[rg + 4i][k] · W[cg + 128j][k], k ascending from 0 (cmhar_gemm_generic's per-output chain).
@@ -37,8 +43,8 @@ template <int RM, int N, int K>
 __device__ __forceinline__ void blk_gemm(const float* __restrict__ W, const float* X, int ldx, float* Ws,
                                          float (&acc)[RM / 4][N / 128], int tid) {
   using C = IMUCfg<RM>;
-  constexpr int KC = C::KC, LDW = C::LDW, NJ = N / 128, RPT = RM / 4, KQ = KC / 4, NF = N * KQ / NT;
-  static_assert((N * KQ) % NT == 0 && K % KC == 0, "chunking");
+  constexpr int KC = C::kc_for(N), LDW = KC + 4, NJ = N / 128, RPT = RM / 4, KQ = KC / 4, NF = N * KQ / NT;
+  static_assert((N * KQ) % NT == 0 && K % KC == 0 && N * LDW <= IFF * C::LDW, "chunking");
   const int cg = tid & 127, rg = tid >> 7;
 #pragma unroll
   for (int i = 0; i < RPT; ++i)
@@ -246,9 +252,10 @@ template <int RM, int NOUT, int NC>
 __device__ __forceinline__ void blk_dgrad(const float* __restrict__ W, const float* X, int ldx, float* Ws,
                                           float (&acc)[RM / 4][NOUT / 128], int tid) {
   using C = IMUBCfg<RM>;
-  constexpr int KC = C::KC, LDW = C::LDF, NJ = NOUT / 128, RPT = RM / 4, NQ = NOUT / 4;
+  // N = 128-wide weights: rows of 132 floats, so 2× (RM = 32) to 2× (RM = 16) the rows per chunk in the same buffer
+  constexpr int KC = NOUT == ID ? CMHAR_IMU_KCX * C::KC : C::KC, LDW = NOUT + 4, NJ = NOUT / 128, RPT = RM / 4, NQ = NOUT / 4;
   constexpr int TOT = KC * NQ, NF = (TOT + NT - 1) / NT;
-  static_assert(NC % KC == 0 && KC % 4 == 0, "chunking");
+  static_assert(NC % KC == 0 && KC % 4 == 0 && KC * LDW <= C::KC * C::LDF, "chunking");
   const int cg = tid & 127, rg = tid >> 7;
 #pragma unroll
   for (int i = 0; i < RPT; ++i)
