@@ -219,3 +219,22 @@ def test_cnn2d_backbones_torchvision_layout():
     venc = VideoEncoder(cfg)
     assert venc.feature_dim == 512 and hasattr(venc, 'temporal_pool')
     assert all(k.startswith(('backbone.', 'projection.')) for k in venc.state_dict())
+
+
+def test_imu_fused_gating():
+    """The one-launch IMU encoder takes the reference geometry (d 128, 8 heads, FF 512, T <= 32, <= 8 layers) and
+    leaves every other geometry to the per-op launches (CPU check of the dispatch only; the kernels are
+    tests/test_imu_fused_gpu.py)."""
+    from cmhar import imu
+    from cmhar.config import Config
+    from cmhar.imu import IMUEncoder
+    ok = []
+    for W, d, nh, nl in ((200, 128, 8, 4), (250, 128, 8, 4), (400, 128, 8, 4), (600, 128, 8, 4), (200, 64, 8, 4),
+                         (200, 128, 4, 4), (200, 128, 8, 9)):
+        cfg = Config()
+        cfg.data.imu_window_size = W
+        cfg.model.imu_d_model, cfg.model.imu_nhead, cfg.model.imu_num_layers = d, nh, nl
+        m = IMUEncoder(cfg)
+        T = min(1 + 6 * ((W - 16) // 16 + 1), m.pos_encoding.shape[1])
+        ok.append(imu._fused_ok(m, T))
+    assert ok == [True, True, True, False, False, False, False]
