@@ -169,12 +169,70 @@ def cpu_baseline(cfg_builder, batch, warmup, steps, frames, image, imu_len):
         fwd()
         log(f'cpu eval forward {i + 1}: {time.perf_counter() - t1:.1f} s')
     dte = time.perf_counter() - t1
-    return {'value': round(batch * steps / dt, 4), 'unit': 'clips/sec', 'cores': threads, 'kind': 'port',
+    rows = {}
+    if image > 112:
+        # BASELINE.md plan: the same procedure at 16x112^2 (the sinusoid position table follows the token count)
+        video112 = torch.randn(batch, frames, 3, 112, 112, generator=g)
+        vsave = video
+
+        def run112(train):
+            nonlocal video
+            video = video112
+            try:
+                if train:
+                    step(warmup + steps + 1)
+                else:
+                    fwd()
+            finally:
+                video = vsave
+        run112(True)
+        t2 = time.perf_counter()
+        for i in range(steps):
+            run112(True)
+        rows['train_112_clips_per_sec'] = round(batch * steps / (time.perf_counter() - t2), 4)
+        run112(False)
+        t2 = time.perf_counter()
+        for i in range(steps):
+            run112(False)
+        rows['eval_fwd_112_clips_per_sec'] = round(batch * steps / (time.perf_counter() - t2), 4)
+        log(f'cpu 112^2 rows: {rows}')
+    # IMU-only (batch 8): the IMU encoder + its projection head + F.normalize, fwd+bwd against fixed unit targets
+    # through the SigLIP loss, clip + AdamW over the IMU-side parameters
+    imu8 = torch.randn(8, 6, imu_len, generator=g)
+    tgt = O.l2_normalize(torch.randn(8, 256, generator=g))
+    inames = [k for k in names if k.startswith(('imu_encoder.', 'imu_proj.'))]
+    im = [torch.zeros_like(sd[k]) for k in inames]
+    iv = [torch.zeros_like(sd[k]) for k in inames]
+
+    def imu_step(i):
+        for k in inames:
+            sd[k].grad = None
+        cls, _ = O.imu_encoder(sd, imu8, patch_size=16, stride=16, nhead=8, num_layers=4, dropout=0.1, training=True,
+                               gen=g)
+        a = O.l2_normalize(O.projection_head(sd, cls, 'imu_proj.', True))
+        O.siglip_loss(a, tgt, lt, lb).backward()
+        with torch.no_grad():
+            grads = [sd[k].grad for k in inames]
+            O.clip_grad_norm(grads, 1.0)
+            O.adamw_step([sd[k] for k in inames], grads, im, iv, i, lr=1e-5)
+    try:
+        for i in range(warmup):
+            imu_step(i + 1)
+        t3 = time.perf_counter()
+        for i in range(steps):
+            imu_step(warmup + i + 1)
+        rows['imu_only_b8_train_windows_per_sec'] = round(8 * steps / (time.perf_counter() - t3), 2)
+    except (TypeError, KeyError) as e:   # an oracle signature mismatch must not take the bench line down
+        log(f'cpu IMU-only row skipped: {e!r}')
+    return {'value': round(batch * steps / dt, 4), 'unit': 'clips/sec', 'cores': threads, 'kind': 'port', **rows,
             'cpu_model': cpu_name,
             'eval_fwd_clips_per_sec': round(batch * steps / dte, 4),
             'sample': f'oracle/cpu_model.py fp32 fwd+bwd+clip+AdamW, batch {batch}, {warmup} warm-up + {steps} timed '
                       f'steps, {frames}x{image}^2 video + 6x{imu_len} IMU, {threads} threads on {cpu_name}; eval row: '
-                      f'eval-mode forward, {steps} timed batches after 1 warm-up'}
+                      f'eval-mode forward, {steps} timed batches after 1 warm-up; 112 rows: the same two procedures on '
+                      f'16x112^2 clips (1 warm-up, {steps} timed); IMU-only row: batch 8 IMU encoder + projection head '
+                      f'+ normalize, SigLIP loss against fixed unit targets, fwd+bwd+clip+AdamW over the IMU-side '
+                      f'parameters, {warmup} warm-up + {steps} timed'}
 
 
 def main():

@@ -99,7 +99,7 @@ class FusedAdamW(torch.optim.Optimizer):
             b1, b2 = group['betas']
             lr, eps, wd = group['lr'], group['eps'], group['weight_decay']
             rows = []
-            steps = set()
+            step_ts = []
             dev = None
             for p in group['params']:
                 if p.grad is None:
@@ -111,17 +111,21 @@ class FusedAdamW(torch.optim.Optimizer):
                     st['step'] = torch.tensor(0.0)
                     st['exp_avg'] = torch.zeros_like(p, memory_format=torch.preserve_format)
                     st['exp_avg_sq'] = torch.zeros_like(p, memory_format=torch.preserve_format)
-                st['step'] += 1
-                steps.add(int(st['step'].item()))
+                step_ts.append(st['step'])
                 bf, cp = slots.get(p, (0, 0))
                 rows.append((p.data_ptr(), p.grad.data_ptr(), st['exp_avg'].data_ptr(),
                              st['exp_avg_sq'].data_ptr(), bf, cp, p.numel(), float(wd), 1.0))
                 dev = p.device
             if not rows:
                 continue
-            if len(steps) != 1:
+            # the per-parameter step counters (torch's state layout: 0-dim CPU tensors) in one foreach op and one
+            # host read, not a tensor add + .item() per parameter (~300 per step on the host)
+            torch._foreach_add_(step_ts, 1)
+            sv = torch.stack(step_ts)
+            lo, hi = sv.aminmax()
+            if lo.item() != hi.item():
                 raise RuntimeError('parameters of one group at different step counts')
-            step = steps.pop()
+            step = int(hi.item())
             bc1 = 1.0 - b1 ** step
             bc2 = 1.0 - b2 ** step
             t, c, n = self._tables.setdefault(gi, _Table()).get(rows, dev)
