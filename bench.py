@@ -21,6 +21,8 @@ import time
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(REPO, 'crossmodal-imu-video-ood-har_amd'))
 
+# kernel arguments in device memory (see cmhar/__init__.py; set before the HIP runtime initialises)
+os.environ.setdefault('HIP_FORCE_DEV_KERNARG', '1')
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
