@@ -165,7 +165,9 @@ class CrossModalModel(nn.Module):
             cur = torch.cuda.current_stream(imu.device)
             side = self._side.get(imu.device)
             if side is None:
-                side = self._side[imu.device] = torch.cuda.Stream(imu.device)
+                # CMHAR_IMU_STREAM_PRIORITY=-1: the side stream at high dispatch priority (A/B knob; default 0)
+                side = self._side[imu.device] = torch.cuda.Stream(
+                    imu.device, priority=int(os.environ.get('CMHAR_IMU_STREAM_PRIORITY', '0')))
             side.wait_stream(cur)
             with torch.cuda.stream(side):
                 imu_out = self._imu_branch(imu)
