@@ -10,6 +10,17 @@ One step = the body of CrossModalTrainer.train_epoch (src/train/trainer.py:130-1
 resident in HBM: model(imu, video) → SigmoidContrastiveLoss → zero_grad → backward (+ RCCL gradient all-reduce
 when N > 1) → clip_grad_norm_(1.0) → AdamW.step.  Weak scaling: every rank processes its own 32 clips; the loss
 is over the gathered global batch (DataParallel semantics).  Rank 0 prints one JSON line.
+
+`--workload` selects the other BASELINE configs with the same JSON schema (so a driver rerun can confirm them):
+  videomae  (default) the headline: VideoMAE-B 16×224² + IMU 6×200, batch 32 per GPU, bf16 (configs 2/3 geometry at
+            `--image 112`);
+  r3d       config 2 with its named backbone: the R3D-18 extension, 16×112² + IMU 6×200, batch 32 per GPU, bf16;
+  fusion    config 4 per GPU: CrossModalFusionClassifier (IMU 400 tokens × VideoMAE-B 32×224² tokens), batch 8
+            per GPU (global 64 on 8 GPUs), CE loss, bf16;
+  ood_fp16  config 5: the OOD evaluation stream, fp16 inference: forward → SigLIP logits → energy score, one step =
+            one batch of 32 clips from a ring of 8 distinct resident batches; default 313 steps = 10 016 clips.
+For the non-headline workloads `roofline` is the whole step's algorithmic FLOP rate against the bf16 / fp16 peak
+(`kernel`: "whole step"); the headline's is the dominant single kernel's (HIP events) with PMC traffic.
 """
 import argparse
 import json
@@ -32,12 +43,20 @@ PEAK_HBM_GBS = 8000.0
 
 
 TRAFFIC_JSON = os.path.join(REPO, 'profiles', 'r02_pmc_traffic.json')
+MFMA_JSON = os.path.join(REPO, 'profiles', 'r03_pmc_mfma.json')
+
+# per-workload defaults of --batch / --frames / --image / --imu-len / --dtype (BASELINE.json configs)
+WORKLOADS = {
+    'videomae': dict(batch=32, frames=16, image=224, imu_len=200, dtype='bf16'),
+    'r3d': dict(batch=32, frames=16, image=112, imu_len=200, dtype='bf16'),
+    'fusion': dict(batch=8, frames=32, image=224, imu_len=400, dtype='bf16'),
+    'ood_fp16': dict(batch=32, frames=16, image=224, imu_len=200, dtype='fp16'),
+}
 
 
-def pmc_traffic(label, path=TRAFFIC_JSON):
-    """HBM bytes per launch of the traced kernel `label` (e.g. 'gemm256_kernel<false,false,float>') from a committed
-    PMC summary of this same bench command (tools/pmc_traffic.py: FETCH_SIZE x2 + WRITE_SIZE per dispatch), with
-    the commit of the build it was measured on; None when the file or the kernel is absent."""
+def _pmc_hits(label, path):
+    """Per-kernel records of a committed PMC summary (tools/pmc_traffic.py / tools/pmc_mfma.py JSON) that belong to
+    the traced kernel `label` (e.g. 'gemm256_kernel<false,false,float>'), and the file's provenance."""
     if not path or not os.path.exists(path) or '<' not in label:
         return None, None
     base, args = label.split('<', 1)
@@ -50,11 +69,33 @@ def pmc_traffic(label, path=TRAFFIC_JSON):
     ks = doc['kernels']
     demangled = base + '<' + ', '.join(a.strip() for a in args.rstrip('>').split(','))   # rocprof demangles some
     hits = [v for k, v in ks.items() if any(mg in k for mg in mangled) or demangled in k]
-    src = {'file': os.path.relpath(path, REPO), 'commit': doc.get('commit'), 'cmd': doc.get('cmd')}
+    return hits, {'file': os.path.relpath(path, REPO), 'commit': doc.get('commit'), 'cmd': doc.get('cmd')}
+
+
+def pmc_traffic(label, path=TRAFFIC_JSON):
+    """HBM bytes per launch of the traced kernel `label` from a committed PMC summary of this same bench command
+    (tools/pmc_traffic.py: FETCH_SIZE x2 + WRITE_SIZE per dispatch), with the commit of the build it was measured
+    on; None when the file or the kernel is absent."""
+    hits, src = _pmc_hits(label, path)
     if not hits:
         return None, src
     n = sum(v['dispatches'] for v in hits)
     return int(sum(v['hbm_bytes_per_launch'] * v['dispatches'] for v in hits) / n), src
+
+
+def mfma_util(label, path=MFMA_JSON):
+    """MFMA-pipe utilisation of the traced kernel from a committed PMC pass of this same bench command
+    (tools/pmc_mfma.py: SQ_VALU_MFMA_BUSY_CYCLES / (4 SIMDs x 256 CUs x GRBM_GUI_ACTIVE / 8 XCDs), i.e. the share of
+    the kernel's SIMD-cycles with the matrix pipe busy at the clock it actually ran), or None."""
+    hits, src = _pmc_hits(label, path)
+    if not hits:
+        return None
+    busy = sum(v['mfma_busy_cycles_per_launch'] * v['dispatches'] for v in hits)
+    grbm = sum(v['grbm_gui_active_per_launch'] * v['dispatches'] for v in hits)
+    n = sum(v['dispatches'] for v in hits)
+    return {'util': round(busy / (grbm / 8 * 256 * 4), 4) if grbm else None,
+            'mfma_busy_cycles_per_launch': int(busy / n), 'grbm_gui_active_per_launch': int(grbm / n),
+            'effective_clock_ghz': hits[0].get('effective_clock_ghz'), 'source': src}
 
 
 def parse():
@@ -62,20 +103,28 @@ def parse():
     ap.add_argument('--gpus', type=int, default=1)
     ap.add_argument('--steps', type=int, default=50)     # >= 50 timed steps after >= 10 warm-up
     ap.add_argument('--warmup', type=int, default=10)
-    ap.add_argument('--batch', type=int, default=32)
-    ap.add_argument('--frames', type=int, default=16)
-    ap.add_argument('--image', type=int, default=224)
-    ap.add_argument('--imu-len', type=int, default=200)
-    ap.add_argument('--dtype', default='bf16', choices=['bf16', 'fp32'])
+    ap.add_argument('--workload', default='videomae', choices=sorted(WORKLOADS))
+    ap.add_argument('--batch', type=int, default=None)
+    ap.add_argument('--frames', type=int, default=None)
+    ap.add_argument('--image', type=int, default=None)
+    ap.add_argument('--imu-len', type=int, default=None)
+    ap.add_argument('--dtype', default=None, choices=['bf16', 'fp32', 'fp16'])
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--cpu-batch', type=int, default=4)       # BASELINE.md CPU-baseline plan: batch 4,
     ap.add_argument('--cpu-warmup', type=int, default=2)      # 2 warm-up + 3 timed steps, all host cores
     ap.add_argument('--cpu-steps', type=int, default=3)
     ap.add_argument('--traffic-json', default=TRAFFIC_JSON)
+    ap.add_argument('--mfma-json', default=MFMA_JSON)
     ap.add_argument('--no-trace', action='store_true')
     ap.add_argument('--imu-stream', choices=['side', 'main'], default='side',
                     help='run the IMU branch on its own HIP stream (overlapping the video branch) or on the main one')
-    return ap.parse_args()
+    args = ap.parse_args()
+    for k, v in WORKLOADS[args.workload].items():
+        if getattr(args, k) is None:
+            setattr(args, k, v)
+    if args.workload == 'ood_fp16' and '--steps' not in sys.argv:
+        args.steps = 313                 # BASELINE config 5: a 10k-clip stream (313 batches of 32)
+    return args
 
 
 def videomae_flops_per_clip(T, H, W, hd=768, layers=12, inter=3072, P=16, tub=2, C=3):
@@ -237,21 +286,41 @@ def cpu_baseline(cfg_builder, batch, warmup, steps, frames, image, imu_len):
                       f'parameters, {warmup} warm-up + {steps} timed'}
 
 
-def main():
-    args = parse()
+def r3d_flops(m, B, T, H, W):
+    """(forward, stem forward) algorithmic FLOPs of the R3D-18 backbone for B clips: 2·M·Cout·K per conv."""
+    from cmhar.r3d import _out_shape
+    shape = (B, T, H, W, 3)
+    tot = 0
+
+    def conv(shp, c):
+        nonlocal tot
+        o = _out_shape(shp, c)
+        f = 2 * math.prod(o[:4]) * c.out_channels * c.weight[0].numel()
+        tot += f
+        return o, f
+
+    shape, stem = conv(shape, m.stem[0])
+    for blk in m.blocks():
+        s1, _ = conv(shape, blk.conv1[0])
+        if blk.downsample is not None:
+            conv(shape, blk.downsample[0])
+        shape, _ = conv(s1, blk.conv2[0])
+    return tot, stem
+
+
+class Workload:
+    """One benchmark configuration: `step()` runs one step on this rank's resident batch; `flops_per_clip` is the
+    step's algorithmic FLOPs per clip (the whole-step roofline numerator)."""
+
+
+def build_workload(args, dev, rank, world):
+    import warnings
     from cmhar import dist as cdist
     from cmhar import kernels as K
     from cmhar.config import Config
-    from cmhar.losses import SigmoidContrastiveLoss
+    from cmhar.losses import SigmoidContrastiveLoss, cross_entropy
     from cmhar.models import CrossModalModel
     from cmhar.optim import FusedAdamW, clip_grad_norm_
-
-    # CMHAR_BENCH_BACKEND / CMHAR_BENCH_DEVICE: rehearsal knobs only (e.g. two gloo ranks sharing the one GPU of a
-    # test box); the measured configuration is one RCCL rank per GPU
-    rank, world, local = cdist.init_from_env(os.environ.get('CMHAR_BENCH_BACKEND') or None)
-    local = int(os.environ.get('CMHAR_BENCH_DEVICE', local))
-    torch.cuda.set_device(local)
-    dev = torch.device('cuda', local)
 
     def make_cfg():
         cfg = Config()
@@ -260,31 +329,97 @@ def main():
         cfg.data.video_frames_per_window = args.frames
         cfg.data.video_resize = (args.image, args.image)
         cfg.model.compute_dtype = args.dtype
+        if args.workload == 'r3d':
+            cfg.model.video_backbone = 'r3d_18'
         return cfg
 
-    import warnings
+    W = Workload()
+    W.make_cfg = make_cfg
     torch.manual_seed(0)
     with warnings.catch_warnings():
         warnings.simplefilter('ignore')          # hub checkpoint not fetchable offline → random init
-        model = CrossModalModel(make_cfg())
+        if args.workload == 'fusion':
+            from cmhar.fusion import CrossModalFusionClassifier
+            model = CrossModalFusionClassifier(make_cfg())
+        else:
+            model = CrossModalModel(make_cfg())
+    B = args.batch
+    g = torch.Generator(device=dev).manual_seed(1000 + rank)
+    embed_f, fwd_f = videomae_flops_per_clip(args.frames, args.image, args.image)
+    W.model, W.B = model, B
+    if args.workload == 'ood_fp16':
+        from cmhar.ood import logits_energy
+        model = model.to(dev).eval()
+        ring = [(torch.randn(B, 6, args.imu_len, device=dev, generator=g),
+                 torch.randn(B, args.frames, 3, args.image, args.image, device=dev, generator=g)) for _ in range(8)]
+        S = torch.empty(B, B, device=dev)
+        bias = torch.full((B,), -10.0, device=dev)
+        it = [0]
+
+        def step():
+            imu, video = ring[it[0] % len(ring)]
+            it[0] += 1
+            with torch.no_grad():
+                a, b = model(imu, video)
+                K.gemm(0, a, b, S, bias=bias, alpha=10.0)       # SigLIP logits exp(log 10)·a·bᵀ + bias
+                pred, energy, _ = logits_energy(S)
+            return energy
+        W.step, W.flops_per_clip = step, fwd_f
+        W.metric = 'clips/sec OOD energy-score eval stream, fp16 inference, 16x224^2 video + 200x6 IMU, batch 32'
+        W.workload = (f'OOD eval stream (BASELINE config 5): CrossModalModel eval forward, VideoMAE-B {args.frames}x'
+                      f'{args.image}^2 + IMU 6x{args.imu_len}, SigLIP logits, energy score; ring of 8 distinct batches')
+        W.training = False
+        return W
+
     model = model.to(dev).train()
-    model.overlap_imu = args.imu_stream == 'side'
+    if args.workload != 'fusion':
+        model.overlap_imu = args.imu_stream == 'side'
     backbone = model.video_encoder.backbone
     cdist.broadcast_parameters(model)
     reducer = cdist.GradReducer(model, backbone=backbone)
-    loss_fn = SigmoidContrastiveLoss().to(dev)
     # LinearLR(start_factor=0.1) of trainer.py:80-105 → step-0 lr = 0.1 * pretrain_lr
-    opt = FusedAdamW(model.parameters(), lr=0.1 * 1e-4, weight_decay=0.01, shadow_sources=[backbone])
-
-    g = torch.Generator(device=dev).manual_seed(1000 + rank)
-    B = args.batch
+    params = [p for n, p in model.named_parameters() if not (args.workload == 'fusion' and
+                                                              n.startswith('video_encoder.projection.'))]
+    opt = FusedAdamW(params, lr=0.1 * 1e-4, weight_decay=0.01,
+                     shadow_sources=[backbone] if args.workload != 'r3d' else [])
     video = torch.randn(B, args.frames, 3, args.image, args.image, device=dev, generator=g)
     imu = torch.randn(B, 6, args.imu_len, device=dev, generator=g)
-    params = list(model.parameters())
+    if args.workload == 'fusion':
+        labels = torch.randint(0, model.fusion.classifier.out_features, (B,), device=dev, generator=g)
+
+        def loss_of():
+            # global-batch mean CE under data parallelism (equal shards): the SUM all-reduce of the gradients of
+            # mean/world gives the gradient of DataParallel's gathered mean
+            loss = cross_entropy(model(imu, video), labels)
+            return loss * (1.0 / world) if world > 1 else loss
+        Lk = (args.frames // 2) * (args.image // 16) ** 2
+        Lq = 1 + (args.imu_len - 16) // 16 + 1
+        fus = 2 * Lk * 768 * 512 + 4 * Lq * Lk * 256          # K|V projection + attention (fwd, per clip)
+        W.flops_per_clip = 3 * fwd_f - embed_f + 3 * fus
+        W.metric = (f'clips/sec fwd+bwd, cross-attention fusion {args.frames}x{args.image}^2 video + '
+                    f'{args.imu_len}x6 IMU, batch {B} per GPU')
+        W.workload = (f'CrossModalFusionClassifier train step (BASELINE config 4): IMU 6x{args.imu_len} tokens x '
+                      f'VideoMAE-B {args.frames}x{args.image}^2 tokens, CE loss, clip 1.0, AdamW')
+    else:
+        loss_fn = SigmoidContrastiveLoss().to(dev)
+
+        def loss_of():
+            a, b = model(imu, video)
+            return loss_fn(a, b)
+        if args.workload == 'r3d':
+            fwd_r, stem = r3d_flops(backbone, B, args.frames, args.image, args.image)
+            W.flops_per_clip = (3 * fwd_r - stem) / B
+            W.metric = f'clips/sec fwd+bwd, R3D-18 {args.frames}x{args.image}^2 video + 200x6 IMU, batch {B}'
+            W.workload = (f'CrossModalModel pretrain step, video_backbone=r3d_18 (BASELINE config 2): R3D-18 '
+                          f'{args.frames}x{args.image}^2 + IMU 6x{args.imu_len}, SigLIP loss, clip 1.0, AdamW')
+        else:
+            W.flops_per_clip = 3 * fwd_f - embed_f     # fwd + 2x bwd, no pixel gradient for the tubelet conv
+            W.metric = 'clips/sec fwd+bwd, 16x224^2 video + 200x6 IMU, batch 32, 1/2/4/8 GPU'
+            W.workload = (f'CrossModalModel pretrain step: VideoMAE-B {args.frames}x{args.image}^2 + '
+                          f'IMU 6x{args.imu_len} PatchTST, SigLIP loss, clip 1.0, AdamW')
 
     def step():
-        a, b = model(imu, video)
-        loss = loss_fn(a, b)
+        loss = loss_of()
         opt.zero_grad(set_to_none=True)
         reducer.start_step()
         loss.backward()
@@ -292,13 +427,33 @@ def main():
         clip_grad_norm_(params, 1.0)
         opt.step()
         return loss
+    W.step, W.training = step, True
+    return W
+
+
+def main():
+    args = parse()
+    from cmhar import dist as cdist
+    from cmhar import kernels as K
+
+    # CMHAR_BENCH_BACKEND / CMHAR_BENCH_DEVICE: rehearsal knobs only (e.g. two gloo ranks sharing the one GPU of a
+    # test box); the measured configuration is one RCCL rank per GPU
+    rank, world, local = cdist.init_from_env(os.environ.get('CMHAR_BENCH_BACKEND') or None)
+    local = int(os.environ.get('CMHAR_BENCH_DEVICE', local))
+    torch.cuda.set_device(local)
+    dev = torch.device('cuda', local)
+    W = build_workload(args, dev, rank, world)
+    step, B = W.step, W.B
+    headline = args.workload == 'videomae'
+    trace = headline and not args.no_trace
 
     # Warm-up; its last step runs with every GEMM / attention launch bracketed by HIP events, which gives the
     # per-kernel-family breakdown and picks the dominant single kernel.  The timed loop then brackets ONLY that
     # kernel's launches (the events of all ~180 traced launches cost ~1.5 ms/step of stream bubbles).
     breakdown = {}
+    loss = None
     for i in range(args.warmup):
-        full = not args.no_trace and i == args.warmup - 1
+        full = trace and i == args.warmup - 1
         if full:
             K.TRACE.records, K.TRACE.only, K.TRACE.active = [], None, True
         loss = step()
@@ -307,7 +462,7 @@ def main():
             K.TRACE.active = False
             breakdown = K.TRACE.summary()
     torch.cuda.synchronize()
-    first_loss = float(loss.item()) if args.warmup else float('nan')
+    first_loss = float(loss.float().mean().item()) if loss is not None else float('nan')
     # every traced label is one kernel symbol except the two-kernel attention backward entry
     single = {k: v for k, v in breakdown.items() if '(' not in k}
     dominant = max(single.items(), key=lambda kv: kv[1][1])[0] if single else None
@@ -316,7 +471,7 @@ def main():
     torch.cuda.synchronize()
     K.TRACE.records = []
     K.TRACE.only = {dominant} if dominant else None
-    K.TRACE.active = not args.no_trace and dominant is not None
+    K.TRACE.active = trace and dominant is not None
     if rank == 0:
         log(f'warm-up done ({args.warmup} steps, loss {first_loss:.5f}); timing {args.steps} steps')
     t0 = time.perf_counter()
@@ -335,12 +490,14 @@ def main():
     clips = world * B * args.steps
     value = clips / elapsed
     ms = 1000 * elapsed / args.steps
+    peak = PEAK_F32_TFLOPS if args.dtype == 'fp32' else PEAK_BF16_TFLOPS     # fp16 dense MFMA = bf16 rate
+    whole_tflops = W.flops_per_clip * clips / elapsed / 1e12
 
     # dominant kernel: the single HIP kernel with the largest traced time in the traced warm-up step (split-K GEMMs
     # are traced without their reduce launch); achieved = its algorithmic FLOPs / its HIP-event-measured time over
     # the timed region
     roof = None
-    summ = K.TRACE.summary() if not args.no_trace else {}
+    summ = K.TRACE.summary() if trace else {}
     if dominant in summ:
         name = dominant
         n, tot_ms, fl, nb = summ[name]
@@ -351,25 +508,26 @@ def main():
                 'kernel': name,
                 'launches': n, 'avg_launch_ms': round(tot_ms / n, 4),
                 'algorithmic_bytes_per_launch': int(nb / n)}
-    embed_f, fwd_f = videomae_flops_per_clip(args.frames, args.image, args.image)
-    step_flops_clip = 3 * fwd_f - embed_f           # fwd + 2x bwd, no pixel gradient for the tubelet conv
-    whole_tflops = step_flops_clip * clips / elapsed / 1e12
+        mf = mfma_util(name, args.mfma_json)
+        if mf is not None:
+            roof['mfma_util'] = mf
+    elif not headline:
+        roof = {'bound': 'mfma', 'achieved': round(whole_tflops, 1), 'peak': peak, 'unit': 'TFLOP/s',
+                'frac': round(whole_tflops / peak, 4), 'traffic': None, 'kernel': 'whole step (all kernels)'}
 
-    out = {'metric': 'clips/sec fwd+bwd, 16x224^2 video + 200x6 IMU, batch 32, 1/2/4/8 GPU', 'value': round(value, 3),
+    out = {'metric': W.metric, 'value': round(value, 3),
            'unit': 'clips/sec', 'n_gpus': world, 'steps': args.steps, 'warmup': args.warmup,
            'ms_per_step': round(ms, 3), 'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None,
-           'dtype': args.dtype, 'data': 'synthetic (randn video/IMU resident in HBM, random-init VideoMAE-B weights)',
-           'config': {'workload': f'CrossModalModel pretrain step: VideoMAE-B {args.frames}x{args.image}^2 + '
-                                  f'IMU 6x{args.imu_len} PatchTST, SigLIP loss, clip 1.0, AdamW',
-                      'global_batch': world * B, 'per_gpu_batch': B, 'parallelism': f'dp{world}'},
+           'dtype': args.dtype, 'data': f'synthetic (randn video/IMU resident in HBM, random-init weights)',
+           'config': {'workload': W.workload, 'global_batch': world * B, 'per_gpu_batch': B,
+                      'parallelism': f'dp{world}'},
            'roofline': roof,
            'whole_step_model_tflops': round(whole_tflops, 1),
-           'whole_step_mfma_frac': round(whole_tflops / (PEAK_F32_TFLOPS if args.dtype == 'fp32' else PEAK_BF16_TFLOPS),
-                                         4),
+           'whole_step_mfma_frac': round(whole_tflops / peak, 4),
            'first_warmup_loss': first_loss,
            'max_mem_gb': round(torch.cuda.max_memory_allocated(dev) / 2 ** 30, 1)}
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        out['cpu_baseline'] = cpu_baseline(make_cfg, args.cpu_batch, args.cpu_warmup, args.cpu_steps, args.frames,
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and headline:
+        out['cpu_baseline'] = cpu_baseline(W.make_cfg, args.cpu_batch, args.cpu_warmup, args.cpu_steps, args.frames,
                                            args.image, args.imu_len)
     if rank == 0:
         if breakdown:   # one traced warm-up step

@@ -171,6 +171,21 @@ def dtype_code(dt):
     raise TypeError(f'unsupported dtype {dt}')
 
 
+class NoReplicate:
+    """Mixin of every cmhar module that runs HIP code.  `nn.DataParallel` over more than one device replicates a
+    module by shallow-copying it per device (torch `replicate.py`), which would share this package's per-device state
+    (packed compute-dtype weight shadows, flat gradient buffers, side streams) between replicas; the copy is refused
+    with a pointer to the supported path.  `nn.DataParallel` over ONE device never replicates and works as is."""
+
+    def _replicate_for_data_parallel(self):
+        raise RuntimeError(
+            f'{type(self).__name__}: nn.DataParallel over several GPUs is not supported by the cmhar HIP modules '
+            f'(they keep per-device weight shadows, gradient buffers and streams).  Run one process per GPU with '
+            f'cmhar.dist instead (`cmhar.dist.init_from_env()`, `cmhar.dist.GradReducer`, launched by torchrun): it '
+            f'keeps DataParallel\'s semantics (global-batch loss, per-replica BatchNorm, summed gradients, device-0 '
+            f'running statistics; reference main.py:89-93).')
+
+
 def epilogue(bias=None, residual=None, aux_in=None, aux_out=None, rowadd=None, rowadd_mod=1, act=ACT_NONE,
              alpha=1.0, beta=0.0, pdrop=0.0, seed=0, rowsum=None, rowsum_beta=0.0, colscale=None):
     """colscale: (lo, hi, s) — columns [lo, hi) multiplied by s before the activation."""

@@ -80,7 +80,7 @@ def _resnet_layer(inplanes, planes, stride):
     return nn.Sequential(BasicBlock(inplanes, planes, stride, ds), BasicBlock(planes, planes))
 
 
-class ResNet18Features(nn.Sequential):
+class ResNet18Features(L.NoReplicate, nn.Sequential):
     """conv1, bn1, relu, maxpool, layer1..layer4 — `nn.Sequential(*list(resnet18().children())[:-2])`."""
     feature_dim = 512
 
@@ -117,7 +117,7 @@ class InvertedResidual(nn.Module):
         self.out_channels = oup
 
 
-class MobileNetV2Features(nn.Sequential):
+class MobileNetV2Features(L.NoReplicate, nn.Sequential):
     """torchvision `mobilenet_v2(width_mult=1.0).features`: 19 entries, last channel 1280."""
     feature_dim = 1280
     SETTING = [[1, 16, 1, 1], [6, 24, 2, 2], [6, 32, 3, 2], [6, 64, 4, 2], [6, 96, 3, 1], [6, 160, 3, 2],

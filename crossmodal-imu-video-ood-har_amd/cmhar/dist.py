@@ -16,11 +16,13 @@ collective sequence whatever order its hooks fire in:
   one flat fp32 buffer (cmhar.grads.FlatGradSink) in backward-production order; the buffer is cut into ~32 MB
   buckets at parameter boundaries, each launched when its last layer is done — no copies;
 * hook buckets — every other trainable parameter (IMU encoder, heads, and any other backbone: R3D-18, the
-  cross-attention fusion model) in reverse registration order (≈ backward order), cut into ~32 MB buckets; a
-  `post_accumulate_grad` hook marks each gradient final, a full bucket is flattened into its persistent buffer
-  and launched, and `finish()` scatters the reduced values back into `.grad`.
+  cross-attention fusion model), cut into ~32 MB buckets in the order the first step's backward produced them
+  (reverse registration order until then); a `post_accumulate_grad` hook marks each gradient final, a full
+  bucket is flattened into its persistent buffer on a communication stream that waits on every stream that
+  produced its gradients, and launched; `finish()` scatters the reduced values back into `.grad`.
 Parameters whose gradient stays None on every rank (unused parameters such as `CrossModalModel.temperature`)
-are skipped consistently: a bucket that never fills is reduced in `finish()` over its non-None gradients.
+are skipped consistently: after the first step they sit in one trailing bucket, reduced in `finish()` over its
+non-None gradients (every rank must agree on which gradients are None, as under DataParallel).
 """
 from __future__ import annotations
 
@@ -101,18 +103,46 @@ def _is_sink_backbone(backbone) -> bool:
 
 
 class _Bucket:
-    __slots__ = ('params', 'kind', 'start', 'end', 'ready', 'launched', 'flat', 'live')
+    __slots__ = ('params', 'kind', 'start', 'end', 'ready', 'launched', 'flat', 'live', 'streams')
 
     def __init__(self, params, kind, start=0, end=0):
         self.params, self.kind, self.start, self.end = params, kind, start, end
-        self.ready, self.launched, self.flat, self.live = set(), False, None, None
+        self.ready, self.launched, self.flat, self.live, self.streams = set(), False, None, None, {}
+
+
+def _cut(params, limit):
+    """Consecutive groups of `params` of at least `limit` elements (the last may be smaller)."""
+    out, cur, size = [], [], 0
+    for p in params:
+        cur.append(p)
+        size += p.numel()
+        if size >= limit:
+            out.append(cur)
+            cur, size = [], 0
+    if cur:
+        out.append(cur)
+    return out
 
 
 class GradReducer:
     """Bucketed, backward-overlapped gradient all-reduce (SUM) for one model replica per process.
 
     `backbone`: the model's video backbone.  A VideoMAE backbone gets the zero-copy flat gradient sink; any other
-    backbone (or None) is covered by the hook buckets like the rest of the model."""
+    backbone (or None) is covered by the hook buckets like the rest of the model.
+
+    Hook buckets are first cut in reverse registration order.  That order is only a guess at backward order, and a
+    bucket holding a parameter that never receives a gradient (`CrossModalModel.temperature` / `bias`,
+    models.py:267-268) would never fill and would hold back every later bucket until `finish()`.  So the first
+    step records the order in which the hooks actually fire; `finish()` of that step takes rank 0's order (one
+    `broadcast_object_list`, so every rank cuts identical buckets), rebuilds the hook buckets from it and puts the
+    parameters that never fired into one trailing bucket reduced in `finish()`.  From the second step on every
+    hook bucket goes out as soon as its last gradient is accumulated (DDP's bucket-rebuild rule).
+
+    Streams: a hook bucket's gradients can come from different HIP streams (the IMU branch of `CrossModalModel`
+    runs its backward on a side stream, the video backbone on the main stream).  Each hook records the stream
+    its gradient was produced on; the bucket is flattened and launched on a dedicated communication stream that
+    first waits on every one of those streams, and `finish()` makes the caller's stream wait on the collectives
+    before the reduced values are copied back into `.grad`."""
 
     def __init__(self, model: torch.nn.Module, backbone=None, bucket_mb: float = 32.0, group=None):
         self.model = model
@@ -122,7 +152,7 @@ class GradReducer:
         self.pending = []
         self.active = False
         self.buckets: List[_Bucket] = []
-        limit = max(int(bucket_mb * (1 << 20) / 4), 1)
+        self.limit = max(int(bucket_mb * (1 << 20) / 4), 1)
         sink_params = set()
         if backbone is not None and _is_sink_backbone(backbone):
             order = backbone_param_order(backbone)
@@ -132,29 +162,35 @@ class GradReducer:
             for p in self.sink.order:               # cut the flat buffer at parameter boundaries
                 cur.append(p)
                 size = self.sink.offsets[p] + p.numel() - start
-                if size >= limit:
+                if size >= self.limit:
                     self.buckets.append(_Bucket(cur, 'sink', start, start + size))
                     start += size
                     cur = []
             if cur:
                 self.buckets.append(_Bucket(cur, 'sink', start, self.sink.numel))
             sink_params = set(self.sink.order)
+        self.n_sink = len(self.buckets)
         self.rest = [p for p in model.parameters() if p.requires_grad and p not in sink_params]
-        cur, size = [], 0
-        for p in reversed(self.rest):
-            cur.append(p)
-            size += p.numel()
-            if size >= limit:
-                self.buckets.append(_Bucket(cur, 'hook'))
-                cur, size = [], 0
-        if cur:
-            self.buckets.append(_Bucket(cur, 'hook'))
-        self._bucket_of = {p: i for i, b in enumerate(self.buckets) for p in b.params}
-        self._next = 0                              # buckets launch strictly in index order
+        self._set_hook_buckets(_cut(list(reversed(self.rest)), self.limit))
+        self.learned = False                        # hook-bucket order taken from an observed backward yet?
+        self._fired = []                            # hook firing order of the current step (learning step only)
+        self._comm = None
+        self.launched_before_finish = 0             # buckets in flight when backward returned (last step)
         self._hooks = []
         if self.world > 1:
             for p in self.rest:
                 self._hooks.append(p.register_post_accumulate_grad_hook(self._on_hook))
+
+    def _set_hook_buckets(self, groups):
+        self.buckets = self.buckets[:self.n_sink] + [_Bucket(g, 'hook') for g in groups]
+        self._bucket_of = {p: i for i, b in enumerate(self.buckets) for p in b.params}
+
+    def _comm_stream(self, device):
+        if device.type != 'cuda':
+            return None
+        if self._comm is None:
+            self._comm = torch.cuda.Stream(device)
+        return self._comm
 
     # -- readiness -------------------------------------------------------------------------------------------
     def _mark(self, p):
@@ -162,6 +198,9 @@ class GradReducer:
         if bi is None:
             return
         b = self.buckets[bi]
+        if b.launched:
+            raise RuntimeError('a parameter received a second gradient contribution after its bucket was '
+                               'all-reduced (parameter used twice in one step); not supported by GradReducer')
         b.ready.add(p)
         self._launch_ready()
 
@@ -172,8 +211,16 @@ class GradReducer:
             self._mark(p)
 
     def _on_hook(self, p):
-        if self.active:
-            self._mark(p)
+        if not self.active:
+            return
+        if p.grad is not None and p.grad.is_cuda:
+            s = torch.cuda.current_stream(p.grad.device)
+            bi = self._bucket_of.get(p)
+            if bi is not None:
+                self.buckets[bi].streams[s.cuda_stream] = s
+        if not self.learned:
+            self._fired.append(p)
+        self._mark(p)
 
     def _launch_ready(self):
         while self._next < len(self.buckets):
@@ -190,19 +237,35 @@ class GradReducer:
             live = [p for p in b.params if p.grad is not None]
             b.live = live
             if live:
-                n = sum(p.numel() for p in live)
-                if b.flat is None or b.flat.numel() != n or b.flat.device != live[0].grad.device:
-                    b.flat = torch.empty(n, dtype=torch.float32, device=live[0].grad.device)
-                torch.cat([p.grad.reshape(-1).float() for p in live], out=b.flat)
-                self.pending.append(dist.all_reduce(b.flat, group=self.group, async_op=True))
+                dev = live[0].grad.device
+                comm = self._comm_stream(dev)
+                if comm is None:
+                    self._flatten_and_reduce(b, live)
+                else:
+                    cur = torch.cuda.current_stream(dev)
+                    comm.wait_stream(cur)
+                    for s in b.streams.values():
+                        if s.cuda_stream != comm.cuda_stream:
+                            comm.wait_stream(s)
+                    with torch.cuda.stream(comm):
+                        self._flatten_and_reduce(b, live)
         b.launched = True
+
+    def _flatten_and_reduce(self, b, live):
+        n = sum(p.numel() for p in live)
+        dev = live[0].grad.device
+        if b.flat is None or b.flat.numel() != n or b.flat.device != dev:
+            b.flat = torch.empty(n, dtype=torch.float32, device=dev)
+        torch.cat([p.grad.reshape(-1).float() for p in live], out=b.flat)
+        self.pending.append(dist.all_reduce(b.flat, group=self.group, async_op=True))
 
     # -- step protocol ---------------------------------------------------------------------------------------
     def start_step(self):
         for b in self.buckets:
-            b.ready, b.launched, b.live = set(), False, None
+            b.ready, b.launched, b.live, b.streams = set(), False, None, {}
         self._next = 0
         self.pending = []
+        self._fired = []
         self.active = self.world > 1
 
     def finish(self):
@@ -211,11 +274,12 @@ class GradReducer:
         self.active = False
         if self.world == 1:
             return
+        self.launched_before_finish = self._next
         for b in self.buckets[self._next:]:
             self._launch(b)
         self._next = len(self.buckets)
         for w in self.pending:
-            w.wait()
+            w.wait()               # NCCL: the caller's current stream waits on the collective
         self.pending = []
         for b in self.buckets:
             if b.kind == 'hook' and b.live:
@@ -224,6 +288,30 @@ class GradReducer:
                     n = p.numel()
                     p.grad.copy_(b.flat[off:off + n].view_as(p.grad))
                     off += n
+        if not self.learned:
+            self._learn_order()
+
+    def _learn_order(self):
+        """Rebuild the hook buckets in rank 0's observed gradient order (identical on every rank)."""
+        index = {p: i for i, p in enumerate(self.rest)}
+        seen, order = set(), []
+        for p in self._fired:
+            if p not in seen:
+                seen.add(p)
+                order.append(index[p])
+        obj = [order]
+        dist.broadcast_object_list(obj, src=0 if self.group is None else dist.get_global_rank(self.group, 0),
+                                   group=self.group)
+        order = obj[0]
+        fired = [self.rest[i] for i in order]
+        fired_set = set(fired)
+        never = [p for p in reversed(self.rest) if p not in fired_set]
+        groups = _cut(fired, self.limit)
+        if never:
+            groups.append(never)   # unused parameters: one trailing bucket, reduced in finish()
+        self._set_hook_buckets(groups)
+        self._fired = []
+        self.learned = True
 
     def close(self):
         for h in self._hooks:

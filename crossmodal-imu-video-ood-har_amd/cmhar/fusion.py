@@ -133,7 +133,7 @@ class _TokenMeanFn(torch.autograd.Function):
         return dx, None, None
 
 
-class CrossAttentionFusion(nn.Module):
+class CrossAttentionFusion(L.NoReplicate, nn.Module):
     def __init__(self, imu_dim=128, video_dim=768, d_model=256, num_heads=4, num_classes=32, eps=1e-5,
                  compute_dtype='bf16'):
         super().__init__()

@@ -13,6 +13,7 @@ import torch
 import torch.nn as nn
 
 from . import kernels as K
+from ._lib import NoReplicate
 
 
 def _blocks(seq: nn.Sequential):
@@ -122,7 +123,7 @@ def run_head(seq: nn.Sequential, x: torch.Tensor, training: bool, seeds: _Seeds)
         return _head_forward(seq, x, training, seed, save=False)[0]
 
 
-class ProjectionHead(nn.Module):
+class ProjectionHead(NoReplicate, nn.Module):
     """models.py:221-234: Linear → BatchNorm1d → ReLU → Linear."""
 
     def __init__(self, in_dim, hidden_dim, out_dim):

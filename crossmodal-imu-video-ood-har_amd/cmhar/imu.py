@@ -52,7 +52,7 @@ class PatchEmbedding(nn.Module):
         return out
 
 
-class IMUEncoder(nn.Module):
+class IMUEncoder(L.NoReplicate, nn.Module):
     """models.py:53-132."""
 
     def __init__(self, config):

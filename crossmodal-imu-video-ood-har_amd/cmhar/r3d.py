@@ -46,7 +46,7 @@ class BasicBlock(nn.Module):
         self.stride = stride
 
 
-class R3D18(nn.Module):
+class R3D18(L.NoReplicate, nn.Module):
     """torchvision `r3d_18(num_classes)` layout; `fc=None` → feature extractor returning (B, 512) fp32."""
 
     def __init__(self, num_classes=None, compute_dtype='bf16'):

@@ -307,15 +307,18 @@ class ClassificationTrainer(BaseTrainer):
 
     @torch.no_grad()
     def validate(self, dataloader) -> Dict[str, float]:
+        """trainer.py:320-353.  The loss is the mean over batches of each (global) batch's mean CE.  Under data
+        parallelism no collective runs per batch: each rank keeps its per-batch Σ CE and row counts on
+        the device, and ONE all_gather_object at the end (with the predictions) forms every global batch i as the
+        union of the ranks' i-th shards — also when ranks hold different numbers of batches."""
         self.model.eval()
-        loss_sum = _DeviceSum(self.device)
+        ce_means, counts = [], []
         correct, preds, labels_all, total = [], [], [], 0
         for batch in _progress(dataloader, self.show_progress, f'[Cls:{self.mode}] Val'):
             imu, labels = self._batch(batch)
             logits = self.model(imu)
-            loss = self.loss_fn(logits, labels)
-            share = self._global_share(labels.shape[0])
-            loss_sum.add(loss if share is None else loss * share)
+            ce_means.append(self.loss_fn(logits, labels).reshape(1))
+            counts.append(int(labels.shape[0]))
             self._score(logits, labels, correct, preds)
             labels_all.append(labels)
             total += labels.shape[0]
@@ -323,15 +326,19 @@ class ClassificationTrainer(BaseTrainer):
         all_preds = torch.cat(preds).cpu().numpy().tolist() if preds else []
         all_labels = torch.cat(labels_all).cpu().numpy().tolist() if labels_all else []
         n_ok = int(torch.cat(correct).sum().item()) if correct else 0
+        sums = [c * n for c, n in zip(torch.cat(ce_means).double().cpu().tolist(), counts)] if ce_means else []
         if D.world_size() > 1:         # metrics of the whole validation set (every rank's shard)
             import torch.distributed as tdist
             parts = [None] * D.world_size()
-            tdist.all_gather_object(parts, (all_preds, all_labels, n_ok, total))
+            tdist.all_gather_object(parts, (all_preds, all_labels, n_ok, total, sums, counts))
             all_preds = [x for pr in parts for x in pr[0]]
             all_labels = [x for pr in parts for x in pr[1]]
             n_ok, total = sum(pr[2] for pr in parts), sum(pr[3] for pr in parts)
-            D.all_reduce_sum_(loss_sum.t)
-        return {'loss': loss_sum.value() / max(len(dataloader), 1),
+            nb = max(len(pr[4]) for pr in parts)
+            sums = [sum(pr[4][i] for pr in parts if i < len(pr[4])) for i in range(nb)]
+            counts = [sum(pr[5][i] for pr in parts if i < len(pr[5])) for i in range(nb)]
+        batch_means = [s / max(n, 1) for s, n in zip(sums, counts)]
+        return {'loss': sum(batch_means) / max(len(batch_means), 1),
                 'accuracy': 100.0 * n_ok / max(total, 1),
                 'balanced_accuracy': 100.0 * balanced_accuracy_score(all_labels, all_preds),
                 'f1_macro': 100.0 * f1_score(all_labels, all_preds, average='macro')}

@@ -116,7 +116,7 @@ class VideoMAEOutput:
         return (self.last_hidden_state,)[i]
 
 
-class VideoMAEBackbone(nn.Module):
+class VideoMAEBackbone(L.NoReplicate, nn.Module):
     """HF-compatible VideoMAEModel whose forward/backward run on the cmhar HIP library."""
 
     def __init__(self, cfg, compute_dtype: str = 'bf16'):

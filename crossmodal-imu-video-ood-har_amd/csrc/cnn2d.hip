@@ -53,7 +53,9 @@ __global__ __launch_bounds__(256) void maxpool_cl_fwd(Pool g, const T* __restric
         const int tap = ih * g.k + iw;
 #pragma unroll
         for (int j = 0; j < 8; ++j)
-          if (v[j] > best[j]) { best[j] = v[j]; arg[j] = tap; }     // strict >: first maximum in scan order
+          // torch's rule (max_pool2d CPU/GPU kernels): strict > keeps the first maximum in scan order, and a NaN
+          // always wins (each later NaN too), so a NaN in the window propagates with the gradient to the last NaN
+          if (v[j] > best[j] || __builtin_isnan(v[j])) { best[j] = v[j]; arg[j] = tap; }
       }
     }
     const size_t o = (size_t)i * 8;

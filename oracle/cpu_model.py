@@ -100,45 +100,134 @@ def sinusoid_table(n_position: int, d_hid: int) -> Tensor:
     return torch.from_numpy(tab.astype(np.float32))
 
 
+class _Round(torch.autograd.Function):
+    """bf16 storage of a tensor: round-to-nearest-even of the forward value (`fwd`) and/or of the gradient that
+    flows back into it (`bwd`), both kept in fp32."""
+
+    @staticmethod
+    def forward(ctx, x, fwd, bwd):
+        ctx.bwd = bwd
+        return x.bfloat16().float() if fwd else x.clone()
+
+    @staticmethod
+    def backward(ctx, g):
+        return (g.bfloat16().float() if ctx.bwd else g), None, None
+
+
+def _rq(x, fwd=True, bwd=True):
+    return _Round.apply(x, fwd, bwd)
+
+
+def _bf(x):
+    return x.bfloat16().float()
+
+
+class _FlashBF16(torch.autograd.Function):
+    """Flash attention with bf16 MFMA operands (csrc/attention.hip): fp32 scores and softmax statistics, the
+    probabilities rounded to bf16 before P·V (forward) and Pᵀ·dO (backward), dS rounded to bf16 before dS·K and
+    dSᵀ·Q; δ = rowsum(dO ∘ O) from the bf16-stored O.  q, k, v: (B, H, L, D) bf16-valued fp32 tensors."""
+
+    @staticmethod
+    def forward(ctx, q, k, v, scale):
+        s = (q @ k.transpose(-1, -2)) * scale
+        m = s.amax(-1, keepdim=True)
+        p = torch.exp(s - m)
+        l = p.sum(-1, keepdim=True)
+        o = (_bf(p) @ v) / l
+        ctx.save_for_backward(q, k, v, o, m + l.log())
+        ctx.scale = scale
+        return o
+
+    @staticmethod
+    def backward(ctx, do):
+        q, k, v, o, lse = ctx.saved_tensors
+        scale = ctx.scale
+        p = torch.exp((q @ k.transpose(-1, -2)) * scale - lse)
+        dv = _bf(p).transpose(-1, -2) @ do
+        dp = do @ v.transpose(-1, -2)
+        delta = (do * _bf(o)).sum(-1, keepdim=True)
+        ds = _bf(p * (dp - delta))
+        dq = (ds @ k) * scale
+        dk = (ds.transpose(-1, -2) @ q) * scale
+        return dq, dk, dv, None
+
+
+class _GeluBF16(torch.autograd.Function):
+    """The FC1 epilogue of the bf16 path: stores bf16(gelu(a)) and bf16(gelu'(a)); the FC2 dgrad epilogue forms
+    dpre = bf16(dY·W2 ∘ gelu'_bf16)."""
+
+    @staticmethod
+    def forward(ctx, a):
+        ad = a.double()
+        cdf = 0.5 * (1.0 + torch.erf(ad / math.sqrt(2.0)))
+        pdf = torch.exp(-0.5 * ad * ad) / math.sqrt(2.0 * math.pi)
+        ctx.save_for_backward(_bf((cdf + ad * pdf).float()))
+        return _bf((ad * cdf).float())
+
+    @staticmethod
+    def backward(ctx, g):
+        (gp,) = ctx.saved_tensors
+        return _bf(g * gp)
+
+
 def videomae(sd: Dict[str, Tensor], video: Tensor, *, num_heads: int, patch_size: int = 16, tubelet: int = 2,
              eps: float = 1e-12, use_mean_pooling: bool = True,
-             prefix: str = 'video_encoder.backbone.') -> Tensor:
-    """last_hidden_state (B, L, Hd) of VideoMAEModel (modeling_videomae.py:398-466)."""
+             prefix: str = 'video_encoder.backbone.', bf16: bool = False) -> Tensor:
+    """last_hidden_state (B, L, Hd) of VideoMAEModel (modeling_videomae.py:398-466).
+
+    `bf16=True` restates the HIP bf16 throughput path's STORAGE (not the reference): bf16 weight shadows, bf16
+    video columns, every activation the path stores in bf16 (residual stream, LN outputs, Q/K/V with the keys
+    pre-scaled by scale·log2(e), attention output, GELU output and GELU'), every stored gradient (dx, dh, dQKV, dO,
+    dpre), and the flash kernels' bf16 P / dS operands; accumulation, softmax statistics and LayerNorm stay
+    fp32.  Its distance to the fp32 run is the error bf16 storage itself causes — the bound the bf16 parity tests
+    scale (tests/test_models_gpu.py)."""
+    rw = (lambda t: _rq(t, True, False)) if bf16 else (lambda t: t)        # weight shadows: straight-through
+    rq = _rq if bf16 else (lambda t, *a: t)
     w = sd[prefix + 'embeddings.patch_embeddings.projection.weight']
     hd = w.shape[0]
     x = video.permute(0, 2, 1, 3, 4)                                 # (B,C,T,H,W)  :165
-    emb = F.conv3d(x, w, sd[prefix + 'embeddings.patch_embeddings.projection.bias'],
+    if bf16:
+        x = _bf(x)
+    emb = F.conv3d(x, rw(w), sd[prefix + 'embeddings.patch_embeddings.projection.bias'],
                    stride=(tubelet, patch_size, patch_size))
     emb = emb.flatten(2).transpose(1, 2)                             # (B,L,Hd)     :166
-    h = emb + sinusoid_table(emb.shape[1], hd)[None]                 # :109-117
+    h = rq(emb + sinusoid_table(emb.shape[1], hd)[None])             # :109-117
     B, L, _ = h.shape
     dh = hd // num_heads
     i = 0
     while f'{prefix}encoder.layer.{i}.layernorm_before.weight' in sd:
         p = f'{prefix}encoder.layer.{i}.'
-        n = F.layer_norm(h, (hd,), sd[p + 'layernorm_before.weight'], sd[p + 'layernorm_before.bias'], eps)
+        n = rq(F.layer_norm(h, (hd,), sd[p + 'layernorm_before.weight'], sd[p + 'layernorm_before.bias'], eps))
         def proj(name):
-            return F.linear(n, sd[p + f'attention.attention.{name}.weight'],
+            return F.linear(n, rw(sd[p + f'attention.attention.{name}.weight']),
                             sd.get(p + f'attention.attention.{name}.bias')).reshape(B, L, num_heads, dh).transpose(1, 2)
-        q, k, v = proj('query'), proj('key'), proj('value')
-        att = torch.softmax((q @ k.transpose(-1, -2)) * dh ** -0.5, dim=-1)
-        o = (att @ v).transpose(1, 2).reshape(B, L, hd)
-        o = F.linear(o, sd[p + 'attention.output.dense.weight'], sd[p + 'attention.output.dense.bias'])
-        h = h + o
-        n2 = F.layer_norm(h, (hd,), sd[p + 'layernorm_after.weight'], sd[p + 'layernorm_after.bias'], eps)
-        f = F.gelu(F.linear(n2, sd[p + 'intermediate.dense.weight'], sd[p + 'intermediate.dense.bias']))
-        h = h + F.linear(f, sd[p + 'output.dense.weight'], sd[p + 'output.dense.bias'])
+        if bf16:
+            c = dh ** -0.5 * math.log2(math.e)
+            q, k, v = rq(proj('query')), rq(proj('key')), rq(proj('value'))
+            k = _rq(k * c, True, False) / c                           # K' = bf16(c·K); dK of the unscaled key
+            o = rq(_FlashBF16.apply(q, k, v, dh ** -0.5))
+        else:
+            q, k, v = proj('query'), proj('key'), proj('value')
+            att = torch.softmax((q @ k.transpose(-1, -2)) * dh ** -0.5, dim=-1)
+            o = att @ v
+        o = o.transpose(1, 2).reshape(B, L, hd)
+        o = F.linear(o, rw(sd[p + 'attention.output.dense.weight']), sd[p + 'attention.output.dense.bias'])
+        h = rq(h + o)
+        n2 = rq(F.layer_norm(h, (hd,), sd[p + 'layernorm_after.weight'], sd[p + 'layernorm_after.bias'], eps))
+        a = F.linear(n2, rw(sd[p + 'intermediate.dense.weight']), sd[p + 'intermediate.dense.bias'])
+        f = _GeluBF16.apply(a) if bf16 else F.gelu(a)
+        h = rq(h + F.linear(f, rw(sd[p + 'output.dense.weight']), sd[p + 'output.dense.bias']))
         i += 1
     if not use_mean_pooling:
-        h = F.layer_norm(h, (hd,), sd[prefix + 'layernorm.weight'], sd[prefix + 'layernorm.bias'], eps)
+        h = rq(F.layer_norm(h, (hd,), sd[prefix + 'layernorm.weight'], sd[prefix + 'layernorm.bias'], eps))
     return h
 
 
 def video_encoder(sd, video, *, num_heads, patch_size=16, tubelet=2, eps=1e-12, use_mean_pooling=True,
-                  prefix='video_encoder.'):
-    """models.py:197-203: token 0 of last_hidden_state → projection."""
+                  prefix='video_encoder.', bf16=False):
+    """models.py:197-203: token 0 of last_hidden_state → projection (`bf16`: see `videomae`)."""
     h = videomae(sd, video, num_heads=num_heads, patch_size=patch_size, tubelet=tubelet, eps=eps,
-                 use_mean_pooling=use_mean_pooling, prefix=prefix + 'backbone.')
+                 use_mean_pooling=use_mean_pooling, prefix=prefix + 'backbone.', bf16=bf16)
     return F.linear(h[:, 0], sd[prefix + 'projection.weight'], sd[prefix + 'projection.bias'])
 
 
@@ -175,14 +264,15 @@ def l2_normalize(x: Tensor, eps: float = 1e-12) -> Tensor:
     return x / x.norm(dim=1, keepdim=True).clamp_min(eps)
 
 
-def crossmodal(sd, imu, video, mcfg, training=True, imu_dropout=0.0, gen=None, update_stats=True):
-    """models.py:270-291 → (imu_proj, video_proj) unit rows."""
+def crossmodal(sd, imu, video, mcfg, training=True, imu_dropout=0.0, gen=None, update_stats=True, bf16=False):
+    """models.py:270-291 → (imu_proj, video_proj) unit rows (`bf16`: the video backbone with the HIP bf16 path's
+    storage emulated, see `videomae`)."""
     cls, _ = imu_encoder(sd, imu, patch_size=mcfg['imu_patch_size'], stride=mcfg['imu_stride'],
                          nhead=mcfg['imu_nhead'], num_layers=mcfg['imu_num_layers'], dropout=imu_dropout,
                          training=training, gen=gen)
     vf = video_encoder(sd, video, num_heads=mcfg['video_num_heads'], patch_size=mcfg.get('video_patch_size', 16),
                        tubelet=mcfg.get('video_tubelet', 2), eps=mcfg.get('video_eps', 1e-12),
-                       use_mean_pooling=mcfg.get('video_use_mean_pooling', True))
+                       use_mean_pooling=mcfg.get('video_use_mean_pooling', True), bf16=bf16)
     a = projection_head(sd, cls, 'imu_proj.', training, update_stats)
     b = projection_head(sd, vf, 'video_proj.', training, update_stats)
     return l2_normalize(a), l2_normalize(b)

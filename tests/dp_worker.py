@@ -1,12 +1,18 @@
 """One rank of the on-device data-parallel check (launched by tests/test_dist_gpu.py, never collected by pytest).
 
-Every rank runs the real `CrossModalModel` (HIP path, fp32 parity mode, tiny geometry) on its shard of a fixed
-global batch: forward → SigLIP loss over the all-gathered global batch → backward with `GradReducer` (SUM
-all-reduce of gradients, bucketed) on process group backend `CMHAR_DP_BACKEND` (gloo: both ranks share the one
-GPU of the test box).  Rank 0 then builds the single-process DataParallel equivalent on the same GPU — the same
-weights, each shard through the model separately (per-replica BatchNorm, reference main.py:89-93), one loss over
-the concatenated embeddings, one backward — and compares loss and every parameter gradient.  Also checked:
-`broadcast_buffers` leaves rank 0's BN running statistics on every rank, and only rank 0 writes checkpoints.
+Every rank runs the real `CrossModalModel` (HIP path, `CMHAR_DP_DTYPE` fp32 parity mode or bf16, tiny geometry) on
+its shard of a fixed global batch: forward → SigLIP loss over the all-gathered global batch → backward with
+`GradReducer` (SUM all-reduce of gradients, bucketed) on process group backend `CMHAR_DP_BACKEND` (gloo: both ranks
+share the one GPU of the test box).  A first step teaches the reducer the hook order; the second, measured step
+records how many buckets were in flight when backward returned.
+
+Rank 0 then computes the reference's `nn.DataParallel` step (main.py:89-93) on the CPU ORACLE (oracle/cpu_model.py,
+pinned to the reference by g1-g9; oracle/r3d_cpu.py for the R3D-18 backbone): the same weights, each shard through
+the model separately (per-replica train-mode BatchNorm, as DataParallel's replicas), one `siglip_loss` over the
+concatenated embeddings, one backward — and writes the loss and every parameter gradient's error.  For bf16 it also
+runs the oracle with the HIP path's bf16 storage emulated, whose distance to the fp32 oracle bounds the bf16 errors.
+Rank 0 also repeats the step single-process on the HIP path (the bit-level "DP = single process" check).  Also
+checked: `broadcast_buffers` leaves rank 0's BN running statistics on every rank, and only rank 0 writes checkpoints.
 Results go to `$CMHAR_DP_OUT/rank{r}.json`.
 """
 import json
@@ -92,6 +98,25 @@ def classify(D, rank, world, dev, out_dir):
             errs[n] = (float((grads[n] - rg).norm()) / max(float(rg.norm()), 1e-30), float(rg.norm()))
         res['grad_errs'] = errs
         res['missing'] = sorted(set(grads) ^ {n for n, p in ref.named_parameters() if p.grad is not None})
+    # validate() with uneven shards: rank 0 holds two batches, rank 1 one; no per-batch collective,
+    # and the loss is the mean over GLOBAL batches (batch 0 = both ranks' first shards, batch 1 = rank 0's second)
+    D.broadcast_buffers(clf)
+    gv = torch.Generator().manual_seed(9)
+    shards = [[(torch.randn(3, 6, 64, generator=gv), torch.randint(0, cfg.model.num_classes, (3,), generator=gv))
+               for _ in range(2)],
+              [(torch.randn(3, 6, 64, generator=gv), torch.randint(0, cfg.model.num_classes, (3,), generator=gv))]]
+    mine = shards[rank] if rank < 2 else []
+    vm = tr.validate([{'imu': x, 'label': y} for x, y in mine])
+    res['val_loss'] = vm['loss']
+    if rank == 0:
+        clf.eval()
+        with torch.no_grad():
+            glob = [[shards[0][0], shards[1][0]], [shards[0][1]]]
+            ces = []
+            for parts in glob:
+                lg = torch.cat([clf(x.to(dev)) for x, _ in parts])
+                ces.append(float(CrossEntropyLoss()(lg, torch.cat([y for _, y in parts]).to(dev)).item()))
+        res['ref_val_loss'] = sum(ces) / len(ces)
     with open(os.path.join(out_dir, f'rank{rank}.json'), 'w') as f:
         json.dump(res, f)
     flat = torch.cat([grads[n].reshape(-1) for n in sorted(grads)])
@@ -100,6 +125,44 @@ def classify(D, rank, world, dev, out_dir):
     with open(os.path.join(out_dir, f'rank{rank}.sum'), 'w') as f:
         json.dump(objs, f)
     dist.destroy_process_group()
+
+
+def oracle_step(backbone, init_sd, cfg, imu_all, video_all, world, bl, bf16):
+    """The reference's DataParallel step on the CPU oracle: per-shard forward with train-mode BN, SigLIP over the
+    gathered global batch, one backward.  Returns (loss, {param name: grad})."""
+    import numpy as np
+    import torch.nn.functional as F
+    sys.path.insert(0, REPO)
+    sys.path.insert(0, os.path.join(REPO, 'tests'))
+    from fixtures import oracle_mcfg
+    from oracle import cpu_model as O
+    from oracle.r3d_cpu import bf16_storage, r3d18_features
+    sd = {k: (v.clone().requires_grad_(True) if v.is_floating_point() and 'running' not in k else v.clone())
+          for k, v in init_sd.items()}
+    mc = oracle_mcfg(cfg)
+    outs = []
+    for r in range(world):
+        imu, video = imu_all[r * bl:(r + 1) * bl], video_all[r * bl:(r + 1) * bl]
+        if backbone == 'videomae':
+            outs.append(O.crossmodal(sd, imu, video, mc, training=True, bf16=bf16))
+            continue
+        pre = 'video_encoder.backbone.'
+        bsd = {k[len(pre):]: v for k, v in sd.items() if k.startswith(pre)}
+        cls, _ = O.imu_encoder(sd, imu, patch_size=mc['imu_patch_size'], stride=mc['imu_stride'],
+                               nhead=mc['imu_nhead'], num_layers=mc['imu_num_layers'])
+        feat = r3d18_features(bsd, video.transpose(1, 2), training=True, q=bf16_storage if bf16 else None)
+        vf = F.linear(feat, sd['video_encoder.projection.weight'], sd['video_encoder.projection.bias'])
+        outs.append((O.l2_normalize(O.projection_head(sd, cls, 'imu_proj.', True)),
+                     O.l2_normalize(O.projection_head(sd, vf, 'video_proj.', True))))
+    loss = O.siglip_loss(torch.cat([o[0] for o in outs]), torch.cat([o[1] for o in outs]),
+                         torch.tensor(float(np.log(10.0))), torch.tensor(-10.0))
+    loss.backward()
+    return float(loss.item()), {k: v.grad for k, v in sd.items() if v.is_floating_point() and v.grad is not None}
+
+
+def _errs(grads, ref):
+    return {n: (float((grads[n] - g).norm()) / max(float(g.norm()), 1e-30), float(g.norm()), float(g.abs().max()))
+            for n, g in ref.items() if n in grads}
 
 
 def main():
@@ -130,23 +193,26 @@ def main():
     reducer = D.GradReducer(model, backbone=model.video_encoder.backbone, bucket_mb=0.25 if backbone == 'videomae' else 8.0)
     loss_fn = SigmoidContrastiveLoss().to(dev)
     sl = slice(rank * bl, (rank + 1) * bl)
-    a, b = model(imu_all[sl].to(dev), video_all[sl].to(dev))
-    loss = loss_fn(a, b)
-    reducer.start_step()
-    loss.backward()
-    reducer.finish()
+    for step in range(2):                # step 0 teaches the reducer the hook order; step 1 is the one checked
+        model.zero_grad(set_to_none=True)
+        a, b = model(imu_all[sl].to(dev), video_all[sl].to(dev))
+        loss = loss_fn(a, b)
+        reducer.start_step()
+        loss.backward()
+        reducer.finish()
     torch.cuda.synchronize()
     grads = {n: p.grad.detach().cpu() for n, p in model.named_parameters() if p.grad is not None}
     res = {'rank': rank, 'loss': float(loss.item()), 'n_buckets': len(reducer.buckets),
-           'sink': reducer.sink is not None, 'n_grads': len(grads)}
+           'sink': reducer.sink is not None, 'n_grads': len(grads), 'learned': reducer.learned,
+           'launched_before_finish': reducer.launched_before_finish,
+           'trailing_unused': [n for n, p in model.named_parameters()
+                               if any(p is q for q in reducer.buckets[-1].params)]}
 
     # BN running statistics: rank 0's everywhere after broadcast_buffers
     bn_key = 'video_proj.net.1.running_mean'
     before = model.state_dict()[bn_key].detach().cpu().clone()
     D.broadcast_buffers(model)
     after = model.state_dict()[bn_key].detach().cpu()
-    ref0 = torch.empty_like(after)
-    ref0.copy_(after)
     obj = [None] * world
     dist.all_gather_object(obj, before.tolist())
     res['bn_broadcast_ok'] = bool(torch.equal(after, torch.tensor(obj[0])))
@@ -160,28 +226,28 @@ def main():
     res['wrote_checkpoint'] = os.path.exists(ck) or (rank == 0 and os.path.exists(os.path.join(out_dir, 'ckpt.pt')))
 
     if rank == 0:
-        # single-process DataParallel equivalent on the same device and kernels
+        # (1) the reference's DataParallel step on the CPU oracle (fp32), and its bf16-storage emulation
+        cfg = model.config
+        res['oracle_loss'], og = oracle_step(backbone, init_sd, cfg, imu_all, video_all, world, bl, False)
+        res['missing_oracle'] = sorted(set(og) ^ set(grads))
+        res['oracle_errs'] = _errs(grads, og)
+        if dtype == 'bf16':
+            res['emul_loss'], eg = oracle_step(backbone, init_sd, cfg, imu_all, video_all, world, bl, True)
+            res['emul_errs'] = _errs(eg, og)
+        # (2) single-process DataParallel equivalent on the same device and kernels
         ref = build(backbone, dtype)
         ref.load_state_dict(init_sd)
         ref = ref.to(dev).train()
         lf = SigmoidContrastiveLoss(group=False).to(dev)
         outs = [ref(imu_all[r * bl:(r + 1) * bl].to(dev), video_all[r * bl:(r + 1) * bl].to(dev))
                 for r in range(world)]
-        ra = torch.cat([o[0] for o in outs])
-        rb = torch.cat([o[1] for o in outs])
-        rloss = lf(ra, rb)
+        rloss = lf(torch.cat([o[0] for o in outs]), torch.cat([o[1] for o in outs]))
         rloss.backward()
         torch.cuda.synchronize()
         rgrads = {n: p.grad.detach().cpu() for n, p in ref.named_parameters() if p.grad is not None}
         res['ref_loss'] = float(rloss.item())
         res['missing'] = sorted(set(rgrads) ^ set(grads))
-        errs = {}
-        for n, rg in rgrads.items():
-            if n not in grads:
-                continue
-            scale = max(float(rg.norm()), 1e-30)
-            errs[n] = (float((grads[n] - rg).norm()) / scale, float(rg.norm()))
-        res['grad_errs'] = errs
+        res['grad_errs'] = {n: e[:2] for n, e in _errs(grads, rgrads).items()}
     with open(os.path.join(out_dir, f'rank{rank}.json'), 'w') as f:
         json.dump(res, f)
     # every rank must hold the same reduced gradients

@@ -238,3 +238,27 @@ def test_imu_fused_gating():
         T = min(1 + 6 * ((W - 16) // 16 + 1), m.pos_encoding.shape[1])
         ok.append(imu._fused_ok(m, T))
     assert ok == [True, True, True, False, False, False, False]
+
+
+@pytest.mark.parametrize('backbone', ['videomae', 'r3d_18', 'resnet18'])
+def test_multi_device_dataparallel_refused_with_pointer(backbone):
+    """VERDICT r02 item 8 (SURVEY §8b threading contract): `nn.DataParallel(model)` over several GPUs replicates
+    each submodule with `_replicate_for_data_parallel` (torch replicate.py); the cmhar HIP modules refuse it and
+    name cmhar.dist, the supported DataParallel-equivalent path."""
+    from cmhar.config import Config
+    from cmhar.models import CrossModalModel
+    cfg = Config()
+    cfg.data.video_frames_per_window, cfg.data.video_resize = 2, (16, 16)
+    m = cfg.model
+    m.video_pretrained = False
+    m.video_backbone = '/nonexistent/videomae' if backbone == 'videomae' else backbone
+    m.videomae_hidden_size, m.videomae_num_layers, m.videomae_num_heads, m.videomae_intermediate_size = 64, 1, 1, 128
+    model = CrossModalModel(cfg)
+    refused = []
+    for name, mod in model.named_modules():
+        try:
+            mod._replicate_for_data_parallel()
+        except RuntimeError as e:
+            assert 'cmhar.dist' in str(e) and 'GradReducer' in str(e)
+            refused.append(name)
+    assert {'imu_encoder', 'video_encoder.backbone', 'imu_proj', 'video_proj'} <= set(refused), refused

@@ -18,17 +18,26 @@ pytestmark = pytest.mark.gpu
 DEV = 'cuda'
 
 
+def _equal_nan(a, b):
+    return bool(((a == b) | (a.isnan() & b.isnan())).all())
+
+
 def rel(a, b):
     a, b = torch.as_tensor(a).detach().double().cpu(), torch.as_tensor(b).detach().double().cpu()
     return ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
 
 
+@pytest.mark.parametrize('nan', [False, True])
 @pytest.mark.parametrize('dt', [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize('N,C,H,W', [(3, 64, 56, 56), (2, 16, 13, 11)])
-def test_maxpool_fwd_bwd_with_ties(dt, N, C, H, W):
+def test_maxpool_fwd_bwd_with_ties(dt, N, C, H, W, nan):
+    """`nan`: ~3 % NaN inputs — the NaN propagates as in torch (output NaN, gradient to the window's last
+    NaN), instead of being skipped."""
     from cmhar import _lib as L
     torch.manual_seed(0)
     x = torch.randint(-3, 4, (N, C, H, W)).float()          # many tied maxima
+    if nan:
+        x[torch.rand(x.shape) < 0.03] = float('nan')
     xr = x.clone().requires_grad_(True)
     ref = F.max_pool2d(xr, 3, 2, 1)
     dy = torch.randint(-4, 5, ref.shape).float()
@@ -39,7 +48,8 @@ def test_maxpool_fwd_bwd_with_ties(dt, N, C, H, W):
     arg = torch.empty(N * Ho * Wo, C, dtype=torch.uint8, device=DEV)
     L.call('cmhar_maxpool2d_cl_fwd', L.dtype_code(dt), N, H, W, C, 3, 2, 1, xc.data_ptr(), y.data_ptr(),
            arg.data_ptr(), L.stream(xc.device))
-    assert torch.equal(y.float().cpu().view(N, Ho, Wo, C).permute(0, 3, 1, 2), ref.detach())
+    assert _equal_nan(y.float().cpu().view(N, Ho, Wo, C).permute(0, 3, 1, 2), ref.detach())
+    assert (ref.isnan().any().item()) == nan
     dyc = dy.permute(0, 2, 3, 1).contiguous().to(DEV, dt)
     dx = torch.empty(N * H * W, C, dtype=dt, device=DEV)
     L.call('cmhar_maxpool2d_cl_bwd', L.dtype_code(dt), N, H, W, C, 3, 2, 1, dyc.data_ptr(), arg.data_ptr(),

@@ -133,6 +133,70 @@ def test_dataparallel_semantics_global_loss_summed_grads():
 
 
 # ---------------------------------------------------------------------------------------------------------------
+class _TwoTowerUnused(_TwoTower):
+    """two parameters that never get a gradient (like `CrossModalModel.temperature` / `bias`) in a
+    submodule registered last, so the reverse-registration guess puts them in the FIRST hook bucket."""
+
+    def __init__(self):
+        super().__init__()
+        self.unused = nn.Module()
+        self.unused.temperature = nn.Parameter(torch.ones([]))
+        self.unused.bias = nn.Parameter(torch.ones([]))
+
+
+def _hook_order_worker(rank, world, port):
+    _init(rank, world, port)
+    from cmhar.dist import GradReducer, broadcast_parameters
+    from cmhar.losses import gather_global
+    from oracle.cpu_model import siglip_loss
+    torch.manual_seed(100)
+    model = _TwoTowerUnused().train()
+    broadcast_parameters(model)
+    reducer = GradReducer(model, backbone=None, bucket_mb=60 * 4 / (1 << 20))   # ~60-element buckets
+    n_hook = len(reducer.buckets)
+    assert n_hook >= 3
+    X, Y = _data(world)
+    bl = X.shape[0] // world
+    launched = []
+    for step in range(3):
+        model.zero_grad(set_to_none=True)
+        a, b = model(X[rank * bl:(rank + 1) * bl], Y[rank * bl:(rank + 1) * bl])
+        a_all, b_all, off = gather_global(a.detach().contiguous(), b.detach().contiguous(), dist.group.WORLD)
+        a_all = torch.cat([a_all[:off], a, a_all[off + bl:]])
+        b_all = torch.cat([b_all[:off], b, b_all[off + bl:]])
+        loss = siglip_loss(a_all, b_all, torch.tensor(10.0).log(), torch.tensor(-10.0))
+        reducer.start_step()
+        loss.backward()
+        launched.append(sum(bk.launched for bk in reducer.buckets))
+        reducer.finish()
+        assert model.unused.temperature.grad is None and model.unused.bias.grad is None
+        # gradients = the single-process DataParallel computation (summed over replicas)
+        ref = _TwoTowerUnused().train()
+        ref.load_state_dict(model.state_dict())
+        outs = [ref(X[r * bl:(r + 1) * bl], Y[r * bl:(r + 1) * bl]) for r in range(world)]
+        rloss = siglip_loss(torch.cat([o[0] for o in outs]), torch.cat([o[1] for o in outs]),
+                            torch.tensor(10.0).log(), torch.tensor(-10.0))
+        rloss.backward()
+        for (n, p), (_, q) in zip(model.named_parameters(), ref.named_parameters()):
+            if q.grad is None:
+                assert p.grad is None, n
+            else:
+                torch.testing.assert_close(p.grad, q.grad, rtol=1e-5, atol=1e-7, msg=n)
+    assert reducer.learned
+    # step 1: the unused parameters' bucket stalls every hook bucket until finish(); afterwards every bucket
+    # except the trailing never-fired one is in flight when backward returns
+    assert launched[0] == 0, launched
+    assert launched[1] == launched[2] == len(reducer.buckets) - 1, (launched, len(reducer.buckets))
+    assert [id(p) for p in reducer.buckets[-1].params] == [id(model.unused.bias), id(model.unused.temperature)]
+    dist.destroy_process_group()
+
+
+def test_grad_reducer_learns_hook_order_and_overlaps():
+    """hook buckets must launch during backward, not all in finish()."""
+    _spawn(_hook_order_worker)
+
+
+# ---------------------------------------------------------------------------------------------------------------
 def _bucket_worker(rank, world, port):
     _init(rank, world, port)
     from cmhar.dist import GradReducer, backbone_param_order

@@ -1,7 +1,9 @@
-"""Data-parallel step of the REAL model on the GPU: two ranks (gloo, sharing the test box's
-one MI355X) run `CrossModalModel` on the HIP path through `GradReducer`; the reduced gradients and the loss must
-equal the single-process DataParallel equivalent (each shard through the model separately — per-replica BN — one
-SigLIP loss over the global batch), reference `main.py:89-93`.
+"""Data-parallel step of the REAL model on the GPU: two ranks (gloo, sharing the test box's one MI355X) run
+`CrossModalModel` on the HIP path through `GradReducer`; the loss and the reduced gradients must equal the
+reference's `nn.DataParallel` step (`main.py:89-93`: each shard through the model separately — per-replica BN — one
+SigLIP loss over the gathered global batch, summed gradients) computed by the CPU oracle (tests/dp_worker.py), in
+fp32 and bf16, for the VideoMAE and R3D-18 backbones.  RCCL itself needs one GPU per rank, which the one-GPU test
+box does not have; the collective sequence is the same code path (`torch.distributed` with backend "nccl").
 
 The ranks are separate processes started with subprocess from this pytest process, whose GPU probe
 (`tests/conftest.py`) does not initialise HIP.
@@ -21,6 +23,10 @@ def _free_port():
     with socket.socket() as s:
         s.bind(('127.0.0.1', 0))
         return s.getsockname()[1]
+
+
+TOL_FP32 = {'videomae': 1e-4, 'r3d_18': 1e-4}
+FLOOR_BF16 = {'videomae': 2e-3, 'r3d_18': 1e-2}
 
 
 def _run(tmp_path, backbone, dtype='fp32', world=2):
@@ -47,21 +53,50 @@ def _run(tmp_path, backbone, dtype='fp32', world=2):
         [json.load(open(tmp_path / f'rank{r}.sum')) for r in range(world)]
 
 
+def _zero_grad(name, gmax, scale):
+    """Mathematically-zero gradients (key biases, biases feeding train-mode BatchNorm) carry only rounding noise in
+    any implementation: compared as ≈0 instead (the convention of tests/test_models_gpu.py)."""
+    return gmax < 1e-5 * scale
+
+
 @pytest.mark.gpu
+@pytest.mark.parametrize('dtype', ['fp32', 'bf16'])
 @pytest.mark.parametrize('backbone', ['videomae', 'r3d_18'])
-def test_dataparallel_real_model_two_ranks(tmp_path, backbone):
-    res, sums = _run(tmp_path, backbone)
+def test_dataparallel_real_model_two_ranks(tmp_path, backbone, dtype):
+    """the two-rank HIP step against the reference's DataParallel step on the CPU oracle.
+    fp32: loss ≤ 1e-6 rel, every gradient ≤ TOL_FP32 rel.  bf16: every gradient within 3× the error that bf16
+    storage itself causes (the oracle run with the HIP path's bf16 storage emulated) + FLOOR_BF16."""
+    res, sums = _run(tmp_path, backbone, dtype)
     r0, r1 = res
     assert r0['sink'] == (backbone == 'videomae')
     assert r0['n_buckets'] >= 2
-    # global-batch loss identical on every rank and equal to the single-process loss
+    # global-batch loss identical on every rank; equal to the oracle's DataParallel loss
     assert r0['loss'] == r1['loss']
+    lt = 1e-6 if dtype == 'fp32' else 3 * abs(r0['emul_loss'] - r0['oracle_loss']) / abs(r0['oracle_loss']) + 1e-4
+    assert abs(r0['loss'] - r0['oracle_loss']) <= lt * abs(r0['oracle_loss']), (r0['loss'], r0['oracle_loss'])
+    assert r0['missing_oracle'] == []
+    scale = max(e[2] for e in r0['oracle_errs'].values())
+    bad = {}
+    for n, (e, norm, gmax) in r0['oracle_errs'].items():
+        if _zero_grad(n, gmax, scale):
+            continue
+        bound = TOL_FP32[backbone] if dtype == 'fp32' else 3 * r0['emul_errs'][n][0] + FLOOR_BF16[backbone]
+        if e > bound:
+            bad[n] = (e, bound)
+    assert not bad, bad
+    # DP step == the single-process step of the same HIP kernels; same reduced gradients on both ranks
     assert abs(r0['loss'] - r0['ref_loss']) <= 1e-6 * abs(r0['ref_loss'])
     assert r0['missing'] == []
     bad = {n: e for n, (e, norm) in r0['grad_errs'].items() if norm > 1e-6 and e > 1e-5}
     assert not bad, bad
-    # same reduced gradients on both ranks (bit-identical sums)
     assert sums[0][0] == sums[0][1]
+    # validate() over uneven shards: global-batch losses, identical on both ranks
+    assert abs(r0['val_loss'] - r0['ref_val_loss']) <= 1e-5 * abs(r0['ref_val_loss'])
+    assert r0['val_loss'] == r1['val_loss']
+    # ADVICE r02: after the first step every hook bucket but the trailing unused one (temperature, bias) is in
+    # flight when backward returns
+    assert r0['learned'] and r0['launched_before_finish'] == r0['n_buckets'] - 1, r0
+    assert sorted(r0['trailing_unused']) == ['bias', 'temperature'], r0['trailing_unused']
     # rank 0's BN running statistics everywhere; one checkpoint writer
     assert r0['bn_differed_before'] and r0['bn_broadcast_ok'] and r1['bn_broadcast_ok']
     assert r0['wrote_checkpoint'] and not r1['wrote_checkpoint']
@@ -78,3 +113,6 @@ def test_dataparallel_classification_global_mean(tmp_path):
     bad = {n: e for n, (e, norm) in r0['grad_errs'].items() if norm > 1e-6 and e > 1e-5}
     assert not bad, bad
     assert sums[0][0] == sums[0][1]
+    # validate() over uneven shards: global-batch losses, identical on both ranks
+    assert abs(r0['val_loss'] - r0['ref_val_loss']) <= 1e-5 * abs(r0['ref_val_loss'])
+    assert r0['val_loss'] == r1['val_loss']

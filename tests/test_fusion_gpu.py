@@ -42,6 +42,123 @@ def test_fusion_matches_oracle(dtype, Lk, B):
         assert rel(p.grad, sd[k].grad) < tol_g, (k, rel(p.grad, sd[k].grad))
 
 
+@pytest.mark.parametrize('dtype', ['fp32', 'bf16', 'fp16'])
+def test_fusion_config4_geometry(dtype):
+    """config 4's own attention geometry — Lq = 26 IMU tokens (CLS + 25 patches of a 400-step
+    window) over Lk = 3136 video tokens (32 × 224² → 16 × 14 × 14 tubelets), B = 2 — against the oracle.  fp32 and
+    bf16 forward + backward at the bounds of `test_fusion_matches_oracle`; fp16 (config 5's inference dtype) forward
+    ≤ 5e-3 (fp16 has no training path)."""
+    from cmhar.fusion import CrossAttentionFusion
+    from oracle.fusion_cpu import fusion_forward
+    B, Lq, Lk = 2, 26, 3136
+    torch.manual_seed(3)
+    m = CrossAttentionFusion(128, 768, 256, 4, 32, compute_dtype=dtype)
+    sd = {k: v.clone().requires_grad_(True) for k, v in m.state_dict().items()}
+    imu = torch.randn(B, Lq, 128, requires_grad=True)
+    vid = torch.randn(B, Lk, 768, requires_grad=True)
+    R = torch.randn(B, 32)
+    logits_ref, fused_ref = fusion_forward(sd, imu, vid, 4)
+    m = m.to(DEV)
+    if dtype == 'fp16':
+        with torch.no_grad():
+            logits, fused = m(imu.detach().to(DEV), vid.detach().to(DEV))
+        assert rel(logits, logits_ref) < 5e-3, rel(logits, logits_ref)
+        assert rel(fused, fused_ref) < 5e-3, rel(fused, fused_ref)
+        return
+    (logits_ref * R).sum().backward()
+    imu_g = imu.detach().to(DEV).requires_grad_(True)
+    vid_g = vid.detach().to(DEV).requires_grad_(True)
+    logits, fused = m(imu_g, vid_g)
+    (logits * R.to(DEV)).sum().backward()
+    tol_f, tol_g = (1e-5, 1e-4) if dtype == 'fp32' else (2e-2, 5e-2)
+    assert rel(logits, logits_ref) < tol_f
+    assert rel(fused, fused_ref) < tol_f
+    assert rel(imu_g.grad, imu.grad) < tol_g
+    assert rel(vid_g.grad, vid.grad) < tol_g
+    for k, p in m.named_parameters():
+        assert rel(p.grad, sd[k].grad) < tol_g, (k, rel(p.grad, sd[k].grad))
+
+
+def _fusion_cfg(dtype, frames=32, imu_w=400):
+    from cmhar.config import Config
+    cfg = Config()
+    cfg.data.imu_window_size = imu_w
+    cfg.data.video_frames_per_window = frames
+    cfg.data.video_resize = (32, 32)
+    m = cfg.model
+    m.video_backbone = '/nonexistent/videomae-fusion'
+    m.video_pretrained = False
+    m.imu_dropout = 0.0
+    m.videomae_hidden_size, m.videomae_num_layers, m.videomae_num_heads = 128, 2, 2
+    m.videomae_intermediate_size = 256
+    m.compute_dtype = dtype
+    return cfg
+
+
+def _fusion_oracle(sd, cfg, imu, video):
+    """IMU encoder (oracle/cpu_model.py, pinned to the reference) → tokens; VideoMAE last_hidden_state (oracle) →
+    tokens; cross-attention fusion (oracle/fusion_cpu.py) → class logits."""
+    from fixtures import oracle_mcfg
+    from oracle import cpu_model as O
+    from oracle.fusion_cpu import fusion_forward
+    mc = oracle_mcfg(cfg)
+    _, tok = O.imu_encoder(sd, imu, patch_size=mc['imu_patch_size'], stride=mc['imu_stride'], nhead=mc['imu_nhead'],
+                           num_layers=mc['imu_num_layers'])
+    vt = O.videomae(sd, video, num_heads=mc['video_num_heads'], patch_size=mc['video_patch_size'],
+                    tubelet=mc['video_tubelet'], eps=mc['video_eps'], use_mean_pooling=mc['video_use_mean_pooling'])
+    logits, _ = fusion_forward(sd, tok, vt, 4, prefix='fusion.')
+    return logits
+
+
+@pytest.mark.parametrize('dtype', ['fp32', 'fp16'])
+def test_fusion_classifier_vs_oracle(dtype):
+    """`CrossModalFusionClassifier` end to end (IMU 400 → 26 tokens, 32-frame clips → 16
+    tubelets × 2 × 2, tiny spatial size) against oracle IMU encoder + oracle VideoMAE + oracle fusion on the same
+    seeded weights.  fp32 training step: logits ≤ 1e-4 rel, every parameter gradient ≤ 1e-3 rel (mathematically-zero
+    ones ≈ 0).  fp16 (config 5's inference dtype): logits ≤ 5e-3 rel."""
+    import warnings
+    from cmhar.fusion import CrossModalFusionClassifier
+    from seeded import seeded_input, seeded_state_dict
+    cfg = _fusion_cfg(dtype)
+    torch.manual_seed(4)
+    with warnings.catch_warnings():
+        warnings.simplefilter('ignore')
+        model = CrossModalFusionClassifier(cfg)
+    sd = seeded_state_dict(model.state_dict(), seed=91)
+    model.load_state_dict(sd, strict=True)
+    model = model.to(DEV)
+    B = 3
+    imu = seeded_input(92, (B, 6, 400))
+    video = seeded_input(93, (B, 32, 3, 32, 32))
+    ref_sd = {k: (v.clone().requires_grad_(True) if v.is_floating_point() else v.clone()) for k, v in sd.items()}
+    R = torch.randn(B, cfg.model.num_classes, generator=torch.Generator().manual_seed(94))
+    if dtype == 'fp16':
+        model.eval()
+        with torch.no_grad():
+            logits = model(imu.to(DEV), video.to(DEV))
+            ref = _fusion_oracle(ref_sd, cfg, imu, video)
+        assert rel(logits, ref) < 5e-3, rel(logits, ref)
+        return
+    model.train()
+    logits = model(imu.to(DEV), video.to(DEV))
+    (logits * R.to(DEV)).sum().backward()
+    ref = _fusion_oracle(ref_sd, cfg, imu, video)
+    (ref * R).sum().backward()
+    assert rel(logits, ref) < 1e-4, rel(logits, ref)
+    gscale = max(float(v.grad.abs().max()) for v in ref_sd.values() if v.is_floating_point() and v.grad is not None)
+    worst = {}
+    for name, p in model.named_parameters():
+        g = ref_sd[name].grad
+        if g is None:
+            assert p.grad is None or name.startswith('video_encoder.projection.'), name
+            continue
+        if float(g.abs().max()) < 1e-5 * gscale:
+            assert p.grad is None or float(p.grad.abs().max()) < 1e-4 * gscale, name
+            continue
+        worst[name] = rel(p.grad, g)
+    assert max(worst.values()) < 1e-3, sorted(worst.items(), key=lambda kv: -kv[1])[:4]
+
+
 def test_fusion_classifier_end_to_end():
     from cmhar.config import Config
     from cmhar.fusion import CrossModalFusionClassifier

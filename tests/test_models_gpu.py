@@ -3,6 +3,7 @@
 
 fp32 mode must match the reference to ≤1e-4 relative (outputs) — the north-star gate is 1e-3 on fp32 logits;
 bf16 mode (the throughput mode) is checked at the tolerance its 8-bit mantissa allows, written per test."""
+import functools
 import json
 
 import numpy as np
@@ -73,8 +74,32 @@ def test_g1_imu_encoder_fp32():
         assert m.patch_embed.projections[c].weight.grad.abs().max().item() == 0.0
 
 
-@pytest.mark.parametrize('dtype,tol_out,tol_grad', [('fp32', 1e-4, 1e-3), ('bf16', 2e-2, 6e-2)])
-def test_g2_crossmodal_forward_backward(dtype, tol_out, tol_grad):
+@functools.lru_cache(maxsize=None)
+def _g2_oracle(bf16):
+    """The oracle's g2 step (fp32, or with the HIP bf16 path's storage emulated): outputs, loss, gradients."""
+    from fixtures import oracle_mcfg, t
+    from oracle import cpu_model as O
+    fx = load('g2_crossmodal_tiny')
+    sd = {k: (v.clone().requires_grad_(True) if v.is_floating_point() else v.clone())
+          for k, v in fixture_state_dict(fx).items()}
+    a, b = O.crossmodal(sd, t(fx['imu']), t(fx['video']), oracle_mcfg(fixture_config(fx)), training=True, bf16=bf16)
+    loss = O.siglip_loss(a, b, torch.tensor(float(np.log(10.0))), torch.tensor(-10.0))
+    loss.backward()
+    return a.detach(), b.detach(), float(loss), {k: v.grad for k, v in sd.items()
+                                                 if v.is_floating_point() and v.grad is not None}
+
+
+def _bf16_bounded(gpu, ref, emul, floor, slack=3.0):
+    """rel(gpu, ref) ≤ slack·rel(emul, ref) + floor: the error bf16 storage alone causes (oracle with the HIP path's
+    bf16 storage emulated, `emul`) sets the bound, so a kernel error shows wherever that error is small."""
+    e_g, e_p = rel(gpu, ref), rel(emul, ref)
+    return e_g <= slack * e_p + floor, e_g, e_p
+
+
+@pytest.mark.parametrize('dtype', ['fp32', 'bf16'])
+def test_g2_crossmodal_forward_backward(dtype):
+    """fp32: outputs ≤ 1e-4, grads ≤ 1e-3 vs the reference's vectors.  bf16: outputs and every
+    gradient within 3× the bf16-storage error of the emulating oracle + 1e-3 / 2e-3 (was a blanket 2e-2 / 6e-2)."""
     from cmhar.losses import SigmoidContrastiveLoss
     fx = load('g2_crossmodal_tiny')
     m, _ = _build('CrossModalModel', fx, dtype)
@@ -83,17 +108,35 @@ def test_g2_crossmodal_forward_backward(dtype, tol_out, tol_grad):
     video = torch.tensor(fx['video'], device=DEV)
     lf = SigmoidContrastiveLoss().to(DEV)
     a, b = m(imu, video)
-    assert rel(a, fx['imu_proj']) < tol_out
-    assert rel(b, fx['video_proj']) < tol_out
     loss = lf(a, b)
-    assert abs(loss.item() - float(fx['loss'])) < tol_out * abs(float(fx['loss']))
     loss.backward()
-    errs = _grad_errors(m, fx, zero_tol=1e-4 if dtype == 'fp32' else 2e-3)   # bf16 rounding noise on zero grads
-    worst = sorted(errs.items(), key=lambda kv: -kv[1])[:5]
-    assert max(errs.values()) < tol_grad, worst
+    if dtype == 'fp32':
+        assert rel(a, fx['imu_proj']) < 1e-4
+        assert rel(b, fx['video_proj']) < 1e-4
+        assert abs(loss.item() - float(fx['loss'])) < 1e-4 * abs(float(fx['loss']))
+        errs = _grad_errors(m, fx, zero_tol=1e-4)
+        assert max(errs.values()) < 1e-3, sorted(errs.items(), key=lambda kv: -kv[1])[:5]
+    else:
+        ra, rb, rloss, rg = _g2_oracle(False)
+        ea, eb, eloss, eg = _g2_oracle(True)
+        assert rel(a, fx['imu_proj']) < 1e-4                       # the IMU branch is fp32 in every mode
+        ok, e_g, e_p = _bf16_bounded(b, rb, eb, 1e-3)
+        assert ok, ('video_proj', e_g, e_p)
+        assert abs(loss.item() - rloss) <= 3 * abs(eloss - rloss) + 1e-4 * abs(rloss)
+        gscale = max(float(g.abs().max()) for g in rg.values())
+        rows = []
+        for name, p in m.named_parameters():
+            g = rg.get(name)
+            if g is None or float(g.abs().max()) < 1e-5 * gscale:     # mathematically-zero gradient
+                assert p.grad is None or p.grad.abs().max().item() < 2e-3 * gscale, name
+                continue
+            ok, e_g, e_p = _bf16_bounded(p.grad, g, eg[name], 2e-3)
+            rows.append((e_g, e_p, name))
+            assert ok, (name, e_g, e_p)
+        print('worst (gpu err, bf16-storage err, param):', sorted(rows, reverse=True)[:4])
     for key in fx.files:
         if key.startswith('bn.') and 'running' in key:
-            assert rel(m.state_dict()[key[3:]], fx[key]) < max(tol_out, 1e-5), key
+            assert rel(m.state_dict()[key[3:]], fx[key]) < (1e-5 if dtype == 'fp32' else 1e-2), key
 
 
 def test_g2_two_trainer_steps_fused_optimizer():
@@ -151,10 +194,7 @@ def test_g4_classifier_train_eval():
     assert rel(le, fx['logits_eval']) < 1e-5
 
 
-@pytest.mark.parametrize('dtype,tol', [('fp32', 1e-3), ('bf16', 6e-2)])
-def test_g5_videomae_base_full_geometry(dtype, tol):
-    """VideoMAE-B at the metric's clip geometry (16×224², 1568 tokens, 12 layers): token-0 features and the
-    VideoEncoder output vs the reference.  fp32 mode: ≤1e-3 relative (north-star logits gate)."""
+def _g5_encoder(dtype):
     from cmhar.config import Config
     from cmhar.models import VideoEncoder
     fx = load('g5_videomae_base_16x224')
@@ -165,11 +205,83 @@ def test_g5_videomae_base_full_geometry(dtype, tol):
     with pytest.warns(UserWarning):
         venc = VideoEncoder(cfg)
     venc.load_state_dict(fixture_state_dict(fx), strict=True)
-    venc = venc.to(DEV).eval()
+    return venc.to(DEV), fx
+
+
+@functools.lru_cache(maxsize=None)
+def _g5_oracle(bf16, backward):
+    """VideoEncoder at 16×224² on the oracle (fp32, or with the bf16 storage emulated), B = 1: token-0 feature
+    (last_hidden_state[:, 0] → projection) and, with `backward`, every parameter gradient of Σ feat·R."""
+    from oracle import cpu_model as O
+    fx = load('g5_videomae_base_16x224')
+    sd = {k: (v.clone().requires_grad_(backward) if v.is_floating_point() else v.clone())
+          for k, v in fixture_state_dict(fx).items()}
+    video = seeded_input(int(fx['video_seed']), tuple(int(s) for s in fx['video_shape']))
+    with torch.set_grad_enabled(backward):
+        h = O.videomae(sd, video, num_heads=12, prefix='backbone.', bf16=bf16)
+        feat = torch.nn.functional.linear(h[:, 0], sd['projection.weight'], sd['projection.bias'])
+        grads = None
+        if backward:
+            R = torch.randn(feat.shape, generator=torch.Generator().manual_seed(5))
+            (feat * R).sum().backward()
+            grads = {k: v.grad for k, v in sd.items() if v.is_floating_point() and v.grad is not None}
+    return h[:, 0].detach(), h[:, -1].detach(), feat.detach(), grads
+
+
+@pytest.mark.parametrize('dtype', ['fp32', 'bf16'])
+def test_g5_videomae_base_full_geometry(dtype):
+    """VideoMAE-B at the metric's clip geometry (16×224², 1568 tokens, 12 layers): token-0 features and the
+    VideoEncoder output vs the reference.  fp32 mode: ≤1e-3 relative (north-star logits gate).  bf16: within 3× the
+    bf16-storage error of the emulating oracle + 1e-3 (was a blanket 6e-2)."""
+    venc, fx = _g5_encoder(dtype)
+    venc = venc.eval()
     video = seeded_input(int(fx['video_seed']), tuple(int(s) for s in fx['video_shape'])).to(DEV)
     with torch.no_grad():
         feat = venc(video)
         hs = venc.backbone(video).last_hidden_state
-    assert rel(hs[:, 0], fx['token0']) < tol
-    assert rel(hs[:, -1], fx['last_row']) < tol
-    assert rel(feat, fx['feat']) < tol
+    if dtype == 'fp32':
+        assert rel(hs[:, 0], fx['token0']) < 1e-3
+        assert rel(hs[:, -1], fx['last_row']) < 1e-3
+        assert rel(feat, fx['feat']) < 1e-3
+        return
+    e0, el, ef, _ = _g5_oracle(True, False)
+    for got, key, emul in ((hs[:, 0], 'token0', e0), (hs[:, -1], 'last_row', el), (feat, 'feat', ef)):
+        ok, e_g, e_p = _bf16_bounded(got, torch.as_tensor(np.asarray(fx[key])), emul, 1e-3)
+        assert ok, (key, e_g, e_p)
+
+
+@pytest.mark.parametrize('dtype', ['fp32', 'bf16'])
+def test_videomae_base_full_geometry_backward(dtype):
+    """the backward through VideoEncoder.forward (models.py:197-203) at 16×224² (1568 tokens,
+    12 layers, B = 1) against the oracle: every parameter gradient ≤ 1e-3 relative in fp32; in bf16 within 3× the
+    bf16-storage error of the emulating oracle + 2e-3."""
+    venc, fx = _g5_encoder(dtype)
+    venc = venc.train()
+    video = seeded_input(int(fx['video_seed']), tuple(int(s) for s in fx['video_shape'])).to(DEV)
+    feat = venc(video)
+    R = torch.randn(feat.shape, generator=torch.Generator().manual_seed(5))
+    (feat * R.to(DEV)).sum().backward()
+    _, _, rf, rg = _g5_oracle(False, True)
+    assert rel(feat, rf) < (1e-3 if dtype == 'fp32' else 5e-2)
+    if dtype == 'bf16':
+        _, _, ef, eg = _g5_oracle(True, True)
+        ok, e_g, e_p = _bf16_bounded(feat, rf, ef, 1e-3)
+        assert ok, ('feat', e_g, e_p)
+    gscale = max(float(g.abs().max()) for g in rg.values())
+    rows, bad = [], {}
+    for name, p in venc.named_parameters():
+        g = rg[name]
+        if float(g.abs().max()) < 1e-5 * gscale:                    # mathematically-zero (key biases)
+            continue
+        if dtype == 'fp32':
+            e = rel(p.grad, g)
+            rows.append((e, name))
+            if e > 1e-3:
+                bad[name] = e
+        else:
+            ok, e_g, e_p = _bf16_bounded(p.grad, g, eg[name], 2e-3)
+            rows.append((e_g, e_p, name))
+            if not ok:
+                bad[name] = (e_g, e_p)
+    print('worst:', sorted(rows, reverse=True)[:5])
+    assert not bad, bad
