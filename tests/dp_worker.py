@@ -132,8 +132,8 @@ def oracle_step(backbone, init_sd, cfg, imu_all, video_all, world, bl, bf16):
     gathered global batch, one backward.  Returns (loss, {param name: grad})."""
     import numpy as np
     import torch.nn.functional as F
-    sys.path.insert(0, REPO)
-    sys.path.insert(0, os.path.join(REPO, 'tests'))
+    for d in (REPO, os.path.join(REPO, 'tests'), os.path.join(REPO, 'tests', 'golden')):
+        sys.path.insert(0, d)
     from fixtures import oracle_mcfg
     from oracle import cpu_model as O
     from oracle.r3d_cpu import bf16_storage, r3d18_features
