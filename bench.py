@@ -320,7 +320,7 @@ def build_workload(args, dev, rank, world):
     from cmhar.config import Config
     from cmhar.losses import SigmoidContrastiveLoss, cross_entropy
     from cmhar.models import CrossModalModel
-    from cmhar.optim import FusedAdamW, clip_grad_norm_
+    from cmhar.optim import FusedAdamW
 
     def make_cfg():
         cfg = Config()
@@ -380,8 +380,9 @@ def build_workload(args, dev, rank, world):
     # LinearLR(start_factor=0.1) of trainer.py:80-105 → step-0 lr = 0.1 * pretrain_lr
     params = [p for n, p in model.named_parameters() if not (args.workload == 'fusion' and
                                                               n.startswith('video_encoder.projection.'))]
+    # max_grad_norm: clip_grad_norm_(params, 1.0) folded into the AdamW pass, as CrossModalTrainer does
     opt = FusedAdamW(params, lr=0.1 * 1e-4, weight_decay=0.01,
-                     shadow_sources=[backbone] if args.workload != 'r3d' else [])
+                     shadow_sources=[backbone] if args.workload != 'r3d' else [], max_grad_norm=1.0)
     video = torch.randn(B, args.frames, 3, args.image, args.image, device=dev, generator=g)
     imu = torch.randn(B, 6, args.imu_len, device=dev, generator=g)
     if args.workload == 'fusion':
@@ -424,8 +425,7 @@ def build_workload(args, dev, rank, world):
         reducer.start_step()
         loss.backward()
         reducer.finish()
-        clip_grad_norm_(params, 1.0)
-        opt.step()
+        opt.step()               # clip_grad_norm_(params, 1.0) + AdamW (trainer.py:140-141)
         return loss
     W.step, W.training = step, True
     return W

@@ -94,6 +94,7 @@ _SIGS = {
                                   i64, f32, f32, vp, vp, vp]),
     'cmhar_mt_grad_norm': (i32, [vp, vp, i32, vp, vp, f32, i32, vp]),
     'cmhar_mt_adamw': (i32, [vp, vp, i32, f32, f32, f32, f32, f32, f32, f32, vp, vp]),
+    'cmhar_mt_adamw_clip': (i32, [vp, vp, i32, f32, f32, f32, f32, f32, f32, f32, vp, i32, vp]),
     'cmhar_mt_cast_bf16': (i32, [vp, vp, i32, vp]),
     'cmhar_conv3d_im2col': (i32, [i32, i32, vp, vp, vp, vp]),
     'cmhar_conv3d_col2im': (i32, [i32, vp, vp, vp, i32, vp]),

@@ -54,15 +54,21 @@ def clip_grad_norm_(parameters, max_norm: float, norm_type: float = 2.0, error_i
     params = [p for p in parameters if p.grad is not None]
     if not params:
         return torch.tensor(0.0)
+    return _grad_norm(params, float(max_norm), apply_clip=True)[0]
+
+
+def _grad_norm(params, max_norm, apply_clip):
+    """[total L2 norm, clip coefficient min(max_norm / (norm + 1e-6), 1)] as a device tensor; with apply_clip the
+    gradients are scaled in place (clip_grad_norm_)."""
     dev = params[0].grad.device
     rows = [(p.data_ptr(), p.grad.data_ptr(), 0, 0, 0, 0, p.grad.numel(), 0.0, 1.0) for p in params]
     tab = _NORM_TABLES.setdefault(str(dev), _Table())
     t, c, n = tab.get(rows, dev)
     part = torch.empty(max(n, 1), dtype=torch.float32, device=dev)
     out = torch.empty(2, dtype=torch.float32, device=dev)
-    L.call('cmhar_mt_grad_norm', t.data_ptr(), c.data_ptr(), n, part.data_ptr(), out.data_ptr(), float(max_norm), 1,
-           L.stream(dev))
-    return out[0]
+    L.call('cmhar_mt_grad_norm', t.data_ptr(), c.data_ptr(), n, part.data_ptr(), out.data_ptr(), max_norm,
+           int(apply_clip), L.stream(dev))
+    return out
 
 
 class FusedAdamW(torch.optim.Optimizer):
@@ -70,13 +76,25 @@ class FusedAdamW(torch.optim.Optimizer):
 
     State layout matches torch (`state[p] = {'step', 'exp_avg', 'exp_avg_sq'}`), so optimizer state dicts
     interchange.  `shadow_sources`: modules whose `_packs` (cmhar.weights.PackedWeights) hold compute copies of
-    parameters; those copies are rewritten in the same pass."""
+    parameters; those copies are rewritten in the same pass.
 
-    def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-2, shadow_sources=()):
+    `max_grad_norm` (opt-in): `step()` first performs trainer.py:140's `clip_grad_norm_(params, max_grad_norm)` over
+    every parameter of the optimizer that has a gradient — the norm pass as in `clip_grad_norm_`, but the clip
+    coefficient is applied inside the AdamW pass instead of by a separate in-place scale pass over the gradients
+    (one read + one write of every gradient less).  The update is bit-identical to clip-then-step.  With
+    `write_clipped_grad=True` (default) the AdamW pass also stores the clipped gradient back, so `.grad` after the
+    step is exactly what `clip_grad_norm_` leaves; `False` leaves `.grad` unclipped (saves that write too).  The
+    total norm of the last step is `last_grad_norm` (0-dim device tensor, as `clip_grad_norm_` returns)."""
+
+    def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-2, shadow_sources=(),
+                 max_grad_norm=None, write_clipped_grad=True):
         defaults = dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay)
         super().__init__(params, defaults)
         self.shadow_sources = list(shadow_sources)
         self._tables = {}
+        self.max_grad_norm = max_grad_norm
+        self.write_clipped_grad = bool(write_clipped_grad)
+        self.last_grad_norm = None
 
     def _slots(self):
         slots = {}
@@ -95,6 +113,13 @@ class FusedAdamW(torch.optim.Optimizer):
             with torch.enable_grad():
                 loss = closure()
         slots, packs = self._slots()
+        gscale = None
+        if self.max_grad_norm is not None:
+            allp = [p for g in self.param_groups for p in g['params'] if p.grad is not None]
+            if allp:
+                norm_out = _grad_norm(allp, float(self.max_grad_norm), apply_clip=False)
+                self.last_grad_norm = norm_out[0]
+                gscale = norm_out
         for gi, group in enumerate(self.param_groups):
             b1, b2 = group['betas']
             lr, eps, wd = group['lr'], group['eps'], group['weight_decay']
@@ -129,8 +154,9 @@ class FusedAdamW(torch.optim.Optimizer):
             bc1 = 1.0 - b1 ** step
             bc2 = 1.0 - b2 ** step
             t, c, n = self._tables.setdefault(gi, _Table()).get(rows, dev)
-            L.call('cmhar_mt_adamw', t.data_ptr(), c.data_ptr(), n, float(lr), float(1.0 - b1), float(b2),
-                   float(1.0 - b2), float(eps), float(lr / bc1), float(math.sqrt(bc2)), None, L.stream(dev))
+            L.call('cmhar_mt_adamw_clip', t.data_ptr(), c.data_ptr(), n, float(lr), float(1.0 - b1), float(b2),
+                   float(1.0 - b2), float(eps), float(lr / bc1), float(math.sqrt(bc2)),
+                   None if gscale is None else gscale.data_ptr(), int(self.write_clipped_grad), L.stream(dev))
         for pk in packs:
             pk.mark_fresh()
         return loss

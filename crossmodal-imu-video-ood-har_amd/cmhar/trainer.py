@@ -7,8 +7,9 @@ Same constructors, attributes (`model`, `config`, `device`, `optimizer`, `schedu
 switch by changing the import.  What differs is only what the MI355X wants:
 
 * the optimizer is `cmhar.optim.FusedAdamW` (one multi-tensor launch; torch.optim.AdamW arithmetic and state
-  layout, so `optimizer_state_dict` interchanges) and clipping is `cmhar.optim.clip_grad_norm_` (device-side
-  coefficient); the LR schedule is the reference's own torch LinearLR → CosineAnnealingLR (SequentialLR);
+  layout, so `optimizer_state_dict` interchanges) with the reference's `clip_grad_norm_(..., 1.0)` folded into its
+  pass (`max_grad_norm=1.0`: device-side norm and coefficient, bit-identical update and clipped `.grad`); the LR
+  schedule is the reference's own torch LinearLR → CosineAnnealingLR (SequentialLR);
 * the per-step `loss.item()` host syncs of the reference loop (`trainer.py:143-144,307-310`) are replaced by
   device-side accumulation; the epoch means are read once per epoch (same values);
 * data parallel: pass a `cmhar.dist.GradReducer` (one process per GPU, RCCL all-reduce SUM of gradients
@@ -32,7 +33,7 @@ from torch.optim.lr_scheduler import CosineAnnealingLR, LinearLR, SequentialLR
 from . import dist as D
 from . import kernels as K
 from .losses import CrossEntropyLoss
-from .optim import FusedAdamW, clip_grad_norm_
+from .optim import FusedAdamW
 
 __all__ = ['BaseTrainer', 'CrossModalTrainer', 'ClassificationTrainer']
 
@@ -108,9 +109,11 @@ class CrossModalTrainer(BaseTrainer):
         self.best_val_loss = float('inf')
         self.grad_reducer = grad_reducer
         self.show_progress = show_progress
+        # max_grad_norm: trainer.py:140's clip_grad_norm_(model.parameters(), 1.0) folded into the AdamW pass
+        # (bit-identical update and post-clip .grad; one scale pass over the gradients less)
         self.optimizer = FusedAdamW(self.model.parameters(), lr=config.training.pretrain_lr,
                                     weight_decay=config.training.pretrain_weight_decay,
-                                    shadow_sources=_shadow_sources(self.model))
+                                    shadow_sources=_shadow_sources(self.model), max_grad_norm=1.0)
         num_epochs = int(config.training.pretrain_epochs)
         warmup_epochs = int(getattr(config.training, 'pretrain_warmup_epochs', 0))
         if warmup_epochs <= 0:
@@ -146,8 +149,7 @@ class CrossModalTrainer(BaseTrainer):
         loss.backward()
         if self.grad_reducer is not None:
             self.grad_reducer.finish()
-        clip_grad_norm_(self.model.parameters(), 1.0)
-        self.optimizer.step()
+        self.optimizer.step()          # clip_grad_norm_(model.parameters(), 1.0) + AdamW.step (trainer.py:140-141)
         return loss
 
     def train_epoch(self, dataloader) -> float:
@@ -226,7 +228,7 @@ class ClassificationTrainer(BaseTrainer):
             for p in model.imu_encoder.parameters():
                 p.requires_grad = False
             self.optimizer = FusedAdamW(model.classifier.parameters(), lr=config.training.train_lr_head,
-                                        weight_decay=config.training.pretrain_weight_decay)
+                                        weight_decay=config.training.pretrain_weight_decay, max_grad_norm=1.0)
         else:
             if hasattr(model, 'unfreeze_encoder'):
                 model.unfreeze_encoder()
@@ -236,7 +238,7 @@ class ClassificationTrainer(BaseTrainer):
             self.optimizer = FusedAdamW(
                 [{'params': model.imu_encoder.parameters(), 'lr': config.training.train_lr_encoder},
                  {'params': model.classifier.parameters(), 'lr': config.training.train_lr_head}],
-                weight_decay=config.training.pretrain_weight_decay)
+                weight_decay=config.training.pretrain_weight_decay, max_grad_norm=1.0)
         self.scheduler = CosineAnnealingLR(self.optimizer, T_max=max(int(config.training.train_epochs), 1),
                                            eta_min=1e-7)
 
@@ -283,8 +285,7 @@ class ClassificationTrainer(BaseTrainer):
         loss.backward()
         if self.grad_reducer is not None:
             self.grad_reducer.finish()
-        clip_grad_norm_(self.model.parameters(), 1.0)
-        self.optimizer.step()
+        self.optimizer.step()          # clip_grad_norm_(model.parameters(), 1.0) + AdamW.step (trainer.py:303-304)
         return logits, loss
 
     def train_epoch(self, dataloader) -> Dict[str, float]:

@@ -188,28 +188,70 @@ __global__ __launch_bounds__(256) void mt_scale_kernel(const MTTensor* __restric
 
 // torch.optim.AdamW math order (lerp for exp_avg, mul+addcmul for exp_avg_sq, denom = sqrt(v)/sqrt(bc2) + eps,
 // p *= 1 - lr*wd, p += -step_size * m/denom).  All step scalars are computed by the host in double precision, as
-// torch does in Python floats.  Optional grad scale from device memory (clip coefficient, out[1]); bf16 shadow.
+// torch does in Python floats.  Optional grad scale from device memory (clip coefficient, out[1]); with write_g the
+// scaled gradient is stored back (the clipped .grad of clip_grad_norm_, produced in the same pass); bf16 shadow.
+// Four elements per thread-iteration when every stream of the tensor is 16-B aligned (8-B for the bf16 shadow) —
+// the same per-element arithmetic as the scalar loop.
+__device__ __forceinline__ void adamw_elem(float g, float& p, float& m, float& v, float decay, float omb1,
+                                           float beta2, float omb2, float eps, float ss, float bc2_sqrt) {
+  p = p * decay;
+  m = m + omb1 * (g - m);
+  v = beta2 * v + omb2 * (g * g);
+  const float denom = sqrtf(v) / bc2_sqrt + eps;
+  p = p + (-ss) * (m / denom);
+}
+
 __global__ __launch_bounds__(256) void mt_adamw_kernel(const MTTensor* __restrict__ tens,
                                                        const MTChunk* __restrict__ chunks, float lr, float omb1,
                                                        float beta2, float omb2, float eps, float step_size,
-                                                       float bc2_sqrt, const float* __restrict__ gscale) {
+                                                       float bc2_sqrt, const float* __restrict__ gscale, int write_g) {
   const MTChunk ch = chunks[blockIdx.x];
   const MTTensor T = tens[ch.t];
   if (!T.g) return;
   const float gs = gscale ? gscale[1] : 1.f;
+  const bool wg = write_g && gscale;
   const float ss = step_size * T.lr_scale;
   const float decay = 1.f - lr * T.lr_scale * T.wd;
-  for (long i = ch.start + threadIdx.x; i < ch.start + ch.len; i += 256) {
+  float* G = const_cast<float*>(T.g);
+  const unsigned long al = (unsigned long)T.p | (unsigned long)T.g | (unsigned long)T.m | (unsigned long)T.v |
+                           (unsigned long)T.pcopy;
+  const bool vec = (al & 15) == 0 && ((unsigned long)T.pbf & 7) == 0 && (ch.start & 3) == 0;
+  long i0 = ch.start;
+  const long end = ch.start + ch.len;
+  if (vec) {
+    const long nv = (ch.len >> 2) << 2;
+    for (long i = ch.start + threadIdx.x * 4; i < ch.start + nv; i += 1024) {
+      floatx4 g4 = *(const floatx4*)(T.g + i), p4 = *(const floatx4*)(T.p + i);
+      floatx4 m4 = *(const floatx4*)(T.m + i), v4 = *(const floatx4*)(T.v + i);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        g4[j] *= gs;
+        float pj = p4[j], mj = m4[j], vj = v4[j];
+        adamw_elem(g4[j], pj, mj, vj, decay, omb1, beta2, omb2, eps, ss, bc2_sqrt);
+        p4[j] = pj; m4[j] = mj; v4[j] = vj;
+      }
+      *(floatx4*)(T.p + i) = p4;
+      *(floatx4*)(T.m + i) = m4;
+      *(floatx4*)(T.v + i) = v4;
+      if (wg) *(floatx4*)(G + i) = g4;
+      if (T.pbf) {
+        bf16 __attribute__((ext_vector_type(4))) b4;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) b4[j] = (bf16)p4[j];
+        *(decltype(b4)*)(T.pbf + i) = b4;
+      }
+      if (T.pcopy) *(floatx4*)(T.pcopy + i) = p4;
+    }
+    i0 = ch.start + nv;
+  }
+  for (long i = i0 + threadIdx.x; i < end; i += 256) {
     const float g = T.g[i] * gs;
-    float p = T.p[i] * decay;
-    float m = T.m[i];
-    m = m + omb1 * (g - m);
-    const float v = beta2 * T.v[i] + omb2 * (g * g);
-    const float denom = sqrtf(v) / bc2_sqrt + eps;
-    p = p + (-ss) * (m / denom);
+    float p = T.p[i], m = T.m[i], v = T.v[i];
+    adamw_elem(g, p, m, v, decay, omb1, beta2, omb2, eps, ss, bc2_sqrt);
     T.p[i] = p;
     T.m[i] = m;
     T.v[i] = v;
+    if (wg) G[i] = g;
     if (T.pbf) T.pbf[i] = (bf16)p;
     if (T.pcopy) T.pcopy[i] = p;
   }
@@ -303,9 +345,15 @@ extern "C" int cmhar_mt_grad_norm(const void* tens, const void* chunks, int nchu
 extern "C" int cmhar_mt_adamw(const void* tens, const void* chunks, int nchunks, float lr, float omb1, float beta2,
                               float omb2, float eps, float step_size, float bc2_sqrt, const float* gscale,
                               hipStream_t st) {
+  return cmhar_mt_adamw_clip(tens, chunks, nchunks, lr, omb1, beta2, omb2, eps, step_size, bc2_sqrt, gscale, 0, st);
+}
+
+extern "C" int cmhar_mt_adamw_clip(const void* tens, const void* chunks, int nchunks, float lr, float omb1,
+                                   float beta2, float omb2, float eps, float step_size, float bc2_sqrt,
+                                   const float* gscale, int write_grad, hipStream_t st) {
   if (nchunks <= 0) return 0;
   mt_adamw_kernel<<<nchunks, 256, 0, st>>>((const MTTensor*)tens, (const MTChunk*)chunks, lr, omb1, beta2, omb2, eps,
-                                           step_size, bc2_sqrt, gscale);
+                                           step_size, bc2_sqrt, gscale, write_grad);
   CMHAR_CHECK_LAUNCH();
   return 0;
 }

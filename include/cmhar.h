@@ -261,6 +261,13 @@ int cmhar_mt_grad_norm(const void* tens, const void* chunks, int nchunks, float*
 int cmhar_mt_adamw(const void* tens, const void* chunks, int nchunks, float lr, float one_minus_beta1, float beta2,
                    float one_minus_beta2, float eps, float step_size, float bias_correction2_sqrt,
                    const float* gscale, hipStream_t stream);
+/* cmhar_mt_adamw with the gradient clipping folded in (FusedAdamW(max_grad_norm=...)): the gradient is scaled by the
+   device-side clip coefficient gscale[1] written by cmhar_mt_grad_norm(apply_clip = 0), replacing the separate
+   in-place scale pass of trainer.py:140 clip_grad_norm_; write_grad != 0 also stores the clipped gradient back into
+   .grad in the same pass (torch's post-clip .grad).  Same update, bit for bit, as clip-then-step. */
+int cmhar_mt_adamw_clip(const void* tens, const void* chunks, int nchunks, float lr, float one_minus_beta1,
+                        float beta2, float one_minus_beta2, float eps, float step_size, float bias_correction2_sqrt,
+                        const float* gscale, int write_grad, hipStream_t stream);
 /* refresh the compute shadows (p_bf16 / p_copy) from p, e.g. after a foreign optimizer updated p. */
 int cmhar_mt_cast_bf16(const void* tens, const void* chunks, int nchunks, hipStream_t stream);
 

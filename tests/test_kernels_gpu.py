@@ -478,6 +478,40 @@ def test_clip_and_fused_adamw_match_torch():
         assert rel(opt_a.state[a]['exp_avg_sq'], opt_b.state[b]['exp_avg_sq']) < 1e-6
 
 
+@pytest.mark.parametrize('write_grad', [True, False])
+def test_fused_adamw_folded_clip_bit_identical(write_grad):
+    """FusedAdamW(max_grad_norm=1.0) (the clip coefficient applied inside the AdamW pass) against clip_grad_norm_ +
+    FusedAdamW.step: bit-identical parameters, moments and bf16 shadows; `.grad` afterwards is the clipped gradient
+    (write_clipped_grad=True) or left unclipped (False).  Covers the vectorised body, ragged tails and parameters
+    whose storage is not 16-B aligned (views at odd offsets: the scalar path)."""
+    from cmhar.optim import FusedAdamW, clip_grad_norm_
+    torch.manual_seed(11)
+    flat = torch.randn(4096 + 3, device=DEV)
+    base = [torch.randn(s, device=DEV) for s in [(300, 77), (1000,), (3, 5, 7), (65536 + 17,)]] + \
+        [flat[1:1 + 999].view(999), flat[1003:1003 + 2048].view(32, 64)]
+    ours = [torch.nn.Parameter(p.clone()) for p in base[:4]] + [torch.nn.Parameter(p) for p in base[4:]]
+    flat2 = flat.clone()
+    theirs = [torch.nn.Parameter(p.clone()) for p in base[:4]] + \
+        [torch.nn.Parameter(flat2[1:1 + 999].view(999)), torch.nn.Parameter(flat2[1003:1003 + 2048].view(32, 64))]
+    assert ours[4].data_ptr() % 16 != 0
+    opt_a = FusedAdamW(ours, lr=1e-3, weight_decay=0.01, max_grad_norm=1.0, write_clipped_grad=write_grad)
+    opt_b = FusedAdamW(theirs, lr=1e-3, weight_decay=0.01)
+    for step in range(3):
+        grads = [torch.randn_like(a) * (10 if step != 1 else 0.01) for a in ours]
+        for a, b, g in zip(ours, theirs, grads):
+            a.grad, b.grad = g.clone(), g.clone()
+        opt_a.step()
+        nb = clip_grad_norm_(theirs, 1.0)
+        opt_b.step()
+        assert opt_a.last_grad_norm.item() == nb.item()
+        for a, b, g in zip(ours, theirs, grads):
+            assert torch.equal(a.grad, b.grad if write_grad else g)
+    for a, b in zip(ours, theirs):
+        assert torch.equal(a, b)
+        assert torch.equal(opt_a.state[a]['exp_avg'], opt_b.state[b]['exp_avg'])
+        assert torch.equal(opt_a.state[a]['exp_avg_sq'], opt_b.state[b]['exp_avg_sq'])
+
+
 @pytest.mark.parametrize('D', [16, 32])
 def test_attention_bf16_storage_small_head(D):
     """bf16 tensors with a head dim the flash kernel does not cover run the exact-math path on bf16 storage."""
