@@ -650,6 +650,380 @@ __global__ __launch_bounds__(256, QB == 1 ? CMHAR_DQ_OCC : 2) void attn_bwd_dq_b
 #undef Vs
 
 // ---------------------------------------------------------------------------------------------------------------
+// Ragged tails.  At 16×224² L = 1568 = 12·128 + 32: each head leaves ≤ 32 queries (forward, dQ) or keys (dK/dV)
+// beyond the last full block.  As a block of the kernels above, such a tail runs ONE active wave over the whole other
+// sequence (1/4 of its workgroup's slots).  The tail kernels below give the tail a workgroup of its own per
+// (batch, head) whose 4 waves take the SAME ≤ 32 rows and split the OTHER sequence: per step the workgroup stages
+// 128 rows of it (two [64][64] att_off images per operand, LDS-DMA, double-buffered), each wave works on its own
+// 32, and the 4 partial results are merged through LDS at the end — (m, l, O) flash-decoding merge for the forward,
+// plain sums for dQ and dK/dV.  Deterministic (fixed merge order); the same per-element arithmetic as the kernels
+// above except the order in which the four key (query) quarters are summed.
+// ---------------------------------------------------------------------------------------------------------------
+__device__ __forceinline__ void stage128(const TileDma& t, int r0, char* lds, int wave) {
+  t.tile(r0, lds, wave);
+  t.tile(r0 + 64, lds + 8192, wave);
+}
+
+template <typename E>
+__global__ __launch_bounds__(256, 2) void attn_fwd_tail_bf16(int H, int Lq, int Lk, int q_base,
+                                                             const bf16* __restrict__ Q, long ldq,
+                                                             const bf16* __restrict__ K, long ldk,
+                                                             const bf16* __restrict__ V, long ldv, E* __restrict__ O,
+                                                             long ldo, float* __restrict__ lse, float scale) {
+  __shared__ __attribute__((aligned(16))) char smem[65536];   // [2 buf][K 128 rows 16 KB | V 16 KB]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5;
+  const int hd = blockIdx.y, b = blockIdx.z;
+  const bf16* Kb = K + (long)b * Lk * ldk + hd * 64;
+  const bf16* Vb = V + (long)b * Lk * ldv + hd * 64;
+  const float c = scale * LOG2E;
+  const int myq = min(q_base + (lane & 31), Lq - 1);
+  bf16x8 qf[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) qf[t] = *(const bf16x8*)(Q + ((long)b * Lq + myq) * ldq + hd * 64 + 16 * t + 8 * h);
+  floatx16 o[2];
+#pragma unroll
+  for (int d = 0; d < 2; ++d)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) o[d][r] = 0.f;
+  float m = -INFINITY, l = 0.f;
+  const int nt = (Lk + 127) / 128;
+  TileDma tk, tv;
+  tk.init(Kb, ldk, Lk, wave, lane);
+  tv.init(Vb, ldv, Lk, wave, lane);
+  stage128(tk, 0, smem, wave);
+  stage128(tv, 0, smem + 16384, wave);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  const int sub = (wave >> 1) * 8192, r0 = 32 * (wave & 1);   // this wave's 32 keys of the 128-key stage
+  for (int st = 0; st < nt; ++st) {
+    char* Ks_ = smem + (st & 1) * 32768;
+    char* Vs_ = Ks_ + 16384;
+    const bool more = st + 1 < nt;
+    if (more) {
+      stage128(tk, (st + 1) * 128, smem + ((st + 1) & 1) * 32768, wave);
+      stage128(tv, (st + 1) * 128, smem + ((st + 1) & 1) * 32768 + 16384, wave);
+    }
+    const int kbase = st * 128 + 32 * wave;
+    if (kbase < Lk) {      // a wave with no valid key in this step skips it (its m, l, O stay untouched)
+      floatx16 s;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) s[r] = 0.f;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) s = mma32<E>(row_frag(Ks_ + sub, r0, t, lane), qf[t], s);
+      if (kbase + 32 > Lk) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          if (kbase + acc_row(r, h) >= Lk) s[r] = -INFINITY;
+      }
+      float mt = -INFINITY;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) mt = fmaxf(mt, s[r]);
+      mt = fmaxf(mt, xhalf(mt)) * c;
+      if (__builtin_amdgcn_ballot_w64(mt > m + 8.f) != 0) {      // lazy rescale, as attn_fwd_bf16
+        const float mn = fmaxf(m, mt);
+        const float alpha = fexp2(m - mn);
+        m = mn;
+        l *= alpha;
+#pragma unroll
+        for (int d = 0; d < 2; ++d)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) o[d][r] *= alpha;
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float p = fexp2(fmaf(s[r], c, -m));
+        s[r] = p;
+        l += p;
+      }
+      bf16x8 pb[2];
+#pragma unroll
+      for (int ss = 0; ss < 2; ++ss) pb[ss] = pack8<E>(s, ss);
+#pragma unroll
+      for (int ss = 0; ss < 2; ++ss)
+#pragma unroll
+        for (int d = 0; d < 2; ++d) o[d] = mma32<E>(tr_frag(Vs_ + sub, r0, ss, d * 32, lane), pb[ss], o[d]);
+    }
+    if (more) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  // merge the four key quarters: m* = max m_w, L = Σ 2^(m_w − m*) l_w, O = Σ 2^(m_w − m*) O_w / L
+  float* Mw = (float*)smem;            // [4][32]
+  float* Lw = Mw + 128;                // [4][32]
+  float* Ow = Lw + 128;                // [4][32][64]
+  const float lt = l + xhalf(l);
+  const int ql = lane & 31;
+  if (h == 0) { Mw[wave * 32 + ql] = m; Lw[wave * 32 + ql] = lt; }
+#pragma unroll
+  for (int d = 0; d < 2; ++d)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) Ow[(wave * 32 + ql) * 64 + d * 32 + acc_row(r, h)] = o[d][r];
+  __syncthreads();
+  const int qi = tid >> 3, d0 = (tid & 7) * 8;
+  float mw[4], mx = -INFINITY;
+#pragma unroll
+  for (int w = 0; w < 4; ++w) { mw[w] = Mw[w * 32 + qi]; mx = fmaxf(mx, mw[w]); }
+  float wsum = 0.f, acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int w = 0; w < 4; ++w) {
+    const float f = fexp2(mw[w] - mx);       // a quarter that saw no key: m_w = −inf → weight 0
+    wsum += f * Lw[w * 32 + qi];
+    const float* src = Ow + (w * 32 + qi) * 64 + d0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] += f * src[j];
+  }
+  const int q = q_base + qi;
+  if (q < Lq) {
+    const float inv = 1.f / wsum;
+    typedef E __attribute__((ext_vector_type(8))) e8;
+    e8 v;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = (E)(acc[j] * inv);
+    *(e8*)(O + ((long)b * Lq + q) * ldo + hd * 64 + d0) = v;
+    if ((tid & 7) == 0) lse[((long)b * H + hd) * Lq + q] = mx + log2f(wsum);
+  }
+}
+
+template <bool PS>
+__global__ __launch_bounds__(256, 2) void attn_bwd_dq_tail_bf16(int H, int Lq, int Lk, int q_base,
+                                                                const bf16* __restrict__ Q, long ldq,
+                                                                const bf16* __restrict__ K, long ldk,
+                                                                const bf16* __restrict__ V, long ldv,
+                                                                const bf16* __restrict__ O, long ldo,
+                                                                const bf16* __restrict__ dO, long lddo,
+                                                                const float* __restrict__ lse,
+                                                                float* __restrict__ delta, bf16* __restrict__ dQ,
+                                                                long lddq, float scale) {
+  __shared__ __attribute__((aligned(16))) char smem[65536];   // [2 buf][K 16 KB | V 16 KB]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5;
+  const int hd = blockIdx.y, b = blockIdx.z;
+  const bf16* Kb = K + (long)b * Lk * ldk + hd * 64;
+  const bf16* Vb = V + (long)b * Lk * ldv + hd * 64;
+  const float c = scale * LOG2E;
+  const int myq = min(q_base + (lane & 31), Lq - 1);
+  bf16x8 qf[4], gf[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    qf[t] = *(const bf16x8*)(Q + ((long)b * Lq + myq) * ldq + hd * 64 + 16 * t + 8 * h);
+    gf[t] = *(const bf16x8*)(dO + ((long)b * Lq + myq) * lddo + hd * 64 + 16 * t + 8 * h);
+  }
+  const float sL = -lse[((long)b * H + hd) * Lq + myq] / c;
+  float Dl = 0.f;
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const bf16x8 ov = *(const bf16x8*)(O + ((long)b * Lq + myq) * ldo + hd * 64 + 16 * t + 8 * h);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) Dl = fmaf((float)gf[t][e], (float)ov[e], Dl);
+  }
+  Dl += xhalf(Dl);
+  if (wave == 0 && h == 0 && q_base + (lane & 31) < Lq) delta[((long)b * H + hd) * Lq + myq] = Dl;
+  floatx16 dq[2];
+#pragma unroll
+  for (int d = 0; d < 2; ++d)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) dq[d][r] = 0.f;
+  const int nt = (Lk + 127) / 128;
+  TileDma tk, tv;
+  tk.init(Kb, ldk, Lk, wave, lane);
+  tv.init(Vb, ldv, Lk, wave, lane);
+  stage128(tk, 0, smem, wave);
+  stage128(tv, 0, smem + 16384, wave);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  const int sub = (wave >> 1) * 8192, r0 = 32 * (wave & 1);
+  for (int st = 0; st < nt; ++st) {
+    char* Ks_ = smem + (st & 1) * 32768;
+    char* Vs_ = Ks_ + 16384;
+    const bool more = st + 1 < nt;
+    if (more) {
+      stage128(tk, (st + 1) * 128, smem + ((st + 1) & 1) * 32768, wave);
+      stage128(tv, (st + 1) * 128, smem + ((st + 1) & 1) * 32768 + 16384, wave);
+    }
+    const int kbase = st * 128 + 32 * wave;
+    if (kbase < Lk) {
+      floatx16 s, dp;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) { s[r] = sL; dp[r] = -Dl; }
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag(Ks_ + sub, r0, t, lane), qf[t], s, 0, 0, 0);
+        dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag(Vs_ + sub, r0, t, lane), gf[t], dp, 0, 0, 0);
+      }
+      if (kbase + 32 > Lk) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          if (kbase + acc_row(r, h) >= Lk) s[r] = -INFINITY;
+      }
+      bf16x8 db[2];
+#pragma unroll
+      for (int r = 0; r < 16; r += 2) {
+        const float2_t pv = PS ? float2_t{fexp2(s[r]), fexp2(s[r + 1])} : float2_t{fexp2(s[r] * c), fexp2(s[r + 1] * c)};
+        const bf16x2_t dd = __builtin_convertvector(pv * float2_t{dp[r], dp[r + 1]}, bf16x2_t);
+        db[r >> 3][r & 7] = dd[0];
+        db[r >> 3][(r & 7) + 1] = dd[1];
+      }
+#pragma unroll
+      for (int ss = 0; ss < 2; ++ss)
+#pragma unroll
+        for (int d = 0; d < 2; ++d)
+          dq[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_frag(Ks_ + sub, r0, ss, d * 32, lane), db[ss], dq[d], 0, 0,
+                                                          0);
+    }
+    if (more) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  float* Dw = (float*)smem;            // [4][32][64]
+  const int ql = lane & 31;
+#pragma unroll
+  for (int d = 0; d < 2; ++d)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) Dw[(wave * 32 + ql) * 64 + d * 32 + acc_row(r, h)] = dq[d][r];
+  __syncthreads();
+  const int qi = tid >> 3, d0 = (tid & 7) * 8;
+  const int q = q_base + qi;
+  if (q < Lq) {
+    bf16x8 v;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float a = 0.f;
+#pragma unroll
+      for (int w = 0; w < 4; ++w) a += Dw[(w * 32 + qi) * 64 + d0 + j];
+      v[j] = (bf16)(a * scale);
+    }
+    *(bf16x8*)(dQ + ((long)b * Lq + q) * lddq + hd * 64 + d0) = v;
+  }
+}
+
+template <bool PS>
+__global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_tail_bf16(int H, int Lq, int Lk, int k_base,
+                                                                  const bf16* __restrict__ Q, long ldq,
+                                                                  const bf16* __restrict__ K, long ldk,
+                                                                  const bf16* __restrict__ V, long ldv,
+                                                                  const bf16* __restrict__ dO, long lddo,
+                                                                  const float* __restrict__ lse,
+                                                                  const float* __restrict__ delta,
+                                                                  bf16* __restrict__ dK, long lddk,
+                                                                  bf16* __restrict__ dV, long lddv, float scale,
+                                                                  float kscale) {
+  __shared__ __attribute__((aligned(16))) char smem[65536 + 2 * 2 * 128 * 4];   // [2][Q 16 KB | dO 16 KB] + consts
+  float* Ls = (float*)(smem + 65536);          // [2][128] −lse/c
+  float* Ds = Ls + 256;                        // [2][128] −δ
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5;
+  const int hd = blockIdx.y, b = blockIdx.z;
+  const bf16* Qb = Q + (long)b * Lq * ldq + hd * 64;
+  const bf16* Gb = dO + (long)b * Lq * lddo + hd * 64;
+  const float* lseb = lse + ((long)b * H + hd) * Lq;
+  const float* delb = delta + ((long)b * H + hd) * Lq;
+  const float c = scale * LOG2E;
+  const float inv_c = 1.f / c;
+  const int myk = min(k_base + (lane & 31), Lk - 1);
+  bf16x8 kf[4], vf[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    kf[t] = *(const bf16x8*)(K + ((long)b * Lk + myk) * ldk + hd * 64 + 16 * t + 8 * h);
+    vf[t] = *(const bf16x8*)(V + ((long)b * Lk + myk) * ldv + hd * 64 + 16 * t + 8 * h);
+  }
+  floatx16 dk[2], dv[2];
+#pragma unroll
+  for (int d = 0; d < 2; ++d)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) { dk[d][r] = 0.f; dv[d][r] = 0.f; }
+  const int nt = (Lq + 127) / 128;
+  TileDma tq, tg;
+  tq.init(Qb, ldq, Lq, wave, lane);
+  tg.init(Gb, lddo, Lq, wave, lane);
+  float lv = 0.f, dv_ = 0.f;
+  auto load = [&](int st) {
+    char* buf = smem + (st & 1) * 32768;
+    stage128(tq, st * 128, buf, wave);
+    stage128(tg, st * 128, buf + 16384, wave);
+    if (tid < 128) {
+      const int q = st * 128 + tid;
+      lv = q < Lq ? -lseb[q] * inv_c : -INFINITY;
+      dv_ = q < Lq ? -delb[q] : 0.f;
+    }
+  };
+  auto store_consts = [&](int st) {
+    if (tid < 128) { Ls[(st & 1) * 128 + tid] = lv; Ds[(st & 1) * 128 + tid] = dv_; }
+  };
+  load(0);
+  store_consts(0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  const int sub = (wave >> 1) * 8192, r0 = 32 * (wave & 1);   // this wave's 32 queries of the 128-query stage
+  for (int st = 0; st < nt; ++st) {
+    const char* Qs_ = smem + (st & 1) * 32768;
+    const char* Gs_ = Qs_ + 16384;
+    const float* L_ = Ls + (st & 1) * 128 + 32 * wave;
+    const float* D_ = Ds + (st & 1) * 128 + 32 * wave;
+    const bool more = st + 1 < nt;
+    if (more) load(st + 1);
+    if (st * 128 + 32 * wave < Lq) {
+      floatx16 s, dp;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) { s[r] = L_[acc_row(r, h)]; dp[r] = D_[acc_row(r, h)]; }
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag(Qs_ + sub, r0, t, lane), kf[t], s, 0, 0, 0);
+        dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag(Gs_ + sub, r0, t, lane), vf[t], dp, 0, 0, 0);
+      }
+      bf16x8 pbv[2], dbv[2];
+#pragma unroll
+      for (int r = 0; r < 16; r += 2) {
+        const float2_t pv = PS ? float2_t{fexp2(s[r]), fexp2(s[r + 1])} : float2_t{fexp2(s[r] * c), fexp2(s[r + 1] * c)};
+        const float2_t dv2 = pv * float2_t{dp[r], dp[r + 1]};
+        const bf16x2_t pp = __builtin_convertvector(pv, bf16x2_t);
+        const bf16x2_t dd = __builtin_convertvector(dv2, bf16x2_t);
+        pbv[r >> 3][r & 7] = pp[0];
+        pbv[r >> 3][(r & 7) + 1] = pp[1];
+        dbv[r >> 3][r & 7] = dd[0];
+        dbv[r >> 3][(r & 7) + 1] = dd[1];
+      }
+#pragma unroll
+      for (int ss = 0; ss < 2; ++ss)
+#pragma unroll
+        for (int d = 0; d < 2; ++d) {
+          dv[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_frag(Gs_ + sub, r0, ss, d * 32, lane), pbv[ss], dv[d], 0, 0, 0);
+          dk[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_frag(Qs_ + sub, r0, ss, d * 32, lane), dbv[ss], dk[d], 0, 0, 0);
+        }
+    }
+    if (more) {
+      store_consts(st + 1);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+  }
+  float* Kw = (float*)smem;            // [4][32][64] dK partials
+  float* Vw = Kw + 4 * 32 * 64;        // [4][32][64] dV partials
+  const int kl = lane & 31;
+#pragma unroll
+  for (int d = 0; d < 2; ++d)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      Kw[(wave * 32 + kl) * 64 + d * 32 + acc_row(r, h)] = dk[d][r];
+      Vw[(wave * 32 + kl) * 64 + d * 32 + acc_row(r, h)] = dv[d][r];
+    }
+  __syncthreads();
+  const int ki = tid >> 3, d0 = (tid & 7) * 8;
+  const int key = k_base + ki;
+  if (key < Lk) {
+    bf16x8 a, v;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float sk = 0.f, sv = 0.f;
+#pragma unroll
+      for (int w = 0; w < 4; ++w) {
+        sk += Kw[(w * 32 + ki) * 64 + d0 + j];
+        sv += Vw[(w * 32 + ki) * 64 + d0 + j];
+      }
+      a[j] = (bf16)(sk * kscale);
+      v[j] = (bf16)sv;
+    }
+    *(bf16x8*)(dK + ((long)b * Lk + key) * lddk + hd * 64 + d0) = a;
+    *(bf16x8*)(dV + ((long)b * Lk + key) * lddv + hd * 64 + d0) = v;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------------------------
 // exact fp32 path (any head dim <= 64), with optional attention-prob dropout (nn.MultiheadAttention semantics)
 // ---------------------------------------------------------------------------------------------------------------
 template <typename T, int D>
@@ -783,6 +1157,10 @@ __global__ __launch_bounds__(64) void attn_bwd_dkdv_f32(int H, int Lq, int Lk, c
 #ifndef CMHAR_ATTN_DQ_QB
 #define CMHAR_ATTN_DQ_QB 1
 #endif
+// the ragged-tail kernels take tails of up to this many rows (0: off, the one-active-wave blocks run them; A/B knob)
+#ifndef CMHAR_ATTN_TAIL
+#define CMHAR_ATTN_TAIL 32
+#endif
 
 // f32-MFMA flash kernels (csrc/attention_f32.hip) for fp32 storage, D = 64, no dropout
 void cmhar_attn_f32m_fwd(int B, int H, int Lq, int Lk, const float* Q, long ldq, const float* K, long ldk,
@@ -818,7 +1196,10 @@ extern "C" int cmhar_attention_fwd(int dtype, int B, int H, int Lq, int Lk, int 
     if (bulk > 0)                                                                                                \
       attn_fwd_bf16<E, 2><<<dim3(bulk / 256, H, B), 256, 0, st>>>(H, Lq, Lk, 0, (const bf16*)Q, ldq, (const bf16*)K, \
                                                                   ldk, (const bf16*)V, ldv, (E*)O, ldo, lse, scale); \
-    if (Lq > bulk)                                                                                               \
+    if (Lq > bulk && Lq - bulk <= CMHAR_ATTN_TAIL)                                                             \
+      attn_fwd_tail_bf16<E><<<dim3(1, H, B), 256, 0, st>>>(H, Lq, Lk, bulk, (const bf16*)Q, ldq, (const bf16*)K, ldk, \
+                                                           (const bf16*)V, ldv, (E*)O, ldo, lse, scale);        \
+    else if (Lq > bulk)                                                                                          \
       attn_fwd_bf16<E, 1><<<dim3(cdiv(Lq - bulk, 128), H, B), 256, 0, st>>>(H, Lq, Lk, bulk, (const bf16*)Q, ldq,   \
                                                                             (const bf16*)K, ldk, (const bf16*)V, ldv, \
                                                                             (E*)O, ldo, lse, scale);             \
@@ -860,14 +1241,29 @@ static void flash_bwd_bf16(int B, int H, int Lq, int Lk, const void* Q, long ldq
                                                                     ldk, (const bf16*)V, ldv, (const bf16*)O, ldo,
                                                                     (const bf16*)dO, lddo, lse, delta, (bf16*)dQ,
                                                                     lddq, s_in);
-  if (Lq > bulk)
-    attn_bwd_dq_bf16<1, PS><<<dim3(cdiv(Lq - bulk, 128), H, B), 256, 0, st>>>(
+  // a tail of <= CMHAR_ATTN_TAIL queries / keys beyond the last full 128-row block goes to the tail kernels
+  const int qfull = bulk + ((Lq - bulk) / 128) * 128;
+  const bool qtail = Lq > qfull && Lq - qfull <= CMHAR_ATTN_TAIL;
+  const int qend = qtail ? qfull : Lq;
+  if (qend > bulk)
+    attn_bwd_dq_bf16<1, PS><<<dim3(cdiv(qend - bulk, 128), H, B), 256, 0, st>>>(
         H, Lq, Lk, bulk, (const bf16*)Q, ldq, (const bf16*)K, ldk, (const bf16*)V, ldv, (const bf16*)O, ldo,
         (const bf16*)dO, lddo, lse, delta, (bf16*)dQ, lddq, s_in);
-  attn_bwd_dkdv_bf16<PS><<<dim3(cdiv(Lk, 128), H, B), 256, 0, st>>>(H, Lq, Lk, (const bf16*)Q, ldq, (const bf16*)K,
-                                                                    ldk, (const bf16*)V, ldv, (const bf16*)dO, lddo,
-                                                                    lse, delta, (bf16*)dK, lddk, (bf16*)dV, lddv, s_in,
-                                                                    scale);
+  if (qtail)
+    attn_bwd_dq_tail_bf16<PS><<<dim3(1, H, B), 256, 0, st>>>(H, Lq, Lk, qfull, (const bf16*)Q, ldq, (const bf16*)K,
+                                                             ldk, (const bf16*)V, ldv, (const bf16*)O, ldo,
+                                                             (const bf16*)dO, lddo, lse, delta, (bf16*)dQ, lddq, s_in);
+  const int kfull = (Lk / 128) * 128;
+  const bool ktail = Lk > kfull && Lk - kfull <= CMHAR_ATTN_TAIL;
+  const int kblocks = ktail ? kfull / 128 : cdiv(Lk, 128);
+  if (kblocks > 0)
+    attn_bwd_dkdv_bf16<PS><<<dim3(kblocks, H, B), 256, 0, st>>>(H, Lq, Lk, (const bf16*)Q, ldq, (const bf16*)K, ldk,
+                                                                (const bf16*)V, ldv, (const bf16*)dO, lddo, lse, delta,
+                                                                (bf16*)dK, lddk, (bf16*)dV, lddv, s_in, scale);
+  if (ktail)
+    attn_bwd_dkdv_tail_bf16<PS><<<dim3(1, H, B), 256, 0, st>>>(H, Lq, Lk, kfull, (const bf16*)Q, ldq, (const bf16*)K,
+                                                               ldk, (const bf16*)V, ldv, (const bf16*)dO, lddo, lse,
+                                                               delta, (bf16*)dK, lddk, (bf16*)dV, lddv, s_in, scale);
 }
 
 extern "C" int cmhar_attention_bwd_prescaled(int B, int H, int Lq, int Lk, const void* Q, long ldq, const void* K,

@@ -225,7 +225,7 @@ __global__ __launch_bounds__(256) void mt_adamw_kernel(const MTTensor* __restric
       floatx4 m4 = *(const floatx4*)(T.m + i), v4 = *(const floatx4*)(T.v + i);
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        g4[j] *= gs;
+        g4[j] = __fmul_rn(g4[j], gs);     // rounded product (no FMA contraction): the value a scale pass would store
         float pj = p4[j], mj = m4[j], vj = v4[j];
         adamw_elem(g4[j], pj, mj, vj, decay, omb1, beta2, omb2, eps, ss, bc2_sqrt);
         p4[j] = pj; m4[j] = mj; v4[j] = vj;
@@ -245,7 +245,7 @@ __global__ __launch_bounds__(256) void mt_adamw_kernel(const MTTensor* __restric
     i0 = ch.start + nv;
   }
   for (long i = i0 + threadIdx.x; i < end; i += 256) {
-    const float g = T.g[i] * gs;
+    const float g = __fmul_rn(T.g[i], gs);
     float p = T.p[i], m = T.m[i], v = T.v[i];
     adamw_elem(g, p, m, v, decay, omb1, beta2, omb2, eps, ss, bc2_sqrt);
     T.p[i] = p;

@@ -273,6 +273,37 @@ def test_flash_attention_bf16_fwd_bwd(L_):
     assert rel(dqkv[:, 2 * H * D:], gv) < 2e-2
 
 
+@pytest.mark.parametrize('Lq,Lk', [(1568, 1568), (129, 257), (32, 200), (1, 64), (300, 33), (26, 3136), (13, 392)])
+def test_flash_attention_ragged_tails(Lq, Lk):
+    """The split-sequence tail kernels (csrc/attention.hip, tails of <= 32 queries / keys past the last full block):
+    forward O, dQ, dK, dV vs torch fp32 autograd, with the TAIL rows checked on their own (a tail bug would hide in a
+    whole-tensor norm), at cross-attention shapes (Lq != Lk) including a whole-tail-only sequence (Lq <= 32)."""
+    torch.manual_seed(13)
+    B, H, D = 2, 2, 64
+    scale = D ** -0.5
+    q = (torch.randn(B * Lq, H * D, device=DEV) * 1.5).bfloat16()
+    kv = (torch.randn(B * Lk, 2 * H * D, device=DEV) * 1.5).bfloat16()
+    k, v = kv[:, :H * D], kv[:, H * D:]
+    o = torch.empty(B * Lq, H * D, dtype=torch.bfloat16, device=DEV)
+    lse = torch.empty(B * H * Lq, device=DEV)
+    K().attention_fwd(q, k, v, o, lse, B=B, H=H, Lq=Lq, Lk=Lk, D=D, scale=scale)
+    qr, kr, vr = (t.float().clone().requires_grad_(True) for t in (q, k, v))
+    ref = _attn_ref(qr, kr, vr, B, H, Lq, Lk, D, scale)
+    do = torch.randn(B * Lq, H * D, device=DEV).bfloat16()
+    gq, gk, gv = torch.autograd.grad(ref, (qr, kr, vr), do.float())
+    dq = torch.empty_like(q)
+    dkv = torch.empty_like(kv)
+    K().attention_bwd(q, k, v, o, do, lse, dq, dkv[:, :H * D], dkv[:, H * D:], B=B, H=H, Lq=Lq, Lk=Lk, D=D,
+                      scale=scale)
+    qt = (Lq // 128) * 128 if Lq % 128 else max(Lq - 128, 0)      # first row of the query tail region
+    kt = (Lk // 128) * 128 if Lk % 128 else max(Lk - 128, 0)
+    rows_q = lambda t, r0: t.view(B, -1, t.shape[-1])[:, r0:]     # noqa: E731
+    for got, want, r0, tol in ((o, ref, qt, 1e-2), (dq, gq, qt, 2e-2), (dkv[:, :H * D], gk, kt, 2e-2),
+                               (dkv[:, H * D:], gv, kt, 2e-2)):
+        assert rel(got, want) < tol
+        assert rel(rows_q(got, r0), rows_q(want, r0)) < tol
+
+
 @pytest.mark.parametrize('L_', [200, 1568])
 def test_flash_attention_prescaled_keys(L_):
     """The VideoMAE bf16 training form: the QKV GEMM's epilogue writes K pre-scaled by scale·log2(e) (colscale), the
