@@ -192,6 +192,13 @@ __global__ __launch_bounds__(256) void mt_scale_kernel(const MTTensor* __restric
 // scaled gradient is stored back (the clipped .grad of clip_grad_norm_, produced in the same pass); bf16 shadow.
 // Four elements per thread-iteration when every stream of the tensor is 16-B aligned (8-B for the bf16 shadow) —
 // the same per-element arithmetic as the scalar loop.
+// g·scale rounded to fp32 as its own instruction: no FMA contraction into the moment updates (the folded clip must
+// see exactly the value a separate scale pass would have stored).  (__fmul_rn alone still contracted.)
+__device__ __forceinline__ float mul_nocontract(float a, float b) {
+#pragma clang fp contract(off)
+  return a * b;
+}
+
 __device__ __forceinline__ void adamw_elem(float g, float& p, float& m, float& v, float decay, float omb1,
                                            float beta2, float omb2, float eps, float ss, float bc2_sqrt) {
   p = p * decay;
@@ -225,7 +232,7 @@ __global__ __launch_bounds__(256) void mt_adamw_kernel(const MTTensor* __restric
       floatx4 m4 = *(const floatx4*)(T.m + i), v4 = *(const floatx4*)(T.v + i);
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        g4[j] = __fmul_rn(g4[j], gs);     // rounded product (no FMA contraction): the value a scale pass would store
+        g4[j] = mul_nocontract(g4[j], gs);     // rounded product (no FMA contraction): the value a scale pass would store
         float pj = p4[j], mj = m4[j], vj = v4[j];
         adamw_elem(g4[j], pj, mj, vj, decay, omb1, beta2, omb2, eps, ss, bc2_sqrt);
         p4[j] = pj; m4[j] = mj; v4[j] = vj;
@@ -245,7 +252,7 @@ __global__ __launch_bounds__(256) void mt_adamw_kernel(const MTTensor* __restric
     i0 = ch.start + nv;
   }
   for (long i = i0 + threadIdx.x; i < end; i += 256) {
-    const float g = __fmul_rn(T.g[i], gs);
+    const float g = mul_nocontract(T.g[i], gs);
     float p = T.p[i], m = T.m[i], v = T.v[i];
     adamw_elem(g, p, m, v, decay, omb1, beta2, omb2, eps, ss, bc2_sqrt);
     T.p[i] = p;

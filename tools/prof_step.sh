@@ -1,0 +1,10 @@
+#!/bin/bash
+# rocprofv3 kernel trace of a short bench run → per-kernel summary.  tools/prof_step.sh TAG [bench args...]
+export TMPDIR=/tmp
+TAG=$1; shift
+rm -rf gpurun_out/${TAG}_prof
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${TAG}_prof -o run -- \
+  python bench.py --steps 4 --warmup 2 --no-cpu-baseline "$@" > gpurun_out/${TAG}_prof.log 2>&1 || exit $?
+python tools/kstats.py gpurun_out/${TAG}_prof > gpurun_out/${TAG}_kernels.txt
+find gpurun_out/${TAG}_prof -name "*kernel_trace.csv" -delete
+tail -3 gpurun_out/${TAG}_kernels.txt
