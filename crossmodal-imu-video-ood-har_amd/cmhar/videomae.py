@@ -11,7 +11,10 @@ autograd node whose body is a sequence of HIP launches:
   → out-proj GEMM(+bias +residual) → LN → FC1 GEMM(+bias, GELU, pre-act saved) → FC2 GEMM(+bias +residual)]
 
 and the mirrored backward (dgrad GEMMs with fused GELU'/residual epilogues, split-K fp32 wgrad GEMMs that also
-emit the bias gradients, flash attention backward, fused LN backward with the residual gradient).  Compute dtype: bf16 (MFMA, fp32 accumulate),
+emit the bias gradients, flash attention backward, fused LN backward with the residual gradient).  When only
+`last_hidden_state[:, 0]` is consumed (VideoEncoder, models.py:201) the LAST layer runs its query side, attention
+output, MLP and LayerNorm 2 on the token-0 rows only (_last_layer_token0_fwd / _bwd): the same outputs and gradients,
+none of the rows the reference computes and drops.  Compute dtype: bf16 (MFMA, fp32 accumulate),
 fp32 (exact parity mode), or fp16 (MFMA, fp32 accumulate; forward only — the inference path of BASELINE config 5);
 master weights and their gradients stay fp32.
 """
@@ -214,7 +217,52 @@ def _layer_params(layer):
                 f2w=layer.output.dense.weight, f2b=layer.output.dense.bias)
 
 
-def _forward_impl(m: VideoMAEBackbone, video: torch.Tensor, save: bool):
+def _token0_last_ok(m, B, dt):
+    """Whether the last layer may run on the token-0 rows only (see _last_layer_token0_fwd): the bf16 weight-gradient
+    GEMMs contract over the B token-0 rows, which the bf16 kernels need in multiples of 8; CMHAR_TOKEN0_LAST=0 turns
+    it off (A/B knob)."""
+    if os.environ.get('CMHAR_TOKEN0_LAST', '1') == '0' or len(m.encoder.layer) == 0:
+        return False
+    return dt == torch.float32 or B % 8 == 0
+
+
+def _last_layer_token0_fwd(m, layer, li, x, W, geom, colscale, fscale, save):
+    """The LAST encoder layer when only `last_hidden_state[:, 0]` is consumed (VideoEncoder, models.py:201).
+
+    Row t of the layer output depends on row t of the attention output and MLP only, so for token 0 of each clip
+    only these rows are needed: LN1 (all rows, for the keys / values), K|V projection (all rows), Q projection of
+    the token-0 rows, attention with ONE query per (clip, head) over all 1568 keys, out-projection, LN2, FC1 and FC2
+    on the B token-0 rows.  The values computed — and, through _last_layer_token0_bwd, every parameter gradient —
+    are those of the full layer: the rows skipped feed nothing the model returns (the reference computes them and
+    drops them at models.py:201).  Returns the token-0 output rows [B, Hd] and the saved state."""
+    B, Lt, M, Hd, nh, D, scale = geom
+    p = _layer_params(layer)
+    h1, mu1, rs1 = K.layernorm_fwd(x, p['ln1w'], p['ln1b'], layer.layernorm_before.eps)
+    wqkv, bqkv = W[f'qkv{li}'], W.get(f'bqkv{li}')
+    wq, wkv = wqkv[:Hd], wqkv[Hd:]
+    bq = bqkv[:Hd] if bqkv is not None else None
+    bkv = bqkv[Hd:] if bqkv is not None else None
+    kv = K.linear(h1, wkv, bkv, colscale=None if colscale is None else (0, Hd, colscale[2]))
+    h1_0 = h1.view(B, Lt, Hd)[:, 0]
+    q0 = K.linear(h1_0, wq, bq)
+    o0 = torch.empty(B, Hd, dtype=x.dtype, device=x.device)
+    lse0 = torch.empty(B * nh, dtype=torch.float32, device=x.device)
+    K.attention_fwd(q0, kv[:, :Hd], kv[:, Hd:], o0, lse0, B=B, H=nh, Lq=1, Lk=Lt, D=D, scale=fscale)
+    x_0 = x.view(B, Lt, Hd)[:, 0]
+    x1_0 = K.linear(o0, W[f'o{li}'], p['ob'], residual=x_0)
+    h2_0, mu2, rs2 = K.layernorm_fwd(x1_0, p['ln2w'], p['ln2b'], layer.layernorm_after.eps)
+    pre0 = torch.empty(B, m_inter(layer), dtype=x.dtype, device=x.device) if save else None
+    g0 = K.linear(h2_0, W[f'fc1_{li}'], p['f1b'], act=L.ACT_GELU_SAVEGRAD if save else L.ACT_GELU, aux_out=pre0)
+    x2_0 = K.linear(g0, W[f'fc2_{li}'], p['f2b'], residual=x1_0)
+    saved = ('token0', x, h1, mu1, rs1, q0, kv, o0, lse0, x1_0, h2_0, mu2, rs2, pre0, g0) if save else None
+    return x2_0, saved
+
+
+def m_inter(layer):
+    return layer.intermediate.dense.weight.shape[0]
+
+
+def _forward_impl(m: VideoMAEBackbone, video: torch.Tensor, save: bool, token0_only: bool = False):
     cfg = m.config
     W = m._weights()
     dt = W.dtype
@@ -243,7 +291,13 @@ def _forward_impl(m: VideoMAEBackbone, video: torch.Tensor, save: bool):
     st.prescaled = dt == torch.bfloat16 and D == 64
     colscale = (Hd, 2 * Hd, scale * K.LOG2E) if st.prescaled else None
     fscale = 1.0 / K.LOG2E if st.prescaled else scale
+    st.token0 = token0_only and _token0_last_ok(m, B, dt)
+    nlayer = len(m.encoder.layer)
     for layer in m.encoder.layer:
+        if st.token0 and len(st.layers) == nlayer - 1:
+            x, saved = _last_layer_token0_fwd(m, layer, len(st.layers), x, W, st.geom, colscale, fscale, save)
+            st.layers.append(saved)
+            break
         p = _layer_params(layer)
         eps = layer.layernorm_before.eps
         h1, mu1, rs1 = K.layernorm_fwd(x, p['ln1w'], p['ln1b'], eps)
@@ -332,6 +386,10 @@ def _backward_impl(m: VideoMAEBackbone, st, dx, sink, overlap_wgrad=True):
     for li in reversed(range(len(m.encoder.layer))):
         layer = m.encoder.layer[li]
         p = _layer_params(layer)
+        if isinstance(st.layers[li][0], str):           # 'token0': the pruned last layer
+            dx = _last_layer_token0_bwd(st, li, p, W, dx, wgrad, ln_grads, sink, dev)
+            done([q for q in p.values() if q is not None])
+            continue
         x, h1, mu1, rs1, qkv, o, lse, x1, h2, mu2, rs2, pre, g = st.layers[li]
         st.layers[li] = None
         # x2 = x1 + FC2(gelu(FC1(LN2(x1))))
@@ -368,16 +426,60 @@ def _backward_impl(m: VideoMAEBackbone, st, dx, sink, overlap_wgrad=True):
     st.patches = None
 
 
+def _last_layer_token0_bwd(st, li, p, W, dx0, wgrad, ln_grads, sink, dev):
+    """Backward of _last_layer_token0_fwd.  dx0: [B, Hd] gradient of the token-0 output rows (the only rows the model
+    returns, so the gradient of every other row of the layer output is zero).  The MLP, LN2, out-projection and the
+    attention's query side run on the B token-0 rows; the keys / values receive their (dense) gradients from the one
+    query per (clip, head); LN1's backward and the QKV weight gradients cover every row.  Returns dx [M, Hd]."""
+    B, Lt, M, Hd, nh, D, scale = st.geom
+    _, x, h1, mu1, rs1, q0, kv, o0, lse0, x1_0, h2_0, mu2, rs2, pre0, g0 = st.layers[li]
+    st.layers[li] = None
+    dpre0 = K.linear_dgrad(dx0, W[f'fc2_{li}'], act=L.ACT_MULAUX, aux_in=pre0)
+    wgrad([p['f2w']], dx0, g0, p['f2w'].shape, [p['f2b']])
+    dh2_0 = K.linear_dgrad(dpre0, W[f'fc1_{li}'])
+    wgrad([p['f1w']], dpre0, h2_0, p['f1w'].shape, [p['f1b']])
+    del dpre0, pre0, g0
+    gw2, gb2, beta = ln_grads(p['ln2w'], p['ln2b'])
+    dx1_0 = K.layernorm_bwd(dh2_0, x1_0, p['ln2w'], mu2, rs2, gw2, gb2, dres=dx0, beta_acc=beta)
+    do0 = K.linear_dgrad(dx1_0, W[f'o{li}'])
+    wgrad([p['ow']], dx1_0, o0, p['ow'].shape, [p['ob']])
+    dq0 = torch.empty(B, Hd, dtype=dx0.dtype, device=dev)
+    dkv = torch.empty(M, 2 * Hd, dtype=dx0.dtype, device=dev)
+    attn_bwd = K.attention_bwd_prescaled if st.prescaled else K.attention_bwd
+    attn_bwd(q0, kv[:, :Hd], kv[:, Hd:], o0, do0, lse0, dq0, dkv[:, :Hd], dkv[:, Hd:], B=B, H=nh, Lq=1, Lk=Lt, D=D,
+             scale=scale)
+    del do0, o0
+    wqkv = W[f'qkv{li}']
+    dh1 = K.linear_dgrad(dkv, wqkv[Hd:])                        # K|V rows: every token
+    dh1_0 = dh1.view(B, Lt, Hd)[:, 0]
+    K.gemm(1, dq0, wqkv[:Hd], dh1_0, residual=dh1_0)            # + Q rows: the token-0 rows (one rounding)
+    # QKV weight / bias gradients into the packed [3Hd, Hd] destination: Q rows from the token-0 rows, K|V rows
+    # from every row
+    out, wbeta = sink.dest([p['qw'], p['kw'], p['vw']], (3 * Hd, Hd), dev)
+    bout, bbeta = (None, 0.0)
+    if p['qb'] is not None:
+        bout, bbeta = sink.dest([p['qb'], p['kb'], p['vb']], (3 * Hd,), dev)
+    h1_0 = h1.view(B, Lt, Hd)[:, 0]
+    K.linear_wgrad(dq0, h1_0, out=out[:Hd], beta=wbeta, bias_out=None if bout is None else bout[:Hd],
+                   bias_beta=bbeta)
+    K.linear_wgrad(dkv, h1, out=out[Hd:], beta=wbeta, bias_out=None if bout is None else bout[Hd:], bias_beta=bbeta)
+    del dkv, kv, q0
+    gw1, gb1, beta = ln_grads(p['ln1w'], p['ln1b'])
+    dx = K.layernorm_bwd(dh1, x, p['ln1w'], mu1, rs1, gw1, gb1, beta_acc=beta)
+    K.copy2d(dx1_0, dx.view(B, Lt, Hd)[:, 0], beta=1.0)         # residual path: nonzero on the token-0 rows only
+    return dx
+
+
 class _BackboneFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, video, module, token0_only, *params):
-        x, st = _forward_impl(module, video, save=True)
+        x, st = _forward_impl(module, video, save=True, token0_only=token0_only)
         ctx.module, ctx.st, ctx.token0_only = module, st, token0_only
         ctx.params = params
         B, Lt, M, Hd = st.geom[:4]
         if token0_only:
             out = torch.empty(B, Hd, dtype=torch.float32, device=x.device)
-            K.copy2d(x.view(B, Lt * Hd)[:, :Hd], out)
+            K.copy2d(x if st.token0 else x.view(B, Lt * Hd)[:, :Hd], out)
         else:
             out = torch.empty(B, Lt, Hd, dtype=torch.float32, device=x.device)
             K.copy2d(x, out.view(M, Hd))
@@ -390,7 +492,10 @@ class _BackboneFn(torch.autograd.Function):
         B, Lt, M, Hd = st.geom[:4]
         dt = m._weights().dtype
         gout = gout.contiguous()
-        if ctx.token0_only:
+        if ctx.token0_only and st.token0:
+            dx = torch.empty(B, Hd, dtype=dt, device=gout.device)        # the token-0 rows' gradient only
+            K.copy2d(gout, dx)
+        elif ctx.token0_only:
             dx = torch.zeros(M, Hd, dtype=dt, device=gout.device)
             K.copy2d(gout, dx.view(B, Lt * Hd)[:, :Hd])
         else:
@@ -415,11 +520,11 @@ def run_backbone(m: VideoMAEBackbone, video: torch.Tensor, token0_only: bool) ->
                                "torch.no_grad() / with frozen parameters, or use 'bf16' / 'fp32' for training")
         return _BackboneFn.apply(video, m, token0_only, *params)
     with torch.no_grad():
-        x, st = _forward_impl(m, video, save=False)
+        x, st = _forward_impl(m, video, save=False, token0_only=token0_only)
         B, Lt, M, Hd = st.geom[:4]
         if token0_only:
             out = torch.empty(B, Hd, dtype=torch.float32, device=x.device)
-            K.copy2d(x.view(B, Lt * Hd)[:, :Hd], out)
+            K.copy2d(x if st.token0 else x.view(B, Lt * Hd)[:, :Hd], out)
         else:
             out = torch.empty(B, Lt, Hd, dtype=torch.float32, device=x.device)
             K.copy2d(x, out.view(M, Hd))

@@ -285,3 +285,45 @@ def test_videomae_base_full_geometry_backward(dtype):
                 bad[name] = (e_g, e_p)
     print('worst:', sorted(rows, reverse=True)[:5])
     assert not bad, bad
+
+
+@pytest.mark.parametrize('dtype', ['fp32', 'bf16'])
+def test_last_layer_token0_pruning_matches_full_layer(dtype, monkeypatch):
+    """The VideoEncoder computes the last VideoMAE layer's query side, MLP and LayerNorm 2 on the token-0 rows only
+    (cmhar/videomae.py _last_layer_token0_fwd / _bwd).  Against the full last layer (CMHAR_TOKEN0_LAST=0) on the
+    same weights and inputs: projections, loss and every parameter gradient agree to rounding (fp32 ≤ 1e-5; bf16
+    ≤ 1e-2, where the two paths round different intermediate rows), at B = 8 clips of 32 tokens."""
+    from cmhar.config import Config
+    from cmhar.losses import SigmoidContrastiveLoss
+    from cmhar.models import CrossModalModel
+    cfg = Config()
+    cfg.data.imu_window_size, cfg.data.video_frames_per_window, cfg.data.video_resize = 64, 4, (64, 64)
+    m = cfg.model
+    m.video_backbone, m.video_pretrained, m.compute_dtype = '/nonexistent/videomae-t0', False, dtype
+    m.imu_d_model, m.imu_nhead, m.imu_num_layers, m.imu_dropout = 32, 4, 2, 0.0
+    m.videomae_hidden_size, m.videomae_num_layers, m.videomae_num_heads, m.videomae_intermediate_size = 128, 2, 2, 256
+    m.video_d_model, m.projection_hidden_dim, m.projection_dim = 64, 64, 32
+    torch.manual_seed(3)
+    model = CrossModalModel(cfg).to(DEV).train()
+    g = torch.Generator().manual_seed(4)
+    imu = torch.randn(8, 6, 64, generator=g).to(DEV)
+    video = torch.randn(8, 4, 3, 64, 64, generator=g).to(DEV)
+    lf = SigmoidContrastiveLoss().to(DEV)
+
+    def run(flag):
+        monkeypatch.setenv('CMHAR_TOKEN0_LAST', flag)
+        model.zero_grad(set_to_none=True)
+        a, b = model(imu, video)
+        loss = lf(a, b)
+        loss.backward()
+        return a.detach().clone(), b.detach().clone(), loss.item(), \
+            {n: p.grad.detach().clone() for n, p in model.named_parameters() if p.grad is not None}
+    a1, b1, l1, g1 = run('1')
+    a0, b0, l0, g0 = run('0')
+    tol = 1e-5 if dtype == 'fp32' else 1e-2
+    assert torch.equal(a1, a0)                                  # the IMU branch does not change
+    assert rel(b1, b0.cpu()) < tol and abs(l1 - l0) <= tol * abs(l0)
+    assert set(g1) == set(g0)
+    gscale = max(float(v.abs().max()) for v in g0.values())
+    worst = {n: rel(g1[n], g0[n].cpu()) for n in g0 if float(g0[n].abs().max()) > 1e-5 * gscale}
+    assert max(worst.values()) < tol, sorted(worst.items(), key=lambda kv: -kv[1])[:4]
