@@ -350,7 +350,12 @@ struct DmaSrc {
   const char* base;   // operand + tile origin (bytes)
   long kstride;       // bytes per k step
   int voff[4];
+  int pf_off;         // L2 prefetch: this lane's 128-B line of a tile (see l2_prefetch)
   __device__ __forceinline__ void init(const bf16* __restrict__ P, long ld, int r0, int wave, int lane) {
+    {   // tile line idx (0..255) = this thread's index within its operand's half of the workgroup
+      const int idx = (wave & 3) * 64 + lane;
+      pf_off = KC ? (int)((long)idx * ld * 2) : (int)((long)(idx >> 2) * ld * 2 + (idx & 3) * 128);
+    }
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
       const int i = wave * 4 + t;                          // 1 KiB piece index (32 per tile)
@@ -379,7 +384,17 @@ struct DmaSrc {
 #pragma unroll
     for (int t = 0; t < 4; ++t) piece(r, lds, wave, t);
   }
+  // Touch every 128-B line of the tile at k0 (256 lines, one per lane of 4 waves) with a 4-byte LDS-DMA into a junk
+  // LDS slot: the lines are pulled into this XCD's L2 a tile ahead of the DMA that stages them, so that DMA hits L2.
+  __device__ __forceinline__ void l2_prefetch(int k0, char* junk) const {
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc(k0), (lds_void_ptr)junk, 4, pf_off, 0, 0, 0);
+  }
 };
+
+// L2 prefetch of K-tile kt+2 in the two-buffer weight-gradient K loop (CMHAR_GEMM_L2PF=1; A/B knob)
+#ifndef CMHAR_GEMM_L2PF
+#define CMHAR_GEMM_L2PF 1
+#endif
 
 template <bool KC>
 __device__ __forceinline__ bf16x8 frag256(const char* lds, int r0, int kk, int lane) {
@@ -409,7 +424,8 @@ __global__ __launch_bounds__(NT2, 2) void gemm256_kernel(int M, int N, int K, co
                                                          long ldc, Epilogue e, int klen, long split_stride,
                                                          int raw_out, float* __restrict__ sk_ws, int n_dp,
                                                          int sk_klen) {
-  __shared__ __attribute__((aligned(16))) char smem[NA == 3 ? 163840 : SMEM2];
+  constexpr bool PF = CMHAR_GEMM_L2PF && NA == 2 && MODE == 0;
+  __shared__ __attribute__((aligned(16))) char smem[NA == 3 ? 163840 : SMEM2 + (PF ? 2048 : 0)];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = wave >> 2, wc = wave & 3;
@@ -510,6 +526,7 @@ __global__ __launch_bounds__(NT2, 2) void gemm256_kernel(int M, int N, int K, co
     // issued a tile earlier) can leave A(kt+2)'s 4 pieces in flight.  (Spreading the 8 pieces one per 4-MFMA group
     // instead of this burst measured neutral on forward/dgrad and 1.3-1.7x slower on the NA = 2 weight-gradient layout,
     // whose vmcnt(0) then waits on the last, late piece.)
+    const bool pf = PF && kt + 2 < nk;
     if (MODE != 7) {
       if (NA == 3) {
         if (more) db.tile(kbeg + (kt + 1) * TK2, nxt_b, wave);
@@ -517,6 +534,10 @@ __global__ __launch_bounds__(NT2, 2) void gemm256_kernel(int M, int N, int K, co
       } else if (more) {
         da.tile(kbeg + (kt + 1) * TK2, nxt, wave);
         db.tile(kbeg + (kt + 1) * TK2, nxt_b, wave);
+        if (pf) {       // after the DMA pieces: the vmcnt(1) below leaves this one in flight
+          if (wave < 4) da.l2_prefetch(kbeg + (kt + 2) * TK2, smem + SMEM2 + wave * 256);
+          else db.l2_prefetch(kbeg + (kt + 2) * TK2, smem + SMEM2 + wave * 256);
+        }
       }
     }
     __builtin_amdgcn_sched_barrier(0);
@@ -540,6 +561,7 @@ __global__ __launch_bounds__(NT2, 2) void gemm256_kernel(int M, int N, int K, co
     if (more) {
       // own DMA of tile kt+1 landed, own reads of tile kt returned; then everyone's
       if (more2) asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      else if (pf) asm volatile("s_waitcnt vmcnt(1) lgkmcnt(0)\n\ts_barrier" ::: "memory");
       else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
       load_k0(nxt, nxt_b, 0, 4, true);                     // slots 0-3 and bf0 are free now
     }
