@@ -1242,8 +1242,11 @@ static void flash_bwd_bf16(int B, int H, int Lq, int Lk, const void* Q, long ldq
                                                                     (const bf16*)dO, lddo, lse, delta, (bf16*)dQ,
                                                                     lddq, s_in);
   // a tail of <= CMHAR_ATTN_TAIL queries / keys beyond the last full 128-row block goes to the tail kernels
+  // (the dQ tail kernel measured slower than the in-grid one-active-wave block at L = 1568 — 351.6 + 31.8 µs vs 367.1
+  // µs per layer — so it only takes sequences that are ALL tail, Lq <= CMHAR_ATTN_TAIL: the one-query rows of the
+  // token-0 last layer, the cross-attention fusion's IMU queries)
   const int qfull = bulk + ((Lq - bulk) / 128) * 128;
-  const bool qtail = Lq > qfull && Lq - qfull <= CMHAR_ATTN_TAIL;
+  const bool qtail = qfull == 0 && Lq - qfull <= CMHAR_ATTN_TAIL;
   const int qend = qtail ? qfull : Lq;
   if (qend > bulk)
     attn_bwd_dq_bf16<1, PS><<<dim3(cdiv(qend - bulk, 128), H, B), 256, 0, st>>>(

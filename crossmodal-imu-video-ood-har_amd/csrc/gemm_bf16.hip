@@ -391,9 +391,11 @@ struct DmaSrc {
   }
 };
 
-// L2 prefetch of K-tile kt+2 in the two-buffer weight-gradient K loop (CMHAR_GEMM_L2PF=1; A/B knob)
+// L2 prefetch of K-tile kt+2 in the two-buffer weight-gradient K loop (CMHAR_GEMM_L2PF=1; A/B knob, off: measured
+// 12 % SLOWER on the VideoMAE weight gradients — 242.6 vs 216.6 µs average in the step trace — the extra line
+// requests cost more L2 / TA issue than the misses they pre-empt)
 #ifndef CMHAR_GEMM_L2PF
-#define CMHAR_GEMM_L2PF 1
+#define CMHAR_GEMM_L2PF 0
 #endif
 
 template <bool KC>

@@ -291,8 +291,9 @@ def test_videomae_base_full_geometry_backward(dtype):
 def test_last_layer_token0_pruning_matches_full_layer(dtype, monkeypatch):
     """The VideoEncoder computes the last VideoMAE layer's query side, MLP and LayerNorm 2 on the token-0 rows only
     (cmhar/videomae.py _last_layer_token0_fwd / _bwd).  Against the full last layer (CMHAR_TOKEN0_LAST=0) on the
-    same weights and inputs: projections, loss and every parameter gradient agree to rounding (fp32 ≤ 1e-5; bf16
-    ≤ 1e-2, where the two paths round different intermediate rows), at B = 8 clips of 32 tokens."""
+    same weights and inputs, at B = 8 clips of 32 tokens: fp32 — projections, loss and every parameter gradient agree
+    to ≤ 1e-5; bf16 — the two paths round different intermediate rows, so each is compared with the fp32 result:
+    the pruned path's error is at most 1.5× the full path's (+2e-3) on every output and gradient."""
     from cmhar.config import Config
     from cmhar.losses import SigmoidContrastiveLoss
     from cmhar.models import CrossModalModel
@@ -310,20 +311,29 @@ def test_last_layer_token0_pruning_matches_full_layer(dtype, monkeypatch):
     video = torch.randn(8, 4, 3, 64, 64, generator=g).to(DEV)
     lf = SigmoidContrastiveLoss().to(DEV)
 
-    def run(flag):
+    def run(flag, dt):
         monkeypatch.setenv('CMHAR_TOKEN0_LAST', flag)
+        model.video_encoder.backbone.compute_dtype = dt
         model.zero_grad(set_to_none=True)
         a, b = model(imu, video)
         loss = lf(a, b)
         loss.backward()
-        return a.detach().clone(), b.detach().clone(), loss.item(), \
-            {n: p.grad.detach().clone() for n, p in model.named_parameters() if p.grad is not None}
-    a1, b1, l1, g1 = run('1')
-    a0, b0, l0, g0 = run('0')
-    tol = 1e-5 if dtype == 'fp32' else 1e-2
+        return a.detach().cpu(), b.detach().cpu(), loss.item(), \
+            {n: p.grad.detach().cpu() for n, p in model.named_parameters() if p.grad is not None}
+    a1, b1, l1, g1 = run('1', dtype)
+    a0, b0, l0, g0 = run('0', dtype)
     assert torch.equal(a1, a0)                                  # the IMU branch does not change
-    assert rel(b1, b0.cpu()) < tol and abs(l1 - l0) <= tol * abs(l0)
     assert set(g1) == set(g0)
     gscale = max(float(v.abs().max()) for v in g0.values())
-    worst = {n: rel(g1[n], g0[n].cpu()) for n in g0 if float(g0[n].abs().max()) > 1e-5 * gscale}
-    assert max(worst.values()) < tol, sorted(worst.items(), key=lambda kv: -kv[1])[:4]
+    keys = [n for n in g0 if float(g0[n].abs().max()) > 1e-5 * gscale]
+    if dtype == 'fp32':
+        assert rel(b1, b0) < 1e-5 and abs(l1 - l0) <= 1e-5 * abs(l0)
+        worst = {n: rel(g1[n], g0[n]) for n in keys}
+        assert max(worst.values()) < 1e-5, sorted(worst.items(), key=lambda kv: -kv[1])[:4]
+        return
+    _, bf, lf32, gf = run('0', 'fp32')
+    assert rel(b1, bf) <= 1.5 * rel(b0, bf) + 2e-3
+    assert abs(l1 - lf32) <= 1.5 * abs(l0 - lf32) + 2e-3 * abs(lf32)
+    bad = {n: (rel(g1[n], gf[n]), rel(g0[n], gf[n])) for n in keys
+           if rel(g1[n], gf[n]) > 1.5 * rel(g0[n], gf[n]) + 2e-3}
+    assert not bad, bad
