@@ -42,7 +42,7 @@ PEAK_F32_TFLOPS = 157.3        # f32-input MFMA (= the f32 vector rate; no xf32 
 PEAK_HBM_GBS = 8000.0
 
 
-TRAFFIC_JSON = os.path.join(REPO, 'profiles', 'r02_pmc_traffic.json')
+TRAFFIC_JSON = os.path.join(REPO, 'profiles', 'r03_pmc_traffic.json')
 MFMA_JSON = os.path.join(REPO, 'profiles', 'r03_pmc_mfma.json')
 
 # per-workload defaults of --batch / --frames / --image / --imu-len / --dtype (BASELINE.json configs)
@@ -133,6 +133,17 @@ def videomae_flops_per_clip(T, H, W, hd=768, layers=12, inter=3072, P=16, tub=2,
     embed = 2 * N * (C * tub * P * P) * hd
     per_layer = 2 * N * hd * (4 * hd + 2 * inter) + 4 * N * N * hd
     return embed, embed + layers * per_layer
+
+
+def token0_last_layer_saving(T, H, W, hd=768, inter=3072, P=16, tub=2):
+    """(forward, forward+backward) FLOPs per clip that the token-0 last layer (cmhar/videomae.py
+    _last_layer_token0_fwd / _bwd) does not execute: the query projection, attention, out-projection and MLP of the
+    N − 1 rows whose outputs the model never returns.  Backward = 2× forward for the GEMMs, 2.5× for attention
+    (10·L²·D vs 4·L²·D), the convention of SURVEY §8d's 3·F_fwd total."""
+    N = (T // tub) * (H // P) * (W // P)
+    gemm = 2 * (N - 1) * hd * (2 * hd + 2 * inter)       # Q projection + out-projection + FC1 + FC2
+    attn = 4 * (N * N - N) * hd
+    return gemm + attn, 3 * gemm + 3.5 * attn
 
 
 def host_cpu():
@@ -415,6 +426,9 @@ def build_workload(args, dev, rank, world):
                           f'{args.frames}x{args.image}^2 + IMU 6x{args.imu_len}, SigLIP loss, clip 1.0, AdamW')
         else:
             W.flops_per_clip = 3 * fwd_f - embed_f     # fwd + 2x bwd, no pixel gradient for the tubelet conv
+            if os.environ.get('CMHAR_TOKEN0_LAST', '1') != '0' and (B % 8 == 0 or args.dtype == 'fp32'):
+                W.executed_flops_per_clip = W.flops_per_clip - token0_last_layer_saving(args.frames, args.image,
+                                                                                        args.image)[1]
             W.metric = 'clips/sec fwd+bwd, 16x224^2 video + 200x6 IMU, batch 32, 1/2/4/8 GPU'
             W.workload = (f'CrossModalModel pretrain step: VideoMAE-B {args.frames}x{args.image}^2 + '
                           f'IMU 6x{args.imu_len} PatchTST, SigLIP loss, clip 1.0, AdamW')
@@ -491,7 +505,10 @@ def main():
     value = clips / elapsed
     ms = 1000 * elapsed / args.steps
     peak = PEAK_F32_TFLOPS if args.dtype == 'fp32' else PEAK_BF16_TFLOPS     # fp16 dense MFMA = bf16 rate
-    whole_tflops = W.flops_per_clip * clips / elapsed / 1e12
+    # model FLOP rate over the FLOPs the step EXECUTES (the token-0 last layer skips rows the model never returns);
+    # the reference model's algorithmic total is reported beside it
+    exec_flops = getattr(W, 'executed_flops_per_clip', W.flops_per_clip)
+    whole_tflops = exec_flops * clips / elapsed / 1e12
 
     # dominant kernel: the single HIP kernel with the largest traced time in the traced warm-up step (split-K GEMMs
     # are traced without their reduce launch); achieved = its algorithmic FLOPs / its HIP-event-measured time over
@@ -524,6 +541,8 @@ def main():
            'roofline': roof,
            'whole_step_model_tflops': round(whole_tflops, 1),
            'whole_step_mfma_frac': round(whole_tflops / peak, 4),
+           'executed_gflop_per_clip': round(exec_flops / 1e9, 2),
+           'reference_algorithmic_gflop_per_clip': round(W.flops_per_clip / 1e9, 2),
            'first_warmup_loss': first_loss,
            'max_mem_gb': round(torch.cuda.max_memory_allocated(dev) / 2 ** 30, 1)}
     if rank == 0 and world == 1 and not args.no_cpu_baseline and headline:
