@@ -227,9 +227,9 @@ __global__ __launch_bounds__(256) void mt_adamw_kernel(const MTTensor* __restric
   const long end = ch.start + ch.len;
   if (vec) {
     const long nv = (ch.len >> 2) << 2;
-    for (long i = ch.start + threadIdx.x * 4; i < ch.start + nv; i += 1024) {
-      floatx4 g4 = *(const floatx4*)(T.g + i), p4 = *(const floatx4*)(T.p + i);
-      floatx4 m4 = *(const floatx4*)(T.m + i), v4 = *(const floatx4*)(T.v + i);
+    // two float4 groups per thread per iteration, all eight loads issued before the first store (more bytes in
+    // flight per thread: the pass is HBM-latency bound at one group)
+    auto step4 = [&](long i, floatx4 g4, floatx4 p4, floatx4 m4, floatx4 v4) __attribute__((always_inline)) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         g4[j] = mul_nocontract(g4[j], gs);     // rounded product (no FMA contraction): the value a scale pass would store
@@ -248,7 +248,19 @@ __global__ __launch_bounds__(256) void mt_adamw_kernel(const MTTensor* __restric
         *(decltype(b4)*)(T.pbf + i) = b4;
       }
       if (T.pcopy) *(floatx4*)(T.pcopy + i) = p4;
+    };
+    long i = ch.start + threadIdx.x * 4;
+    for (; i + 1024 < ch.start + nv; i += 2048) {
+      const floatx4 ga = *(const floatx4*)(T.g + i), pa = *(const floatx4*)(T.p + i);
+      const floatx4 ma = *(const floatx4*)(T.m + i), va = *(const floatx4*)(T.v + i);
+      const floatx4 gb = *(const floatx4*)(T.g + i + 1024), pb = *(const floatx4*)(T.p + i + 1024);
+      const floatx4 mb = *(const floatx4*)(T.m + i + 1024), vb = *(const floatx4*)(T.v + i + 1024);
+      step4(i, ga, pa, ma, va);
+      step4(i + 1024, gb, pb, mb, vb);
     }
+    if (i < ch.start + nv)
+      step4(i, *(const floatx4*)(T.g + i), *(const floatx4*)(T.p + i), *(const floatx4*)(T.m + i),
+            *(const floatx4*)(T.v + i));
     i0 = ch.start + nv;
   }
   for (long i = i0 + threadIdx.x; i < end; i += 256) {
