@@ -63,9 +63,10 @@ def _gemm_trace_name(layout, M, N, K, s, has_ws, rowsum, out_dtype):
     plan = _PLAN.get(key)
     if plan is None:
         plan = _PLAN[key] = int(L.lib().cmhar_gemm_bf16_plan(layout, M, N, K, s, int(has_ws), int(rowsum)))
-    o = 'float' if (plan in (3, 5) or out_dtype == torch.float32) else 'bf16'
-    if plan == 4:
-        return f'gemm8p_kernel<{"true" if layout == 0 else "false"},{o}>'
+    o = 'float' if (plan in (3, 5, 6) or out_dtype == torch.float32) else 'bf16'
+    if plan in (4, 6):
+        ak, bk = layout != 2, layout == 0
+        return f'gemm8p_kernel<{str(ak).lower()},{str(bk).lower()},{o}>'
     name = _GEMM_SYMBOL[layout].format(o=o)
     if plan in (1, 2, 3):
         name = name.replace('gemm_bf16_kernel', 'gemm256_kernel')
@@ -73,8 +74,8 @@ def _gemm_trace_name(layout, M, N, K, s, has_ws, rowsum, out_dtype):
 
 
 def _gemm_has_reduce(layout, M, N, K, s, has_ws, rowsum):
-    """Whether the call's plan ends with a split-K / tail reduce launch (plans 2, 3, 5)."""
-    return _PLAN[(layout, M, N, K, s, has_ws, rowsum)] in (2, 3, 5)
+    """Whether the call's plan ends with a split-K / tail reduce launch (plans 2, 3, 5, 6)."""
+    return _PLAN[(layout, M, N, K, s, has_ws, rowsum)] in (2, 3, 5, 6)
 
 # ------------------------------------------------------------------------------------------------------------
 # workspaces (one growing fp32 buffer per (device, stream))

@@ -14,6 +14,8 @@
 // cmhar_splitk_reduce combines with the epilogue.
 #include "common.h"
 
+#include <type_traits>
+
 namespace {
 
 constexpr int BM = 128, BN = 128, BK = 64, NT = 256;
@@ -697,19 +699,79 @@ struct DmaHalf {
   }
 };
 
-template <typename E, bool B_KC, typename OutT>
+// The weight-gradient A operand (dYᵀ: [k][m], m contiguous) on the 8-phase schedule, staged in COLUMN halves: the
+// schedule hands A's half h (rows 128h.. of the output tile) to wave group h only, so each half is its own
+// [64 k][128 m] image at h * 16 KiB (256-B rows, the mc_off swizzle, whose XOR never leaves a half's 16 chunks); a
+// 1 KiB DMA piece = 4 k-rows of 256 B.
+struct DmaHalfM {
+  const char* base;
+  long kstride;
+  int voff[2][2];
+  __device__ __forceinline__ void init(const bf16* __restrict__ P, long ld, int c0, int wave, int lane) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const int k = 4 * (2 * wave + t) + (lane >> 4);
+        const int lc = (lane & 15) ^ mc_swz(k);
+        voff[h][t] = (int)(((long)k * ld + h * 128 + lc * 8) * 2);
+      }
+    base = (const char*)(P + c0);
+    kstride = ld * 2;
+  }
+  __device__ __forceinline__ void half(int k0, char* lds, int h, int wave) const {
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void*)(base + (long)k0 * kstride), (short)0,
+                                                                       0x7fffffff, 0x00020000);
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void_ptr)(lds + h * 16384 + (2 * wave + t) * 1024), 16,
+                                               voff[h][t], 0, 0, 0);
+  }
+};
+
+// A-operand fragment of the 8-phase kernel: K-contiguous image (frag256<true>) or DmaHalfM's column halves (the
+// transposed reads of frag256<false> on 256-B rows).
+template <bool A_KC>
+__device__ __forceinline__ bf16x8 frag8p_a(const char* lds, int r0, int kk, int lane) {
+  if (A_KC) return frag256<true>(lds, r0, kk, lane);
+  const char* hb = lds + (r0 >> 7) * 16384;
+  const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+  const int chunk = ((r0 & 127) >> 3) + (p >> 1);
+  const int k = kk * 32 + 8 * g + q;
+  const short4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(short4_t, hb + mc_off(k, chunk) + (p & 1) * 8));
+  const short4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(short4_t, hb + mc_off(k + 4, chunk) + (p & 1) * 8));
+  short8_t v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+// A_KC = false: the weight-gradient layout (dW = dYᵀX, both operands row-contraction), split-K capable: blockIdx.z =
+// K-split of klen (fp32 partial slabs at split_stride when raw_out, reduced by splitk_reduce_kernel), with the bias
+// gradient Σ_k A(m,k) (Epilogue::rowsum) on the same MFMA operand fragments as gemm256_kernel; the per-output
+// accumulation order (K-tile, then kk) is gemm256_kernel's, so the two kernels give identical bits.
+template <typename E, bool A_KC, bool B_KC, typename OutT>
 __global__ __launch_bounds__(NT2, 2) void gemm8p_kernel(int M, int N, int K, const bf16* __restrict__ A, long lda,
                                                         const bf16* __restrict__ B, long ldb, OutT* __restrict__ C,
-                                                        long ldc, Epilogue e) {
+                                                        long ldc, Epilogue e, int klen, long split_stride,
+                                                        int raw_out) {
   __shared__ __attribute__((aligned(16))) char smem[SMEM2];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = wave >> 2, wc = wave & 3;
-  const int tiles_n = N / TN2;
-  const int bid = xcd_remap(blockIdx.x, (M / TM2) * tiles_n);
-  const int bm = (bid / tiles_n) * TM2, bn = (bid % tiles_n) * TN2;
-  const int nk = K / TK2;   // >= 2 (host-checked)
-  DmaHalf<true> da;
+  const int tiles_n = N / TN2, tiles_m = M / TM2, ntile = tiles_m * tiles_n;
+  // split index folded into the XCD remap (as gemm256_kernel): one XCD runs whole splits
+  const int rlin = xcd_remap(blockIdx.x + ntile * blockIdx.z, ntile * gridDim.z);
+  const int bid = rlin % ntile, split = rlin / ntile;
+  const int kbeg = split * klen, kend = min(K, kbeg + klen);
+  const int tm = bid / tiles_n, tn = bid % tiles_n;
+  const int bm = tm * TM2, bn = tn * TN2;
+  const int nk = (kend - kbeg) / TK2;   // >= 2 (host-checked)
+  float* const rs_slab = raw_out ? (float*)C + (long)gridDim.z * split_stride + (long)split * M : nullptr;
+  C += (long)split * split_stride;
+  const bool rs = !A_KC && e.rowsum != nullptr && tn == tm % tiles_n;
+  const float one8[8] = {1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f};
+  const bf16x8 ones = pack_frag8<E>(one8);
+  floatx4 accb[2] = {floatx4{0.f, 0.f, 0.f, 0.f}, floatx4{0.f, 0.f, 0.f, 0.f}};
+  std::conditional_t<A_KC, DmaHalf<true>, DmaHalfM> da;
   DmaHalf<B_KC> db;
   da.init(A, lda, bm, wave, lane);
   db.init(B, ldb, bn, wave, lane);
@@ -725,11 +787,11 @@ __global__ __launch_bounds__(NT2, 2) void gemm8p_kernel(int M, int N, int K, con
   bf16x8 af[2][4], b0[2][2], b1[2][2];
 
   // prologue: K-tile 0 whole + K-tile 1's A upper half; wait for tile 0
-  da.half(0, abuf(0), 0, wave);
-  da.half(0, abuf(0), 1, wave);
-  db.half(0, bbuf(0), 0, wave);
-  db.half(0, bbuf(0), 1, wave);
-  da.half(TK2, abuf(1), 0, wave);
+  da.half(kbeg, abuf(0), 0, wave);
+  da.half(kbeg, abuf(0), 1, wave);
+  db.half(kbeg, bbuf(0), 0, wave);
+  db.half(kbeg, bbuf(0), 1, wave);
+  da.half(kbeg + TK2, abuf(1), 0, wave);
   asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
   __builtin_amdgcn_s_barrier();
   if (wr == 1) __builtin_amdgcn_s_barrier();   // group 1 runs one interval behind
@@ -745,6 +807,10 @@ __global__ __launch_bounds__(NT2, 2) void gemm8p_kernel(int M, int N, int K, con
     _Pragma("unroll") for (int j = 0; j < 2; ++j)                                                             \
       acc[(QM) * 4 + i][qn_ * 2 + j] = mma16<E>(af[kk][i], BF[kk][j],           \
                                                                              acc[(QM) * 4 + i][qn_ * 2 + j]); \
+    if (!A_KC && rs && qn_ == (QM)) /* bias gradient: each A fragment once, at its first quadrant */         \
+      _Pragma("unroll") for (int kk = 0; kk < 2; ++kk)                                                        \
+      _Pragma("unroll") for (int i = 0; i < 4; ++i)                                                           \
+        if (wc == ((QM) * 4 + i) >> 1) accb[i & 1] = mma16<E>(af[kk][i], ones, accb[i & 1]);                   \
     __builtin_amdgcn_s_setprio(0);                                                                            \
     __builtin_amdgcn_sched_barrier(0);                                                                        \
     __builtin_amdgcn_s_barrier();                                                                             \
@@ -761,14 +827,14 @@ __global__ __launch_bounds__(NT2, 2) void gemm8p_kernel(int M, int N, int K, con
     const char* as = abuf(t);
     const char* bs = bbuf(t);
     const bool n1 = t + 1 < nk, n2 = t + 2 < nk;
-    const int k1 = (t + 1) * TK2, k2 = (t + 2) * TK2;
+    const int k1 = kbeg + (t + 1) * TK2, k2 = kbeg + (t + 2) * TK2;
     // phase 1: A0 + B0, stage A lower half of t+1; MFMA quadrant (0,0)
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
 #pragma unroll
       for (int j = 0; j < 2; ++j) b0[kk][j] = frag256<B_KC>(bs, wc * 64 + j * 16, kk, lane);
 #pragma unroll
-      for (int i = 0; i < 4; ++i) af[kk][i] = frag256<true>(as, wr * 128 + i * 16, kk, lane);
+      for (int i = 0; i < 4; ++i) af[kk][i] = frag8p_a<A_KC>(as, wr * 128 + i * 16, kk, lane);
     }
     if (n1) da.half(k1, abuf(t + 1), 1, wave);
     END_LOADS();
@@ -794,7 +860,7 @@ __global__ __launch_bounds__(NT2, 2) void gemm8p_kernel(int M, int N, int K, con
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) af[kk][i] = frag256<true>(as, wr * 128 + 64 + i * 16, kk, lane);
+      for (int i = 0; i < 4; ++i) af[kk][i] = frag8p_a<A_KC>(as, wr * 128 + 64 + i * 16, kk, lane);
     END_LOADS();
     {
       constexpr int qn_ = 1;
@@ -812,6 +878,16 @@ __global__ __launch_bounds__(NT2, 2) void gemm8p_kernel(int M, int N, int K, con
 #undef MFMA_Q
 #undef END_LOADS
   if (wr == 0) __builtin_amdgcn_s_barrier();   // re-align the groups
+  if (!A_KC && rs && (lane & 15) == 0) {       // every column of a ones-product holds the row sum: lanes 0,16,32,48
+#pragma unroll
+    for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = bm + wr * 128 + (2 * wc + ii) * 16 + 4 * (lane >> 4) + r;
+        if (rs_slab) rs_slab[m] = accb[ii][r];
+        else e.rowsum[m] = e.rowsum_beta != 0.f ? accb[ii][r] + e.rowsum_beta * e.rowsum[m] : accb[ii][r];
+      }
+  }
   __syncthreads();
 
   // epilogue: as gemm256_kernel — per wave, two passes of 64x64 through a private LDS slab, 16-B stores
@@ -833,10 +909,16 @@ __global__ __launch_bounds__(NT2, 2) void gemm8p_kernel(int M, int N, int K, con
       const int rr = it * 8 + (lane >> 3);
       const int m = bm + wr * 128 + pass * 64 + rr;
       const floatx4 lo = *(const floatx4*)&T[rr * EPI2_LD + cg], hi = *(const floatx4*)&T[rr * EPI2_LD + cg + 4];
-      float v[8];
+      if (raw_out) {
+        float* dst = (float*)C + (long)m * ldc + n0;
+        *(floatx4*)dst = lo;
+        *(floatx4*)(dst + 4) = hi;
+      } else {
+        float v[8];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) { v[j] = lo[j]; v[4 + j] = hi[j]; }
-      epilogue_store8<OutT>(e, C, ldc, m, n0, v);
+        for (int j = 0; j < 4; ++j) { v[j] = lo[j]; v[4 + j] = hi[j]; }
+        epilogue_store8<OutT>(e, C, ldc, m, n0, v);
+      }
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   }
@@ -892,8 +974,23 @@ static bool use_8p() {
 #endif
 static bool use_8p_dgrad() { return CMHAR_GEMM_8P_DGRAD != 0; }
 
+// The weight-gradient layout (both operands row-contraction, split-K, fused bias gradient) on the 8-phase schedule;
+// CMHAR_GEMM_8P_WGRAD=0/1 overrides the build default (A/B measurements; the two kernels give identical bits).
+#ifndef CMHAR_GEMM_8P_WGRAD_DEFAULT
+#define CMHAR_GEMM_8P_WGRAD_DEFAULT 1
+#endif
+static bool use_8p_wgrad() {
+  static const bool v = [] {
+    const char* s = getenv("CMHAR_GEMM_8P_WGRAD");
+    return s ? atoi(s) != 0 : CMHAR_GEMM_8P_WGRAD_DEFAULT != 0;
+  }();
+  return v;
+}
+
 // Which kernel(s) a cmhar_gemm_bf16 call launches (also exported for trace labels: cmhar_gemm_bf16_plan).
-enum GemmPlan { PLAN_128 = 0, PLAN_256 = 1, PLAN_256_TAIL = 2, PLAN_256_SPLITK = 3, PLAN_8P = 4, PLAN_128_SPLITK = 5 };
+enum GemmPlan {
+  PLAN_128 = 0, PLAN_256 = 1, PLAN_256_TAIL = 2, PLAN_256_SPLITK = 3, PLAN_8P = 4, PLAN_128_SPLITK = 5, PLAN_8P_SPLITK = 6
+};
 static int gemm_plan(bool ak, bool bkc, int M, int N, int K, int splits, bool has_ws, bool rowsum) {
   const bool big = M % TM2 == 0 && N % TN2 == 0 && K % TK2 == 0;
   if (!big) {
@@ -901,7 +998,11 @@ static int gemm_plan(bool ak, bool bkc, int M, int N, int K, int splits, bool ha
     return cdiv(K, klen) > 1 ? PLAN_128_SPLITK : PLAN_128;
   }
   const int klen = splits > 1 ? cdiv(cdiv(K, splits), TK2) * TK2 : K;
-  if (cdiv(K, klen) > 1) return PLAN_256_SPLITK;
+  const int nsplit = cdiv(K, klen);
+  // the 8-phase loop needs >= 2 K-tiles in every split (the last one included)
+  const bool wgrad8p = !ak && use_8p_wgrad() && klen >= 2 * TK2 && K - (nsplit - 1) * klen >= 2 * TK2;
+  if (nsplit > 1) return wgrad8p ? PLAN_8P_SPLITK : PLAN_256_SPLITK;
+  if (wgrad8p) return PLAN_8P;
   if (has_ws && !rowsum && tail_split(M, N, K).n_dp > 0) return PLAN_256_TAIL;   // (8-phase instead: FC2 fwd 5 % slower)
   if (ak && K >= 2 * TK2 && use_8p() && (bkc || use_8p_dgrad())) return PLAN_8P;
   return PLAN_256;
@@ -936,7 +1037,11 @@ int launch(int M, int N, int K, const bf16* A, long lda, const bf16* B, long ldb
         splitk_reduce_kernel<OutT><<<reduce_blocks(tail_rows, N), 256, 0, st>>>(
             tail_rows, N, ts.nsplit, ws, (long)tail_rows * N, C, ldc, e, ts.tail_m0);
     } else if (plan == PLAN_8P) {
-      if (ph_gemm) gemm8p_kernel<E, BKc, OutT><<<grid, NT2, 0, st>>>(M, N, K, A, lda, B, ldb, C, ldc, e);
+      if (ph_gemm) gemm8p_kernel<E, AK, BKc, OutT><<<grid, NT2, 0, st>>>(M, N, K, A, lda, B, ldb, C, ldc, e, K, 0, 0);
+    } else if (plan == PLAN_8P_SPLITK) {
+      if (ph_gemm)
+        gemm8p_kernel<E, AK, BKc, float><<<grid, NT2, 0, st>>>(M, N, K, A, lda, B, ldb, ws, N, e, klen, ss, 1);
+      if (ph_red) splitk_reduce_kernel<OutT><<<reduce_blocks(M, N), 256, 0, st>>>(M, N, nsplit, ws, ss, C, ldc, e);
     } else if (plan == PLAN_256) {
       if (ph_gemm)
         gemm256_kernel<E, AK, BKc, OutT, 0, kNA><<<grid, NT2, 0, st>>>(M, N, K, A, lda, B, ldb, C, ldc, e, klen, 0, 0, nullptr,
@@ -981,7 +1086,8 @@ extern "C" long cmhar_gemm_bf16_ws(int M, int N, int K) {
 }
 
 // The kernel plan of a cmhar_gemm_bf16 call with these arguments (GemmPlan: 0 = 128² tile, 1 = 256² tile, 2 = 256²
-// + tail split + reduce, 3 = 256² split-K + reduce, 4 = 8-phase 256², 5 = 128² split-K + reduce), -1 on a bad layout.
+// + tail split + reduce, 3 = 256² split-K + reduce, 4 = 8-phase 256², 5 = 128² split-K + reduce, 6 = 8-phase 256²
+// split-K + reduce), -1 on a bad layout.
 extern "C" int cmhar_gemm_bf16_plan(int layout, int M, int N, int K, int splits, int has_ws, int rowsum) {
   if (layout < 0 || layout > 2) return -1;
   return gemm_plan(layout != 2, layout == 0, M, N, K, splits, has_ws != 0, rowsum != 0);

@@ -64,7 +64,8 @@ int cmhar_gemm_bf16(int layout, int out_dtype, int M, int N, int K, const void* 
 long cmhar_gemm_bf16_ws(int M, int N, int K);
 /* The kernel plan cmhar_gemm_bf16 would run for these arguments (has_ws: ws != NULL; rowsum: epi->rowsum set):
  * 0 = 128² tile, 1 = 256² tile, 2 = 256² + tail split + reduce, 3 = 256² split-K + reduce, 4 = 8-phase 256²
- * (forward layout), 5 = 128² split-K + reduce; -1 = bad layout.  Used for trace labels (bench.py kernel breakdown). */
+ * (forward / weight-gradient layouts), 5 = 128² split-K + reduce, 6 = 8-phase 256² split-K + reduce (weight
+ * gradients); -1 = bad layout.  Used for trace labels (bench.py kernel breakdown). */
 int cmhar_gemm_bf16_plan(int layout, int M, int N, int K, int splits, int has_ws, int rowsum);
 /* cmhar_gemm_bf16 restricted to a phase mask: bit 0 = the GEMM kernel, bit 1 = the split-K / tail reduce (3 = the
  * whole call).  Calling phases 1 then 2 on one stream equals one cmhar_gemm_bf16 call; bench.py uses the split to

@@ -197,6 +197,33 @@ def test_wgrad_fused_bias_rowsum_exact(splits, beta):
     assert torch.equal(db, dy.float().sum(0) + 2.0 * beta)
 
 
+def test_wgrad_8phase_bit_identical_to_two_phase(tmp_path):
+    """The weight-gradient GEMM on the 8-phase schedule (plans 4 / 6) against the two-phase gemm256_kernel (plans 1 /
+    3): same per-output accumulation order, so every dW and fused bias gradient must be bit-identical (worker:
+    tests/wgrad8p_worker.py, one process per kernel choice)."""
+    import os
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+    def run(v):
+        out = tmp_path / f'w{v}.pt'
+        env = dict(os.environ, CMHAR_GEMM_8P_WGRAD=str(v), CMHAR_AB_OUT=str(out))
+        p = subprocess.run([sys.executable, '-u', os.path.join(repo, 'tests', 'wgrad8p_worker.py')], env=env,
+                           stdout=subprocess.PIPE, stderr=subprocess.STDOUT, timeout=100)
+        assert p.returncode == 0, p.stdout.decode(errors='replace')[-4000:]
+        return torch.load(out, weights_only=True)
+
+    a, b = run(1), run(0)
+    assert a.keys() == b.keys()
+    for k in a:
+        if k.startswith('plan'):
+            assert a[k].item() in (4, 6) and b[k].item() in (1, 3), (k, a[k].item(), b[k].item())
+            continue
+        assert torch.isfinite(a[k]).all(), k
+        assert torch.equal(a[k], b[k]), (k, (a[k] - b[k]).abs().max().item())
+
+
 def test_wgrad_bias_fallback_shapes():
     """Shapes off the 256-tile path get the bias gradient from the column-sum kernel instead."""
     torch.manual_seed(5)
