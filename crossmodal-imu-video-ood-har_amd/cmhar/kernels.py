@@ -161,10 +161,12 @@ def _tail_ws(M, N, K):
 # ------------------------------------------------------------------------------------------------------------
 def gemm(layout: int, a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, *, bias=None, residual=None,
          aux_in=None, aux_out=None, rowadd=None, rowadd_mod=1, act=L.ACT_NONE, alpha=1.0, beta=0.0, splits=None,
-         pdrop=0.0, seed=0, rowsum=None, rowsum_beta=0.0, colscale=None):
+         pdrop=0.0, seed=0, rowsum=None, rowsum_beta=0.0, colscale=None, reduce_stream=None):
     """layout 0: out[M,N] = a[M,K]·b[N,K]ᵀ;  1: a[M,K]·b[K,N];  2: a[K,M]ᵀ·b[K,N].
     rowsum (layout 2, bf16, 256-tile shapes): rowsum[m] = Σ_k a[k,m] + rowsum_beta·rowsum[m] (bias gradient).
-    colscale (lo, hi, s): columns [lo, hi) (multiples of 8) of the product + bias scaled by s before the activation."""
+    colscale (lo, hi, s): columns [lo, hi) (multiples of 8) of the product + bias scaled by s before the activation.
+    reduce_stream (bf16 split-K plans): the split-K reduce (which writes `out` / `rowsum`) runs on that stream, after
+    the GEMM kernel, from a partial-slab buffer of its own; the caller orders its readers of `out` after that stream."""
     for t, n in ((a, 'A'), (b, 'B'), (out, 'C')):
         _check_2d(t, n)
     if layout == 0:
@@ -237,7 +239,10 @@ def gemm(layout: int, a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, *, bi
             raise TypeError('out dtype')
         s = _splits_for(M, N, K) if splits is None else splits
         ws = None
-        if s > 1:
+        if s > 1 and reduce_stream is not None:
+            # slabs of their own (the stream-ordered caching allocator keeps them until the reduce stream is done)
+            ws = torch.empty(s * M * N + (s * M if rowsum is not None else 0), dtype=torch.float32, device=out.device)
+        elif s > 1:
             ws = workspace(s * M * N + (s * M if rowsum is not None else 0), out.device)
         elif splits is None and rowsum is None:
             n = _tail_ws(M, N, K)
@@ -247,7 +252,14 @@ def gemm(layout: int, a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, *, bi
         if TRACE.active:
             name = _gemm_trace_name(layout, M, N, K, s, ws is not None, rowsum is not None, out.dtype)
             ev = TRACE.begin(name)
-        if ev is None:
+        if ev is None and reduce_stream is not None and s > 1:
+            args = (layout, L.dtype_code(out.dtype), M, N, K, ptr(a), a.stride(0), ptr(b), b.stride(0), ptr(out),
+                    out.stride(0), C.byref(epi), s, ptr(ws))
+            call('cmhar_gemm_bf16_phased', *args, st, 1)
+            reduce_stream.wait_stream(torch.cuda.current_stream(out.device))
+            call('cmhar_gemm_bf16_phased', *args, reduce_stream.cuda_stream, 2)
+            ws.record_stream(reduce_stream)
+        elif ev is None:
             call('cmhar_gemm_bf16', layout, L.dtype_code(out.dtype), M, N, K, ptr(a), a.stride(0), ptr(b),
                  b.stride(0), ptr(out), out.stride(0), C.byref(epi), s, ptr(ws), st)
         else:
@@ -300,17 +312,17 @@ def rowsum_supported(layout, dtype, M, N, K):
     return layout == 2 and dtype == torch.bfloat16 and M % 256 == 0 and N % 256 == 0 and K % 64 == 0
 
 
-def linear_wgrad(dy, x, *, out=None, beta=0.0, bias_out=None, bias_beta=0.0):
+def linear_wgrad(dy, x, *, out=None, beta=0.0, bias_out=None, bias_beta=0.0, reduce_stream=None):
     """dW[N,K] (fp32) = dyᵀ·x;  bias_out[N] (fp32, optional) = Σ_m dy[m, :] (+ bias_beta·bias_out).
     The bias gradient rides on the wgrad GEMM's own MFMA operand tiles when the shape allows it, else it is a
-    separate column-sum launch."""
+    separate column-sum launch.  reduce_stream: see gemm()."""
     N, K = dy.shape[1], x.shape[1]
     if out is None:
         out = torch.empty(N, K, dtype=torch.float32, device=dy.device)
     if bias_out is not None and not rowsum_supported(2, dy.dtype, N, K, dy.shape[0]):
         colsum(dy, bias_out, beta=bias_beta)
         bias_out = None
-    return gemm(2, dy, x, out, beta=beta, rowsum=bias_out, rowsum_beta=bias_beta)
+    return gemm(2, dy, x, out, beta=beta, rowsum=bias_out, rowsum_beta=bias_beta, reduce_stream=reduce_stream)
 
 
 def colsum(x, out=None, *, alpha=1.0, beta=0.0):

@@ -324,6 +324,10 @@ def _forward_impl(m: VideoMAEBackbone, video: torch.Tensor, save: bool, token0_o
 
 
 _WGRAD_STREAMS = {}
+# backward's weight-gradient stream use (module attribute `overlap_wgrad` overrides): '0' (default) = all on the main
+# stream, '1' = whole weight-gradient GEMMs on the side stream, 'reduce' = only their split-K reduces there (measured
+# at B = 32, alternated runs on one box: 683.1 / 682.3 clips/s all-main vs 679.5 / 678.6 reduces-on-side)
+_OVERLAP_WGRAD = {'1': True, 'reduce': 'reduce'}.get(os.environ.get('CMHAR_OVERLAP_WGRAD', '0'), False)
 
 
 def _wgrad_stream(dev):
@@ -345,8 +349,12 @@ def _backward_impl(m: VideoMAEBackbone, st, dx, sink, overlap_wgrad=True):
     # idle; parameter groups are then declared final (gradient bucket all-reduce) from that stream, after it has
     # caught up with the main stream's LayerNorm gradients.  Measured on MI355X at B=32: no gain (the two GEMMs
     # slow each other through shared L2), so it is off by default.
+    # overlap_wgrad = 'reduce': the weight-gradient GEMMs stay on the main stream and only their split-K
+    # reduces (memory-bound, off the critical path: nothing in the backward reads dW) go to the side stream, from
+    # partial slabs of their own; parameter groups are declared final from the side stream as above.
     cur = torch.cuda.current_stream(dev)
     side = _wgrad_stream(dev) if overlap_wgrad else cur
+    reduce_only = overlap_wgrad == 'reduce'
 
     def wgrad(params, dy, x, shape, bias=None):
         """Weight gradient GEMM; the bias gradient (Σ_tokens dy) rides on the same GEMM's MFMA operand tiles."""
@@ -354,8 +362,9 @@ def _backward_impl(m: VideoMAEBackbone, st, dx, sink, overlap_wgrad=True):
         bout, bbeta = (None, 0.0)
         if bias:
             bout, bbeta = sink.dest(bias, (sum(q.numel() for q in bias),), dev)
-        if side is cur:
-            K.linear_wgrad(dy, x, out=out, beta=beta, bias_out=bout, bias_beta=bbeta)
+        if side is cur or reduce_only:
+            K.linear_wgrad(dy, x, out=out, beta=beta, bias_out=bout, bias_beta=bbeta,
+                           reduce_stream=side if reduce_only else None)
             return
         side.wait_stream(cur)
         with torch.cuda.stream(side):
@@ -502,7 +511,7 @@ class _BackboneFn(torch.autograd.Function):
             dx = torch.empty(M, Hd, dtype=dt, device=gout.device)
             K.copy2d(gout.view(M, Hd), dx)
         sink = getattr(m, '_grad_sink', None) or AutogradSink()
-        _backward_impl(m, st, dx, sink, overlap_wgrad=getattr(m, "overlap_wgrad", False))
+        _backward_impl(m, st, dx, sink, overlap_wgrad=getattr(m, "overlap_wgrad", _OVERLAP_WGRAD))
         ctx.st = None
         out = [None, None, None]
         for p in ctx.params:

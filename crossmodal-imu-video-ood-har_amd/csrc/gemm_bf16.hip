@@ -972,7 +972,13 @@ static bool use_8p() {
 #ifndef CMHAR_GEMM_8P_DGRAD
 #define CMHAR_GEMM_8P_DGRAD 0
 #endif
-static bool use_8p_dgrad() { return CMHAR_GEMM_8P_DGRAD != 0; }
+static bool use_8p_dgrad() {
+  static const bool v = [] {
+    const char* s = getenv("CMHAR_GEMM_8P_DGRAD");
+    return s ? atoi(s) != 0 : CMHAR_GEMM_8P_DGRAD != 0;
+  }();
+  return v;
+}
 
 // The weight-gradient layout (both operands row-contraction, split-K, fused bias gradient) on the 8-phase schedule;
 // CMHAR_GEMM_8P_WGRAD=0/1 overrides the build default (A/B measurements; the two kernels give identical bits).
