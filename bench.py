@@ -98,6 +98,11 @@ def mfma_util(label, path=MFMA_JSON):
             'effective_clock_ghz': hits[0].get('effective_clock_ghz'), 'source': src}
 
 
+def _videomae_overlap():
+    from cmhar import videomae
+    return bool(videomae._OVERLAP_WGRAD)
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
@@ -464,17 +469,24 @@ def main():
     # Warm-up; its last step runs with every GEMM / attention launch bracketed by HIP events, which gives the
     # per-kernel-family breakdown and picks the dominant single kernel.  The timed loop then brackets ONLY that
     # kernel's launches (the events of all ~180 traced launches cost ~1.5 ms/step of stream bubbles).
+    # The traced warm-up step runs the backward's weight gradients on the main stream (overlap_wgrad off): its
+    # per-kernel times are then each kernel alone on the chip, not shares of two concurrent streams.
     breakdown = {}
     loss = None
+    bb = getattr(getattr(W.model, 'video_encoder', None), 'backbone', None)
     for i in range(args.warmup):
         full = trace and i == args.warmup - 1
         if full:
             K.TRACE.records, K.TRACE.only, K.TRACE.active = [], None, True
+            if bb is not None:
+                bb.overlap_wgrad = False
         loss = step()
         if full:
             torch.cuda.synchronize()
             K.TRACE.active = False
             breakdown = K.TRACE.summary()
+            if bb is not None:
+                del bb.overlap_wgrad
     torch.cuda.synchronize()
     first_loss = float(loss.float().mean().item()) if loss is not None else float('nan')
     # every traced label is one kernel symbol except the two-kernel attention backward entry
@@ -512,7 +524,9 @@ def main():
 
     # dominant kernel: the single HIP kernel with the largest traced time in the traced warm-up step (split-K GEMMs
     # are traced without their reduce launch); achieved = its algorithmic FLOPs / its HIP-event-measured time over
-    # the timed region
+    # the timed region.  In the timed region the backward's weight gradients run on a second stream, so a backward
+    # kernel's launch duration there is its share of a chip it splits with the other stream; `isolated_*` is the same
+    # kernel in the serial traced warm-up step.
     roof = None
     summ = K.TRACE.summary() if trace else {}
     if dominant in summ:
@@ -525,6 +539,13 @@ def main():
                 'kernel': name,
                 'launches': n, 'avg_launch_ms': round(tot_ms / n, 4),
                 'algorithmic_bytes_per_launch': int(nb / n)}
+        if name in breakdown:
+            bn_, btm, bfl, _ = breakdown[name]
+            iso = bfl / (btm / 1e3) / 1e12
+            roof.update({'isolated_avg_launch_ms': round(btm / bn_, 4), 'isolated_achieved': round(iso, 1),
+                         'isolated_frac': round(iso / PEAK_BF16_TFLOPS, 4),
+                         'concurrent_streams': 'backward weight gradients on a second stream'
+                         if bb is not None and _videomae_overlap() else None})
         mf = mfma_util(name, args.mfma_json)
         if mf is not None:
             roof['mfma_util'] = mf

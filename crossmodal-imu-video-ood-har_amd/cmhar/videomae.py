@@ -324,10 +324,12 @@ def _forward_impl(m: VideoMAEBackbone, video: torch.Tensor, save: bool, token0_o
 
 
 _WGRAD_STREAMS = {}
-# backward's weight-gradient stream use (module attribute `overlap_wgrad` overrides): '0' (default) = all on the main
-# stream, '1' = whole weight-gradient GEMMs on the side stream, 'reduce' = only their split-K reduces there (measured
-# at B = 32, alternated runs on one box: 683.1 / 682.3 clips/s all-main vs 679.5 / 678.6 reduces-on-side)
-_OVERLAP_WGRAD = {'1': True, 'reduce': 'reduce'}.get(os.environ.get('CMHAR_OVERLAP_WGRAD', '0'), False)
+# backward's weight-gradient stream use (module attribute `overlap_wgrad` overrides): '1' (default) = the weight-
+# gradient GEMMs (+ their split-K reduces) on the side stream, '0' = all on the main stream, 'reduce' = only the
+# split-K reduces on the side stream.  Measured at B = 32, alternated runs on one box: with the 8-phase weight-gradient
+# kernel 682.5 / 681.4 clips/s side stream vs 675.0 / 675.2 all-main; 'reduce' 679.5 / 678.6 vs 683.1 / 682.3
+# all-main on another box (with the two-phase kernel the side stream had measured no gain).
+_OVERLAP_WGRAD = {'0': False, 'reduce': 'reduce'}.get(os.environ.get('CMHAR_OVERLAP_WGRAD', '1'), True)
 
 
 def _wgrad_stream(dev):
@@ -347,8 +349,7 @@ def _backward_impl(m: VideoMAEBackbone, st, dx, sink, overlap_wgrad=True):
     # Optionally (module attribute `overlap_wgrad`) the weight gradients (dW = dYᵀX, split-K), which do not feed the
     # rest of the backward, run on their own stream so their workgroups can fill CUs the critical-path kernels leave
     # idle; parameter groups are then declared final (gradient bucket all-reduce) from that stream, after it has
-    # caught up with the main stream's LayerNorm gradients.  Measured on MI355X at B=32: no gain (the two GEMMs
-    # slow each other through shared L2), so it is off by default.
+    # caught up with the main stream's LayerNorm gradients (default: see _OVERLAP_WGRAD for the measurements).
     # overlap_wgrad = 'reduce': the weight-gradient GEMMs stay on the main stream and only their split-K
     # reduces (memory-bound, off the critical path: nothing in the backward reads dW) go to the side stream, from
     # partial slabs of their own; parameter groups are declared final from the side stream as above.

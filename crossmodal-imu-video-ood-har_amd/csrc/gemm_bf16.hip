@@ -699,6 +699,10 @@ struct DmaHalf {
   }
 };
 
+#ifndef CMHAR_GEMM8P_ABLATE
+#define CMHAR_GEMM8P_ABLATE 0
+#endif
+
 // The weight-gradient A operand (dYᵀ: [k][m], m contiguous) on the 8-phase schedule, staged in COLUMN halves: the
 // schedule hands A's half h (rows 128h.. of the output tile) to wave group h only, so each half is its own
 // [64 k][128 m] image at h * 16 KiB (256-B rows, the mc_off swizzle, whose XOR never leaves a half's 16 chunks); a
@@ -889,6 +893,17 @@ __global__ __launch_bounds__(NT2, 2) void gemm8p_kernel(int M, int N, int K, con
       }
   }
   __syncthreads();
+#if CMHAR_GEMM8P_ABLATE == 1   // ablation build (tools/debug): K loop only, every accumulator kept live
+  {
+    float t = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) t += acc[i][j][0] + acc[i][j][1] + acc[i][j][2] + acc[i][j][3];
+    if (t == 1234.5f) ((float*)C)[tid] = t;
+    return;
+  }
+#endif
 
   // epilogue: as gemm256_kernel — per wave, two passes of 64x64 through a private LDS slab, 16-B stores
   float* T = (float*)(smem + wave * 64 * EPI2_LD * 4);
@@ -909,7 +924,9 @@ __global__ __launch_bounds__(NT2, 2) void gemm8p_kernel(int M, int N, int K, con
       const int rr = it * 8 + (lane >> 3);
       const int m = bm + wr * 128 + pass * 64 + rr;
       const floatx4 lo = *(const floatx4*)&T[rr * EPI2_LD + cg], hi = *(const floatx4*)&T[rr * EPI2_LD + cg + 4];
-      if (raw_out) {
+      if (CMHAR_GEMM8P_ABLATE == 2) {   // ablation build: LDS staging + read-back, no global stores
+        if (lo[0] + hi[3] == 1234.5f) ((float*)C)[tid] = lo[1];
+      } else if (raw_out) {
         float* dst = (float*)C + (long)m * ldc + n0;
         *(floatx4*)dst = lo;
         *(floatx4*)(dst + 4) = hi;
