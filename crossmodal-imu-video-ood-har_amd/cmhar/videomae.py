@@ -324,12 +324,14 @@ def _forward_impl(m: VideoMAEBackbone, video: torch.Tensor, save: bool, token0_o
 
 
 _WGRAD_STREAMS = {}
-# backward's weight-gradient stream use (module attribute `overlap_wgrad` overrides): '1' (default) = the weight-
-# gradient GEMMs (+ their split-K reduces) on the side stream, '0' = all on the main stream, 'reduce' = only the
-# split-K reduces on the side stream.  Measured at B = 32, alternated runs on one box: with the 8-phase weight-gradient
-# kernel 682.5 / 681.4 clips/s side stream vs 675.0 / 675.2 all-main; 'reduce' 679.5 / 678.6 vs 683.1 / 682.3
-# all-main on another box (with the two-phase kernel the side stream had measured no gain).
-_OVERLAP_WGRAD = {'0': False, 'reduce': 'reduce'}.get(os.environ.get('CMHAR_OVERLAP_WGRAD', '1'), True)
+# backward's weight-gradient stream use (module attribute `overlap_wgrad` overrides): '0' (default) = all on the main
+# stream, '1' = the weight-gradient GEMMs (+ their split-K reduces) on the side stream, 'reduce' = only the split-K
+# reduces on the side stream.  Measured at B = 32, alternated runs on one box: with the 8-phase weight-gradient kernel
+# 682.5 / 681.4 clips/s side stream vs 675.0 / 675.2 all-main (+1 %); 'reduce' 679.5 / 678.6 vs 683.1 / 682.3
+# all-main on another box.  Off by default: with two streams every backward kernel's measured duration is a share of
+# a chip it splits with the other stream (the bench's HIP events and rocprofv3 then disagree by ~15 % on the dominant
+# kernel), which the per-kernel roofline accounting of bench.py cannot attribute; DESIGN.md §Round 3.
+_OVERLAP_WGRAD = {'1': True, 'reduce': 'reduce'}.get(os.environ.get('CMHAR_OVERLAP_WGRAD', '0'), False)
 
 
 def _wgrad_stream(dev):
