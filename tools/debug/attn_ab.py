@@ -20,6 +20,9 @@ from gemm_ab import load, timed  # noqa: E402
 def main():
     args = sys.argv[1:]
     rounds = 7
+    prescaled = '--prescaled' in args      # the bf16 training path's scale (c = scale·log2e = 1, pre-scaled keys)
+    if prescaled:
+        args.remove('--prescaled')
     if '--rounds' in args:
         i = args.index('--rounds')
         rounds = int(args[i + 1])
@@ -35,7 +38,7 @@ def main():
     do = torch.randn(B * L, H * D, device='cuda', generator=g).bfloat16()
     dqkv = torch.empty_like(qkv)
     dq, dk, dv = dqkv[:, :H * D], dqkv[:, H * D:2 * H * D], dqkv[:, 2 * H * D:]
-    sc = D ** -0.5
+    sc = 1.0 / K.LOG2E if prescaled else D ** -0.5
     fl = 4 * B * H * L * L * D
     cases = [('fwd', 1.0, lambda: K.attention_fwd(q, k, v, o, lse, B=B, H=H, Lq=L, Lk=L, D=D, scale=sc), lambda: o),
              ('bwd', 2.5, lambda: K.attention_bwd(q, k, v, o, do, lse, dq, dk, dv, B=B, H=H, Lq=L, Lk=L, D=D,
@@ -54,6 +57,7 @@ def main():
             torch.cuda.synchronize()
             outs.append(res().clone())
         same = [torch.equal(outs[0], x) for x in outs[1:]]
+        diff = [((outs[0].float() - x.float()).norm() / outs[0].float().norm()).item() for x in outs[1:]]
         ts = [[] for _ in range(nv)]
         for _ in range(rounds):
             for vi in range(nv):
@@ -62,7 +66,7 @@ def main():
         med = [statistics.median(t) for t in ts]
         cols = ' | '.join(f'{chr(65 + vi)} {med[vi] * 1e3:7.1f} us {mult * fl / med[vi] / 1e9:5.0f} TF'
                           for vi in range(nv))
-        print(f'{tag} {cols} | bitwise-equal-to-A={same}', flush=True)
+        print(f'{tag} {cols} | bitwise-equal-to-A={same} rel-diff-to-A={["%.2e" % d for d in diff]}', flush=True)
 
 
 if __name__ == '__main__':
