@@ -1,4 +1,4 @@
-"""Which Python call sites issue torch ops (aten::fill_ / zero_ / copy_ …) inside one bench training step:
+"""(Used in round 3 to check which torch ops a bench step still issues — DESIGN.md §Round 3.)  Which Python call sites issue torch ops (aten::fill_ / zero_ / copy_ …) inside one bench training step:
 torch.profiler CPU activity with Python stacks over one warm step of bench.py's headline workload."""
 import collections
 import os
