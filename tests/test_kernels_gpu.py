@@ -423,7 +423,7 @@ def test_attention_fp32_dropout_consistent():
 # norms / small ops
 # ---------------------------------------------------------------------------------------------------------------
 @pytest.mark.parametrize('dt', [torch.float32, torch.bfloat16])
-@pytest.mark.parametrize('N', [768, 128])
+@pytest.mark.parametrize('N', [768, 128, 256, 1024])
 def test_layernorm_fwd_bwd(dt, N):
     torch.manual_seed(5)
     M = 333
@@ -437,6 +437,9 @@ def test_layernorm_fwd_bwd(dt, N):
     ref = torch.nn.functional.layer_norm(xr, (N,), gr, br, eps)
     tol = 1e-5 if dt == torch.float32 else 8e-3
     assert rel(y, ref) < tol
+    x64 = x.double()
+    assert rel(mu, x64.mean(1)) < 1e-6
+    assert rel(rs, 1 / (x64.var(1, unbiased=False) + eps).sqrt()) < 1e-5
     dy = torch.randn(M, N, device=DEV).to(dt)
     dres = torch.randn(M, N, device=DEV).to(dt)
     gx, gg, gb = torch.autograd.grad(ref, (xr, gr, br), dy.float())
