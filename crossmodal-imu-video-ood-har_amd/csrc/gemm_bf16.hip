@@ -100,6 +100,14 @@ __device__ __forceinline__ void load8(const OutT* __restrict__ p, float (&x)[8])
     for (int j = 0; j < 4; ++j) { x[j] = a[j]; x[4 + j] = b[j]; }
   }
 }
+// 16-bit epilogue outputs (C and aux_out) are stored non-temporal: written once, read by a later kernel, they no
+// longer displace this GEMM's operand panels from L2.  Measured in the bench step (tools/debug/lib_step_ab.sh,
+// alternated on one box): 684.2 / 685.4 -> 700.0 / 701.6 clips/s (QKV forward 206 -> 192 us, FC1 forward 363 -> 338);
+// bit-identical outputs.  The same for the 8-phase kernel's fp32 split-K slabs (re-read by the reduce) was slower
+// (693 clips/s), and for the bf16 Vec8 stores of the norm / elementwise kernels neutral.  CMHAR_NT_STORE=0: plain.
+#ifndef CMHAR_NT_STORE
+#define CMHAR_NT_STORE 1
+#endif
 template <typename OutT>
 __device__ __forceinline__ void store8(OutT* __restrict__ p, const float (&x)[8]) {
   if constexpr (sizeof(OutT) == 2) {
@@ -107,7 +115,12 @@ __device__ __forceinline__ void store8(OutT* __restrict__ p, const float (&x)[8]
     v8 v;
 #pragma unroll
     for (int j = 0; j < 8; ++j) v[j] = (OutT)x[j];
-    *(v8*)p = v;
+    if (CMHAR_NT_STORE) {
+      typedef int __attribute__((ext_vector_type(4))) i4;
+      __builtin_nontemporal_store(__builtin_bit_cast(i4, v), (i4*)p);
+    } else {
+      *(v8*)p = v;
+    }
   } else {
     *(floatx4*)p = floatx4{x[0], x[1], x[2], x[3]};
     *(floatx4*)(p + 4) = floatx4{x[4], x[5], x[6], x[7]};
