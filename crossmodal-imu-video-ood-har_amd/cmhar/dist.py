@@ -144,10 +144,14 @@ class GradReducer:
     first waits on every one of those streams, and `finish()` makes the caller's stream wait on the collectives
     before the reduced values are copied back into `.grad`."""
 
-    def __init__(self, model: torch.nn.Module, backbone=None, bucket_mb: float = 32.0, group=None):
+    def __init__(self, model: torch.nn.Module, backbone=None, bucket_mb: float = 32.0, group=None,
+                 reduce_single: bool = False):
         self.model = model
         self.group = group
         self.world = world_size(group)
+        # reduce_single: run the whole bucket / hook / collective protocol even in a one-rank group (a SUM over one
+        # rank is the identity) — exercises the RCCL path on a one-GPU machine, where two ranks cannot share the GPU
+        self._reduce = self.world > 1 or (reduce_single and dist.is_initialized())
         self.sink = None
         self.pending = []
         self.active = False
@@ -176,8 +180,9 @@ class GradReducer:
         self._fired = []                            # hook firing order of the current step (learning step only)
         self._comm = None
         self.launched_before_finish = 0             # buckets in flight when backward returned (last step)
+        self.n_collectives = 0                      # all-reduces issued (last step)
         self._hooks = []
-        if self.world > 1:
+        if self._reduce:
             for p in self.rest:
                 self._hooks.append(p.register_post_accumulate_grad_hook(self._on_hook))
 
@@ -205,7 +210,7 @@ class GradReducer:
         self._launch_ready()
 
     def _on_sink_ready(self, params):
-        if self.world == 1:
+        if not self._reduce:
             return
         for p in params:
             self._mark(p)
@@ -233,6 +238,7 @@ class GradReducer:
     def _launch(self, b: _Bucket):
         if b.kind == 'sink':
             self.pending.append(dist.all_reduce(self.sink.flat[b.start:b.end], group=self.group, async_op=True))
+            self.n_collectives += 1
         else:
             live = [p for p in b.params if p.grad is not None]
             b.live = live
@@ -258,6 +264,7 @@ class GradReducer:
             b.flat = torch.empty(n, dtype=torch.float32, device=dev)
         torch.cat([p.grad.reshape(-1).float() for p in live], out=b.flat)
         self.pending.append(dist.all_reduce(b.flat, group=self.group, async_op=True))
+        self.n_collectives += 1
 
     # -- step protocol ---------------------------------------------------------------------------------------
     def start_step(self):
@@ -265,14 +272,15 @@ class GradReducer:
             b.ready, b.launched, b.live, b.streams = set(), False, None, {}
         self._next = 0
         self.pending = []
+        self.n_collectives = 0
         self._fired = []
-        self.active = self.world > 1
+        self.active = self._reduce
 
     def finish(self):
         """Call after loss.backward(): launches the buckets that never filled (parameters without a gradient),
         waits for every all-reduce and writes the hook buckets' reduced values back into `.grad`."""
         self.active = False
-        if self.world == 1:
+        if not self._reduce:
             return
         self.launched_before_finish = self._next
         for b in self.buckets[self._next:]:

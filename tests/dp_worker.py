@@ -174,6 +174,10 @@ def main():
     out_dir = os.environ['CMHAR_DP_OUT']
     rank, world, _ = D.init_from_env(os.environ.get('CMHAR_DP_BACKEND', 'gloo'))
     torch.cuda.set_device(0)
+    force = os.environ.get('CMHAR_DP_FORCE_REDUCE') == '1'
+    if world == 1 and not dist.is_initialized():
+        # one rank over RCCL: the reducer runs its full protocol (GradReducer(reduce_single=True))
+        dist.init_process_group(os.environ.get('CMHAR_DP_BACKEND', 'gloo'), rank=0, world_size=1)
     dev = torch.device('cuda', 0)
     if backbone == 'classify':
         return classify(D, rank, world, dev, out_dir)
@@ -190,7 +194,8 @@ def main():
             for p in model.parameters():
                 p.add_(0.5)
     D.broadcast_parameters(model)
-    reducer = D.GradReducer(model, backbone=model.video_encoder.backbone, bucket_mb=0.25 if backbone == 'videomae' else 8.0)
+    reducer = D.GradReducer(model, backbone=model.video_encoder.backbone,
+                            bucket_mb=0.25 if backbone == 'videomae' else 8.0, reduce_single=force)
     loss_fn = SigmoidContrastiveLoss().to(dev)
     sl = slice(rank * bl, (rank + 1) * bl)
     for step in range(2):                # step 0 teaches the reducer the hook order; step 1 is the one checked
@@ -203,6 +208,7 @@ def main():
     torch.cuda.synchronize()
     grads = {n: p.grad.detach().cpu() for n, p in model.named_parameters() if p.grad is not None}
     res = {'rank': rank, 'loss': float(loss.item()), 'n_buckets': len(reducer.buckets),
+           'backend': dist.get_backend(), 'n_collectives': reducer.n_collectives,
            'sink': reducer.sink is not None, 'n_grads': len(grads), 'learned': reducer.learned,
            'launched_before_finish': reducer.launched_before_finish,
            'trailing_unused': [n for n, p in model.named_parameters()
