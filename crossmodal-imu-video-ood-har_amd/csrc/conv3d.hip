@@ -20,6 +20,22 @@ template <typename T, int V> __device__ __forceinline__ void vstore(T* p, const 
   if constexpr (V == 8) Vec8<T>::store(p, v);
   else for (int j = 0; j < V; ++j) p[j] = from_f<T>(v[j]);
 }
+// conv epilogue output (8 bf16), non-temporal as the GEMM epilogues (R3D-18 step 1659 / 1662 -> 1672 / 1671 clips/s,
+// tools/debug/lib_workload_ab.sh); CMHAR_CONV_NT=0: plain stores
+#ifndef CMHAR_CONV_NT
+#define CMHAR_CONV_NT 1
+#endif
+__device__ __forceinline__ void zstore8(bf16* p, const float* v) {
+  if (CMHAR_CONV_NT) {
+    bf16x8 r;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) r[j] = (bf16)v[j];
+    typedef int __attribute__((ext_vector_type(4))) i4;
+    __builtin_nontemporal_store(__builtin_bit_cast(i4, r), (i4*)p);
+  } else {
+    Vec8<bf16>::store(p, v);
+  }
+}
 
 struct Geom {
   int N, T, H, W, C;
@@ -1237,7 +1253,7 @@ __global__ __launch_bounds__(256, 2) void conv3d_fwd_rows(Geom g, int M, int Cou
 #pragma unroll
       for (int j = 0; j < 8; ++j) v[j] += q[j];
     }
-    vstore<bf16, 8>(z + (long)m * Cout + bn + cg, v);
+    zstore8(z + (long)m * Cout + bn + cg, v);
   }
   if (tstats) {
     // one statistics column per (128-row half, Cout column)
@@ -1385,7 +1401,7 @@ __global__ __launch_bounds__(256, 2) void conv3d_fwd_rows3(Geom g, int R, int Ls
 #pragma unroll
       for (int j = 0; j < 8; ++j) v[j] += q[j];
     }
-    vstore<bf16, 8>(z + m * TN + cg, v);
+    zstore8(z + m * TN + cg, v);
   }
   if (tstats)
     tile_col_stats<NT>(TN, (float*)(smem + 256 * ELD * 4), tid, [&](int c, int r) { return T[r * ELD + c]; },
@@ -1490,7 +1506,7 @@ __global__ __launch_bounds__(256, 2) void conv3d_stem_fwd(Geom g, int R, int cpf
     float v[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) v[j] = T[rr * ELD + cg + j];
-    vstore<bf16, 8>(z + (m0 + rr) * 64 + cg, v);
+    zstore8(z + (m0 + rr) * 64 + cg, v);
   }
   if (tstats)
     tile_col_stats<256>(64, (float*)(smem + 256 * ELD * 4), tid, [&](int c, int r) { return T[r * ELD + c]; },
