@@ -87,11 +87,20 @@ __device__ __forceinline__ bf16x8 frag(const char* lds, int r0, int kk, int lane
 
 
 // 8 consecutive elements of an OutT row as fp32 / back, with single 16-B (bf16) or 2 x 16-B (fp32) accesses.
+// The epilogue's streamed 16-bit operands (aux_in, residual: each element read once) and the split-K reduce's slabs
+// are loaded non-temporal, like the outputs are stored: step 696.8 / 696.5 -> 700.1 / 701.4 clips/s with both
+// (tools/debug/lib_step_ab.sh, alternated on one box; each alone half of that).  CMHAR_NT_EPI_LOAD /
+// CMHAR_NT_REDUCE_LOAD = 0: plain loads.
+#ifndef CMHAR_NT_EPI_LOAD
+#define CMHAR_NT_EPI_LOAD 1
+#endif
 template <typename OutT>
-__device__ __forceinline__ void load8(const OutT* __restrict__ p, float (&x)[8]) {
+__device__ __forceinline__ void load8(const OutT* __restrict__ p, float (&x)[8], bool nt = false) {
   if constexpr (sizeof(OutT) == 2) {
     typedef OutT __attribute__((ext_vector_type(8))) v8;
-    const v8 v = *(const v8*)p;
+    typedef int __attribute__((ext_vector_type(4))) i4;
+    const v8 v = (CMHAR_NT_EPI_LOAD && nt) ? __builtin_bit_cast(v8, __builtin_nontemporal_load((const i4*)p))
+                                           : *(const v8*)p;
 #pragma unroll
     for (int j = 0; j < 8; ++j) x[j] = (float)v[j];
   } else {
@@ -159,11 +168,11 @@ __device__ __forceinline__ void epilogue_store8(const Epilogue& e, OutT* __restr
 #pragma unroll
     for (int j = 0; j < 8; ++j) x[j] = fmaxf(x[j], 0.f);
   } else if (e.act == ACT_DGELU) {
-    load8<OutT>((const OutT*)e.aux_in + (long)m * e.lda + n0, t);
+    load8<OutT>((const OutT*)e.aux_in + (long)m * e.lda + n0, t, true);
 #pragma unroll
     for (int j = 0; j < 8; ++j) x[j] *= gelu_grad_for<OutT>(t[j]);
   } else if (e.act == ACT_DRELU) {
-    load8<OutT>((const OutT*)e.aux_in + (long)m * e.lda + n0, t);
+    load8<OutT>((const OutT*)e.aux_in + (long)m * e.lda + n0, t, true);
 #pragma unroll
     for (int j = 0; j < 8; ++j) x[j] = t[j] > 0.f ? x[j] : 0.f;
   } else if (e.act == ACT_GELU_SAVEGRAD) {
@@ -171,7 +180,7 @@ __device__ __forceinline__ void epilogue_store8(const Epilogue& e, OutT* __restr
     for (int j = 0; j < 8; ++j) gelu_pair_for<OutT>(x[j], x[j], t[j]);
     if (e.aux_out) store8<OutT>((OutT*)e.aux_out + (long)m * e.ldo + n0, t);
   } else if (e.act == ACT_MULAUX) {
-    load8<OutT>((const OutT*)e.aux_in + (long)m * e.lda + n0, t);
+    load8<OutT>((const OutT*)e.aux_in + (long)m * e.lda + n0, t, true);
 #pragma unroll
     for (int j = 0; j < 8; ++j) x[j] *= t[j];
   }
@@ -180,7 +189,7 @@ __device__ __forceinline__ void epilogue_store8(const Epilogue& e, OutT* __restr
     for (int j = 0; j < 8; ++j) x[j] *= drop_mask(e.seed, e.pdrop, m, n0 + j);
   }
   if (e.residual) {
-    load8<OutT>((const OutT*)e.residual + (long)m * e.ldr + n0, t);
+    load8<OutT>((const OutT*)e.residual + (long)m * e.ldr + n0, t, true);
 #pragma unroll
     for (int j = 0; j < 8; ++j) x[j] += t[j];
   }
@@ -302,6 +311,10 @@ __global__ __launch_bounds__(NT, 2) void gemm_bf16_kernel(int M, int N, int K, c
 #undef As
 #undef Bs
 
+// the split-K reduce reads its slabs non-temporal (see CMHAR_NT_EPI_LOAD)
+#ifndef CMHAR_NT_REDUCE_LOAD
+#define CMHAR_NT_REDUCE_LOAD 1
+#endif
 // Sum split-K fp32 partial slabs and apply the epilogue; 8 consecutive columns per thread when N % 8 == 0.
 // m_base: the slabs hold rows m_base .. m_base+M-1 of C (tail-split hybrid); 0 for a plain split-K GEMM.
 template <typename OutT>
@@ -314,7 +327,14 @@ __global__ void splitk_reduce_kernel(int M, int N, int splits, const float* __re
     const int m = (int)(e0 / N) + m_base, n0 = (int)(e0 % N);
     float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     for (int z = 0; z < splits; ++z) {
-      const floatx4 a = *(const floatx4*)(P + z * split_stride + e0), b = *(const floatx4*)(P + z * split_stride + e0 + 4);
+      floatx4 a, b;
+      if (CMHAR_NT_REDUCE_LOAD) {   // the slabs are dead after this pass
+        a = __builtin_nontemporal_load((const floatx4*)(P + z * split_stride + e0));
+        b = __builtin_nontemporal_load((const floatx4*)(P + z * split_stride + e0 + 4));
+      } else {
+        a = *(const floatx4*)(P + z * split_stride + e0);
+        b = *(const floatx4*)(P + z * split_stride + e0 + 4);
+      }
 #pragma unroll
       for (int j = 0; j < 4; ++j) { s[j] += a[j]; s[4 + j] += b[j]; }
     }
