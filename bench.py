@@ -392,7 +392,10 @@ def build_workload(args, dev, rank, world):
         model.overlap_imu = args.imu_stream == 'side'
     backbone = model.video_encoder.backbone
     cdist.broadcast_parameters(model)
-    reducer = cdist.GradReducer(model, backbone=backbone)
+    # CMHAR_BENCH_REDUCE_SINGLE=1 (rehearsal): on one GPU, the reducer runs its whole bucket / RCCL protocol in a
+    # one-rank group — the per-step cost of the data-parallel machinery without the transfers
+    reducer = cdist.GradReducer(model, backbone=backbone,
+                                reduce_single=os.environ.get('CMHAR_BENCH_REDUCE_SINGLE') == '1')
     # LinearLR(start_factor=0.1) of trainer.py:80-105 → step-0 lr = 0.1 * pretrain_lr
     params = [p for n, p in model.named_parameters() if not (args.workload == 'fusion' and
                                                               n.startswith('video_encoder.projection.'))]
@@ -460,6 +463,10 @@ def main():
     rank, world, local = cdist.init_from_env(os.environ.get('CMHAR_BENCH_BACKEND') or None)
     local = int(os.environ.get('CMHAR_BENCH_DEVICE', local))
     torch.cuda.set_device(local)
+    if world == 1 and os.environ.get('CMHAR_BENCH_REDUCE_SINGLE') == '1' and not dist.is_initialized():
+        os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
+        os.environ.setdefault('MASTER_PORT', '29533')
+        dist.init_process_group(os.environ.get('CMHAR_BENCH_BACKEND') or 'nccl', rank=0, world_size=1)
     dev = torch.device('cuda', local)
     W = build_workload(args, dev, rank, world)
     step, B = W.step, W.B
@@ -574,7 +581,7 @@ def main():
             out['kernels'] = {k: {'launches': n, 'ms_per_step': round(tm, 3),
                                   'tflops': round(f / (tm / 1e3) / 1e12, 1)} for k, (n, tm, f, b) in breakdown.items()}
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if dist.is_initialized():
         dist.destroy_process_group()
 
 
