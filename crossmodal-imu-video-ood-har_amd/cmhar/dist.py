@@ -98,8 +98,17 @@ def backbone_param_order(backbone) -> List[torch.nn.Parameter]:
 
 
 def _is_sink_backbone(backbone) -> bool:
+    from .r3d import R3D18
     from .videomae import VideoMAEBackbone
-    return isinstance(backbone, VideoMAEBackbone)
+    return isinstance(backbone, (VideoMAEBackbone, R3D18))
+
+
+def sink_param_order(backbone) -> List[torch.nn.Parameter]:
+    """The flat gradient buffer's layout for a sink backbone: its backward-production order."""
+    from .r3d import R3D18, unit_param_order
+    if isinstance(backbone, R3D18):
+        return unit_param_order(backbone)
+    return backbone_param_order(backbone)
 
 
 class _Bucket:
@@ -127,8 +136,9 @@ def _cut(params, limit):
 class GradReducer:
     """Bucketed, backward-overlapped gradient all-reduce (SUM) for one model replica per process.
 
-    `backbone`: the model's video backbone.  A VideoMAE backbone gets the zero-copy flat gradient sink; any other
-    backbone (or None) is covered by the hook buckets like the rest of the model.
+    `backbone`: the model's video backbone.  A VideoMAE or R3D-18 backbone gets the zero-copy flat gradient sink (its
+    backward writes every parameter gradient straight into the bucket buffer); any other backbone (or None) is
+    covered by the hook buckets like the rest of the model.
 
     Hook buckets are first cut in reverse registration order.  That order is only a guess at backward order, and a
     bucket holding a parameter that never receives a gradient (`CrossModalModel.temperature` / `bias`,
@@ -159,7 +169,7 @@ class GradReducer:
         self.limit = max(int(bucket_mb * (1 << 20) / 4), 1)
         sink_params = set()
         if backbone is not None and _is_sink_backbone(backbone):
-            order = backbone_param_order(backbone)
+            order = sink_param_order(backbone)
             self.sink = FlatGradSink(order, order[0].device, on_ready=self._on_sink_ready)
             backbone._grad_sink = self.sink
             cur, start = [], 0
@@ -289,13 +299,17 @@ class GradReducer:
         for w in self.pending:
             w.wait()               # NCCL: the caller's current stream waits on the collective
         self.pending = []
+        dst, src = [], []
         for b in self.buckets:
             if b.kind == 'hook' and b.live:
                 off = 0
                 for p in b.live:
                     n = p.numel()
-                    p.grad.copy_(b.flat[off:off + n].view_as(p.grad))
+                    dst.append(p.grad)
+                    src.append(b.flat[off:off + n].view_as(p.grad))
                     off += n
+        if dst:
+            torch._foreach_copy_(dst, src)     # the reduced values back into .grad: one multi-tensor launch
         if not self.learned:
             self._learn_order()
 

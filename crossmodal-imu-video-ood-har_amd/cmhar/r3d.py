@@ -289,15 +289,57 @@ def _dgrad_igemm(dz, conv, oshape, x, dx_acc=None, wf=None):
     return dx
 
 
+def _grad_dest(grads, p, dev):
+    """Where p's fp32 gradient is written: (destination, accumulate_into).  `grads` is a dict (a fresh tensor is
+    recorded in it) or a gradient sink (cmhar.grads: AutogradSink, or the data-parallel FlatGradSink whose
+    destination is p's slice of the flat bucket buffer).  When the sink asks for accumulation (β = 1: `.grad` already
+    held a value) the gradient goes to a temporary that `_grad_acc` adds into the destination."""
+    if isinstance(grads, dict) or not p.requires_grad:
+        g = torch.empty(p.shape, dtype=torch.float32, device=dev)
+        if isinstance(grads, dict):
+            grads[p] = g
+        return g, None                        # (a frozen parameter's gradient is computed and dropped)
+    out, beta = grads.dest([p], tuple(p.shape), dev)
+    if beta == 0.0:
+        return out, None
+    return torch.empty(p.shape, dtype=torch.float32, device=dev), out
+
+
+def _grad_acc(tmp, acc):
+    if acc is not None:
+        acc.add_(tmp)
+
+
 def _store_wgrad(conv, src, rs, cs, grads):
     """Packed fp32 weight gradient [Cout, Kp] → a contiguous gradient in the parameter's own layout (one HIP pass;
     a strided view here would make autograd's gradient accumulation copy it with a torch kernel)."""
     w = conv.weight
     co, ci, kt, kh, kw = w.shape
     p = getattr(conv, 'param', None)          # a 2-D conv run as (1, kh, kw): gradient in the parameter's shape
-    g = torch.empty(w.shape if p is None else p.shape, dtype=torch.float32, device=src.device)
+    g, acc = _grad_dest(grads, w if p is None else p, src.device)
     call('cmhar_conv_grad_unpack', co, ci, kt * kh, kw, src.shape[1], rs, cs, ptr(src), ptr(g), L.stream(src.device))
-    grads[w if p is None else p] = g
+    _grad_acc(g, acc)
+
+
+def _unit_grads_done(grads, u):
+    """A unit's three parameter gradients (BN weight, BN bias, conv weight) are final: tell a gradient sink (the
+    data-parallel reducer all-reduces a bucket as soon as every gradient in it is written)."""
+    if not isinstance(grads, dict):
+        p = getattr(u.conv, 'param', None)
+        grads.done([u.bn.weight, u.bn.bias, u.conv.weight if p is None else p])
+
+
+def unit_param_order(m: 'R3D18'):
+    """Backward-production order of the R3D-18 parameters (`_backward_impl`: blocks last→first, per block conv2,
+    downsample, conv1, then the stem; per unit BN weight, BN bias, conv weight) — the flat gradient buffer's layout,
+    so that the reducer's buckets fill in order during the backward."""
+    order = []
+    for blk in reversed(list(m.blocks())):
+        seqs = [blk.conv2] + ([blk.downsample] if blk.downsample is not None else []) + [blk.conv1]
+        for sq in seqs:
+            order += [sq[1].weight, sq[1].bias, sq[0].weight]
+    order += [m.stem[1].weight, m.stem[1].bias, m.stem[0].weight]
+    return order
 
 
 def _unit_bwd(u, dy, grads, training, need_dx, want_dres, dx_acc=None):
@@ -308,14 +350,14 @@ def _unit_bwd(u, dy, grads, training, need_dx, want_dres, dx_acc=None):
     if u.rows > M:
         dz[M:].zero_()
     dres = torch.empty(M, Cc, dtype=dt, device=dy.device) if want_dres else None
-    dw_bn = torch.empty(Cc, dtype=torch.float32, device=dy.device)
-    db_bn = torch.empty(Cc, dtype=torch.float32, device=dy.device)
+    dw_bn, acc_w = _grad_dest(grads, u.bn.weight, dy.device)
+    db_bn, acc_b = _grad_dest(grads, u.bn.bias, dy.device)
     ws = K.workspace(L.lib().cmhar_bn_cl_ws(M, Cc), dy.device)
     call('cmhar_bn_cl_bwd', L.dtype_code(dt), M, Cc, ptr(u.z), ptr(u.y), ptr(dy), ptr(u.bn.weight), ptr(u.sm),
          ptr(u.sr), ptr(dz), ptr(dres), ptr(dw_bn), ptr(db_bn), int(training or not u.bn.track_running_stats), int(u.relu), ptr(ws),
          L.stream(dy.device))
-    grads[u.bn.weight] = dw_bn
-    grads[u.bn.bias] = db_bn
+    _grad_acc(dw_bn, acc_w)
+    _grad_acc(db_bn, acc_b)
     w = u.conv.weight
     if u.stem:
         dims = _dims(u.shape, u.conv, _stem_kp(u.conv))
@@ -323,6 +365,7 @@ def _unit_bwd(u, dy, grads, training, need_dx, want_dres, dx_acc=None):
         ws = K.workspace(L.lib().cmhar_conv3d_stem_wgrad_ws(dims, Cc), dy.device)
         call('cmhar_conv3d_stem_wgrad', dims, Cc, ptr(u.x), ptr(dz), ptr(dw4), ptr(ws), L.stream(dy.device))
         _store_wgrad(u.conv, dw4, 32, 4, grads)
+        _unit_grads_done(grads, u)
         if need_dx:
             raise RuntimeError('the implicit stem has no input gradient (its input is the video)')
         return None, dres
@@ -344,6 +387,7 @@ def _unit_bwd(u, dy, grads, training, need_dx, want_dres, dx_acc=None):
         K.gemm(2, dz, col, dwp, splits=splits)
         del col
     _store_wgrad(u.conv, dwp, w.shape[4] * w.shape[1], w.shape[1], grads)
+    _unit_grads_done(grads, u)
     dx = None
     if need_dx and u.igemm and _dgrad_igemm_ok(u.conv):
         dx = _dgrad_igemm(dz, u.conv, u.oshape, u.x, dx_acc, u.wf)
@@ -409,9 +453,11 @@ def _forward_impl(m: R3D18, video, training, save):
     return feat, st
 
 
-def _backward_impl(m: R3D18, st, dfeat, training):
+def _backward_impl(m: R3D18, st, dfeat, training, grads=None):
+    """Parameter gradients into `grads` (a dict, returned; or a gradient sink, cmhar.grads)."""
     units, shape = st
-    grads = {}
+    if grads is None:
+        grads = {}
     N, To, Ho, Wo, Co = shape
     dt = units[-1].z.dtype
     dh = torch.empty(N * To * Ho * Wo, Co, dtype=dt, device=dfeat.device)
@@ -445,14 +491,16 @@ class _R3DFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dfeat):
         m = ctx.module
-        grads = _backward_impl(m, ctx.st, dfeat, ctx.training)
+        from .grads import AutogradSink
+        sink = getattr(m, '_grad_sink', None) or AutogradSink()
+        _backward_impl(m, ctx.st, dfeat, ctx.training, sink)
         ctx.st = None
         out = []
         for p in m.parameters():
             if m.fc is not None and (p is m.fc.weight or p is m.fc.bias):
                 out.append(None)
             else:
-                out.append(grads.get(p) if p.requires_grad else None)
+                out.append(sink.result(p) if p.requires_grad else None)
         return (None, None, None, *out)
 
 

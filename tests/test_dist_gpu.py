@@ -70,7 +70,7 @@ def test_dataparallel_real_model_two_ranks(tmp_path, backbone, dtype):
     storage itself causes (the oracle run with the HIP path's bf16 storage emulated) + FLOOR_BF16."""
     res, sums = _run(tmp_path, backbone, dtype)
     r0, r1 = res
-    assert r0['sink'] == (backbone == 'videomae')
+    assert r0['sink']            # VideoMAE and R3D-18 backward write into the reducer's flat bucket buffer
     assert r0['n_buckets'] >= 2
     # global-batch loss identical on every rank; equal to the oracle's DataParallel loss
     assert r0['loss'] == r1['loss']
@@ -122,8 +122,9 @@ def test_dataparallel_classification_global_mean(tmp_path):
 def test_dataparallel_rccl_single_rank(tmp_path, backbone):
     """VERDICT r02 weak 5 (DP never touched RCCL): two ranks cannot share one GPU under RCCL ("Duplicate GPU
     detected", tools/debug/rccl_probe.py), so this runs ONE rank over backend "nccl" with the reducer's full
-    protocol forced (GradReducer(reduce_single=True)): bf16 flat-sink buckets (VideoMAE) / hook buckets flattened
-    on the communication stream (R3D-18), all launched through RCCL, learned hook order, copy-back.  A SUM over
+    protocol forced (GradReducer(reduce_single=True)): the backbone's flat-sink buckets (bf16 VideoMAE / R3D-18
+    backward writing straight into the bucket buffer) and the IMU / head hook buckets flattened on the communication
+    stream, all launched through RCCL, learned hook order, copy-back.  A SUM over
     one rank is the identity, so the gradients must equal the plain single-process step bit for bit, and the loss
     the oracle's."""
     res, sums = _run(tmp_path, backbone, 'bf16', world=1, backend='nccl', force_reduce=True)
