@@ -23,7 +23,7 @@ import torch.nn as nn
 from . import _lib as L
 from . import kernels as K
 from ._lib import call, ptr
-from .r3d import _bn_fwd, _dgrad_igemm_ok, _pack, _stem_ok, _unit_bwd, _unit_fwd
+from .r3d import _bn_fwd, _dgrad_igemm_ok, _grad_acc, _grad_dest, _pack, _stem_ok, _unit_bwd, _unit_fwd
 
 RELU, RELU6 = 1, 2
 
@@ -172,21 +172,23 @@ def _dw_bwd(u, dy, grads, training):
     dt = u.z.dtype
     dev = dy.device
     dz = torch.empty(M, C, dtype=dt, device=dev)
-    dw_bn = torch.empty(C, dtype=torch.float32, device=dev)
-    db_bn = torch.empty(C, dtype=torch.float32, device=dev)
+    dw_bn, acc_w = _grad_dest(grads, u.bn.weight, dev)
+    db_bn, acc_b = _grad_dest(grads, u.bn.bias, dev)
     ws = K.workspace(L.lib().cmhar_bn_cl_ws(M, C), dev)
     call('cmhar_bn_cl_bwd', L.dtype_code(dt), M, C, ptr(u.z), ptr(u.y), ptr(dy), ptr(u.bn.weight), ptr(u.sm),
          ptr(u.sr), ptr(dz), None, ptr(dw_bn), ptr(db_bn), int(training or not u.bn.track_running_stats), u.relu,
          ptr(ws), L.stream(dev))
-    grads[u.bn.weight] = dw_bn
-    grads[u.bn.bias] = db_bn
+    _grad_acc(dw_bn, acc_w)
+    _grad_acc(db_bn, acc_b)
     N, H, W, C_, k, s, p, _, _ = _geom(u.shape, u.conv)
-    dwt = torch.empty(u.conv.weight.shape, dtype=torch.float32, device=dev)
+    dwt, acc = _grad_dest(grads, u.conv.weight, dev)
     n = L.lib().cmhar_dwconv2d_cl_wgrad_ws(N, H, W, C, k, s, p)
     wsw = K.workspace(n, dev)
     call('cmhar_dwconv2d_cl_wgrad', L.dtype_code(dt), N, H, W, C, k, s, p, ptr(u.x), ptr(dz), ptr(dwt), ptr(wsw),
          L.stream(dev))
-    grads[u.conv.weight] = dwt
+    _grad_acc(dwt, acc)
+    if not isinstance(grads, dict):
+        grads.done([u.bn.weight, u.bn.bias, u.conv.weight])
     dx = torch.empty_like(u.x)
     call('cmhar_dwconv2d_cl_dgrad', L.dtype_code(dt), N, H, W, C, k, s, p, ptr(dz), ptr(u.conv.weight.detach()),
          ptr(dx), L.stream(dev))
@@ -260,9 +262,8 @@ def _resnet_forward(m: ResNet18Features, video, training, save):
     return h, shape, ((units, pool_st, shape) if save else None)
 
 
-def _resnet_backward(m: ResNet18Features, st, dh, training):
+def _resnet_backward(m: ResNet18Features, st, dh, training, grads):
     units, pool_st, _ = st
-    grads = {}
     i = len(units) - 1
     for layer in reversed(list(m)[4:8]):
         for blk in reversed(list(layer)):
@@ -306,9 +307,8 @@ def _mobilenet_forward(m: MobileNetV2Features, video, training, save):
     return h, shape, ((units,) if save else None)
 
 
-def _mobilenet_backward(m: MobileNetV2Features, st, dh, training):
+def _mobilenet_backward(m: MobileNetV2Features, st, dh, training, grads):
     (units,) = st
-    grads = {}
     i = len(units) - 1
     dh, _ = _unit_bwd(units[i], dh, grads, training, True, False)
     i -= 1
@@ -334,6 +334,35 @@ _IMPL = {ResNet18Features: (_resnet_forward, _resnet_backward),
          MobileNetV2Features: (_mobilenet_forward, _mobilenet_backward)}
 
 
+def unit_param_order(m):
+    """Backward-production order of a per-frame CNN backbone's parameters (`_resnet_backward` /
+    `_mobilenet_backward`: units last→first, per unit BN weight, BN bias, conv weight) — the layout of the
+    data-parallel reducer's flat gradient buffer (cmhar.dist)."""
+    order = []
+
+    def unit(conv, bn):
+        order.extend([bn.weight, bn.bias, conv.weight])
+    if isinstance(m, ResNet18Features):
+        for layer in reversed(list(m)[4:8]):
+            for blk in reversed(list(layer)):
+                unit(blk.conv2, blk.bn2)
+                if blk.downsample is not None:
+                    unit(blk.downsample[0], blk.downsample[1])
+                unit(blk.conv1, blk.bn1)
+        unit(m[0], m[1])
+    else:
+        unit(m[-1][0], m[-1][1])
+        for blk in reversed(list(m)[1:-1]):
+            seq = list(blk.conv)
+            unit(seq[-2], seq[-1])
+            dw = seq[1] if len(seq) == 4 else seq[0]
+            unit(dw[0], dw[1])
+            if len(seq) == 4:
+                unit(seq[0][0], seq[0][1])
+        unit(m[0][0], m[0][1])
+    return order
+
+
 def _pool(h, shape, dev):
     N, _, Ho, Wo, Cf = shape
     feat = torch.empty(N, Cf, dtype=torch.float32, device=dev)
@@ -357,9 +386,11 @@ class _CNNFn(torch.autograd.Function):
         call('cmhar_avgpool_cl_bwd', L.dtype_code(ctx.dt), N, Ho * Wo, Cf, ptr(dfeat.contiguous()), ptr(dh),
              L.stream(dfeat.device))
         _, bwd = _IMPL[type(m)]
-        grads = bwd(m, ctx.st, dh, ctx.training)
+        from .grads import AutogradSink
+        sink = getattr(m, '_grad_sink', None) or AutogradSink()
+        bwd(m, ctx.st, dh, ctx.training, sink)
         ctx.st = None
-        return (None, None, None, *[grads.get(p) if p.requires_grad else None for p in m.parameters()])
+        return (None, None, None, *[sink.result(p) if p.requires_grad else None for p in m.parameters()])
 
 
 def run_cnn2d(m, video: torch.Tensor, training: bool) -> torch.Tensor:

@@ -98,16 +98,19 @@ def backbone_param_order(backbone) -> List[torch.nn.Parameter]:
 
 
 def _is_sink_backbone(backbone) -> bool:
+    from .cnn2d import MobileNetV2Features, ResNet18Features
     from .r3d import R3D18
     from .videomae import VideoMAEBackbone
-    return isinstance(backbone, (VideoMAEBackbone, R3D18))
+    return isinstance(backbone, (VideoMAEBackbone, R3D18, ResNet18Features, MobileNetV2Features))
 
 
 def sink_param_order(backbone) -> List[torch.nn.Parameter]:
     """The flat gradient buffer's layout for a sink backbone: its backward-production order."""
-    from .r3d import R3D18, unit_param_order
-    if isinstance(backbone, R3D18):
-        return unit_param_order(backbone)
+    from . import cnn2d, r3d
+    if isinstance(backbone, r3d.R3D18):
+        return r3d.unit_param_order(backbone)
+    if isinstance(backbone, (cnn2d.ResNet18Features, cnn2d.MobileNetV2Features)):
+        return cnn2d.unit_param_order(backbone)
     return backbone_param_order(backbone)
 
 
@@ -136,9 +139,9 @@ def _cut(params, limit):
 class GradReducer:
     """Bucketed, backward-overlapped gradient all-reduce (SUM) for one model replica per process.
 
-    `backbone`: the model's video backbone.  A VideoMAE or R3D-18 backbone gets the zero-copy flat gradient sink (its
-    backward writes every parameter gradient straight into the bucket buffer); any other backbone (or None) is
-    covered by the hook buckets like the rest of the model.
+    `backbone`: the model's video backbone.  Every cmhar video backbone (VideoMAE, R3D-18, the per-frame ResNet-18 /
+    MobileNetV2) gets the zero-copy flat gradient sink (its backward writes every parameter gradient straight into
+    the bucket buffer); any other backbone (or None) is covered by the hook buckets like the rest of the model.
 
     Hook buckets are first cut in reverse registration order.  That order is only a guess at backward order, and a
     bucket holding a parameter that never receives a gradient (`CrossModalModel.temperature` / `bias`,
