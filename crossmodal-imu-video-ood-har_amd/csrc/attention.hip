@@ -1178,48 +1178,6 @@ static bool f32m_ok(int dtype, int D, float pdrop, std::initializer_list<std::pa
   return true;
 }
 
-// The ragged-tail kernels on a side stream (CMHAR_ATTN_TAIL_STREAM=1, A/B knob): the tail launch (384 one-workgroup
-// (batch, head) items at L = 1568, half the chip's slots) then runs beside the bulk kernel instead of after it.
-// One side stream and two events per (host thread, device): no state shared between threads.
-struct TailStream {
-  hipStream_t s = nullptr;
-  hipEvent_t ready = nullptr, done = nullptr;
-};
-static bool tail_stream_on() {
-  static const bool v = [] {
-    const char* e = getenv("CMHAR_ATTN_TAIL_STREAM");
-    return e && atoi(e) != 0;
-  }();
-  return v;
-}
-static TailStream* tail_stream() {
-  thread_local TailStream ts[16];
-  int d = 0;
-  if (hipGetDevice(&d) != hipSuccess || d < 0 || d >= 16) return nullptr;
-  TailStream& t = ts[d];
-  if (!t.s) {
-    if (hipStreamCreateWithFlags(&t.s, hipStreamNonBlocking) != hipSuccess) return nullptr;
-    if (hipEventCreateWithFlags(&t.ready, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&t.done, hipEventDisableTiming) != hipSuccess)
-      return nullptr;
-  }
-  return &t;
-}
-// Fork: the side stream waits for everything issued on `st` so far; returns the stream the tail goes to.
-static hipStream_t tail_fork(hipStream_t st, TailStream*& ts) {
-  ts = tail_stream_on() ? tail_stream() : nullptr;
-  if (!ts) return st;
-  (void)hipEventRecord(ts->ready, st);
-  (void)hipStreamWaitEvent(ts->s, ts->ready, 0);
-  return ts->s;
-}
-// Join: `st` waits for the tail.
-static void tail_join(hipStream_t st, TailStream* ts) {
-  if (!ts) return;
-  (void)hipEventRecord(ts->done, ts->s);
-  (void)hipStreamWaitEvent(st, ts->done, 0);
-}
-
 // ----------------------------------------------------------------------------------------------------------------
 // C ABI.  Tensors are [B*L, ld] row-major with head h at columns h*D .. h*D+D-1.
 // lse / delta: fp32 [B*H*Lq] workspaces owned by the caller.
@@ -1235,21 +1193,13 @@ extern "C" int cmhar_attention_fwd(int dtype, int B, int H, int Lq, int Lk, int 
     const int bulk = CMHAR_ATTN_FWD_ONE_LAUNCH ? cdiv(Lq, 256) * 256 : (Lq / 256) * 256;
 #define FL(E)                                                                                                    \
   do {                                                                                                           \
-    const bool tl = Lq > bulk && Lq - bulk <= CMHAR_ATTN_TAIL;                                                   \
-    TailStream* ts = nullptr;                                                                                    \
-    const hipStream_t tst = tl && bulk > 0 ? tail_fork(st, ts) : st;                                             \
-    for (int pass = 0; pass < 2; ++pass) { /* side-stream tail first (it overlaps the bulk), else after it */    \
-      if (tl && pass == (ts ? 0 : 1))                                                                            \
-        attn_fwd_tail_bf16<E><<<dim3(1, H, B), 256, 0, tst>>>(H, Lq, Lk, bulk, (const bf16*)Q, ldq, (const bf16*)K,  \
-                                                              ldk, (const bf16*)V, ldv, (E*)O, ldo, lse, scale); \
-      if (bulk > 0 && pass == 0)                                                                                 \
-        attn_fwd_bf16<E, 2><<<dim3(bulk / 256, H, B), 256, 0, st>>>(H, Lq, Lk, 0, (const bf16*)Q, ldq,            \
-                                                                    (const bf16*)K, ldk, (const bf16*)V, ldv, (E*)O, \
-                                                                    ldo, lse, scale);                            \
-    }                                                                                                            \
-    tail_join(st, ts);                                                                                           \
-    if (tl) {                                                                                                    \
-    } else if (Lq > bulk)                                                                                        \
+    if (bulk > 0)                                                                                                \
+      attn_fwd_bf16<E, 2><<<dim3(bulk / 256, H, B), 256, 0, st>>>(H, Lq, Lk, 0, (const bf16*)Q, ldq, (const bf16*)K, \
+                                                                  ldk, (const bf16*)V, ldv, (E*)O, ldo, lse, scale); \
+    if (Lq > bulk && Lq - bulk <= CMHAR_ATTN_TAIL)                                                             \
+      attn_fwd_tail_bf16<E><<<dim3(1, H, B), 256, 0, st>>>(H, Lq, Lk, bulk, (const bf16*)Q, ldq, (const bf16*)K, ldk, \
+                                                           (const bf16*)V, ldv, (E*)O, ldo, lse, scale);        \
+    else if (Lq > bulk)                                                                                          \
       attn_fwd_bf16<E, 1><<<dim3(cdiv(Lq - bulk, 128), H, B), 256, 0, st>>>(H, Lq, Lk, bulk, (const bf16*)Q, ldq,   \
                                                                             (const bf16*)K, ldk, (const bf16*)V, ldv, \
                                                                             (E*)O, ldo, lse, scale);             \
@@ -1309,22 +1259,14 @@ static void flash_bwd_bf16(int B, int H, int Lq, int Lk, const void* Q, long ldq
   const int kfull = (Lk / 128) * 128;
   const bool ktail = Lk > kfull && Lk - kfull <= CMHAR_ATTN_TAIL;
   const int kblocks = ktail ? kfull / 128 : cdiv(Lk, 128);
-  // (the tail reads δ, written by the dQ launches above: the fork comes after them)
-  TailStream* ts = nullptr;
-  const hipStream_t tst = ktail && kblocks > 0 ? tail_fork(st, ts) : st;
-  for (int pass = 0; pass < 2; ++pass) {   // side-stream tail first (it overlaps the bulk), else after it
-    if (ktail && pass == (ts ? 0 : 1))
-      attn_bwd_dkdv_tail_bf16<PS><<<dim3(1, H, B), 256, 0, tst>>>(H, Lq, Lk, kfull, (const bf16*)Q, ldq,
-                                                                  (const bf16*)K, ldk, (const bf16*)V, ldv,
-                                                                  (const bf16*)dO, lddo, lse, delta, (bf16*)dK, lddk,
-                                                                  (bf16*)dV, lddv, s_in, scale);
-    if (kblocks > 0 && pass == 0)
-      attn_bwd_dkdv_bf16<PS><<<dim3(kblocks, H, B), 256, 0, st>>>(H, Lq, Lk, (const bf16*)Q, ldq, (const bf16*)K,
-                                                                  ldk, (const bf16*)V, ldv, (const bf16*)dO, lddo, lse,
-                                                                  delta, (bf16*)dK, lddk, (bf16*)dV, lddv, s_in,
-                                                                  scale);
-  }
-  tail_join(st, ts);
+  if (kblocks > 0)
+    attn_bwd_dkdv_bf16<PS><<<dim3(kblocks, H, B), 256, 0, st>>>(H, Lq, Lk, (const bf16*)Q, ldq, (const bf16*)K, ldk,
+                                                                (const bf16*)V, ldv, (const bf16*)dO, lddo, lse, delta,
+                                                                (bf16*)dK, lddk, (bf16*)dV, lddv, s_in, scale);
+  if (ktail)
+    attn_bwd_dkdv_tail_bf16<PS><<<dim3(1, H, B), 256, 0, st>>>(H, Lq, Lk, kfull, (const bf16*)Q, ldq, (const bf16*)K,
+                                                               ldk, (const bf16*)V, ldv, (const bf16*)dO, lddo, lse,
+                                                               delta, (bf16*)dK, lddk, (bf16*)dV, lddv, s_in, scale);
 }
 
 extern "C" int cmhar_attention_bwd_prescaled(int B, int H, int Lq, int Lk, const void* Q, long ldq, const void* K,
