@@ -665,7 +665,7 @@ __device__ __forceinline__ void stage128(const TileDma& t, int r0, char* lds, in
 }
 
 template <typename E>
-__global__ __launch_bounds__(256, 2) void attn_fwd_tail_bf16(int H, int Lq, int Lk, int q_base,
+__global__ __launch_bounds__(256, 2) void attn_fwd_tail_bf16(int H, int Lq, int Lk, int q_base0,
                                                              const bf16* __restrict__ Q, long ldq,
                                                              const bf16* __restrict__ K, long ldk,
                                                              const bf16* __restrict__ V, long ldv, E* __restrict__ O,
@@ -673,6 +673,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_tail_bf16(int H, int Lq, int 
   __shared__ __attribute__((aligned(16))) char smem[65536];   // [2 buf][K 128 rows 16 KB | V 16 KB]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5;
   const int hd = blockIdx.y, b = blockIdx.z;
+  const int q_base = q_base0 + 32 * blockIdx.x;   // grid.x = ⌈tail / 32⌉ groups of 32 rows
   const bf16* Kb = K + (long)b * Lk * ldk + hd * 64;
   const bf16* Vb = V + (long)b * Lk * ldv + hd * 64;
   const float c = scale * LOG2E;
@@ -784,7 +785,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_tail_bf16(int H, int Lq, int 
 }
 
 template <bool PS>
-__global__ __launch_bounds__(256, 2) void attn_bwd_dq_tail_bf16(int H, int Lq, int Lk, int q_base,
+__global__ __launch_bounds__(256, 2) void attn_bwd_dq_tail_bf16(int H, int Lq, int Lk, int q_base0,
                                                                 const bf16* __restrict__ Q, long ldq,
                                                                 const bf16* __restrict__ K, long ldk,
                                                                 const bf16* __restrict__ V, long ldv,
@@ -796,6 +797,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_tail_bf16(int H, int Lq, i
   __shared__ __attribute__((aligned(16))) char smem[65536];   // [2 buf][K 16 KB | V 16 KB]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5;
   const int hd = blockIdx.y, b = blockIdx.z;
+  const int q_base = q_base0 + 32 * blockIdx.x;   // grid.x = ⌈tail / 32⌉ groups of 32 rows
   const bf16* Kb = K + (long)b * Lk * ldk + hd * 64;
   const bf16* Vb = V + (long)b * Lk * ldv + hd * 64;
   const float c = scale * LOG2E;
@@ -894,7 +896,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_tail_bf16(int H, int Lq, i
 }
 
 template <bool PS>
-__global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_tail_bf16(int H, int Lq, int Lk, int k_base,
+__global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_tail_bf16(int H, int Lq, int Lk, int k_base0,
                                                                   const bf16* __restrict__ Q, long ldq,
                                                                   const bf16* __restrict__ K, long ldk,
                                                                   const bf16* __restrict__ V, long ldv,
@@ -909,6 +911,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_tail_bf16(int H, int Lq,
   float* Ds = Ls + 256;                        // [2][128] −δ
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5;
   const int hd = blockIdx.y, b = blockIdx.z;
+  const int k_base = k_base0 + 32 * blockIdx.x;   // grid.x = ⌈tail / 32⌉ groups of 32 keys
   const bf16* Qb = Q + (long)b * Lq * ldq + hd * 64;
   const bf16* Gb = dO + (long)b * Lq * lddo + hd * 64;
   const float* lseb = lse + ((long)b * H + hd) * Lq;
@@ -1157,9 +1160,10 @@ __global__ __launch_bounds__(64) void attn_bwd_dkdv_f32(int H, int Lq, int Lk, c
 #ifndef CMHAR_ATTN_DQ_QB
 #define CMHAR_ATTN_DQ_QB 1
 #endif
-// the ragged-tail kernels take tails of up to this many rows (0: off, the one-active-wave blocks run them; A/B knob)
+// the ragged-tail kernels take tails of up to this many rows, in workgroups of 32 (0: off, the partly active blocks
+// run them; A/B knob).  64: the 32-frame geometry's L = 3136 = 12·256 + 64 (forward) = 24·128 + 64 (dK/dV) tails.
 #ifndef CMHAR_ATTN_TAIL
-#define CMHAR_ATTN_TAIL 32
+#define CMHAR_ATTN_TAIL 64
 #endif
 
 // f32-MFMA flash kernels (csrc/attention_f32.hip) for fp32 storage, D = 64, no dropout
@@ -1197,7 +1201,8 @@ extern "C" int cmhar_attention_fwd(int dtype, int B, int H, int Lq, int Lk, int 
       attn_fwd_bf16<E, 2><<<dim3(bulk / 256, H, B), 256, 0, st>>>(H, Lq, Lk, 0, (const bf16*)Q, ldq, (const bf16*)K, \
                                                                   ldk, (const bf16*)V, ldv, (E*)O, ldo, lse, scale); \
     if (Lq > bulk && Lq - bulk <= CMHAR_ATTN_TAIL)                                                             \
-      attn_fwd_tail_bf16<E><<<dim3(1, H, B), 256, 0, st>>>(H, Lq, Lk, bulk, (const bf16*)Q, ldq, (const bf16*)K, ldk, \
+      attn_fwd_tail_bf16<E><<<dim3(cdiv(Lq - bulk, 32), H, B), 256, 0, st>>>(H, Lq, Lk, bulk, (const bf16*)Q, ldq,   \
+                                                                             (const bf16*)K, ldk,                \
                                                            (const bf16*)V, ldv, (E*)O, ldo, lse, scale);        \
     else if (Lq > bulk)                                                                                          \
       attn_fwd_bf16<E, 1><<<dim3(cdiv(Lq - bulk, 128), H, B), 256, 0, st>>>(H, Lq, Lk, bulk, (const bf16*)Q, ldq,   \
@@ -1253,7 +1258,8 @@ static void flash_bwd_bf16(int B, int H, int Lq, int Lk, const void* Q, long ldq
         H, Lq, Lk, bulk, (const bf16*)Q, ldq, (const bf16*)K, ldk, (const bf16*)V, ldv, (const bf16*)O, ldo,
         (const bf16*)dO, lddo, lse, delta, (bf16*)dQ, lddq, s_in);
   if (qtail)
-    attn_bwd_dq_tail_bf16<PS><<<dim3(1, H, B), 256, 0, st>>>(H, Lq, Lk, qfull, (const bf16*)Q, ldq, (const bf16*)K,
+    attn_bwd_dq_tail_bf16<PS><<<dim3(cdiv(Lq - qfull, 32), H, B), 256, 0, st>>>(H, Lq, Lk, qfull, (const bf16*)Q, ldq,
+                                                                                (const bf16*)K,
                                                              ldk, (const bf16*)V, ldv, (const bf16*)O, ldo,
                                                              (const bf16*)dO, lddo, lse, delta, (bf16*)dQ, lddq, s_in);
   const int kfull = (Lk / 128) * 128;
@@ -1264,7 +1270,8 @@ static void flash_bwd_bf16(int B, int H, int Lq, int Lk, const void* Q, long ldq
                                                                 (const bf16*)V, ldv, (const bf16*)dO, lddo, lse, delta,
                                                                 (bf16*)dK, lddk, (bf16*)dV, lddv, s_in, scale);
   if (ktail)
-    attn_bwd_dkdv_tail_bf16<PS><<<dim3(1, H, B), 256, 0, st>>>(H, Lq, Lk, kfull, (const bf16*)Q, ldq, (const bf16*)K,
+    attn_bwd_dkdv_tail_bf16<PS><<<dim3(cdiv(Lk - kfull, 32), H, B), 256, 0, st>>>(H, Lq, Lk, kfull, (const bf16*)Q,
+                                                                                  ldq, (const bf16*)K,
                                                                ldk, (const bf16*)V, ldv, (const bf16*)dO, lddo, lse,
                                                                delta, (bf16*)dK, lddk, (bf16*)dV, lddv, s_in, scale);
 }

@@ -300,9 +300,11 @@ def test_flash_attention_bf16_fwd_bwd(L_):
     assert rel(dqkv[:, 2 * H * D:], gv) < 2e-2
 
 
-@pytest.mark.parametrize('Lq,Lk', [(1568, 1568), (129, 257), (32, 200), (1, 64), (300, 33), (26, 3136), (13, 392)])
+@pytest.mark.parametrize('Lq,Lk', [(1568, 1568), (129, 257), (32, 200), (1, 64), (300, 33), (26, 3136), (13, 392),
+                                   (3136, 3136), (320, 320), (64, 100)])
 def test_flash_attention_ragged_tails(Lq, Lk):
-    """The split-sequence tail kernels (csrc/attention.hip, tails of <= 32 queries / keys past the last full block):
+    """The split-sequence tail kernels (csrc/attention.hip, tails of <= 64 queries / keys past the last full block, in
+    workgroups of 32 rows — 3136 = 12·256 + 64 is the 32-frame geometry):
     forward O, dQ, dK, dV vs torch fp32 autograd, with the TAIL rows checked on their own (a tail bug would hide in a
     whole-tensor norm), at cross-attention shapes (Lq != Lk) including a whole-tail-only sequence (Lq <= 32)."""
     torch.manual_seed(13)
