@@ -139,9 +139,35 @@ __device__ __forceinline__ void store8(OutT* __restrict__ p, const float (&x)[8]
 // Vectorised epilogue for 8 consecutive columns n0..n0+7 of row m: every operand is moved with 16-B accesses
 // (callers guarantee 16-B alignment: N % 8 == 0 on this path, leading dimensions % 8 == 0, checked on the host).
 // Each optional stage is a wave-uniform branch on a kernel argument.
+// The [M,N] 16-bit operand an epilogue streams per element — aux_in of act 3 / 4 / 6, else the residual — or null.
+// Kernels instantiated with PFS (launched only for epilogues that have one) load it two row groups ahead of its use,
+// the first two under the accumulator staging, and hand each row's vector to epilogue_store8 as `pre`.
+#ifndef CMHAR_EPI_PF2
+#define CMHAR_EPI_PF2 1
+#endif
+template <typename OutT>
+__device__ __forceinline__ const OutT* epi_stream(const Epilogue& e, long& ld) {
+  if (e.act == ACT_DGELU || e.act == ACT_DRELU || e.act == ACT_MULAUX) { ld = e.lda; return (const OutT*)e.aux_in; }
+  ld = e.ldr;
+  return (const OutT*)e.residual;
+}
+static inline bool epi_has_stream(const Epilogue& e) {
+  return e.residual != nullptr || e.act == ACT_DGELU || e.act == ACT_DRELU || e.act == ACT_MULAUX;
+}
+template <typename OutT>
+__device__ __forceinline__ void decode8(const uint4_t& r, float (&x)[8]) {
+  typedef OutT __attribute__((ext_vector_type(8))) v8;
+  const v8 v = __builtin_bit_cast(v8, r);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) x[j] = (float)v[j];
+}
+
 template <typename OutT>
 __device__ __forceinline__ void epilogue_store8(const Epilogue& e, OutT* __restrict__ C, long ldc, int m, int n0,
-                                                float (&v)[8]) {
+                                                float (&v)[8], bool has_pre = false,
+                                                uint4_t pre = uint4_t{0u, 0u, 0u, 0u}) {
+  // pre (has_pre): this row's 8 values of epi_stream(e), already loaded (16-bit OutT only)
+  const bool pre_aux = has_pre && (e.act == ACT_DGELU || e.act == ACT_DRELU || e.act == ACT_MULAUX);
   float x[8], t[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) x[j] = e.alpha * v[j];
@@ -168,11 +194,19 @@ __device__ __forceinline__ void epilogue_store8(const Epilogue& e, OutT* __restr
 #pragma unroll
     for (int j = 0; j < 8; ++j) x[j] = fmaxf(x[j], 0.f);
   } else if (e.act == ACT_DGELU) {
-    load8<OutT>((const OutT*)e.aux_in + (long)m * e.lda + n0, t, true);
+    if constexpr (sizeof(OutT) == 2) {
+      if (pre_aux) decode8<OutT>(pre, t); else load8<OutT>((const OutT*)e.aux_in + (long)m * e.lda + n0, t, true);
+    } else {
+      load8<OutT>((const OutT*)e.aux_in + (long)m * e.lda + n0, t, true);
+    }
 #pragma unroll
     for (int j = 0; j < 8; ++j) x[j] *= gelu_grad_for<OutT>(t[j]);
   } else if (e.act == ACT_DRELU) {
-    load8<OutT>((const OutT*)e.aux_in + (long)m * e.lda + n0, t, true);
+    if constexpr (sizeof(OutT) == 2) {
+      if (pre_aux) decode8<OutT>(pre, t); else load8<OutT>((const OutT*)e.aux_in + (long)m * e.lda + n0, t, true);
+    } else {
+      load8<OutT>((const OutT*)e.aux_in + (long)m * e.lda + n0, t, true);
+    }
 #pragma unroll
     for (int j = 0; j < 8; ++j) x[j] = t[j] > 0.f ? x[j] : 0.f;
   } else if (e.act == ACT_GELU_SAVEGRAD) {
@@ -180,7 +214,11 @@ __device__ __forceinline__ void epilogue_store8(const Epilogue& e, OutT* __restr
     for (int j = 0; j < 8; ++j) gelu_pair_for<OutT>(x[j], x[j], t[j]);
     if (e.aux_out) store8<OutT>((OutT*)e.aux_out + (long)m * e.ldo + n0, t);
   } else if (e.act == ACT_MULAUX) {
-    load8<OutT>((const OutT*)e.aux_in + (long)m * e.lda + n0, t, true);
+    if constexpr (sizeof(OutT) == 2) {
+      if (pre_aux) decode8<OutT>(pre, t); else load8<OutT>((const OutT*)e.aux_in + (long)m * e.lda + n0, t, true);
+    } else {
+      load8<OutT>((const OutT*)e.aux_in + (long)m * e.lda + n0, t, true);
+    }
 #pragma unroll
     for (int j = 0; j < 8; ++j) x[j] *= t[j];
   }
@@ -189,7 +227,12 @@ __device__ __forceinline__ void epilogue_store8(const Epilogue& e, OutT* __restr
     for (int j = 0; j < 8; ++j) x[j] *= drop_mask(e.seed, e.pdrop, m, n0 + j);
   }
   if (e.residual) {
-    load8<OutT>((const OutT*)e.residual + (long)m * e.ldr + n0, t, true);
+    if constexpr (sizeof(OutT) == 2) {
+      if (has_pre && !pre_aux) decode8<OutT>(pre, t);
+      else load8<OutT>((const OutT*)e.residual + (long)m * e.ldr + n0, t, true);
+    } else {
+      load8<OutT>((const OutT*)e.residual + (long)m * e.ldr + n0, t, true);
+    }
 #pragma unroll
     for (int j = 0; j < 8; ++j) x[j] += t[j];
   }
@@ -455,7 +498,7 @@ __device__ __forceinline__ bf16x8 frag256(const char* lds, int r0, int kk, int l
 // NA: A-operand LDS buffers.  2 = tile k+1 streams in while tile k is consumed (A and B double-buffered, 128 KiB);
 // 3 = the A tile (the HBM-streamed activation panel) is fetched TWO tiles ahead — three 32 KiB A buffers + two
 // 32 KiB B buffers = the whole 160 KiB LDS — so its longer HBM/MALL latency has two K-tiles of MFMAs to hide under.
-template <typename E, bool A_KC, bool B_KC, typename OutT, int MODE = 0, int NA = 2>
+template <typename E, bool A_KC, bool B_KC, typename OutT, int MODE = 0, int NA = 2, bool PFS = false>
 __global__ __launch_bounds__(NT2, 2) void gemm256_kernel(int M, int N, int K, const bf16* __restrict__ A, long lda,
                                                          const bf16* __restrict__ B, long ldb, OutT* __restrict__ C,
                                                          long ldc, Epilogue e, int klen, long split_stride,
@@ -640,8 +683,21 @@ __global__ __launch_bounds__(NT2, 2) void gemm256_kernel(int M, int N, int K, co
 
   // epilogue: per wave, two passes of 64x64 through a private LDS slab, 16-B stores
   float* T = (float*)(smem + wave * 64 * EPI2_LD * 4);
+  long pld = 0;
+  const OutT* const ps = PFS && sizeof(OutT) == 2 && !raw_out && !sk ? epi_stream<OutT>(e, pld) : nullptr;
 #pragma unroll
   for (int pass = 0; pass < 2; ++pass) {
+    const int cg = (lane & 7) * 8;
+    const int n0 = bn + wc * 64 + cg;
+    auto pf = [&](int it) -> uint4_t {
+      return ps ? *(const uint4_t*)(ps + (long)(bm + wr * 128 + pass * 64 + it * 8 + (lane >> 3)) * pld + n0)
+                : uint4_t{0u, 0u, 0u, 0u};
+    };
+    uint4_t p0{0u, 0u, 0u, 0u}, p1{0u, 0u, 0u, 0u};
+    if constexpr (PFS) {
+      p0 = pf(0);
+      p1 = pf(1);
+    }
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -651,10 +707,7 @@ __global__ __launch_bounds__(NT2, 2) void gemm256_kernel(int M, int N, int K, co
           T[(i * 16 + 4 * (lane >> 4) + r) * EPI2_LD + j * 16 + (lane & 15)] = acc[pass * 4 + i][j][r];
     // the slab is private to this wave and a wave's LDS operations complete in order: no workgroup barrier
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    const int cg = (lane & 7) * 8;
-    const int n0 = bn + wc * 64 + cg;
-#pragma unroll 2
-    for (int it = 0; it < 8; ++it) {
+    auto row = [&](int it, uint4_t pre) __attribute__((always_inline)) {
       const int rr = it * 8 + (lane >> 3);
       const int m = bm + wr * 128 + pass * 64 + rr;
       const floatx4 lo = *(const floatx4*)&T[rr * EPI2_LD + cg], hi = *(const floatx4*)&T[rr * EPI2_LD + cg + 4];
@@ -677,8 +730,20 @@ __global__ __launch_bounds__(NT2, 2) void gemm256_kernel(int M, int N, int K, co
         float v[8];
 #pragma unroll
         for (int j = 0; j < 4; ++j) { v[j] = lo[j]; v[4 + j] = hi[j]; }
-        epilogue_store8<OutT>(e, C, ldc, m, n0, v);
+        epilogue_store8<OutT>(e, C, ldc, m, n0, v, ps != nullptr, pre);
       }
+    };
+    if constexpr (PFS) {
+#pragma unroll 1
+      for (int it2 = 0; it2 < 8; it2 += 2) {
+        const uint4_t q0 = p0, q1 = p1;
+        if (it2 + 2 < 8) { p0 = pf(it2 + 2); p1 = pf(it2 + 3); }
+        row(it2, q0);
+        row(it2 + 1, q1);
+      }
+    } else {
+#pragma unroll 2
+      for (int it = 0; it < 8; ++it) row(it, p0);
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this pass' slab reads done before the next overwrite
   }
@@ -785,7 +850,7 @@ __device__ __forceinline__ bf16x8 frag8p_a(const char* lds, int r0, int kk, int 
 // K-split of klen (fp32 partial slabs at split_stride when raw_out, reduced by splitk_reduce_kernel), with the bias
 // gradient Σ_k A(m,k) (Epilogue::rowsum) on the same MFMA operand fragments as gemm256_kernel; the per-output
 // accumulation order (K-tile, then kk) is gemm256_kernel's, so the two kernels give identical bits.
-template <typename E, bool A_KC, bool B_KC, typename OutT>
+template <typename E, bool A_KC, bool B_KC, typename OutT, bool PFS = false>
 __global__ __launch_bounds__(NT2, 2) void gemm8p_kernel(int M, int N, int K, const bf16* __restrict__ A, long lda,
                                                         const bf16* __restrict__ B, long ldb, OutT* __restrict__ C,
                                                         long ldc, Epilogue e, int klen, long split_stride,
@@ -940,8 +1005,21 @@ __global__ __launch_bounds__(NT2, 2) void gemm8p_kernel(int M, int N, int K, con
 
   // epilogue: as gemm256_kernel — per wave, two passes of 64x64 through a private LDS slab, 16-B stores
   float* T = (float*)(smem + wave * 64 * EPI2_LD * 4);
+  long pld = 0;
+  const OutT* const ps = PFS && sizeof(OutT) == 2 && !raw_out ? epi_stream<OutT>(e, pld) : nullptr;
 #pragma unroll
   for (int pass = 0; pass < 2; ++pass) {
+    const int cg = (lane & 7) * 8;
+    const int n0 = bn + wc * 64 + cg;
+    auto pf = [&](int it) -> uint4_t {
+      return ps ? *(const uint4_t*)(ps + (long)(bm + wr * 128 + pass * 64 + it * 8 + (lane >> 3)) * pld + n0)
+                : uint4_t{0u, 0u, 0u, 0u};
+    };
+    uint4_t p0{0u, 0u, 0u, 0u}, p1{0u, 0u, 0u, 0u};
+    if constexpr (PFS) {
+      p0 = pf(0);
+      p1 = pf(1);
+    }
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -950,10 +1028,7 @@ __global__ __launch_bounds__(NT2, 2) void gemm8p_kernel(int M, int N, int K, con
         for (int r = 0; r < 4; ++r)
           T[(i * 16 + 4 * (lane >> 4) + r) * EPI2_LD + j * 16 + (lane & 15)] = acc[pass * 4 + i][j][r];
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    const int cg = (lane & 7) * 8;
-    const int n0 = bn + wc * 64 + cg;
-#pragma unroll 2
-    for (int it = 0; it < 8; ++it) {
+    auto row = [&](int it, uint4_t pre) __attribute__((always_inline)) {
       const int rr = it * 8 + (lane >> 3);
       const int m = bm + wr * 128 + pass * 64 + rr;
       const floatx4 lo = *(const floatx4*)&T[rr * EPI2_LD + cg], hi = *(const floatx4*)&T[rr * EPI2_LD + cg + 4];
@@ -967,8 +1042,20 @@ __global__ __launch_bounds__(NT2, 2) void gemm8p_kernel(int M, int N, int K, con
         float v[8];
 #pragma unroll
         for (int j = 0; j < 4; ++j) { v[j] = lo[j]; v[4 + j] = hi[j]; }
-        epilogue_store8<OutT>(e, C, ldc, m, n0, v);
+        epilogue_store8<OutT>(e, C, ldc, m, n0, v, ps != nullptr, pre);
       }
+    };
+    if constexpr (PFS) {
+#pragma unroll 1
+      for (int it2 = 0; it2 < 8; it2 += 2) {
+        const uint4_t q0 = p0, q1 = p1;
+        if (it2 + 2 < 8) { p0 = pf(it2 + 2); p1 = pf(it2 + 3); }
+        row(it2, q0);
+        row(it2 + 1, q1);
+      }
+    } else {
+#pragma unroll 2
+      for (int it = 0; it < 8; ++it) row(it, p0);
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   }
@@ -1083,9 +1170,16 @@ int launch(int M, int N, int K, const bf16* A, long lda, const bf16* B, long ldb
     const int nsplit = cdiv(K, klen);
     dim3 grid((M / TM2) * (N / TN2), 1, nsplit);
     const int plan = gemm_plan(AK, BKc, M, N, K, splits, ws != nullptr, e.rowsum != nullptr);
+  // epilogues with a streamed 16-bit operand run the PFS instantiation (the operand loaded two row groups ahead);
+  // the others keep the plain store loop (CMHAR_EPI_PF2=0: never)
+  const bool pfs = CMHAR_EPI_PF2 && sizeof(OutT) == 2 && epi_has_stream(e);
     if (plan == PLAN_256_TAIL) {
       const TailSplit ts = tail_split(M, N, K);
-      if (ph_gemm)
+      if (ph_gemm && pfs)
+        gemm256_kernel<E, AK, BKc, OutT, 0, kNA, true><<<ts.n_dp + ts.n_sk, NT2, 0, st>>>(M, N, K, A, lda, B, ldb, C, ldc,
+                                                                                      e, K, 0, 0, ws, ts.n_dp,
+                                                                                      ts.sk_klen);
+      else if (ph_gemm)
         gemm256_kernel<E, AK, BKc, OutT, 0, kNA><<<ts.n_dp + ts.n_sk, NT2, 0, st>>>(M, N, K, A, lda, B, ldb, C, ldc, e, K, 0,
                                                                                 0, ws, ts.n_dp, ts.sk_klen);
       const int tail_rows = M - ts.tail_m0;
@@ -1093,13 +1187,19 @@ int launch(int M, int N, int K, const bf16* A, long lda, const bf16* B, long ldb
         splitk_reduce_kernel<OutT><<<reduce_blocks(tail_rows, N), 256, 0, st>>>(
             tail_rows, N, ts.nsplit, ws, (long)tail_rows * N, C, ldc, e, ts.tail_m0);
     } else if (plan == PLAN_8P) {
-      if (ph_gemm) gemm8p_kernel<E, AK, BKc, OutT><<<grid, NT2, 0, st>>>(M, N, K, A, lda, B, ldb, C, ldc, e, K, 0, 0);
+      if (ph_gemm && pfs)
+        gemm8p_kernel<E, AK, BKc, OutT, true><<<grid, NT2, 0, st>>>(M, N, K, A, lda, B, ldb, C, ldc, e, K, 0, 0);
+      else if (ph_gemm)
+        gemm8p_kernel<E, AK, BKc, OutT><<<grid, NT2, 0, st>>>(M, N, K, A, lda, B, ldb, C, ldc, e, K, 0, 0);
     } else if (plan == PLAN_8P_SPLITK) {
       if (ph_gemm)
         gemm8p_kernel<E, AK, BKc, float><<<grid, NT2, 0, st>>>(M, N, K, A, lda, B, ldb, ws, N, e, klen, ss, 1);
       if (ph_red) splitk_reduce_kernel<OutT><<<reduce_blocks(M, N), 256, 0, st>>>(M, N, nsplit, ws, ss, C, ldc, e);
     } else if (plan == PLAN_256) {
-      if (ph_gemm)
+      if (ph_gemm && pfs)
+        gemm256_kernel<E, AK, BKc, OutT, 0, kNA, true><<<grid, NT2, 0, st>>>(M, N, K, A, lda, B, ldb, C, ldc, e, klen, 0, 0,
+                                                                         nullptr, 0, 0);
+      else if (ph_gemm)
         gemm256_kernel<E, AK, BKc, OutT, 0, kNA><<<grid, NT2, 0, st>>>(M, N, K, A, lda, B, ldb, C, ldc, e, klen, 0, 0, nullptr,
                                                                    0, 0);
     } else {
