@@ -145,6 +145,10 @@ __device__ __forceinline__ void store8(OutT* __restrict__ p, const float (&x)[8]
 #ifndef CMHAR_EPI_PF2
 #define CMHAR_EPI_PF2 1
 #endif
+// row groups loaded ahead (2, 4, 6 or 8; A/B knob)
+#ifndef CMHAR_EPI_PFD
+#define CMHAR_EPI_PFD 8
+#endif
 template <typename OutT>
 __device__ __forceinline__ const OutT* epi_stream(const Epilogue& e, long& ld) {
   if (e.act == ACT_DGELU || e.act == ACT_DRELU || e.act == ACT_MULAUX) { ld = e.lda; return (const OutT*)e.aux_in; }
@@ -693,11 +697,10 @@ __global__ __launch_bounds__(NT2, 2) void gemm256_kernel(int M, int N, int K, co
       return ps ? *(const uint4_t*)(ps + (long)(bm + wr * 128 + pass * 64 + it * 8 + (lane >> 3)) * pld + n0)
                 : uint4_t{0u, 0u, 0u, 0u};
     };
-    uint4_t p0{0u, 0u, 0u, 0u}, p1{0u, 0u, 0u, 0u};
-    if constexpr (PFS) {
-      p0 = pf(0);
-      p1 = pf(1);
-    }
+    constexpr int PD = CMHAR_EPI_PFD;   // row groups in flight (even, 2..8)
+    uint4_t pw[PD];                      // pw[j]: the operand of row group it2 + j (static indices only)
+#pragma unroll
+    for (int j = 0; j < PD; ++j) pw[j] = PFS ? pf(j) : uint4_t{0u, 0u, 0u, 0u};
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -736,14 +739,19 @@ __global__ __launch_bounds__(NT2, 2) void gemm256_kernel(int M, int N, int K, co
     if constexpr (PFS) {
 #pragma unroll 1
       for (int it2 = 0; it2 < 8; it2 += 2) {
-        const uint4_t q0 = p0, q1 = p1;
-        if (it2 + 2 < 8) { p0 = pf(it2 + 2); p1 = pf(it2 + 3); }
+        const uint4_t q0 = pw[0], q1 = pw[1];
+#pragma unroll
+        for (int j = 0; j + 2 < PD; ++j) pw[j] = pw[j + 2];
+        if (it2 + PD < 8) {
+          pw[PD - 2] = pf(it2 + PD);
+          pw[PD - 1] = pf(it2 + PD + 1);
+        }
         row(it2, q0);
         row(it2 + 1, q1);
       }
     } else {
 #pragma unroll 2
-      for (int it = 0; it < 8; ++it) row(it, p0);
+      for (int it = 0; it < 8; ++it) row(it, pw[0]);
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this pass' slab reads done before the next overwrite
   }
@@ -1015,11 +1023,10 @@ __global__ __launch_bounds__(NT2, 2) void gemm8p_kernel(int M, int N, int K, con
       return ps ? *(const uint4_t*)(ps + (long)(bm + wr * 128 + pass * 64 + it * 8 + (lane >> 3)) * pld + n0)
                 : uint4_t{0u, 0u, 0u, 0u};
     };
-    uint4_t p0{0u, 0u, 0u, 0u}, p1{0u, 0u, 0u, 0u};
-    if constexpr (PFS) {
-      p0 = pf(0);
-      p1 = pf(1);
-    }
+    constexpr int PD = CMHAR_EPI_PFD;   // row groups in flight (even, 2..8)
+    uint4_t pw[PD];                      // pw[j]: the operand of row group it2 + j (static indices only)
+#pragma unroll
+    for (int j = 0; j < PD; ++j) pw[j] = PFS ? pf(j) : uint4_t{0u, 0u, 0u, 0u};
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -1048,14 +1055,19 @@ __global__ __launch_bounds__(NT2, 2) void gemm8p_kernel(int M, int N, int K, con
     if constexpr (PFS) {
 #pragma unroll 1
       for (int it2 = 0; it2 < 8; it2 += 2) {
-        const uint4_t q0 = p0, q1 = p1;
-        if (it2 + 2 < 8) { p0 = pf(it2 + 2); p1 = pf(it2 + 3); }
+        const uint4_t q0 = pw[0], q1 = pw[1];
+#pragma unroll
+        for (int j = 0; j + 2 < PD; ++j) pw[j] = pw[j + 2];
+        if (it2 + PD < 8) {
+          pw[PD - 2] = pf(it2 + PD);
+          pw[PD - 1] = pf(it2 + PD + 1);
+        }
         row(it2, q0);
         row(it2 + 1, q1);
       }
     } else {
 #pragma unroll 2
-      for (int it = 0; it < 8; ++it) row(it, p0);
+      for (int it = 0; it < 8; ++it) row(it, pw[0]);
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   }
