@@ -1230,7 +1230,14 @@ __global__ __launch_bounds__(256, 2) void conv3d_fwd_rows(Geom g, int M, int Cou
     if (more) store();
     __syncthreads();
   }
-  // epilogue: fp32 tile through LDS, 8-column bf16 vectors (+ residual), then the 128-row BatchNorm tile statistics
+  // epilogue: fp32 tile through LDS, 8-column bf16 vectors (+ residual), then the 128-row BatchNorm tile statistics;
+  // the residual rows are loaded before the staging (their latency paid once, not per row)
+  uint4_t rq[TM / 32];
+#pragma unroll
+  for (int k = 0; k < TM / 32; ++k) {
+    const int m = bm + (tid >> 3) + 32 * k;
+    rq[k] = res && m < M ? *(const uint4_t*)(res + (long)m * Cout + bn + (tid & 7) * 8) : uint4_t{0u, 0u, 0u, 0u};
+  }
   float* T = (float*)smem;
 #pragma unroll
   for (int i = 0; i < 4; ++i)
@@ -1241,17 +1248,18 @@ __global__ __launch_bounds__(256, 2) void conv3d_fwd_rows(Geom g, int M, int Cou
         T[(64 * wr + 16 * i + 4 * (lane >> 4) + r) * ELD + 16 * JB * wc + 16 * j + (lane & 15)] = acc[i][j][r];
   __syncthreads();
   const int cg = (tid & 7) * 8;
-  for (int rr = tid >> 3; rr < TM; rr += NT / 8) {
+#pragma unroll
+  for (int k = 0; k < TM / 32; ++k) {
+    const int rr = (tid >> 3) + 32 * k;
     const int m = bm + rr;
     if (m >= M) break;
     float v[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) v[j] = T[rr * ELD + cg + j];
     if (res) {
-      float q[8];
-      vload<bf16, 8>(res + (long)m * Cout + bn + cg, q);
+      const bf16x8 q = __builtin_bit_cast(bf16x8, rq[k]);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] += q[j];
+      for (int j = 0; j < 8; ++j) v[j] += (float)q[j];
     }
     zstore8(z + (long)m * Cout + bn + cg, v);
   }
@@ -1382,6 +1390,15 @@ __global__ __launch_bounds__(256, 2) void conv3d_fwd_rows3(Geom g, int R, int Ls
     __syncthreads();
   }
   float* T = (float*)smem;
+  const int cg = (tid & 7) * 8;
+  // the residual (dgrad's dx_acc) rows of this thread, loaded before the accumulator staging: each load's latency
+  // is then paid once, not once per row in the store loop (as the GEMM epilogues' streamed operands)
+  uint4_t rq[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const int rr = (tid >> 3) + 32 * k;
+    rq[k] = res && rr < used ? *(const uint4_t*)(res + (m0 + rr) * TN + cg) : uint4_t{0u, 0u, 0u, 0u};
+  }
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -1389,17 +1406,18 @@ __global__ __launch_bounds__(256, 2) void conv3d_fwd_rows3(Geom g, int R, int Ls
 #pragma unroll
       for (int r = 0; r < 4; ++r) T[(64 * wave + 16 * i + 4 * (lane >> 4) + r) * ELD + 16 * j + (lane & 15)] = acc[i][j][r];
   __syncthreads();
-  const int cg = (tid & 7) * 8;
-  for (int rr = tid >> 3; rr < used; rr += NT / 8) {
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const int rr = (tid >> 3) + 32 * k;
+    if (rr >= used) break;
     const long m = m0 + rr;
     float v[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) v[j] = T[rr * ELD + cg + j];
     if (res) {
-      float q[8];
-      vload<bf16, 8>(res + m * TN + cg, q);
+      const bf16x8 q = __builtin_bit_cast(bf16x8, rq[k]);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] += q[j];
+      for (int j = 0; j < 8; ++j) v[j] += (float)q[j];
     }
     zstore8(z + m * TN + cg, v);
   }
