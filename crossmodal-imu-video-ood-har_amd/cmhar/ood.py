@@ -51,13 +51,10 @@ def auroc(in_scores, out_scores) -> float:
     order = np.argsort(allv, kind='mergesort')
     ranks = np.empty(allv.size, dtype=np.float64)
     sv = allv[order]
-    i = 0
-    while i < sv.size:                          # average ranks over tied runs
-        j = i
-        while j + 1 < sv.size and sv[j + 1] == sv[i]:
-            j += 1
-        ranks[order[i:j + 1]] = 0.5 * (i + j) + 1.0
-        i = j + 1
+    new_run = np.r_[True, sv[1:] != sv[:-1]]    # average ranks over tied runs, vectorised (O(n log n) overall)
+    starts = np.flatnonzero(new_run)
+    ends = np.r_[starts[1:], sv.size] - 1
+    ranks[order] = (0.5 * (starts + ends) + 1.0)[np.cumsum(new_run) - 1]
     u = ranks[:a.size].sum() - a.size * (a.size + 1) / 2.0
     return float(u / (a.size * b.size))
 

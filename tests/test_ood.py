@@ -20,6 +20,30 @@ def test_auroc_matches_sklearn_with_ties():
     assert auroc([2.0], [1.0]) == 1.0 and auroc([1.0], [2.0]) == 0.0 and auroc([1.0], [1.0]) == 0.5
 
 
+@pytest.mark.parametrize('n_in,n_out,decimals', [(1, 5000, 2), (20000, 30000, 1), (50000, 7, 3), (4096, 4096, 0)])
+def test_auroc_large_and_lopsided_vs_sklearn(n_in, n_out, decimals):
+    """Eval-stream sizes (tens of thousands of clips, one side tiny), heavy ties from rounding."""
+    from sklearn.metrics import roc_auc_score
+    from cmhar.ood import auroc
+    rng = np.random.default_rng(n_in + n_out)
+    a = np.round(rng.normal(0.5, 1.0, n_in), decimals)
+    b = np.round(rng.normal(0.0, 1.0, n_out), decimals)
+    want = roc_auc_score(np.r_[np.ones(n_in), np.zeros(n_out)], np.r_[a, b])
+    assert abs(auroc(a, b) - want) < 1e-12
+
+
+def test_auroc_edge_cases():
+    from cmhar.ood import auroc
+    assert auroc(np.full(7, 3.0), np.full(9, 3.0)) == 0.5            # one tied run across both sets
+    assert auroc(np.arange(10.0) + 10, np.arange(10.0)) == 1.0       # perfect separation
+    assert auroc(np.arange(10.0), np.arange(10.0) + 10) == 0.0
+    assert auroc(np.ones((2, 3)), np.zeros((3, 1))) == 1.0           # any shape, flattened
+    with pytest.raises(ValueError):
+        auroc([], [1.0])
+    with pytest.raises(ValueError):
+        auroc([1.0], np.zeros(0))
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize('dtype', [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize('C', [1, 7, 32, 1000])
