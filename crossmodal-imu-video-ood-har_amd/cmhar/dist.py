@@ -168,6 +168,7 @@ class GradReducer:
         self.sink = None
         self.pending = []
         self.active = False
+        self._next = 0                              # first bucket not yet launched (reset by start_step)
         self.buckets: List[_Bucket] = []
         self.limit = max(int(bucket_mb * (1 << 20) / 4), 1)
         sink_params = set()
@@ -175,6 +176,7 @@ class GradReducer:
             order = sink_param_order(backbone)
             self.sink = FlatGradSink(order, order[0].device, on_ready=self._on_sink_ready)
             backbone._grad_sink = self.sink
+            self._sink_owner = backbone
             cur, start = [], 0
             for p in self.sink.order:               # cut the flat buffer at parameter boundaries
                 cur.append(p)
@@ -218,12 +220,15 @@ class GradReducer:
         b = self.buckets[bi]
         if b.launched:
             raise RuntimeError('a parameter received a second gradient contribution after its bucket was '
-                               'all-reduced (parameter used twice in one step); not supported by GradReducer')
+                               'all-reduced: a second backward inside one start_step()/finish() window (gradient '
+                               'accumulation) or a parameter used twice in one step; not supported by GradReducer')
         b.ready.add(p)
         self._launch_ready()
 
     def _on_sink_ready(self, params):
-        if not self._reduce:
+        # a backward outside a start_step()/finish() window (after finish() or close(), an evaluation backward)
+        # leaves its gradients local: launching buckets from it would start an all-reduce on this rank only
+        if not self._reduce or not self.active:
             return
         for p in params:
             self._mark(p)
@@ -245,6 +250,8 @@ class GradReducer:
             b = self.buckets[self._next]
             if len(b.ready) != len(b.params):
                 return
+            if b.kind == 'hook' and not self.learned:
+                return     # learning step: hook buckets wait for finish(), which first checks the ranks agree
             self._launch(b)
             self._next += 1
 
@@ -296,6 +303,7 @@ class GradReducer:
         if not self._reduce:
             return
         self.launched_before_finish = self._next
+        orders = None if self.learned else self._gather_fired()
         for b in self.buckets[self._next:]:
             self._launch(b)
         self._next = len(self.buckets)
@@ -313,21 +321,36 @@ class GradReducer:
                     off += n
         if dst:
             torch._foreach_copy_(dst, src)     # the reduced values back into .grad: one multi-tensor launch
-        if not self.learned:
-            self._learn_order()
+        if orders is not None:
+            self._learn_order(orders)
 
-    def _learn_order(self):
-        """Rebuild the hook buckets in rank 0's observed gradient order (identical on every rank)."""
+    def _gather_fired(self):
+        """Every rank's observed hook order of the learning step.  The ranks must agree on WHICH parameters
+        received a gradient (as under DataParallel) — otherwise their hook buckets would differ in size and the
+        all-reduce would hang — so a mismatch raises here, before any hook bucket is launched."""
         index = {p: i for i, p in enumerate(self.rest)}
         seen, order = set(), []
         for p in self._fired:
             if p not in seen:
                 seen.add(p)
                 order.append(index[p])
-        obj = [order]
-        dist.broadcast_object_list(obj, src=0 if self.group is None else dist.get_global_rank(self.group, 0),
-                                   group=self.group)
-        order = obj[0]
+        orders = [None] * self.world
+        dist.all_gather_object(orders, order, group=self.group)
+        ref = set(orders[0])
+        for r, o in enumerate(orders):
+            if set(o) != ref:
+                self._fired = []
+                for w in self.pending:     # the sink buckets' all-reduces (identical on every rank) complete
+                    w.wait()
+                self.pending = []
+                raise RuntimeError(f'GradReducer: rank {r} produced gradients for a different parameter set than '
+                                   f'rank 0 in its first step ({len(o)} vs {len(ref)} parameters); every rank must '
+                                   f'compute gradients for the same parameters')
+        return orders
+
+    def _learn_order(self, orders):
+        """Rebuild the hook buckets in rank 0's observed gradient order (identical on every rank)."""
+        order = orders[0]
         fired = [self.rest[i] for i in order]
         fired_set = set(fired)
         never = [p for p in reversed(self.rest) if p not in fired_set]
@@ -342,6 +365,11 @@ class GradReducer:
         for h in self._hooks:
             h.remove()
         self._hooks = []
+        self.active = False
+        if self.sink is not None:      # detach the flat sink: the backbone allocates its own gradients again
+            self.sink.on_ready = None
+            if getattr(self._sink_owner, '_grad_sink', None) is self.sink:
+                self._sink_owner._grad_sink = None
 
 
 def broadcast_parameters(model: torch.nn.Module, src: int = 0, group=None):

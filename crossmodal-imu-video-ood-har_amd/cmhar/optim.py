@@ -79,15 +79,18 @@ class FusedAdamW(torch.optim.Optimizer):
     parameters; those copies are rewritten in the same pass.
 
     `max_grad_norm` (opt-in): `step()` first performs trainer.py:140's `clip_grad_norm_(params, max_grad_norm)` over
-    every parameter of the optimizer that has a gradient — the norm pass as in `clip_grad_norm_`, but the clip
+    `clip_params` (the reference clips over `model.parameters()`, trainer.py:140/304 — the trainers pass exactly that;
+    default: every parameter of the optimizer) that have a gradient — the norm pass as in `clip_grad_norm_`, but the clip
     coefficient is applied inside the AdamW pass instead of by a separate in-place scale pass over the gradients
     (one read + one write of every gradient less).  The update is bit-identical to clip-then-step.  With
     `write_clipped_grad=True` (default) the AdamW pass also stores the clipped gradient back, so `.grad` after the
     step is exactly what `clip_grad_norm_` leaves; `False` leaves `.grad` unclipped (saves that write too).  The
-    total norm of the last step is `last_grad_norm` (0-dim device tensor, as `clip_grad_norm_` returns)."""
+    total norm of the last step is `last_grad_norm` (0-dim device tensor, as `clip_grad_norm_` returns).
+    Gradients in `clip_params` that the optimizer does not own enter the norm and are scaled in place by the clip
+    coefficient (one multi-tensor multiply), exactly as `clip_grad_norm_` would leave them."""
 
     def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-2, shadow_sources=(),
-                 max_grad_norm=None, write_clipped_grad=True):
+                 max_grad_norm=None, write_clipped_grad=True, clip_params=None):
         defaults = dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay)
         super().__init__(params, defaults)
         self.shadow_sources = list(shadow_sources)
@@ -95,6 +98,7 @@ class FusedAdamW(torch.optim.Optimizer):
         self.max_grad_norm = max_grad_norm
         self.write_clipped_grad = bool(write_clipped_grad)
         self.last_grad_norm = None
+        self.clip_params = None if clip_params is None else list(clip_params)
 
     def _slots(self):
         slots = {}
@@ -115,11 +119,19 @@ class FusedAdamW(torch.optim.Optimizer):
         slots, packs = self._slots()
         gscale = None
         if self.max_grad_norm is not None:
-            allp = [p for g in self.param_groups for p in g['params'] if p.grad is not None]
+            owned = [p for g in self.param_groups for p in g['params'] if p.grad is not None]
+            if self.clip_params is None:
+                allp, extra = owned, []
+            else:
+                ids = {id(p) for p in owned}
+                allp = [p for p in self.clip_params if p.grad is not None]
+                extra = [p.grad for p in allp if id(p) not in ids]
             if allp:
                 norm_out = _grad_norm(allp, float(self.max_grad_norm), apply_clip=False)
                 self.last_grad_norm = norm_out[0]
                 gscale = norm_out
+                if extra:      # clipped like clip_grad_norm_ leaves them; the owned ones inside the AdamW pass
+                    torch._foreach_mul_(extra, norm_out[1])
         for gi, group in enumerate(self.param_groups):
             b1, b2 = group['betas']
             lr, eps, wd = group['lr'], group['eps'], group['weight_decay']

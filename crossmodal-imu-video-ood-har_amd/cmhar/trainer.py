@@ -113,7 +113,8 @@ class CrossModalTrainer(BaseTrainer):
         # (bit-identical update and post-clip .grad; one scale pass over the gradients less)
         self.optimizer = FusedAdamW(self.model.parameters(), lr=config.training.pretrain_lr,
                                     weight_decay=config.training.pretrain_weight_decay,
-                                    shadow_sources=_shadow_sources(self.model), max_grad_norm=1.0)
+                                    shadow_sources=_shadow_sources(self.model), max_grad_norm=1.0,
+                                    clip_params=self.model.parameters())
         num_epochs = int(config.training.pretrain_epochs)
         warmup_epochs = int(getattr(config.training, 'pretrain_warmup_epochs', 0))
         if warmup_epochs <= 0:
@@ -228,7 +229,8 @@ class ClassificationTrainer(BaseTrainer):
             for p in model.imu_encoder.parameters():
                 p.requires_grad = False
             self.optimizer = FusedAdamW(model.classifier.parameters(), lr=config.training.train_lr_head,
-                                        weight_decay=config.training.pretrain_weight_decay, max_grad_norm=1.0)
+                                        weight_decay=config.training.pretrain_weight_decay, max_grad_norm=1.0,
+                                        clip_params=model.parameters())
         else:
             if hasattr(model, 'unfreeze_encoder'):
                 model.unfreeze_encoder()
@@ -238,7 +240,8 @@ class ClassificationTrainer(BaseTrainer):
             self.optimizer = FusedAdamW(
                 [{'params': model.imu_encoder.parameters(), 'lr': config.training.train_lr_encoder},
                  {'params': model.classifier.parameters(), 'lr': config.training.train_lr_head}],
-                weight_decay=config.training.pretrain_weight_decay, max_grad_norm=1.0)
+                weight_decay=config.training.pretrain_weight_decay, max_grad_norm=1.0,
+                clip_params=model.parameters())
         self.scheduler = CosineAnnealingLR(self.optimizer, T_max=max(int(config.training.train_epochs), 1),
                                            eta_min=1e-7)
 

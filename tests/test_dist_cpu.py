@@ -244,3 +244,54 @@ def _bucket_worker(rank, world, port):
 
 def test_grad_reducer_buckets_overlap_and_sum():
     _spawn(_bucket_worker)
+
+
+# ---------------------------------------------------------------------------------------------------------------
+def _lifecycle_worker(rank, world, port):
+    """a sink backward before the first start_step(), after finish() and after close() stays local
+    (no bucket launched, no AttributeError, no 'used twice' error); a parameter-set mismatch between ranks in the
+    learning step raises instead of hanging the next all-reduce."""
+    _init(rank, world, port)
+    from cmhar.dist import GradReducer
+    from cmhar.videomae import VideoMAEBackbone, default_videomae_config
+    cfg = default_videomae_config(image_size=16, patch_size=8, num_frames=4, hidden_size=32, num_hidden_layers=1,
+                                  num_attention_heads=2, intermediate_size=64)
+    torch.manual_seed(0)
+
+    class Wrap(nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.backbone = VideoMAEBackbone(cfg, compute_dtype='fp32')
+            self.head = nn.Linear(32, 3)
+            self.extra = nn.Linear(3, 3)
+
+    model = Wrap()
+    reducer = GradReducer(model, backbone=model.backbone, bucket_mb=0.01)
+    sink = reducer.sink
+
+    def sink_backward():
+        for p in sink.order:
+            dst, _ = sink.dest([p], p.shape, 'cpu')
+            dst.fill_(1.0)
+            sink.done([p])
+
+    sink_backward()                       # before any start_step(): gradients stay local
+    assert reducer.n_collectives == 0 and not any(b.launched for b in reducer.buckets)
+    reducer.start_step()
+    sink_backward()
+    x = torch.randn(4, 32)
+    out = model.head(x)
+    if rank == 0:
+        out = model.extra(out)            # rank 1 never produces gradients for `extra`
+    out.sum().backward()
+    with pytest.raises(RuntimeError, match='different parameter set'):
+        reducer.finish()
+    sink_backward()                       # after finish(): local, no error
+    reducer.close()
+    assert model.backbone._grad_sink is None and sink.on_ready is None
+    sink_backward()                       # after close(): local, no error
+    dist.destroy_process_group()
+
+
+def test_grad_reducer_lifecycle_outside_step_window():
+    _spawn(_lifecycle_worker)

@@ -594,3 +594,28 @@ def test_attention_bf16_storage_small_head(D):
     dq, dk, dv = (torch.empty_like(o) for _ in range(3))
     K().attention_bwd(q, k, v, o, do, lse, dq, dk, dv, B=B, H=H, Lq=L_, Lk=L_, D=D, scale=scale)
     assert rel(dq, gq) < 1e-2 and rel(dk, gk) < 1e-2 and rel(dv, gv) < 1e-2
+
+
+def test_fused_adamw_clip_params_beyond_owned():
+    """`clip_params` (the trainers pass model.parameters(), as trainer.py:140/304 clip over them) enter the
+    norm even when the optimizer does not own them, and their `.grad` is clipped like clip_grad_norm_ leaves it;
+    the owned parameters' update is bit-identical to clip_grad_norm_(all) + step."""
+    from cmhar.optim import FusedAdamW, clip_grad_norm_
+    torch.manual_seed(12)
+    base = [torch.randn(s, device=DEV) for s in [(300, 77), (1000,), (3, 5, 7), (4099,)]]
+    ours = [torch.nn.Parameter(p.clone()) for p in base]
+    theirs = [torch.nn.Parameter(p.clone()) for p in base]
+    opt_a = FusedAdamW(ours[:2], lr=1e-3, weight_decay=0.01, max_grad_norm=1.0, clip_params=ours)
+    opt_b = FusedAdamW(theirs[:2], lr=1e-3, weight_decay=0.01)
+    for step in range(2):
+        grads = [torch.randn_like(a) * 10 for a in ours]
+        for a, b, g in zip(ours, theirs, grads):
+            a.grad, b.grad = g.clone(), g.clone()
+        opt_a.step()
+        nb = clip_grad_norm_(theirs, 1.0)
+        opt_b.step()
+        assert opt_a.last_grad_norm.item() == nb.item()
+        for a, b in zip(ours, theirs):
+            assert torch.equal(a.grad, b.grad)
+    for a, b in zip(ours, theirs):
+        assert torch.equal(a, b)
