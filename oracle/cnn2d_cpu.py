@@ -8,7 +8,9 @@ then `F.adaptive_avg_pool2d(fmap, 1)` → `view(B, T, F)` → `projection` (Line
 with the (t, c, n, s) table, Conv2dNormActivation = Conv2d + BN + ReLU6; BN eps 1e-5, momentum 0.1) with
 `F.conv2d` / `F.batch_norm` / `F.max_pool2d` / `F.relu6` on parameters from a `cmhar.cnn2d` state_dict (torchvision
 key names).  Parity unpinned w.r.t. the reference (no torchvision to import, no reference fixtures for this branch).
-`q` (optional, e.g. `oracle.r3d_cpu.bf16_storage`) is applied where the HIP bf16 path stores tensors in bf16.
+`q` (optional, e.g. `oracle.r3d_cpu.bf16_storage`) is applied where the HIP bf16 path stores tensors in bf16; `qw`
+(optional, `oracle.r3d_cpu.bf16_weight`) to the dense conv weights, which that path multiplies as bf16 packs (the
+depthwise kernels read the fp32 weights).
 """
 from __future__ import annotations
 
@@ -28,22 +30,23 @@ def _bn(x, sd, pre, training, stats):
     return y
 
 
-def resnet18_features(sd, frames, training=True, stats=None, q=None):
+def resnet18_features(sd, frames, training=True, stats=None, q=None, qw=None):
     """frames (N, 3, H, W) → feature map (N, 512, h, w); sd keys as `nn.Sequential(*resnet18().children()[:-2])`."""
     stats = {} if stats is None else stats
     q = q or _id
-    x = q(F.conv2d(q(frames), sd['0.weight'], stride=2, padding=3))
+    qw = qw or _id
+    x = q(F.conv2d(q(frames), qw(sd['0.weight']), stride=2, padding=3))
     x = q(F.relu(_bn(x, sd, '1.', training, stats)))
     x = q(F.max_pool2d(x, 3, 2, 1))
     for li in range(4):
         for bi in range(2):
             p = f'{4 + li}.{bi}.'
             stride = 2 if (li > 0 and bi == 0) else 1
-            h = q(F.relu(_bn(q(F.conv2d(x, sd[p + 'conv1.weight'], stride=stride, padding=1)), sd, p + 'bn1.',
+            h = q(F.relu(_bn(q(F.conv2d(x, qw(sd[p + 'conv1.weight']), stride=stride, padding=1)), sd, p + 'bn1.',
                              training, stats)))
-            h = _bn(q(F.conv2d(h, sd[p + 'conv2.weight'], padding=1)), sd, p + 'bn2.', training, stats)
+            h = _bn(q(F.conv2d(h, qw(sd[p + 'conv2.weight']), padding=1)), sd, p + 'bn2.', training, stats)
             if p + 'downsample.0.weight' in sd:
-                idn = q(_bn(q(F.conv2d(x, sd[p + 'downsample.0.weight'], stride=stride)), sd, p + 'downsample.1.',
+                idn = q(_bn(q(F.conv2d(x, qw(sd[p + 'downsample.0.weight']), stride=stride)), sd, p + 'downsample.1.',
                             training, stats))
             else:
                 idn = x
@@ -51,13 +54,14 @@ def resnet18_features(sd, frames, training=True, stats=None, q=None):
     return x
 
 
-def mobilenet_v2_features(sd, frames, training=True, stats=None, q=None):
+def mobilenet_v2_features(sd, frames, training=True, stats=None, q=None, qw=None):
     """frames (N, 3, H, W) → feature map (N, 1280, h, w); sd keys as `mobilenet_v2().features`."""
     stats = {} if stats is None else stats
     q = q or _id
+    qw = qw or _id
 
     def cna(x, pre, stride=1, groups=1):
-        w = sd[pre + '0.weight']
+        w = sd[pre + '0.weight'] if groups > 1 else qw(sd[pre + '0.weight'])
         x = q(F.conv2d(x, w, stride=stride, padding=(w.shape[-1] - 1) // 2, groups=groups))
         return q(F.relu6(_bn(x, sd, pre + '1.', training, stats)))
 
@@ -74,7 +78,7 @@ def mobilenet_v2_features(sd, frames, training=True, stats=None, q=None):
                 k = 1
             hidden = cin * t
             h = cna(h, f'{p}{k}.', stride=stride, groups=hidden)
-            h = q(F.conv2d(h, sd[f'{p}{k + 1}.weight']))
+            h = q(F.conv2d(h, qw(sd[f'{p}{k + 1}.weight'])))
             h = _bn(h, sd, f'{p}{k + 2}.', training, stats)
             x = q(x + h if (stride == 1 and cin == c) else h)
             cin = c
@@ -82,13 +86,13 @@ def mobilenet_v2_features(sd, frames, training=True, stats=None, q=None):
     return cna(x, f'{i}.')
 
 
-def video_encoder_cnn(sd, video, backbone, training=True, stats=None, q=None):
+def video_encoder_cnn(sd, video, backbone, training=True, stats=None, q=None, qw=None):
     """models.py:208-216 on a whole `VideoEncoder` state_dict (keys `backbone.*`, `projection.*`):
     video (B, T, C, H, W) → (B, video_d_model)."""
     B, T, C, H, W = video.shape
     bsd = {k[len('backbone.'):]: v for k, v in sd.items() if k.startswith('backbone.')}
     f = resnet18_features if backbone == 'resnet18' else mobilenet_v2_features
-    fmap = f(bsd, video.reshape(B * T, C, H, W), training, stats, q)
+    fmap = f(bsd, video.reshape(B * T, C, H, W), training, stats, q, qw)
     feats = F.adaptive_avg_pool2d(fmap, (1, 1)).squeeze(-1).squeeze(-1).view(B, T, -1)
     feats = F.linear(feats, sd['projection.weight'], sd['projection.bias'])
     return feats.transpose(1, 2).mean(-1)

@@ -136,7 +136,7 @@ def oracle_step(backbone, init_sd, cfg, imu_all, video_all, world, bl, bf16):
         sys.path.insert(0, d)
     from fixtures import oracle_mcfg
     from oracle import cpu_model as O
-    from oracle.r3d_cpu import bf16_storage, r3d18_features
+    from oracle.r3d_cpu import BF16, r3d18_features
     sd = {k: (v.clone().requires_grad_(True) if v.is_floating_point() and 'running' not in k else v.clone())
           for k, v in init_sd.items()}
     mc = oracle_mcfg(cfg)
@@ -150,7 +150,7 @@ def oracle_step(backbone, init_sd, cfg, imu_all, video_all, world, bl, bf16):
         bsd = {k[len(pre):]: v for k, v in sd.items() if k.startswith(pre)}
         cls, _ = O.imu_encoder(sd, imu, patch_size=mc['imu_patch_size'], stride=mc['imu_stride'],
                                nhead=mc['imu_nhead'], num_layers=mc['imu_num_layers'])
-        feat = r3d18_features(bsd, video.transpose(1, 2), training=True, q=bf16_storage if bf16 else None)
+        feat = r3d18_features(bsd, video.transpose(1, 2), training=True, **(BF16 if bf16 else {}))
         vf = F.linear(feat, sd['video_encoder.projection.weight'], sd['video_encoder.projection.bias'])
         outs.append((O.l2_normalize(O.projection_head(sd, cls, 'imu_proj.', True)),
                      O.l2_normalize(O.projection_head(sd, vf, 'video_proj.', True))))

@@ -132,7 +132,7 @@ def test_bn_channels_last_any_width_relu6(C, act, res):
 def _case(backbone, dtype, training=True, B=2, T=2, S=64, emulate=False, fp64=False):
     from cmhar.cnn2d import MobileNetV2Features, ResNet18Features, run_cnn2d
     from oracle import cnn2d_cpu as O
-    from oracle.r3d_cpu import bf16_storage
+    from oracle.r3d_cpu import bf16_storage, bf16_weight
     torch.manual_seed(3)
     m = (ResNet18Features if backbone == 'resnet18' else MobileNetV2Features)(compute_dtype=dtype)
     with torch.no_grad():
@@ -147,11 +147,11 @@ def _case(backbone, dtype, training=True, B=2, T=2, S=64, emulate=False, fp64=Fa
     R = torch.randn(B * T, m.feature_dim)
     f = O.resnet18_features if backbone == 'resnet18' else O.mobilenet_v2_features
 
-    def oracle(q, dt=torch.float32):
+    def oracle(q, dt=torch.float32, qw=None):
         sd_p = {k: (v.clone().to(dt).requires_grad_(True) if v.is_floating_point() and 'running' not in k
                     else (v.clone().to(dt) if v.is_floating_point() else v.clone())) for k, v in sd.items()}
         stats = {}
-        ref = f(sd_p, video.reshape(B * T, 3, S, S).to(dt), training, stats, q).mean(dim=(2, 3))
+        ref = f(sd_p, video.reshape(B * T, 3, S, S).to(dt), training, stats, q, qw).mean(dim=(2, 3))
         (ref * R.to(dt)).sum().backward()
         return sd_p, stats, ref
 
@@ -161,7 +161,7 @@ def _case(backbone, dtype, training=True, B=2, T=2, S=64, emulate=False, fp64=Fa
     (feat * R.to(DEV)).sum().backward()
     out = [m, sd_p, stats, ref, feat]
     if emulate:
-        out.append(oracle(bf16_storage))
+        out.append(oracle(bf16_storage, qw=bf16_weight))
     if fp64:
         out.append(oracle(None, torch.float64))
     return tuple(out)

@@ -2,7 +2,9 @@
 against the CPU restatement oracle/fusion_cpu.py on identical weights and inputs.
 
 fp32 mode: logits / fused ≤ 1e-5 rel, every parameter and input gradient ≤ 1e-4 rel.  bf16 mode (K|V projection and
-flash attention on MFMA): logits ≤ 2e-2 rel, gradients ≤ 5e-2 rel.  Ragged sizes: Lq = 13 IMU tokens (CLS + 12
+flash attention on MFMA): every output / gradient within 3× the error bf16 STORAGE itself causes for it (the oracle
+re-run with the bf16 path's storage emulated, `fusion_forward(..., bf16=True)`) + 1e-3 (outputs) / 2e-3 (gradients),
+the bounds of the VideoMAE bf16 tests (round 3 used blanket 2e-2 / 5e-2).  Ragged sizes: Lq = 13 IMU tokens (CLS + 12
 patches of a 200-step window), Lk = 392 / 200 video tokens (not multiples of the attention tiles)."""
 import pytest
 import torch
@@ -16,30 +18,56 @@ def rel(a, b):
     return ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
 
 
+def _oracle_run(sd0, imu0, vid0, R, bf16, num_heads=4):
+    """fusion_forward on fresh leaf copies → (logits, fused, {param: grad}, imu grad, video grad)."""
+    from oracle.fusion_cpu import fusion_forward
+    sd = {k: v.detach().clone().requires_grad_(True) for k, v in sd0.items()}
+    imu = imu0.detach().clone().requires_grad_(True)
+    vid = vid0.detach().clone().requires_grad_(True)
+    logits, fused = fusion_forward(sd, imu, vid, num_heads, bf16=bf16)
+    (logits * R).sum().backward()
+    return logits.detach(), fused.detach(), {k: v.grad for k, v in sd.items()}, imu.grad, vid.grad
+
+
+def _check_fusion(m, dtype, B, Lq, Lk, seed):
+    torch.manual_seed(seed)
+    sd = {k: v.clone() for k, v in m.state_dict().items()}
+    imu = torch.randn(B, Lq, 128)
+    vid = torch.randn(B, Lk, 768)
+    R = torch.randn(B, 32)
+    ref = _oracle_run(sd, imu, vid, R, False)
+    m = m.to(DEV)
+    imu_g = imu.to(DEV).requires_grad_(True)
+    vid_g = vid.to(DEV).requires_grad_(True)
+    logits, fused = m(imu_g, vid_g)
+    (logits * R.to(DEV)).sum().backward()
+    got = (logits, fused, {k: p.grad for k, p in m.named_parameters()}, imu_g.grad, vid_g.grad)
+    if dtype == 'fp32':
+        emu, slack, f_out, f_grad = None, 0.0, 1e-5, 1e-4
+    else:
+        emu, slack, f_out, f_grad = _oracle_run(sd, imu, vid, R, True), 3.0, 1e-3, 2e-3
+    names = ['logits', 'fused', None, 'imu.grad', 'video.grad']
+    rows = []
+    for i, nm in enumerate(names):
+        if nm is None:
+            for k in got[2]:
+                e_emu = rel(emu[2][k], ref[2][k]) if emu is not None else 0.0
+                rows.append((k, rel(got[2][k], ref[2][k]), slack * e_emu + f_grad))
+            continue
+        e_emu = rel(emu[i], ref[i]) if emu is not None else 0.0
+        rows.append((nm, rel(got[i], ref[i]), slack * e_emu + (f_out if i < 2 else f_grad)))
+    bad = [r for r in rows if not r[1] <= r[2]]
+    assert not bad, bad
+    return rows
+
+
 @pytest.mark.parametrize('dtype,Lk,B', [('fp32', 392, 3), ('bf16', 392, 3), ('bf16', 200, 5)])
 def test_fusion_matches_oracle(dtype, Lk, B):
     from cmhar.fusion import CrossAttentionFusion
-    from oracle.fusion_cpu import fusion_forward
     torch.manual_seed(0)
     m = CrossAttentionFusion(128, 768, 256, 4, 32, compute_dtype=dtype)
-    sd = {k: v.clone().requires_grad_(True) for k, v in m.state_dict().items()}
-    imu = torch.randn(B, 13, 128, requires_grad=True)
-    vid = torch.randn(B, Lk, 768, requires_grad=True)
-    R = torch.randn(B, 32)
-    logits_ref, fused_ref = fusion_forward(sd, imu, vid, 4)
-    (logits_ref * R).sum().backward()
-    m = m.to(DEV)
-    imu_g = imu.detach().to(DEV).requires_grad_(True)
-    vid_g = vid.detach().to(DEV).requires_grad_(True)
-    logits, fused = m(imu_g, vid_g)
-    (logits * R.to(DEV)).sum().backward()
-    tol_f, tol_g = (1e-5, 1e-4) if dtype == 'fp32' else (2e-2, 5e-2)
-    assert rel(logits, logits_ref) < tol_f
-    assert rel(fused, fused_ref) < tol_f
-    assert rel(imu_g.grad, imu.grad) < tol_g
-    assert rel(vid_g.grad, vid.grad) < tol_g
-    for k, p in m.named_parameters():
-        assert rel(p.grad, sd[k].grad) < tol_g, (k, rel(p.grad, sd[k].grad))
+    rows = _check_fusion(m, dtype, B, 13, Lk, seed=1)
+    print(dtype, Lk, 'worst (err, bound):', sorted(rows, key=lambda r: r[1] / r[2], reverse=True)[:3])
 
 
 @pytest.mark.parametrize('dtype', ['fp32', 'bf16', 'fp16'])
@@ -53,30 +81,19 @@ def test_fusion_config4_geometry(dtype):
     B, Lq, Lk = 2, 26, 3136
     torch.manual_seed(3)
     m = CrossAttentionFusion(128, 768, 256, 4, 32, compute_dtype=dtype)
-    sd = {k: v.clone().requires_grad_(True) for k, v in m.state_dict().items()}
-    imu = torch.randn(B, Lq, 128, requires_grad=True)
-    vid = torch.randn(B, Lk, 768, requires_grad=True)
-    R = torch.randn(B, 32)
+    if dtype != 'fp16':
+        rows = _check_fusion(m, dtype, B, Lq, Lk, seed=4)
+        print(dtype, 'worst (err, bound):', sorted(rows, key=lambda r: r[1] / r[2], reverse=True)[:3])
+        return
+    sd = {k: v.clone() for k, v in m.state_dict().items()}
+    imu = torch.randn(B, Lq, 128)
+    vid = torch.randn(B, Lk, 768)
     logits_ref, fused_ref = fusion_forward(sd, imu, vid, 4)
     m = m.to(DEV)
-    if dtype == 'fp16':
-        with torch.no_grad():
-            logits, fused = m(imu.detach().to(DEV), vid.detach().to(DEV))
-        assert rel(logits, logits_ref) < 5e-3, rel(logits, logits_ref)
-        assert rel(fused, fused_ref) < 5e-3, rel(fused, fused_ref)
-        return
-    (logits_ref * R).sum().backward()
-    imu_g = imu.detach().to(DEV).requires_grad_(True)
-    vid_g = vid.detach().to(DEV).requires_grad_(True)
-    logits, fused = m(imu_g, vid_g)
-    (logits * R.to(DEV)).sum().backward()
-    tol_f, tol_g = (1e-5, 1e-4) if dtype == 'fp32' else (2e-2, 5e-2)
-    assert rel(logits, logits_ref) < tol_f
-    assert rel(fused, fused_ref) < tol_f
-    assert rel(imu_g.grad, imu.grad) < tol_g
-    assert rel(vid_g.grad, vid.grad) < tol_g
-    for k, p in m.named_parameters():
-        assert rel(p.grad, sd[k].grad) < tol_g, (k, rel(p.grad, sd[k].grad))
+    with torch.no_grad():
+        logits, fused = m(imu.to(DEV), vid.to(DEV))
+    assert rel(logits, logits_ref) < 5e-3, rel(logits, logits_ref)
+    assert rel(fused, fused_ref) < 5e-3, rel(fused, fused_ref)
 
 
 def _fusion_cfg(dtype, frames=32, imu_w=400):

@@ -102,7 +102,7 @@ def test_bn_channels_last_fwd_bwd(C, relu, res):
 
 def _backbone_case(dtype, training=True, B=2, T=4, S=32, emulate=False):
     from cmhar.r3d import R3D18, run_r3d
-    from oracle.r3d_cpu import bf16_storage, r3d18_features
+    from oracle.r3d_cpu import BF16, r3d18_features
     torch.manual_seed(2)
     m = R3D18(None, compute_dtype=dtype)
     with torch.no_grad():     # non-trivial BN affine parameters / running stats
@@ -116,11 +116,11 @@ def _backbone_case(dtype, training=True, B=2, T=4, S=32, emulate=False):
     video = torch.randn(B, T, 3, S, S)      # (B, T, C, H, W)
     R = torch.randn(B, 512)
 
-    def oracle(q):
+    def oracle(hooks):
         sd_p = {k: (v.clone().requires_grad_(True) if v.is_floating_point() and 'running' not in k else v.clone())
                 for k, v in sd.items()}
         stats = {}
-        ref = r3d18_features(sd_p, video.transpose(1, 2), training=training, stats=stats, q=q)
+        ref = r3d18_features(sd_p, video.transpose(1, 2), training=training, stats=stats, **(hooks or {}))
         (ref * R).sum().backward()
         return sd_p, stats, ref
 
@@ -129,7 +129,7 @@ def _backbone_case(dtype, training=True, B=2, T=4, S=32, emulate=False):
     feat = run_r3d(m, video.to(DEV), training)
     (feat * R.to(DEV)).sum().backward()
     if emulate:
-        return m, sd_p, stats, ref, feat, oracle(bf16_storage)
+        return m, sd_p, stats, ref, feat, oracle(BF16)
     return m, sd_p, stats, ref, feat
 
 

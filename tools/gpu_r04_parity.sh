@@ -1,0 +1,14 @@
+#!/bin/bash
+# Round-4 parity session: R3D-18 per-layer bf16 diagnosis, then the bf16 parity tests of R3D-18 / CNNs / fusion / DP.
+# usage: tools/gpu_r04_parity.sh TAG [pytest -k expression]
+TAG=${1:-r04p}
+KEXPR=${2:-"bf16 or fusion or dataparallel"}
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+set -o pipefail
+echo "== r3d layers"
+timeout -k 10 300 python -u tools/debug/r3d_bf16_layers.py > gpurun_out/${TAG}_r3d_layers.log 2>&1 || exit $?
+tail -20 gpurun_out/${TAG}_r3d_layers.log
+echo "== tests"
+timeout -k 10 900 python -u -m pytest tests -m gpu -q -s -p no:cacheprovider --timeout 300 --timeout-method thread -rf -k "$KEXPR" > gpurun_out/${TAG}_pytest.log 2>&1
+rc=$?; tail -5 gpurun_out/${TAG}_pytest.log; exit $rc
