@@ -1,0 +1,232 @@
+"""Every bf16 GEMM and flash-attention launch of the bench step (VideoMAE-B, 16×224², B = 32 → M = 50 176 token rows,
+bf16) at its PRODUCTION shape, through the same `cmhar.kernels` entry points and epilogue options the model uses
+(`cmhar/videomae.py` `_forward_impl` / `_backward_impl` / the token-0 last layer) — VERDICT r03 item 2.  These are
+the shapes the bench times: QKV 1764 output tiles of 256², FC2 / out-projection 588 tiles with the tail split, the
+FC2 dgrad's prefetching `ACT_MULAUX` epilogue (depth 8, cross-pass), the split-K weight gradients with the fused
+bias row sum.  Smaller-shape tests (tests/test_kernels_gpu.py) do not reach these plans.
+
+Two checks per GEMM launch:
+* integer operands (exact in bf16, products and sums exact in fp32): bit-exact against the fp64 product with the same
+  epilogue — bf16 outputs compared after the same round-to-nearest-even; GELU (transcendental) within one bf16 ulp
+  of the fp64 erf-GELU of the exact pre-activation;
+* random bf16 operands: against torch fp32 matmul of the same operands + the same epilogue in fp32: ≤ 4e-3 rel for
+  bf16 outputs (output rounding, 2^-8), ≤ 1e-5 rel for fp32 outputs (summation order only).
+Flash attention at B·H = 384, L = 1568 (the pre-scaled-key training form): O, dQ, dK, dV against an fp32 reference
+within 3× the error of the same algorithm with the kernel's bf16 operand roundings (P, dS, O) emulated + 1e-3.
+"""
+import math
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = 'cuda'
+B, LT, HD, NH, D, FF, PK = 32, 1568, 768, 12, 64, 3072, 1536
+M = B * LT
+
+
+def K():
+    from cmhar import kernels
+    return kernels
+
+
+def L():
+    from cmhar import _lib
+    return _lib
+
+
+def rel(a, b):
+    a, b = a.double(), b.double()
+    return ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
+
+
+class _Gen:
+    """Operand maker: 'int' = dense integers in [-2, 2] (or sparse {-1, 0, 1}: contraction sums stay < 256 so the
+    bf16 outputs of K = 768 … 3072 products are exact); 'rand' = N(0, σ) rounded to bf16."""
+
+    def __init__(self, kind, seed):
+        self.kind = kind
+        self.g = torch.Generator(device=DEV).manual_seed(seed)
+
+    def op(self, shape, sparse=False, sigma=1.0):
+        if self.kind == 'int':
+            v = torch.randint(-2, 3, shape, generator=self.g, device=DEV).float()
+            if sparse:
+                v = torch.randint(-1, 2, shape, generator=self.g, device=DEV).float()
+                v *= (torch.rand(shape, generator=self.g, device=DEV) < 1.0 / 32).float()
+            return v.bfloat16()
+        return (torch.randn(shape, generator=self.g, device=DEV) * sigma).bfloat16()
+
+    def vec(self, n):
+        if self.kind == 'int':
+            return torch.randint(-2, 3, (n,), generator=self.g, device=DEV).float()
+        return torch.randn(n, generator=self.g, device=DEV) * 0.1
+
+
+def _mm(a, b, kind):
+    """fp64 product for the integer check, fp32 for the random one."""
+    dt = torch.float64 if kind == 'int' else torch.float32
+    return a.to(dt) @ b.to(dt)
+
+
+def _gelu64(x):
+    x = x.double()
+    cdf = 0.5 * torch.erfc(-x / math.sqrt(2))
+    return x * cdf, cdf + x * torch.exp(-0.5 * x * x) / math.sqrt(2 * math.pi)
+
+
+def _compare(got, want, kind, ulp=False):
+    """Integer case: bf16 outputs bit-equal to the reference after the same rounding (ulp=True: within 1 bf16 ulp,
+    the GELU case); fp32 outputs bit-equal.  Random case: relative bounds of the module docstring."""
+    if kind == 'int':
+        w = want.to(got.dtype)
+        if ulp:
+            d = (got.double() - w.double()).abs()
+            tol = want.double().abs() * 2.0 ** -7 + 1e-30
+            assert bool((d <= tol).all()), (d.max().item(), int((d > tol).sum()))
+        else:
+            bad = int((got != w).sum())
+            assert bad == 0, (bad, (got.double() - want.double()).abs().max().item())
+    else:
+        tol = 4e-3 if got.dtype == torch.bfloat16 else 1e-5
+        e = rel(got, want)
+        assert e < tol, e
+
+
+# ---------------------------------------------------------------------------------------------------------------
+# forward GEMMs (layout 0: y[M, N] = x[M, K]·Wᵀ + epilogue)
+# ---------------------------------------------------------------------------------------------------------------
+def _fwd_embed(g, kind):
+    """Tubelet embedding: columns [M, 1536] · W[768, 1536]ᵀ + bias + the sinusoid table as rowadd (modulus = tokens)."""
+    x = g.op((M, PK), sparse=True)
+    w = g.op((HD, PK))
+    bias = g.vec(HD)
+    pos = g.vec(LT * HD).view(LT, HD)
+    y = K().linear(x, w, bias, rowadd=pos, rowadd_mod=LT)
+    dt = torch.float64 if kind == 'int' else torch.float32
+    want = _mm(x, w.T, kind) + bias.to(dt) + pos.repeat(B, 1).to(dt)
+    return [(y, want, False)]
+
+
+def _fwd_qkv(g, kind, token0_kv=False):
+    """QKV (N = 2304) with the key columns pre-scaled (colscale); token0_kv: the last layer's K|V only (N = 1536)."""
+    x = g.op((M, HD), sparse=True)
+    n = 2 * HD if token0_kv else 3 * HD
+    w = g.op((n, HD))
+    bias = g.vec(n)
+    s = 0.25 if kind == 'int' else D ** -0.5 * K().LOG2E       # a power of two keeps the integer check exact
+    lo, hi = (0, HD) if token0_kv else (HD, 2 * HD)
+    y = K().linear(x, w, bias, colscale=(lo, hi, s))
+    want = _mm(x, w.T, kind) + bias.to(torch.float64 if kind == 'int' else torch.float32)
+    want[:, lo:hi] *= s
+    return [(y, want, False)]
+
+
+def _fwd_residual(g, kind, kin):
+    """out-projection (K = 768) / FC2 (K = 3072, tail split): + bias + residual stream."""
+    x = g.op((M, kin), sparse=True)
+    w = g.op((HD, kin))
+    bias = g.vec(HD)
+    res = g.op((M, HD))
+    y = K().linear(x, w, bias, residual=res)
+    dt = torch.float64 if kind == 'int' else torch.float32
+    want = _mm(x, w.T, kind) + bias.to(dt) + res.to(dt)
+    return [(y, want, False)]
+
+
+def _fwd_fc1(g, kind):
+    """FC1 with the GELU pair: out = gelu(a), aux = gelu'(a) (ACT_GELU_SAVEGRAD, as the training step runs it)."""
+    x = g.op((M, HD), sparse=True)
+    w = g.op((FF, HD))
+    bias = g.vec(FF)
+    aux = torch.empty(M, FF, dtype=torch.bfloat16, device=DEV)
+    y = K().linear(x, w, bias, act=L().ACT_GELU_SAVEGRAD, aux_out=aux)
+    pre = _mm(x, w.T, kind) + bias.to(torch.float64 if kind == 'int' else torch.float32)
+    gv, gp = _gelu64(pre)
+    return [(y, gv, True), (aux, gp, True)]
+
+
+# ---------------------------------------------------------------------------------------------------------------
+# input-gradient GEMMs (layout 1: dx[M, K] = dy[M, N]·W[N, K])
+# ---------------------------------------------------------------------------------------------------------------
+def _dgrad(g, kind, n, k, mulaux=False):
+    dy = g.op((M, n), sparse=True)
+    w = g.op((n, k))
+    aux = g.op((M, k)) if mulaux else None
+    if mulaux:       # FC2 dgrad: (dy·W2) ∘ gelu'(a) — the prefetching (PFS) epilogue instantiation
+        dx = K().linear_dgrad(dy, w, act=L().ACT_MULAUX, aux_in=aux)
+    else:
+        dx = K().linear_dgrad(dy, w)
+    want = _mm(dy, w, kind)
+    if mulaux:
+        want = want * aux.to(want.dtype)
+    return [(dx, want, False)]
+
+
+# ---------------------------------------------------------------------------------------------------------------
+# weight-gradient GEMMs (layout 2: dW[N, K] = dyᵀ·x over the M token rows, split-K, bias row sum fused)
+# ---------------------------------------------------------------------------------------------------------------
+def _wgrad(g, kind, n, k):
+    dy = g.op((M, n), sparse=True)
+    x = g.op((M, k))
+    dw = torch.empty(n, k, device=DEV)
+    db = torch.empty(n, device=DEV)
+    K().linear_wgrad(dy, x, out=dw, bias_out=db)
+    dt = torch.float64 if kind == 'int' else torch.float32
+    return [(dw, _mm(dy.T, x, kind), False), (db, dy.to(dt).sum(0), False)]
+
+
+CASES = {
+    'fwd_embed': _fwd_embed,
+    'fwd_qkv': lambda g, k: _fwd_qkv(g, k),
+    'fwd_token0_kv': lambda g, k: _fwd_qkv(g, k, token0_kv=True),
+    'fwd_out_proj': lambda g, k: _fwd_residual(g, k, HD),
+    'fwd_fc1_gelu': _fwd_fc1,
+    'fwd_fc2_tail': lambda g, k: _fwd_residual(g, k, FF),
+    'dgrad_fc2_mulaux': lambda g, k: _dgrad(g, k, HD, FF, mulaux=True),
+    'dgrad_fc1': lambda g, k: _dgrad(g, k, FF, HD),
+    'dgrad_out_proj': lambda g, k: _dgrad(g, k, HD, HD),
+    'dgrad_qkv': lambda g, k: _dgrad(g, k, 3 * HD, HD),
+    'dgrad_token0_kv': lambda g, k: _dgrad(g, k, 2 * HD, HD),
+    'wgrad_fc2': lambda g, k: _wgrad(g, k, HD, FF),
+    'wgrad_fc1': lambda g, k: _wgrad(g, k, FF, HD),
+    'wgrad_out_proj': lambda g, k: _wgrad(g, k, HD, HD),
+    'wgrad_qkv': lambda g, k: _wgrad(g, k, 3 * HD, HD),
+    'wgrad_token0_kv': lambda g, k: _wgrad(g, k, 2 * HD, HD),
+    'wgrad_embed': lambda g, k: _wgrad(g, k, HD, PK),
+}
+
+
+@pytest.mark.parametrize('kind', ['int', 'rand'])
+@pytest.mark.parametrize('case', list(CASES))
+def test_bench_gemm_launch(case, kind):
+    g = _Gen(kind, seed=sum(map(ord, case)) + (7 if kind == 'rand' else 0))
+    with torch.no_grad():
+        outs = CASES[case](g, kind)
+        torch.cuda.synchronize()
+        for got, want, ulp in outs:
+            _compare(got, want, kind, ulp)
+    del outs
+    torch.cuda.empty_cache()
+
+
+def test_bench_gemm_plans_are_the_bench_plans():
+    """The shapes above take the plans the bench step takes (cmhar_gemm_bf16_plan, the library's own launch decision;
+    1 = 256² tile, 2 = 256² + tail split + reduce, 4 = 8-phase 256², 6 = 8-phase split-K + reduce): a production-shape
+    test on another plan would test other code."""
+    lib = L().lib()
+
+    def plan(layout, m, n, k, rowsum=False):
+        splits = K()._splits_for(m, n, k)
+        has_ws = splits > 1 or (not rowsum and K()._tail_ws(m, n, k) > 0)
+        return lib.cmhar_gemm_bf16_plan(layout, m, n, k, splits, int(has_ws), int(rowsum))
+
+    assert [plan(0, M, n, k) for n, k in ((3 * HD, HD), (2 * HD, HD), (HD, HD), (FF, HD), (HD, PK))] == [4] * 5
+    assert plan(0, M, HD, FF) == 2                               # FC2 forward: tail split
+    assert plan(1, M, HD, FF) == 2 and plan(1, M, HD, 3 * HD) == 2   # FC1 / QKV dgrad: tail split
+    assert plan(1, M, FF, HD) == 1 and plan(1, M, HD, HD) == 1 and plan(1, M, HD, 2 * HD) == 1
+    for n, k in ((HD, FF), (FF, HD), (HD, HD), (3 * HD, HD), (2 * HD, HD), (HD, PK)):
+        assert plan(2, n, k, M, rowsum=True) == 6, (n, k)     # weight gradients: 8-phase split-K, bias row sum
+
+
+
