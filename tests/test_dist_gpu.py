@@ -145,3 +145,40 @@ def test_dataparallel_rccl_single_rank(tmp_path, backbone):
     # BatchNorm over 4 clips puts the bf16 loss 2.9e-3 from the fp32 oracle, 6.7x the storage emulation's error)
     lt = 3 * abs(r0['emul_loss'] - r0['oracle_loss']) / abs(r0['oracle_loss']) + FLOOR_BF16[backbone]
     assert abs(r0['loss'] - r0['oracle_loss']) <= lt * abs(r0['oracle_loss'])
+
+
+@pytest.mark.gpu
+def test_bench_two_rank_rehearsal(tmp_path):
+    """the N > 1 branch of bench.py (barrier, MAX over ranks of the timed region, global-batch
+    SigLIP loss, rank-0 JSON line) run as two torchrun-style ranks sharing the test box's one GPU over gloo
+    (`CMHAR_BENCH_BACKEND=gloo`, `CMHAR_BENCH_DEVICE=0`; RCCL refuses two ranks on one GPU).  The headline workload at
+    its own per-GPU batch (32 clips per rank): one JSON line from rank 0 with n_gpus 2, global_batch 64, dp2, the
+    same loss on both ranks, and throughput = 64 clips × steps / max elapsed."""
+    port = _free_port()
+    procs = []
+    for r in range(2):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE='2', MASTER_ADDR='127.0.0.1',
+                   MASTER_PORT=str(port), CMHAR_BENCH_BACKEND='gloo', CMHAR_BENCH_DEVICE='0')
+        procs.append(subprocess.Popen([sys.executable, '-u', os.path.join(REPO, 'bench.py'), '--gpus', '2',
+                                       '--steps', '2', '--warmup', '1', '--no-cpu-baseline'], env=env,
+                                      stdout=subprocess.PIPE, stderr=subprocess.PIPE, cwd=str(tmp_path)))
+    outs = []
+    for p in procs:
+        try:
+            out, err = p.communicate(timeout=240)
+        except subprocess.TimeoutExpired:
+            for q in procs:
+                q.kill()
+            raise
+        outs.append((p.returncode, out.decode(errors='replace'), err.decode(errors='replace')))
+    for rc, out, err in outs:
+        assert rc == 0, err[-3000:]
+    lines0 = [ln for ln in outs[0][1].splitlines() if ln.startswith('{')]
+    lines1 = [ln for ln in outs[1][1].splitlines() if ln.startswith('{')]
+    assert len(lines0) == 1 and not lines1, (outs[0][1][-2000:], outs[1][1][-2000:])
+    rec = json.loads(lines0[0])
+    assert rec['n_gpus'] == 2 and rec['config']['global_batch'] == 64 and rec['config']['parallelism'] == 'dp2'
+    assert rec['scaling'] == 'weak' and rec['steps'] == 2
+    losses = rec['last_loss_per_rank']
+    assert len(losses) == 2 and losses[0] == losses[1], losses
+    assert abs(rec['value'] - 64 * 2 / (rec['ms_per_step'] * 2 / 1000)) <= 1e-3 * rec['value']

@@ -619,3 +619,12 @@ def test_fused_adamw_clip_params_beyond_owned():
             assert torch.equal(a.grad, b.grad)
     for a, b in zip(ours, theirs):
         assert torch.equal(a, b)
+
+
+def test_mfma_peak_probe():
+    """csrc/probe.hip (the on-box MFMA peak bench.py reports as roofline.peak_measured): a plausible dense bf16 rate —
+    above 60 % and not above 110 % of the vendor 2.5 PF — and finite accumulator sums."""
+    import bench
+    tf = bench.measure_mfma_peak(torch.device(DEV), blocks=1024, iters=4000, reps=2)
+    print(f'MFMA peak probe: {tf:.1f} TFLOP/s')
+    assert 1500.0 < tf < 2750.0, tf
