@@ -6,6 +6,9 @@ KEXPR=${2:-"bf16 or fusion or dataparallel"}
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 set -o pipefail
+echo "== dgrad layout A/B"
+timeout -k 10 240 python -u tools/debug/dgrad_layout_ab.py > gpurun_out/${TAG}_dgrad_ab.log 2>&1 || exit $?
+cat gpurun_out/${TAG}_dgrad_ab.log
 echo "== r3d layers"
 timeout -k 10 300 python -u tools/debug/r3d_bf16_layers.py > gpurun_out/${TAG}_r3d_layers.log 2>&1 || exit $?
 tail -20 gpurun_out/${TAG}_r3d_layers.log
