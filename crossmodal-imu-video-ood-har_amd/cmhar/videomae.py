@@ -182,12 +182,12 @@ class VideoMAEBackbone(L.NoReplicate, nn.Module):
             self._packs.add_weight('patch', [pe.weight])
             for i, layer in enumerate(self.encoder.layer):
                 a = layer.attention.attention
-                self._packs.add_weight(f'qkv{i}', [a.query.weight, a.key.weight, a.value.weight])
+                self._packs.add_weight(f'qkv{i}', [a.query.weight, a.key.weight, a.value.weight], transpose=_DGRAD_WT)
                 if a.query.bias is not None:
                     self._packs.add_bias(f'bqkv{i}', [a.query.bias, a.key.bias, a.value.bias])
-                self._packs.add_weight(f'o{i}', [layer.attention.output.dense.weight])
-                self._packs.add_weight(f'fc1_{i}', [layer.intermediate.dense.weight])
-                self._packs.add_weight(f'fc2_{i}', [layer.output.dense.weight])
+                self._packs.add_weight(f'o{i}', [layer.attention.output.dense.weight], transpose=_DGRAD_WT)
+                self._packs.add_weight(f'fc1_{i}', [layer.intermediate.dense.weight], transpose=_DGRAD_WT)
+                self._packs.add_weight(f'fc2_{i}', [layer.output.dense.weight], transpose=_DGRAD_WT)
             self._packs.build()
         self._packs.refresh()
         return self._packs
@@ -197,6 +197,25 @@ class VideoMAEBackbone(L.NoReplicate, nn.Module):
             raise NotImplementedError('masked-token pretraining is not on the accelerated path')
         out = run_backbone(self, pixel_values, token0_only=False)
         return VideoMAEOutput(out)
+
+
+# Input-gradient GEMMs dX = dY·W on the transposed bf16 weight copy Wᵀ [K, N] in the FORWARD layout (K-contiguous B
+# reads, the 8-phase / tail-split forward kernels) instead of the dgrad layout's transposed LDS reads of W [N, K]
+# (cmhar.weights.PackedWeights.transposed: one multi-matrix transpose launch per step after AdamW).  Same fp32 products
+# and epilogues; CMHAR_DGRAD_WT=0 restores the dgrad layout (A/B knob).
+_DGRAD_WT = os.environ.get('CMHAR_DGRAD_WT', '1') != '0'
+
+
+def _dgrad(W, name, dy, rows=None, act=L.ACT_NONE, aux_in=None, residual=None, out=None):
+    """dX = dY · W[name][rows] (+ epilogue) — on Wᵀ in the forward layout when the pack keeps a transposed copy."""
+    wt = W.transposed(name) if hasattr(W, 'transposed') else None
+    if wt is None:
+        w = W[name] if rows is None else W[name][rows]
+        return K.linear_dgrad(dy, w, act=act, aux_in=aux_in, residual=residual, out=out)
+    b = wt if rows is None else wt[:, rows]
+    if out is None:
+        out = torch.empty(dy.shape[0], b.shape[0], dtype=dy.dtype, device=dy.device)
+    return K.gemm(0, dy, b, out, act=act, aux_in=aux_in, residual=residual)
 
 
 # ----------------------------------------------------------------------------------------------------------
@@ -405,24 +424,24 @@ def _backward_impl(m: VideoMAEBackbone, st, dx, sink, overlap_wgrad=True):
         x, h1, mu1, rs1, qkv, o, lse, x1, h2, mu2, rs2, pre, g = st.layers[li]
         st.layers[li] = None
         # x2 = x1 + FC2(gelu(FC1(LN2(x1))))
-        dpre = K.linear_dgrad(dx, W[f'fc2_{li}'], act=L.ACT_MULAUX, aux_in=pre)     # pre holds gelu'(a)
+        dpre = _dgrad(W, f'fc2_{li}', dx, act=L.ACT_MULAUX, aux_in=pre)     # pre holds gelu'(a)
         wgrad([p['f2w']], dx, g, p['f2w'].shape, [p['f2b']])
         del g
-        dh2 = K.linear_dgrad(dpre, W[f'fc1_{li}'])
+        dh2 = _dgrad(W, f'fc1_{li}', dpre)
         wgrad([p['f1w']], dpre, h2, p['f1w'].shape, [p['f1b']])
         del dpre, pre
         gw2, gb2, beta = ln_grads(p['ln2w'], p['ln2b'])
         dx1 = K.layernorm_bwd(dh2, x1, p['ln2w'], mu2, rs2, gw2, gb2, dres=dx, beta_acc=beta)
         del dh2, dx
         # x1 = x + O·Woᵀ + bo
-        do = K.linear_dgrad(dx1, W[f'o{li}'])
+        do = _dgrad(W, f'o{li}', dx1)
         wgrad([p['ow']], dx1, o, p['ow'].shape, [p['ob']])
         dqkv = torch.empty(M, 3 * Hd, dtype=dx1.dtype, device=dev)
         attn_bwd = K.attention_bwd_prescaled if st.prescaled else K.attention_bwd
         attn_bwd(qkv[:, :Hd], qkv[:, Hd:2 * Hd], qkv[:, 2 * Hd:], o, do, lse, dqkv[:, :Hd], dqkv[:, Hd:2 * Hd],
                  dqkv[:, 2 * Hd:], B=B, H=nh, Lq=Lt, Lk=Lt, D=D, scale=scale)
         del do, o, qkv
-        dh1 = K.linear_dgrad(dqkv, W[f'qkv{li}'])
+        dh1 = _dgrad(W, f'qkv{li}', dqkv)
         wgrad([p['qw'], p['kw'], p['vw']], dqkv, h1, (3 * Hd, Hd),
               [p['qb'], p['kb'], p['vb']] if p['qb'] is not None else None)
         del dqkv
@@ -446,14 +465,14 @@ def _last_layer_token0_bwd(st, li, p, W, dx0, wgrad, ln_grads, sink, dev):
     B, Lt, M, Hd, nh, D, scale = st.geom
     _, x, h1, mu1, rs1, q0, kv, o0, lse0, x1_0, h2_0, mu2, rs2, pre0, g0 = st.layers[li]
     st.layers[li] = None
-    dpre0 = K.linear_dgrad(dx0, W[f'fc2_{li}'], act=L.ACT_MULAUX, aux_in=pre0)
+    dpre0 = _dgrad(W, f'fc2_{li}', dx0, act=L.ACT_MULAUX, aux_in=pre0)
     wgrad([p['f2w']], dx0, g0, p['f2w'].shape, [p['f2b']])
-    dh2_0 = K.linear_dgrad(dpre0, W[f'fc1_{li}'])
+    dh2_0 = _dgrad(W, f'fc1_{li}', dpre0)
     wgrad([p['f1w']], dpre0, h2_0, p['f1w'].shape, [p['f1b']])
     del dpre0, pre0, g0
     gw2, gb2, beta = ln_grads(p['ln2w'], p['ln2b'])
     dx1_0 = K.layernorm_bwd(dh2_0, x1_0, p['ln2w'], mu2, rs2, gw2, gb2, dres=dx0, beta_acc=beta)
-    do0 = K.linear_dgrad(dx1_0, W[f'o{li}'])
+    do0 = _dgrad(W, f'o{li}', dx1_0)
     wgrad([p['ow']], dx1_0, o0, p['ow'].shape, [p['ob']])
     dq0 = torch.empty(B, Hd, dtype=dx0.dtype, device=dev)
     dkv = torch.empty(M, 2 * Hd, dtype=dx0.dtype, device=dev)
@@ -461,10 +480,9 @@ def _last_layer_token0_bwd(st, li, p, W, dx0, wgrad, ln_grads, sink, dev):
     attn_bwd(q0, kv[:, :Hd], kv[:, Hd:], o0, do0, lse0, dq0, dkv[:, :Hd], dkv[:, Hd:], B=B, H=nh, Lq=1, Lk=Lt, D=D,
              scale=scale)
     del do0, o0
-    wqkv = W[f'qkv{li}']
-    dh1 = K.linear_dgrad(dkv, wqkv[Hd:])                        # K|V rows: every token
+    dh1 = _dgrad(W, f'qkv{li}', dkv, rows=slice(Hd, None))     # K|V rows: every token
     dh1_0 = dh1.view(B, Lt, Hd)[:, 0]
-    K.gemm(1, dq0, wqkv[:Hd], dh1_0, residual=dh1_0)            # + Q rows: the token-0 rows (one rounding)
+    _dgrad(W, f'qkv{li}', dq0, rows=slice(None, Hd), residual=dh1_0, out=dh1_0)   # + Q rows: token-0 rows (one rounding)
     # QKV weight / bias gradients into the packed [3Hd, Hd] destination: Q rows from the token-0 rows, K|V rows
     # from every row
     out, wbeta = sink.dest([p['qw'], p['kw'], p['vw']], (3 * Hd, Hd), dev)

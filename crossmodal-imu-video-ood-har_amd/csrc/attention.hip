@@ -352,8 +352,11 @@ __global__ __launch_bounds__(256, CMHAR_ATTN_FWD_PERKB ? 3 : 2) void attn_fwd_bf
 // dK, dV: one wave = 32 keys (K, V fragments in registers as B operands), q tiles of 64 staged in LDS.
 // Three waves per SIMD for the dK/dV kernel (168 VGPRs, 12 B/lane spilled): its LDS-DMA staging freed the 64
 // register-staged tile VGPRs; measured 4-7 % faster than two waves per SIMD (tools/debug/attn_ab.py)
+#ifndef CMHAR_DKDV_V2
+#define CMHAR_DKDV_V2 0
+#endif
 #ifndef CMHAR_DKDV_OCC
-#define CMHAR_DKDV_OCC 3
+#define CMHAR_DKDV_OCC (CMHAR_DKDV_V2 ? 2 : 3)
 #endif
 // PS (pre-scaled keys): K holds bf16(scale·log2e·K) written by the QKV GEMM's epilogue (CmharEpilogue.colscale) and
 // the launch passes scale = 1/log2e, so c = 1 and p = exp2(acc) needs no multiply per score (−6 % backward time:
@@ -438,11 +441,27 @@ __global__ __launch_bounds__(256, CMHAR_DKDV_OCC) void attn_bwd_dkdv_bf16(int H,
         s[r] = L_[q];
         dp[r] = D_[q];
       }
+#if CMHAR_DKDV_V2
+      // all eight row fragments issued before the two MFMA chains (32 VGPRs at 2 waves per SIMD): one LDS latency
+      // exposed per block instead of one per MFMA
+      bf16x8 qr[4], gr[4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        qr[t] = row_frag(Qs(cur), qb * 32, t, lane);
+        gr[t] = row_frag(Gs(cur), qb * 32, t, lane);
+      }
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qr[t], kf[t], s, 0, 0, 0);
+        dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(gr[t], vf[t], dp, 0, 0, 0);
+      }
+#else
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
         s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag(Qs(cur), qb * 32, t, lane), kf[t], s, 0, 0, 0);
         dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag(Gs(cur), qb * 32, t, lane), vf[t], dp, 0, 0, 0);
       }
+#endif
       // p = exp2(c·s), dS = P ∘ (dP − δ), then both packed to bf16 — written in aligned register pairs (one
       // v_pk_mul_f32 + one v_cvt_pk_bf16_f32 per pair; element-wise, the compiler paired (1,2),(3,4),... and spent
       // v_mov / v_alignbit / v_perm re-pairing them for the packs; the backward got 3 % faster, bit-identical.  The
@@ -504,8 +523,11 @@ __global__ __launch_bounds__(256, CMHAR_DKDV_OCC) void attn_bwd_dkdv_bf16(int H,
 // and written for the dK/dV kernel, which runs after this one on the same stream.
 // Three waves per SIMD for dQ: with the fragments read just before their MFMAs (not hoisted per key block) the
 // kernel fits 168 VGPRs without spilling; measured 7 % faster than two waves per SIMD
+#ifndef CMHAR_DQ_V2
+#define CMHAR_DQ_V2 0
+#endif
 #ifndef CMHAR_DQ_OCC
-#define CMHAR_DQ_OCC 3
+#define CMHAR_DQ_OCC (CMHAR_DQ_V2 ? 2 : 3)
 #endif
 template <int QB, bool PS = false>
 __global__ __launch_bounds__(256, QB == 1 ? CMHAR_DQ_OCC : 2) void attn_bwd_dq_bf16(int H, int Lq, int Lk, int q_base,
@@ -583,6 +605,21 @@ __global__ __launch_bounds__(256, QB == 1 ? CMHAR_DQ_OCC : 2) void attn_bwd_dq_b
       for (int j = 0; j < QB; ++j)
 #pragma unroll
         for (int r = 0; r < 16; ++r) { s[j][r] = sL[j]; dp[j][r] = -Dl[j]; }
+#if CMHAR_DQ_V2
+      bf16x8 kfr[4], vfr[4];             // all eight row fragments before the two chains (2 waves per SIMD)
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        kfr[t] = row_frag(Ks(cur), kb * 32, t, lane);
+        vfr[t] = row_frag(Vs(cur), kb * 32, t, lane);
+      }
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int j = 0; j < QB; ++j) {
+          s[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kfr[t], qf[j][t], s[j], 0, 0, 0);
+          dp[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vfr[t], gf[j][t], dp[j], 0, 0, 0);
+        }
+#else
 #pragma unroll
       for (int t = 0; t < 4; ++t) {    // each K / V row fragment read once, used by all QB q-blocks
         const bf16x8 kfr = row_frag(Ks(cur), kb * 32, t, lane);
@@ -593,6 +630,7 @@ __global__ __launch_bounds__(256, QB == 1 ? CMHAR_DQ_OCC : 2) void attn_bwd_dq_b
           dp[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vfr, gf[j][t], dp[j], 0, 0, 0);
         }
       }
+#endif
       if (kbase + 64 > Lk) {   // ragged last tile only (wave-uniform branch)
 #pragma unroll
         for (int j = 0; j < QB; ++j)

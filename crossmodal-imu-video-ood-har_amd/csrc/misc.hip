@@ -287,7 +287,55 @@ __global__ __launch_bounds__(256) void mt_cast_kernel(const MTTensor* __restrict
   }
 }
 
+// Transposed bf16 weight shadows (the input-gradient GEMMs read Wᵀ [K, N] K-contiguous in the forward layout instead
+// of W [N, K] through transposed LDS reads).  One launch over every matrix: a workgroup transposes one 64×64 tile,
+// read as 16-B row pieces (coalesced), staged in LDS with a padded row pitch, written as 16-B row pieces of the
+// destination.  rows, cols multiples of 8; a descriptor's tiles start at `tile0` (prefix sums, ascending).
+struct MTTranspose {
+  const bf16* src;
+  bf16* dst;
+  int rows, cols;     // source shape [rows, cols], row-major; destination [cols, rows]
+  int tile0, pad;
+};
+
+__global__ __launch_bounds__(256) void mt_transpose_kernel(const MTTranspose* __restrict__ descs, int ndesc) {
+  __shared__ unsigned short tile[64][64 + 8];
+  int d = 0;
+  while (d + 1 < ndesc && descs[d + 1].tile0 <= (int)blockIdx.x) ++d;
+  const MTTranspose D = descs[d];
+  const int t = blockIdx.x - D.tile0;
+  const int tiles_c = (D.cols + 63) / 64;
+  const int r0 = (t / tiles_c) * 64, c0 = (t % tiles_c) * 64;
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {          // 64 rows × 8 pieces of 16 B
+    const int piece = tid + 256 * i, r = piece >> 3, cp = (piece & 7) * 8;
+    uint4_t v = {0u, 0u, 0u, 0u};
+    if (r0 + r < D.rows && c0 + cp < D.cols) v = *(const uint4_t*)(D.src + (long)(r0 + r) * D.cols + c0 + cp);
+    *(uint4_t*)&tile[r][cp] = v;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {          // destination rows = source columns
+    const int piece = tid + 256 * i, c = piece >> 3, rp = (piece & 7) * 8;
+    if (c0 + c >= D.cols || r0 + rp >= D.rows) continue;
+    unsigned short e[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) e[j] = tile[rp + j][c];
+    uint4_t v = {e[0] | ((unsigned)e[1] << 16), e[2] | ((unsigned)e[3] << 16), e[4] | ((unsigned)e[5] << 16),
+                 e[6] | ((unsigned)e[7] << 16)};
+    *(uint4_t*)(D.dst + (long)(c0 + c) * D.rows + r0 + rp) = v;
+  }
+}
+
 }  // namespace
+
+extern "C" int cmhar_mt_transpose_bf16(const void* descs, int ndesc, int ntiles, hipStream_t st) {
+  if (ndesc <= 0 || ntiles <= 0) return 0;
+  mt_transpose_kernel<<<ntiles, 256, 0, st>>>((const MTTranspose*)descs, ndesc);
+  CMHAR_CHECK_LAUNCH();
+  return 0;
+}
 
 extern "C" int cmhar_tubelet_im2col(int out_dtype, int B, int T, int C, int H, int W, int tub, int P,
                                     const float* video, void* out, hipStream_t st) {

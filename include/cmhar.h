@@ -271,6 +271,10 @@ int cmhar_mt_adamw_clip(const void* tens, const void* chunks, int nchunks, float
                         const float* gscale, int write_grad, hipStream_t stream);
 /* refresh the compute shadows (p_bf16 / p_copy) from p, e.g. after a foreign optimizer updated p. */
 int cmhar_mt_cast_bf16(const void* tens, const void* chunks, int nchunks, hipStream_t stream);
+/* Transposed bf16 copies of weight shadows (the input-gradient GEMMs' forward-layout operand Wᵀ): descs = ndesc
+ * records {const bf16* src; bf16* dst; int rows; int cols; int tile0; int pad;} (32 B; src [rows, cols] → dst
+ * [cols, rows], rows and cols multiples of 8, tile0 = first 64×64 tile of the record, ascending), ntiles = total. */
+int cmhar_mt_transpose_bf16(const void* descs, int ndesc, int ntiles, hipStream_t stream);
 
 /* ---- R3D-18 video backbone (north_star extension; no reference code — the reference's CNN options are per-frame
  * 2-D torchvision models, models.py:160-216; replaces torchvision.models.video.r3d_18's Conv3d / BatchNorm3d /

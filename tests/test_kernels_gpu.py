@@ -628,3 +628,58 @@ def test_mfma_peak_probe():
     tf = bench.measure_mfma_peak(torch.device(DEV), blocks=1024, iters=4000, reps=2)
     print(f'MFMA peak probe: {tf:.1f} TFLOP/s')
     assert 1500.0 < tf < 2750.0, tf
+
+
+def test_packed_weights_transposed_copies():
+    """PackedWeights(transpose=True): cmhar_mt_transpose_bf16 builds Wᵀ of every pack in one launch (ragged 64-tile
+    edges included), rebuilt only after the shadows change (FusedAdamW.mark_fresh / a version-triggered cast)."""
+    from cmhar.weights import PackedWeights
+    torch.manual_seed(14)
+    ps = [torch.nn.Parameter(torch.randn(s, device=DEV)) for s in [(200, 72), (136, 72), (64, 520), (768, 768)]]
+    pk = PackedWeights(DEV, torch.bfloat16)
+    pk.add_weight('a', ps[:2], transpose=True)
+    pk.add_weight('b', [ps[2]], transpose=True)
+    pk.add_weight('c', [ps[3]])
+    pk.build()
+    pk.refresh(force=True)
+    ta, tb = pk.transposed('a'), pk.transposed('b')
+    assert pk.transposed('c') is None
+    assert torch.equal(ta, pk['a'].t()) and torch.equal(tb, pk['b'].t())
+    assert torch.equal(ta, torch.cat([ps[0], ps[1]]).detach().bfloat16().t())
+    with torch.no_grad():
+        ps[2].mul_(-2.0)
+    pk.refresh()
+    assert torch.equal(pk.transposed('b'), (ps[2].detach() * 1.0).bfloat16().t())
+
+
+def test_videomae_dgrad_transposed_weights_match_dgrad_layout(tmp_path):
+    """The VideoMAE backward's input-gradient GEMMs on the transposed weight copies (forward layout, default) against
+    the dgrad layout (CMHAR_DGRAD_WT=0), two processes on the same seeded bf16 model (full 12-layer backbone at a small
+    clip, incl. the token-0 last layer): every parameter gradient within 1e-3 relative of the other (the two layouts
+    order the K accumulation differently inside an MFMA step; same fp32 products, one bf16 rounding each)."""
+    import subprocess
+    import sys
+    import os
+    script = r'''
+import os, sys, torch
+sys.path[:0] = [os.environ["REPO"], os.path.join(os.environ["REPO"], "crossmodal-imu-video-ood-har_amd")]
+from cmhar.videomae import VideoMAEBackbone, default_videomae_config, run_backbone
+cfg = default_videomae_config(image_size=64, num_frames=4)
+torch.manual_seed(0)
+m = VideoMAEBackbone(cfg, compute_dtype="bf16").cuda().train()
+x = torch.randn(8, 4, 3, 64, 64, device="cuda")
+out = run_backbone(m, x, token0_only=True)
+g = torch.randn_like(out.float())
+(out.float() * g).sum().backward()
+torch.save({n: p.grad.cpu() for n, p in m.named_parameters()}, sys.argv[1])
+'''
+    outs = []
+    for v in ('1', '0'):
+        f = tmp_path / f'g{v}.pt'
+        env = dict(os.environ, CMHAR_DGRAD_WT=v, REPO=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        r = subprocess.run([sys.executable, '-c', script, str(f)], env=env, capture_output=True, text=True, timeout=200)
+        assert r.returncode == 0, r.stderr[-3000:]
+        outs.append(torch.load(f, weights_only=True))
+    worst = max(rel(outs[0][n], outs[1][n]) for n in outs[0] if outs[1][n].norm() > 0)
+    print('worst rel diff transposed vs dgrad layout:', worst)
+    assert worst < 1e-3, worst

@@ -41,8 +41,10 @@ def main():
     sc = 1.0 / K.LOG2E if prescaled else D ** -0.5
     fl = 4 * B * H * L * L * D
     cases = [('fwd', 1.0, lambda: K.attention_fwd(q, k, v, o, lse, B=B, H=H, Lq=L, Lk=L, D=D, scale=sc), lambda: o),
-             ('bwd', 2.5, lambda: K.attention_bwd(q, k, v, o, do, lse, dq, dk, dv, B=B, H=H, Lq=L, Lk=L, D=D,
-                                                  scale=sc), lambda: dqkv)]
+             ('bwd', 2.5, (lambda: K.attention_bwd_prescaled(q, k, v, o, do, lse, dq, dk, dv, B=B, H=H, Lq=L, Lk=L,
+                                                             D=D, scale=D ** -0.5)) if prescaled else
+              (lambda: K.attention_bwd(q, k, v, o, do, lse, dq, dk, dv, B=B, H=H, Lq=L, Lk=L, D=D, scale=sc)),
+              lambda: dqkv)]
     _lib._lib = libs[0]
     K.attention_fwd(q, k, v, o, lse, B=B, H=H, Lq=L, Lk=L, D=D, scale=sc)
     for tag, mult, fn, res in cases:

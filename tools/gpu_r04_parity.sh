@@ -9,6 +9,11 @@ set -o pipefail
 echo "== dgrad layout A/B"
 timeout -k 10 240 python -u tools/debug/dgrad_layout_ab.py > gpurun_out/${TAG}_dgrad_ab.log 2>&1 || exit $?
 cat gpurun_out/${TAG}_dgrad_ab.log
+if [ -f var/libA.so ] && [ -f var/libB.so ]; then
+  echo "== attention A/B (var/libA.so vs var/libB.so)"
+  timeout -k 10 300 python -u tools/debug/attn_ab.py var/libA.so var/libB.so var/libC.so --prescaled > gpurun_out/${TAG}_attn_ab.log 2>&1 || exit $?
+  cat gpurun_out/${TAG}_attn_ab.log
+fi
 echo "== r3d layers"
 timeout -k 10 300 python -u tools/debug/r3d_bf16_layers.py > gpurun_out/${TAG}_r3d_layers.log 2>&1 || exit $?
 tail -20 gpurun_out/${TAG}_r3d_layers.log
