@@ -496,7 +496,14 @@ def _last_layer_token0_bwd(st, li, p, W, dx0, wgrad, ln_grads, sink, dev):
     del dkv, kv, q0
     gw1, gb1, beta = ln_grads(p['ln1w'], p['ln1b'])
     dx = K.layernorm_bwd(dh1, x, p['ln1w'], mu1, rs1, gw1, gb1, beta_acc=beta)
-    K.copy2d(dx1_0, dx.view(B, Lt, Hd)[:, 0], beta=1.0)         # residual path: nonzero on the token-0 rows only
+    # the residual path's gradient is nonzero on the token-0 rows only: those B rows' LN backward again, with dx1_0 in
+    # its dres epilogue, so each is ONE bf16 rounding of LN'(dh1) + dx1_0 as in the full layer's fused backward (a
+    # copy-add after the first pass rounded them twice); that pass's dγ / dβ of the B rows are discarded
+    mu0 = K.copy2d(mu1.view(B, Lt)[:, :1], torch.empty(B, 1, dtype=torch.float32, device=dev)).view(B)
+    rs0 = K.copy2d(rs1.view(B, Lt)[:, :1], torch.empty(B, 1, dtype=torch.float32, device=dev)).view(B)
+    scratch = torch.empty(2, Hd, dtype=torch.float32, device=dev)
+    K.layernorm_bwd(dh1.view(B, Lt, Hd)[:, 0], x.view(B, Lt, Hd)[:, 0], p['ln1w'], mu0, rs0, scratch[0], scratch[1],
+                    dres=dx1_0, dh=dx.view(B, Lt, Hd)[:, 0])
     return dx
 
 

@@ -287,18 +287,20 @@ def test_videomae_base_full_geometry_backward(dtype):
     assert not bad, bad
 
 
-@pytest.mark.parametrize('dtype', ['fp32', 'bf16'])
-def test_last_layer_token0_pruning_matches_full_layer(dtype, monkeypatch):
+@pytest.mark.parametrize('dtype,frames,size', [('fp32', 4, 64), ('bf16', 4, 64), ('bf16', 16, 224)])
+def test_last_layer_token0_pruning_matches_full_layer(dtype, frames, size, monkeypatch):
     """The VideoEncoder computes the last VideoMAE layer's query side, MLP and LayerNorm 2 on the token-0 rows only
     (cmhar/videomae.py _last_layer_token0_fwd / _bwd).  Against the full last layer (CMHAR_TOKEN0_LAST=0) on the
-    same weights and inputs, at B = 8 clips of 32 tokens: fp32 — projections, loss and every parameter gradient agree
+    same weights and inputs, at B = 8 clips of 32 tokens and of the production 1568 tokens (16 × 224², ADVICE r03: one
+    query per clip and head over 1568 keys, the token-0 rows' LN backward with the residual gradient fused): fp32 —
+    projections, loss and every parameter gradient agree
     to ≤ 1e-5; bf16 — the two paths round different intermediate rows, so each is compared with the fp32 result:
     the pruned path's error is at most 1.5× the full path's (+2e-3) on every output and gradient."""
     from cmhar.config import Config
     from cmhar.losses import SigmoidContrastiveLoss
     from cmhar.models import CrossModalModel
     cfg = Config()
-    cfg.data.imu_window_size, cfg.data.video_frames_per_window, cfg.data.video_resize = 64, 4, (64, 64)
+    cfg.data.imu_window_size, cfg.data.video_frames_per_window, cfg.data.video_resize = 64, frames, (size, size)
     m = cfg.model
     m.video_backbone, m.video_pretrained, m.compute_dtype = '/nonexistent/videomae-t0', False, dtype
     m.imu_d_model, m.imu_nhead, m.imu_num_layers, m.imu_dropout = 32, 4, 2, 0.0
@@ -308,7 +310,7 @@ def test_last_layer_token0_pruning_matches_full_layer(dtype, monkeypatch):
     model = CrossModalModel(cfg).to(DEV).train()
     g = torch.Generator().manual_seed(4)
     imu = torch.randn(8, 6, 64, generator=g).to(DEV)
-    video = torch.randn(8, 4, 3, 64, 64, generator=g).to(DEV)
+    video = torch.randn(8, frames, 3, size, size, generator=g).to(DEV)
     lf = SigmoidContrastiveLoss().to(DEV)
 
     def run(flag, dt):
