@@ -34,6 +34,9 @@ __device__ __forceinline__ int att_off(int row, int chunk) {
 }
 
 typedef __attribute__((address_space(3))) void* att_lds_ptr;
+#ifndef CMHAR_ATTN_DMA_ASM
+#define CMHAR_ATTN_DMA_ASM 0
+#endif
 typedef __attribute__((ext_vector_type(2))) float float2_t;
 typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2_t;
 
@@ -60,11 +63,31 @@ struct TileDma {
   __device__ __forceinline__ void tile(int r0, char* lds, int wave) const {
     const long off = (long)r0 * row_bytes;
     const long left = valid - off;
-    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)(base + off), (short)0, (int)(left > 0 ? (left < 0x7fffffff ? left : 0x7fffffff) : 0), 0x00020000);
+    const int nrec = (int)(left > 0 ? (left < 0x7fffffff ? left : 0x7fffffff) : 0);
+#if CMHAR_ATTN_DMA_ASM
+    // the same buffer_load_dwordx4 … lds, issued by inline asm: hipcc then does not see an LDS write in flight, so it
+    // no longer drains it (`s_waitcnt vmcnt(0)`) before the first transposed LDS read of the tile being computed —
+    // it did so in all three flash kernels, which serialised the next tile's prefetch with the current tile's work.
+    // The kernels order every DMA with explicit counted vmcnt waits + barriers (as before).  M0 is written here; no
+    // compiler-generated code in these kernels uses M0 (checked in the .s), so nothing relies on it across the asm.
+    const unsigned long long a = (unsigned long long)(base + off);
+    uint4_t rs;
+    rs[0] = __builtin_amdgcn_readfirstlane((unsigned)a);
+    rs[1] = __builtin_amdgcn_readfirstlane((unsigned)(a >> 32)) & 0xffffu;
+    rs[2] = __builtin_amdgcn_readfirstlane((unsigned)nrec);
+    rs[3] = 0x00020000u;
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const unsigned la = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(att_lds_ptr)(lds + (2 * wave + t) * 1024));
+      asm volatile("s_mov_b32 m0, %0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds" :: "s"(la), "v"(voff[t]), "s"(rs)
+                   : "memory");
+    }
+#else
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)(base + off), (short)0, nrec, 0x00020000);
 #pragma unroll
     for (int t = 0; t < 2; ++t)
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (att_lds_ptr)(lds + (2 * wave + t) * 1024), 16, voff[t], 0, 0, 0);
+#endif
   }
 };
 
@@ -84,6 +107,43 @@ __device__ __forceinline__ bf16x8 tr_frag(const char* lds, int r0, int s, int c0
   short4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(short4_t, lds + att_off(ra + 8, ch) + hb));
   short8_t v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
   return __builtin_bit_cast(bf16x8, v);
+}
+
+// The same transposed fragment read by inline asm.  hipcc (ROCm 7.2) cannot tell a ds_read_tr16 builtin from an
+// access to the LDS-DMA destination, so it puts an `s_waitcnt vmcnt(0)` in front of the first one after any DMA
+// issue — which drains the NEXT tile's prefetch in the middle of the current tile (seen in the .s of all three flash
+// kernels).  The asm reads are invisible to its LDS-DMA tracking; their results are consumed only behind
+// `tr_wait()` (lgkmcnt(0) + a scheduling fence, so no consumer is hoisted above the wait).  The compiler's own
+// counted lgkmcnt waits stay correct beside them: LDS returns in order, so extra reads in flight only make a count
+// conservative.  CMHAR_ATTN_TRASM=0 restores the builtin (A/B).
+#ifndef CMHAR_ATTN_TRASM
+#define CMHAR_ATTN_TRASM 0
+#endif
+__device__ __forceinline__ short4_t ds_tr16_asm(const char* p) {
+  short4_t v;
+  const unsigned a = (unsigned)(uintptr_t)(att_lds_ptr)(p);
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(v) : "v"(a) : "memory");
+  return v;
+}
+__device__ __forceinline__ bf16x8 tr_frag_a(const char* lds, int r0, int s, int c0, int lane) {
+#if CMHAR_ATTN_TRASM
+  const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3, h = g >> 1;
+  const int col = c0 + 16 * (g & 1) + 4 * p;
+  const int ch = col >> 3, hb = (col & 7) * 2;
+  const int ra = r0 + 16 * s + 4 * h + q;
+  const short4_t lo = ds_tr16_asm(lds + att_off(ra, ch) + hb);
+  const short4_t hi = ds_tr16_asm(lds + att_off(ra + 8, ch) + hb);
+  short8_t v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8, v);
+#else
+  return tr_frag(lds, r0, s, c0, lane);
+#endif
+}
+__device__ __forceinline__ void tr_wait() {
+#if CMHAR_ATTN_TRASM
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+#endif
 }
 
 // Accumulator registers 8s..8s+7 → 16-bit operand fragment in format E (bf16, or fp16 on the inference path).
@@ -191,6 +251,13 @@ __global__ __launch_bounds__(256, CMHAR_ATTN_FWD_PERKB ? 3 : 2) void attn_fwd_bf
 #pragma unroll
           for (int j = 0; j < QB; ++j) s[j] = mma32<E>(kf, qf[j][t], s[j]);
         }
+#if CMHAR_ATTN_TRASM
+        bf16x8 vtr[2][2];                  // V transposed fragments in flight under the softmax
+#pragma unroll
+        for (int ss = 0; ss < 2; ++ss)
+#pragma unroll
+          for (int d = 0; d < 2; ++d) vtr[ss][d] = tr_frag_a(Vs(cur), kb * 32, ss, d * 32, lane);
+#endif
         if (kbase + kb * 32 + 32 > Lk) {   // ragged last half-tile only (wave-uniform branch)
 #pragma unroll
           for (int j = 0; j < QB; ++j)
@@ -226,6 +293,15 @@ __global__ __launch_bounds__(256, CMHAR_ATTN_FWD_PERKB ? 3 : 2) void attn_fwd_bf
 #pragma unroll
           for (int ss = 0; ss < 2; ++ss) pb[j][ss] = pack8<E>(s[j], ss);
         }
+#if CMHAR_ATTN_TRASM
+        tr_wait();
+#pragma unroll
+        for (int ss = 0; ss < 2; ++ss)
+#pragma unroll
+          for (int d = 0; d < 2; ++d)
+#pragma unroll
+            for (int j = 0; j < QB; ++j) o[j][d] = mma32<E>(vtr[ss][d], pb[j][ss], o[j][d]);
+#else
 #pragma unroll
         for (int ss = 0; ss < 2; ++ss)
 #pragma unroll
@@ -234,6 +310,7 @@ __global__ __launch_bounds__(256, CMHAR_ATTN_FWD_PERKB ? 3 : 2) void attn_fwd_bf
 #pragma unroll
             for (int j = 0; j < QB; ++j) o[j][d] = mma32<E>(vf, pb[j][ss], o[j][d]);
           }
+#endif
       }
     }
 #else
@@ -363,7 +440,8 @@ __global__ __launch_bounds__(256, CMHAR_ATTN_FWD_PERKB ? 3 : 2) void attn_fwd_bf
 // the kernels are VALU-issue bound beside their MFMAs); kscale is the dK output factor (the true softmax scale, so
 // dK is the gradient of the unscaled key and the QKV backward is unchanged).
 template <bool PS = false>
-__global__ __launch_bounds__(256, CMHAR_DKDV_OCC) void attn_bwd_dkdv_bf16(int H, int Lq, int Lk, const bf16* __restrict__ Q,
+__global__ __launch_bounds__(256, CMHAR_DKDV_OCC) void attn_bwd_dkdv_bf16(int H, int Lq, int Lk, int k_base,
+                                                             const bf16* __restrict__ Q,
                                                              long ldq, const bf16* __restrict__ K, long ldk,
                                                              const bf16* __restrict__ V, long ldv,
                                                              const bf16* __restrict__ dO, long lddo,
@@ -379,7 +457,7 @@ __global__ __launch_bounds__(256, CMHAR_DKDV_OCC) void attn_bwd_dkdv_bf16(int H,
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5;
   const BlkIdx bi = flash_block(H);
   const int hd = bi.hd, b = bi.b;
-  const int k0 = bi.blk * 128 + wave * 32;
+  const int k0 = k_base + bi.blk * 128 + wave * 32;
   const bf16* Qb = Q + (long)b * Lq * ldq + hd * 64;
   const bf16* Gb = dO + (long)b * Lq * lddo + hd * 64;
   const float* lseb = lse + ((long)b * H + hd) * Lq;
@@ -405,17 +483,21 @@ __global__ __launch_bounds__(256, CMHAR_DKDV_OCC) void attn_bwd_dkdv_bf16(int H,
   tq.init(Qb, ldq, Lq, wave, lane);
   tg.init(Gb, lddo, Lq, wave, lane);
   float lv = 0.f, dv_ = 0.f;
+  int lq = 0;
+  // row constants, staged pre-negated (and -lse pre-divided by c) as accumulator seeds.  Every lane loads (no branch
+  // around the loads: hipcc waited vmcnt(0) right after a branch-guarded load, draining the tile DMA just issued)
   auto load_rows = [&](int qt, char* qs, char* gs) {
     tq.tile(qt * 64, qs, wave);
     tg.tile(qt * 64, gs, wave);
-    if (tid < 64) {   // row constants staged pre-negated (and -lse pre-divided by c): accumulator seeds
-      const int q = qt * 64 + tid;
-      lv = q < Lq ? -lseb[q] * inv_c : -INFINITY;
-      dv_ = q < Lq ? -delb[q] : 0.f;
-    }
+    lq = qt * 64 + lane;
+    lv = lseb[min(lq, Lq - 1)];
+    dv_ = delb[min(lq, Lq - 1)];
   };
   auto store_rows = [&](int buf) {
-    if (tid < 64) { Ls[buf * 64 + tid] = lv; Ds[buf * 64 + tid] = dv_; }
+    if (tid < 64) {
+      Ls[buf * 64 + tid] = lq < Lq ? -lv * inv_c : -INFINITY;
+      Ds[buf * 64 + tid] = lq < Lq ? -dv_ : 0.f;
+    }
   };
   load_rows(0, Qs(0), Gs(0));
   store_rows(0);
@@ -466,6 +548,16 @@ __global__ __launch_bounds__(256, CMHAR_DKDV_OCC) void attn_bwd_dkdv_bf16(int H,
       // v_pk_mul_f32 + one v_cvt_pk_bf16_f32 per pair; element-wise, the compiler paired (1,2),(3,4),... and spent
       // v_mov / v_alignbit / v_perm re-pairing them for the packs; the backward got 3 % faster, bit-identical.  The
       // same rewrite of the forward's softmax measured 5 % slower and is not used)
+#if CMHAR_ATTN_TRASM
+      bf16x8 gtr[2][2], qtr[2][2];         // dOᵀ / Qᵀ fragments in flight under the softmax
+#pragma unroll
+      for (int ss = 0; ss < 2; ++ss)
+#pragma unroll
+        for (int d = 0; d < 2; ++d) {
+          gtr[ss][d] = tr_frag_a(Gs(cur), qb * 32, ss, d * 32, lane);
+          qtr[ss][d] = tr_frag_a(Qs(cur), qb * 32, ss, d * 32, lane);
+        }
+#endif
       bf16x8 pbv[2], dbv[2];
 #pragma unroll
       for (int r = 0; r < 16; r += 2) {
@@ -478,13 +570,21 @@ __global__ __launch_bounds__(256, CMHAR_DKDV_OCC) void attn_bwd_dkdv_bf16(int H,
         dbv[r >> 3][r & 7] = dd[0];
         dbv[r >> 3][(r & 7) + 1] = dd[1];
       }
+#if CMHAR_ATTN_TRASM
+      tr_wait();
+#endif
 #pragma unroll
       for (int ss = 0; ss < 2; ++ss) {
         const bf16x8 pb = pbv[ss], db = dbv[ss];
 #pragma unroll
         for (int d = 0; d < 2; ++d) {
+#if CMHAR_ATTN_TRASM
+          dv[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(gtr[ss][d], pb, dv[d], 0, 0, 0);
+          dk[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qtr[ss][d], db, dk[d], 0, 0, 0);
+#else
           dv[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_frag(Gs(cur), qb * 32, ss, d * 32, lane), pb, dv[d], 0, 0, 0);
           dk[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_frag(Qs(cur), qb * 32, ss, d * 32, lane), db, dk[d], 0, 0, 0);
+#endif
         }
       }
     }
@@ -512,6 +612,232 @@ __global__ __launch_bounds__(256, CMHAR_DKDV_OCC) void attn_bwd_dkdv_bf16(int H,
         *(bf16x4*)(krow + d * 32 + 8 * g + 4 * h) = a;
         *(bf16x4*)(vrow + d * 32 + 8 * g + 4 * h) = v;
       }
+  }
+}
+
+// dK, dV with 64 keys per wave at ONE wave per SIMD (a workgroup = 4 waves = 256 keys; round 4), for the pre-scaled
+// bf16 training path.  The 32-key form above reads every Q / dO fragment from LDS for one 32-key MFMA block — its
+// LDS traffic is half its MFMA time — and its waves stall on per-MFMA read latency (PMC: MFMA pipes 49 % busy).  Here
+// each fragment feeds the wave's two 32-key blocks (half the LDS bytes per MFMA) and the 512-register file holds two
+// query blocks of S / dP: the loop is software-pipelined so a block's S and dP products issue beside the previous
+// block's softmax VALU and its dV / dK products beside the next block's.  Q / dO tiles of 64 queries AND their lse /
+// δ rows arrive by LDS-DMA into a ring of four slots two tiles ahead, every DMA issued by inline asm (async_dma16 /
+// async_dma4): hipcc then sees no LDS write in flight and emits no `vmcnt(0)` before the LDS reads of the current
+// tile (the builtin form drained the prefetch in the middle of every tile); the kernel orders the DMA itself with a
+// counted vmcnt + barrier per tile.  The rows arrive RAW: the key and value fragments are negated once at entry, so
+// the S / dP accumulators seeded with +lse / +δ hold −(Q·Kᵀ − lse) and −(dO·Vᵀ − δ) — exactly the negations of the
+// 32-key kernel's seeded sums (IEEE rounding is sign-symmetric) — p = exp2(−acc) takes the sign as a source modifier,
+// dS comes out negated and the final dK factor is −kscale: dK / dV are bit-identical to attn_bwd_dkdv_bf16<true>.
+#ifndef CMHAR_DKDV_K64
+#define CMHAR_DKDV_K64 0
+#endif
+// one 1-KiB LDS-DMA piece (lane-linear 16 B per lane) / one 256-B row piece (4 B per lane) by inline asm; rs = the
+// buffer resource (wave-uniform), la = the piece's LDS byte address (wave-uniform)
+__device__ __forceinline__ void async_dma16(uint4_t rs, unsigned la, int voff) {
+  asm volatile("s_mov_b32 m0, %0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds" :: "s"(la), "v"(voff), "s"(rs) : "memory");
+}
+__device__ __forceinline__ void async_dma4(uint4_t rs, unsigned la, int voff) {
+  asm volatile("s_mov_b32 m0, %0\n\tbuffer_load_dword %1, %2, 0 offen lds" :: "s"(la), "v"(voff), "s"(rs) : "memory");
+}
+__device__ __forceinline__ uint4_t buf_rsrc(const void* p, long bytes) {
+  const unsigned long long a = (unsigned long long)p;
+  uint4_t rs;
+  rs[0] = __builtin_amdgcn_readfirstlane((unsigned)a);
+  rs[1] = __builtin_amdgcn_readfirstlane((unsigned)(a >> 32)) & 0xffffu;
+  rs[2] = __builtin_amdgcn_readfirstlane((unsigned)(bytes > 0 ? (bytes < 0x7fffffff ? bytes : 0x7fffffff) : 0));
+  rs[3] = 0x00020000u;
+  return rs;
+}
+__device__ __forceinline__ unsigned lds_addr(const char* p) {
+  return __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(att_lds_ptr)(p));
+}
+
+__global__ __launch_bounds__(256, 1) void attn_bwd_dkdv_k64(int H, int Lq, int Lk, const bf16* __restrict__ Q,
+                                                            long ldq, const bf16* __restrict__ K, long ldk,
+                                                            const bf16* __restrict__ V, long ldv,
+                                                            const bf16* __restrict__ dO, long lddo,
+                                                            const float* __restrict__ lse,
+                                                            const float* __restrict__ delta, bf16* __restrict__ dK,
+                                                            long lddk, bf16* __restrict__ dV, long lddv, float kscale) {
+  constexpr int TB = 16384 + 512;               // one ring slot: Q [64][64] | dO [64][64] | lse [64] | δ [64]
+  __shared__ __attribute__((aligned(16))) char smem[4 * TB];
+#define QS(i) (smem + TB * (i))
+#define GS(i) (smem + TB * (i) + 8192)
+#define LS(i) ((const float*)(smem + TB * (i) + 16384))
+#define DS(i) ((const float*)(smem + TB * (i) + 16384 + 256))
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5;
+  const BlkIdx bi = flash_block(H);
+  const int hd = bi.hd, b = bi.b;
+  const int k0 = bi.blk * 256 + wave * 64;
+  const char* Qb = (const char*)(Q + (long)b * Lq * ldq + hd * 64);
+  const char* Gb = (const char*)(dO + (long)b * Lq * lddo + hd * 64);
+  const float* rowb = ((wave & 1) ? delta : lse) + ((long)b * H + hd) * Lq;   // wave w stages lse (even) / δ (odd)
+
+  // −K, −V fragments (bf16 sign flips: exact)
+  bf16x8 kf[2][4], vf[2][4];
+#pragma unroll
+  for (int kb = 0; kb < 2; ++kb) {
+    const int myk = min(k0 + 32 * kb + (lane & 31), Lk - 1);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const uint4_t kk = *(const uint4_t*)(K + ((long)b * Lk + myk) * ldk + hd * 64 + 16 * t + 8 * h);
+      const uint4_t vv = *(const uint4_t*)(V + ((long)b * Lk + myk) * ldv + hd * 64 + 16 * t + 8 * h);
+      kf[kb][t] = __builtin_bit_cast(bf16x8, kk ^ 0x80008000u);
+      vf[kb][t] = __builtin_bit_cast(bf16x8, vv ^ 0x80008000u);
+    }
+  }
+  floatx16 dk[2][2], dv[2][2];
+#pragma unroll
+  for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+    for (int d = 0; d < 2; ++d)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) { dk[kb][d][r] = 0.f; dv[kb][d][r] = 0.f; }
+
+  const int nt = (Lq + 63) / 64;
+  // per-lane DMA offsets: Q / dO piece t of this wave = rows 8(2·wave + t) .. +7, the att_off swizzle on the SOURCE
+  int qoff[2], goff[2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    const int row = 8 * (2 * wave + t) + (lane >> 3);
+    const int f = (((row >> 1) & 1) << 2) | ((row >> 3) & 3);
+    qoff[t] = (int)(row * ldq * 2 + (((lane & 7) ^ f) << 4));
+    goff[t] = (int)(row * lddo * 2 + (((lane & 7) ^ f) << 4));
+  }
+  // one tile: 2 Q pieces + 2 dO pieces + this wave's 256-B row piece (waves 0 / 2 lse, 1 / 3 δ: each row piece is
+  // staged twice, identically) = 5 DMA per wave
+  auto issue = [&](int qt, char* slot) __attribute__((always_inline)) {
+    const long r0 = (long)qt * 64;
+    const uint4_t rq = buf_rsrc(Qb + r0 * ldq * 2, (long)(Lq - 1 - r0) * ldq * 2 + 128);
+    const uint4_t rg = buf_rsrc(Gb + r0 * lddo * 2, (long)(Lq - 1 - r0) * lddo * 2 + 128);
+    const uint4_t rr = buf_rsrc(rowb + r0, (long)(Lq - r0) * 4);
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      async_dma16(rq, lds_addr(slot + (2 * wave + t) * 1024), qoff[t]);
+      async_dma16(rg, lds_addr(slot + 8192 + (2 * wave + t) * 1024), goff[t]);
+    }
+    async_dma4(rr, lds_addr(slot + 16384 + (wave & 1) * 256), lane * 4);
+  };
+  issue(0, QS(0));
+  if (nt > 1) issue(1, QS(1));
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+
+  // S / dP of query block qb of a slot (key on the lane), seeded with +lse / +δ over −K / −V: acc = −(true − seed)
+  auto sdp = [&](const char* qs, const char* gs, const float* L_, const float* D_, int qb, floatx16 (&s)[2],
+                 floatx16 (&dp)[2]) __attribute__((always_inline)) {
+    bf16x8 qr[4], gr[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      qr[t] = row_frag(qs, qb * 32, t, lane);
+      gr[t] = row_frag(gs, qb * 32, t, lane);
+    }
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int q = qb * 32 + acc_row(r, h);
+        s[kb][r] = L_[q];
+        dp[kb][r] = D_[q];
+      }
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb) {
+        s[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qr[t], kf[kb][t], s[kb], 0, 0, 0);
+        dp[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(gr[t], vf[kb][t], dp[kb], 0, 0, 0);
+      }
+  };
+  // p = exp2(−acc_s), −dS = p ∘ acc_dp: bf16 packs in aligned register pairs
+  auto soft = [&](const floatx16 (&s)[2], const floatx16 (&dp)[2], bf16x8 (&pb)[2][2], bf16x8 (&db)[2][2])
+      __attribute__((always_inline)) {
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int r = 0; r < 16; r += 2) {
+        const float2_t pv = float2_t{fexp2(-s[kb][r]), fexp2(-s[kb][r + 1])};
+        const float2_t dv2 = pv * float2_t{dp[kb][r], dp[kb][r + 1]};
+        const bf16x2_t pp = __builtin_convertvector(pv, bf16x2_t);
+        const bf16x2_t dd = __builtin_convertvector(dv2, bf16x2_t);
+        pb[kb][r >> 3][r & 7] = pp[0];
+        pb[kb][r >> 3][(r & 7) + 1] = pp[1];
+        db[kb][r >> 3][r & 7] = dd[0];
+        db[kb][r >> 3][(r & 7) + 1] = dd[1];
+      }
+  };
+  // dVᵀ += dOᵀ·P, −dKᵀ += Qᵀ·(−dS) for both key blocks; each transposed fragment feeds two MFMAs
+  auto dvdk = [&](const char* qs, const char* gs, int qb, const bf16x8 (&pb)[2][2], const bf16x8 (&db)[2][2])
+      __attribute__((always_inline)) {
+#pragma unroll
+    for (int ss = 0; ss < 2; ++ss)
+#pragma unroll
+      for (int d = 0; d < 2; ++d) {
+        const bf16x8 gt = tr_frag(gs, qb * 32, ss, d * 32, lane);
+        const bf16x8 qt = tr_frag(qs, qb * 32, ss, d * 32, lane);
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb) {
+          dv[kb][d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(gt, pb[kb][ss], dv[kb][d], 0, 0, 0);
+          dk[kb][d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qt, db[kb][ss], dk[kb][d], 0, 0, 0);
+        }
+      }
+  };
+
+  // Software pipeline over the 2·nt query blocks (block (t, qb) = rows 32qb.. of tile t).  Iteration t: S/dP of (t, 0)
+  // beside the softmax of (t−1, 1); dV/dK of (t−1, 1); S/dP of (t, 1) beside the softmax of (t, 0); dV/dK of (t, 0).
+  // Ring slot of tile t = t % 4; the DMA of tile t + 2 goes to the slot tile t − 2 used (last read in iteration
+  // t − 1, behind its closing barrier) and is waited for at the end of iteration t + 1.
+  floatx16 sA[2], dpA[2], sB[2], dpB[2];       // A: (t, 0); B: (t, 1) — B carries into the next iteration
+  bf16x8 pb[2][2], db[2][2];
+  auto iter = [&](auto CUR, int t) __attribute__((always_inline)) {
+    constexpr int cur = decltype(CUR)::value, prv = (cur + 3) & 3, nx2 = (cur + 2) & 3;
+    const bool more2 = t + 2 < nt;
+    if (more2) issue(t + 2, QS(nx2));
+    sdp(QS(cur), GS(cur), LS(cur), DS(cur), 0, sA, dpA);
+    if (t > 0) {
+      soft(sB, dpB, pb, db);
+      dvdk(QS(prv), GS(prv), 1, pb, db);
+    }
+    sdp(QS(cur), GS(cur), LS(cur), DS(cur), 1, sB, dpB);
+    soft(sA, dpA, pb, db);
+    dvdk(QS(cur), GS(cur), 0, pb, db);
+    // tile t + 1 landed (issued one iteration earlier): leave only tile t + 2's 5 pieces in flight
+    if (more2) asm volatile("s_waitcnt vmcnt(5) lgkmcnt(0)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  };
+  for (int t = 0; t < nt; t += 4) {
+    iter(std::integral_constant<int, 0>{}, t);
+    if (t + 1 < nt) iter(std::integral_constant<int, 1>{}, t + 1);
+    if (t + 2 < nt) iter(std::integral_constant<int, 2>{}, t + 2);
+    if (t + 3 < nt) iter(std::integral_constant<int, 3>{}, t + 3);
+  }
+  {   // the last block (nt − 1, 1): its S/dP were issued in the last iteration
+    const int lb = (nt - 1) & 3;
+    soft(sB, dpB, pb, db);
+    dvdk(QS(lb), GS(lb), 1, pb, db);
+  }
+#undef QS
+#undef GS
+#undef LS
+#undef DS
+  const float nks = -kscale;
+#pragma unroll
+  for (int kb = 0; kb < 2; ++kb) {
+    const int key = k0 + 32 * kb + (lane & 31);
+    if (key < Lk) {
+      bf16* krow = dK + ((long)b * Lk + key) * lddk + hd * 64;
+      bf16* vrow = dV + ((long)b * Lk + key) * lddv + hd * 64;
+#pragma unroll
+      for (int d = 0; d < 2; ++d)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          bf16x4 a, v;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) { a[j] = (bf16)(dk[kb][d][4 * g + j] * nks); v[j] = (bf16)dv[kb][d][4 * g + j]; }
+          *(bf16x4*)(krow + d * 32 + 8 * g + 4 * h) = a;
+          *(bf16x4*)(vrow + d * 32 + 8 * g + 4 * h) = v;
+        }
+    }
   }
 }
 
@@ -631,6 +957,13 @@ __global__ __launch_bounds__(256, QB == 1 ? CMHAR_DQ_OCC : 2) void attn_bwd_dq_b
         }
       }
 #endif
+#if CMHAR_ATTN_TRASM
+      bf16x8 ktrs[2][2];                   // Kᵀ fragments in flight under the dS arithmetic
+#pragma unroll
+      for (int ss = 0; ss < 2; ++ss)
+#pragma unroll
+        for (int d = 0; d < 2; ++d) ktrs[ss][d] = tr_frag_a(Ks(cur), kb * 32, ss, d * 32, lane);
+#endif
       if (kbase + 64 > Lk) {   // ragged last tile only (wave-uniform branch)
 #pragma unroll
         for (int j = 0; j < QB; ++j)
@@ -650,6 +983,16 @@ __global__ __launch_bounds__(256, QB == 1 ? CMHAR_DQ_OCC : 2) void attn_bwd_dq_b
           db[j][r >> 3][(r & 7) + 1] = dd[1];
         }
       }
+#if CMHAR_ATTN_TRASM
+      tr_wait();
+#pragma unroll
+      for (int ss = 0; ss < 2; ++ss)
+#pragma unroll
+        for (int d = 0; d < 2; ++d)
+#pragma unroll
+          for (int j = 0; j < QB; ++j)
+            dq[j][d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ktrs[ss][d], db[j][ss], dq[j][d], 0, 0, 0);
+#else
 #pragma unroll
       for (int ss = 0; ss < 2; ++ss)
 #pragma unroll
@@ -659,6 +1002,7 @@ __global__ __launch_bounds__(256, QB == 1 ? CMHAR_DQ_OCC : 2) void attn_bwd_dq_b
           for (int j = 0; j < QB; ++j)
             dq[j][d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ktr, db[j][ss], dq[j][d], 0, 0, 0);
         }
+#endif
     }
     if (more) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // own pieces of the next tile landed
     __syncthreads();
@@ -1302,11 +1646,17 @@ static void flash_bwd_bf16(int B, int H, int Lq, int Lk, const void* Q, long ldq
                                                              (const bf16*)dO, lddo, lse, delta, (bf16*)dQ, lddq, s_in);
   const int kfull = (Lk / 128) * 128;
   const bool ktail = Lk > kfull && Lk - kfull <= CMHAR_ATTN_TAIL;
-  const int kblocks = ktail ? kfull / 128 : cdiv(Lk, 128);
+  // 256-key workgroups of the 64-keys-per-wave kernel over the bulk (round 4), 128-key ones for the rest
+  const int k256 = (PS && CMHAR_DKDV_K64) ? (Lk / 256) * 256 : 0;
+  if (k256 > 0)
+    attn_bwd_dkdv_k64<<<dim3(k256 / 256, H, B), 256, 0, st>>>(H, Lq, Lk, (const bf16*)Q, ldq, (const bf16*)K, ldk,
+                                                              (const bf16*)V, ldv, (const bf16*)dO, lddo, lse, delta,
+                                                              (bf16*)dK, lddk, (bf16*)dV, lddv, scale);
+  const int kblocks = (ktail ? kfull : cdiv(Lk, 128) * 128) / 128 - k256 / 128;
   if (kblocks > 0)
-    attn_bwd_dkdv_bf16<PS><<<dim3(kblocks, H, B), 256, 0, st>>>(H, Lq, Lk, (const bf16*)Q, ldq, (const bf16*)K, ldk,
-                                                                (const bf16*)V, ldv, (const bf16*)dO, lddo, lse, delta,
-                                                                (bf16*)dK, lddk, (bf16*)dV, lddv, s_in, scale);
+    attn_bwd_dkdv_bf16<PS><<<dim3(kblocks, H, B), 256, 0, st>>>(H, Lq, Lk, k256, (const bf16*)Q, ldq, (const bf16*)K,
+                                                                ldk, (const bf16*)V, ldv, (const bf16*)dO, lddo, lse,
+                                                                delta, (bf16*)dK, lddk, (bf16*)dV, lddv, s_in, scale);
   if (ktail)
     attn_bwd_dkdv_tail_bf16<PS><<<dim3(cdiv(Lk - kfull, 32), H, B), 256, 0, st>>>(H, Lq, Lk, kfull, (const bf16*)Q,
                                                                                   ldq, (const bf16*)K,
