@@ -1031,6 +1031,185 @@ __global__ __launch_bounds__(256, QB == 1 ? CMHAR_DQ_OCC : 2) void attn_bwd_dq_b
 #undef Ks
 #undef Vs
 
+// dQ with 64 queries per wave at ONE wave per SIMD (a workgroup = 4 waves = 256 queries; round 4), pre-scaled bf16
+// training path — the counterpart of attn_bwd_dkdv_k64: every K / V fragment read from LDS feeds both of the wave's
+// 32-query blocks, K / V tiles of 64 keys arrive by inline-asm LDS-DMA into a four-slot ring two tiles ahead, and the
+// loop is software-pipelined over 32-key halves (S / dP of a half beside the previous half's dS arithmetic, dQ of a
+// half beside the next one's).  Per-element arithmetic and accumulation order are those of attn_bwd_dq_bf16<QB, true>
+// (seeds −lse and −δ, p = exp2(acc), dS packs, dQ over the key halves in order): bit-identical dQ and δ.
+#ifndef CMHAR_DQ_Q64
+#define CMHAR_DQ_Q64 0
+#endif
+__global__ __launch_bounds__(256, 1) void attn_bwd_dq_q64(int H, int Lq, int Lk, const bf16* __restrict__ Q, long ldq,
+                                                          const bf16* __restrict__ K, long ldk,
+                                                          const bf16* __restrict__ V, long ldv,
+                                                          const bf16* __restrict__ O, long ldo,
+                                                          const bf16* __restrict__ dO, long lddo,
+                                                          const float* __restrict__ lse, float* __restrict__ delta,
+                                                          bf16* __restrict__ dQ, long lddq, float scale) {
+  constexpr int TB = 16384;                     // one ring slot: K [64][64] | V [64][64]
+  __shared__ __attribute__((aligned(16))) char smem[4 * TB];
+#define KS(i) (smem + TB * (i))
+#define VS(i) (smem + TB * (i) + 8192)
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5;
+  const BlkIdx bi = flash_block(H);
+  const int hd = bi.hd, b = bi.b;
+  const int q0 = bi.blk * 256 + wave * 64;
+  const char* Kb = (const char*)(K + (long)b * Lk * ldk + hd * 64);
+  const char* Vb = (const char*)(V + (long)b * Lk * ldv + hd * 64);
+  bf16x8 qf[2][4], gf[2][4];
+  float sL[2], Dl[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int myq = min(q0 + 32 * j + (lane & 31), Lq - 1);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      qf[j][t] = *(const bf16x8*)(Q + ((long)b * Lq + myq) * ldq + hd * 64 + 16 * t + 8 * h);
+      gf[j][t] = *(const bf16x8*)(dO + ((long)b * Lq + myq) * lddo + hd * 64 + 16 * t + 8 * h);
+    }
+    sL[j] = -lse[((long)b * H + hd) * Lq + myq];      // c = 1 (pre-scaled keys): p = exp2(acc)
+    float d_ = 0.f;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const bf16x8 ov = *(const bf16x8*)(O + ((long)b * Lq + myq) * ldo + hd * 64 + 16 * t + 8 * h);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) d_ = fmaf((float)gf[j][t][e], (float)ov[e], d_);
+    }
+    d_ += xhalf(d_);
+    Dl[j] = d_;
+    if (h == 0 && q0 + 32 * j + (lane & 31) < Lq) delta[((long)b * H + hd) * Lq + myq] = d_;
+  }
+  floatx16 dq[2][2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int d = 0; d < 2; ++d)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) dq[j][d][r] = 0.f;
+
+  const int nt = (Lk + 63) / 64;
+  int koff[2], voff[2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    const int row = 8 * (2 * wave + t) + (lane >> 3);
+    const int f = (((row >> 1) & 1) << 2) | ((row >> 3) & 3);
+    koff[t] = (int)(row * ldk * 2 + (((lane & 7) ^ f) << 4));
+    voff[t] = (int)(row * ldv * 2 + (((lane & 7) ^ f) << 4));
+  }
+  auto issue = [&](int kt, char* slot) __attribute__((always_inline)) {   // 4 DMA per wave
+    const long r0 = (long)kt * 64;
+    const uint4_t rk = buf_rsrc(Kb + r0 * ldk * 2, (long)(Lk - 1 - r0) * ldk * 2 + 128);
+    const uint4_t rv = buf_rsrc(Vb + r0 * ldv * 2, (long)(Lk - 1 - r0) * ldv * 2 + 128);
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      async_dma16(rk, lds_addr(slot + (2 * wave + t) * 1024), koff[t]);
+      async_dma16(rv, lds_addr(slot + 8192 + (2 * wave + t) * 1024), voff[t]);
+    }
+  };
+  issue(0, KS(0));
+  if (nt > 1) issue(1, KS(1));
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+
+  // Sᵀ / dPᵀ of key half kb of a slot for both query blocks (query on the lane), seeded with −lse / −δ
+  auto sdp = [&](const char* ks, const char* vs, int kb, int kbase, floatx16 (&s)[2], floatx16 (&dp)[2])
+      __attribute__((always_inline)) {
+    bf16x8 kr[4], vr[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      kr[t] = row_frag(ks, kb * 32, t, lane);
+      vr[t] = row_frag(vs, kb * 32, t, lane);
+    }
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) { s[j][r] = sL[j]; dp[j][r] = -Dl[j]; }
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        s[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kr[t], qf[j][t], s[j], 0, 0, 0);
+        dp[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vr[t], gf[j][t], dp[j], 0, 0, 0);
+      }
+    if (kbase + kb * 32 + 32 > Lk) {         // ragged last half only (wave-uniform branch)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          if (kbase + kb * 32 + acc_row(r, h) >= Lk) s[j][r] = -INFINITY;
+    }
+  };
+  auto soft = [&](const floatx16 (&s)[2], const floatx16 (&dp)[2], bf16x8 (&db)[2][2]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; r += 2) {
+        const float2_t pv = float2_t{fexp2(s[j][r]), fexp2(s[j][r + 1])};
+        const bf16x2_t dd = __builtin_convertvector(pv * float2_t{dp[j][r], dp[j][r + 1]}, bf16x2_t);
+        db[j][r >> 3][r & 7] = dd[0];
+        db[j][r >> 3][(r & 7) + 1] = dd[1];
+      }
+  };
+  auto dqs = [&](const char* ks, int kb, const bf16x8 (&db)[2][2]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int ss = 0; ss < 2; ++ss)
+#pragma unroll
+      for (int d = 0; d < 2; ++d) {
+        const bf16x8 ktr = tr_frag(ks, kb * 32, ss, d * 32, lane);
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          dq[j][d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ktr, db[j][ss], dq[j][d], 0, 0, 0);
+      }
+  };
+  floatx16 sA[2], dpA[2], sB[2], dpB[2];
+  bf16x8 db[2][2];
+  auto iter = [&](auto CUR, int t) __attribute__((always_inline)) {
+    constexpr int cur = decltype(CUR)::value, prv = (cur + 3) & 3, nx2 = (cur + 2) & 3;
+    const bool more2 = t + 2 < nt;
+    if (more2) issue(t + 2, KS(nx2));
+    sdp(KS(cur), VS(cur), 0, t * 64, sA, dpA);
+    if (t > 0) {
+      soft(sB, dpB, db);
+      dqs(KS(prv), 1, db);
+    }
+    sdp(KS(cur), VS(cur), 1, t * 64, sB, dpB);
+    soft(sA, dpA, db);
+    dqs(KS(cur), 0, db);
+    if (more2) asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  };
+  for (int t = 0; t < nt; t += 4) {
+    iter(std::integral_constant<int, 0>{}, t);
+    if (t + 1 < nt) iter(std::integral_constant<int, 1>{}, t + 1);
+    if (t + 2 < nt) iter(std::integral_constant<int, 2>{}, t + 2);
+    if (t + 3 < nt) iter(std::integral_constant<int, 3>{}, t + 3);
+  }
+  {
+    const int lb = (nt - 1) & 3;
+    soft(sB, dpB, db);
+    dqs(KS(lb), 1, db);
+  }
+#undef KS
+#undef VS
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int q = q0 + 32 * j + (lane & 31);
+    if (q < Lq) {
+      bf16* row = dQ + ((long)b * Lq + q) * lddq + hd * 64;
+#pragma unroll
+      for (int d = 0; d < 2; ++d)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          bf16x4 v;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = (bf16)(dq[j][d][4 * g + e] * scale);
+          *(bf16x4*)(row + d * 32 + 8 * g + 4 * h) = v;
+        }
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------------------------------------------
 // Ragged tails.  At 16×224² L = 1568 = 12·128 + 32: each head leaves ≤ 32 queries (forward, dQ) or keys (dK/dV)
 // beyond the last full block.  As a block of the kernels above, such a tail runs ONE active wave over the whole other
@@ -1622,8 +1801,13 @@ static void flash_bwd_bf16(int B, int H, int Lq, int Lk, const void* Q, long ldq
                            long lddv, float scale, hipStream_t st) {
   const float s_in = PS ? 1.f / LOG2E : scale;   // c = s_in·log2e (1 when PS) and the dQ output factor
   // 256-query workgroups (QB = 2) over the bulk, 128-query workgroups for the rest (as the forward)
-  const int bulk = CMHAR_ATTN_DQ_QB == 2 ? (Lq / 256) * 256 : 0;
-  if (bulk > 0)
+  const bool q64 = PS && CMHAR_DQ_Q64;
+  const int bulk = (CMHAR_ATTN_DQ_QB == 2 || q64) ? (Lq / 256) * 256 : 0;
+  if (bulk > 0 && q64)
+    attn_bwd_dq_q64<<<dim3(bulk / 256, H, B), 256, 0, st>>>(H, Lq, Lk, (const bf16*)Q, ldq, (const bf16*)K, ldk,
+                                                            (const bf16*)V, ldv, (const bf16*)O, ldo, (const bf16*)dO,
+                                                            lddo, lse, delta, (bf16*)dQ, lddq, s_in);
+  else if (bulk > 0)
     attn_bwd_dq_bf16<2, PS><<<dim3(bulk / 256, H, B), 256, 0, st>>>(H, Lq, Lk, 0, (const bf16*)Q, ldq, (const bf16*)K,
                                                                     ldk, (const bf16*)V, ldv, (const bf16*)O, ldo,
                                                                     (const bf16*)dO, lddo, lse, delta, (bf16*)dQ,
