@@ -91,6 +91,27 @@ struct TileDma {
   }
 };
 
+// one 1-KiB LDS-DMA piece (lane-linear 16 B per lane) / one 256-B row piece (4 B per lane) by inline asm; rs = the
+// buffer resource (wave-uniform), la = the piece's LDS byte address (wave-uniform)
+__device__ __forceinline__ void async_dma16(uint4_t rs, unsigned la, int voff) {
+  asm volatile("s_mov_b32 m0, %0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds" :: "s"(la), "v"(voff), "s"(rs) : "memory");
+}
+__device__ __forceinline__ void async_dma4(uint4_t rs, unsigned la, int voff) {
+  asm volatile("s_mov_b32 m0, %0\n\tbuffer_load_dword %1, %2, 0 offen lds" :: "s"(la), "v"(voff), "s"(rs) : "memory");
+}
+__device__ __forceinline__ uint4_t buf_rsrc(const void* p, long bytes) {
+  const unsigned long long a = (unsigned long long)p;
+  uint4_t rs;
+  rs[0] = __builtin_amdgcn_readfirstlane((unsigned)a);
+  rs[1] = __builtin_amdgcn_readfirstlane((unsigned)(a >> 32)) & 0xffffu;
+  rs[2] = __builtin_amdgcn_readfirstlane((unsigned)(bytes > 0 ? (bytes < 0x7fffffff ? bytes : 0x7fffffff) : 0));
+  rs[3] = 0x00020000u;
+  return rs;
+}
+__device__ __forceinline__ unsigned lds_addr(const char* p) {
+  return __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(att_lds_ptr)(p));
+}
+
 // Row fragment for a 32x32x16 A operand: lane holds row (r0 + lane&31), cols 16t + 8(lane>>5) .. +8.
 __device__ __forceinline__ bf16x8 row_frag(const char* lds, int r0, int t, int lane) {
   return *(const bf16x8*)(lds + att_off(r0 + (lane & 31), 2 * t + (lane >> 5)));
@@ -426,6 +447,176 @@ __global__ __launch_bounds__(256, CMHAR_ATTN_FWD_PERKB ? 3 : 2) void attn_fwd_bf
   }
 }
 
+// Forward, round-4 form: 64 queries per wave (two 32-query blocks), 4 waves = 256 queries, two workgroups per CU; K / V
+// tiles of 64 keys arrive by inline-asm LDS-DMA (see attn_bwd_dkdv_k64) into a four-slot ring two tiles ahead, so no
+// compiler-inserted `vmcnt(0)` drains the prefetch before the V transposed reads; and the loop is software-pipelined
+// over 32-key halves: the S products of a half issue beside the previous half's softmax and P·V.  Halves are consumed
+// in key order, so the online softmax (lazy rescale, running max / sum) and every accumulation are those of
+// attn_fwd_bf16<E, 2>: bit-identical O and LSE.
+#ifndef CMHAR_ATTN_FWD_P2
+#define CMHAR_ATTN_FWD_P2 0
+#endif
+template <typename E>
+__global__ __launch_bounds__(256, 2) void attn_fwd_p2(int H, int Lq, int Lk, const bf16* __restrict__ Q, long ldq,
+                                                      const bf16* __restrict__ K, long ldk,
+                                                      const bf16* __restrict__ V, long ldv, E* __restrict__ O,
+                                                      long ldo, float* __restrict__ lse, float scale) {
+  constexpr int TB = 16384;                     // one ring slot: K [64][64] | V [64][64]
+  __shared__ __attribute__((aligned(16))) char smem[4 * TB];
+#define KS(i) (smem + TB * (i))
+#define VS(i) (smem + TB * (i) + 8192)
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5;
+  const BlkIdx bi = flash_block(H);
+  const int hd = bi.hd, b = bi.b;
+  const int q0 = bi.blk * 256 + wave * 64;
+  const bf16* Qb = Q + (long)b * Lq * ldq + hd * 64;
+  const char* Kb = (const char*)(K + (long)b * Lk * ldk + hd * 64);
+  const char* Vb = (const char*)(V + (long)b * Lk * ldv + hd * 64);
+  const float c = scale * LOG2E;
+  bf16x8 qf[2][4];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int myq = min(q0 + 32 * j + (lane & 31), Lq - 1);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) qf[j][t] = *(const bf16x8*)(Qb + (long)myq * ldq + 16 * t + 8 * h);
+  }
+  floatx16 o[2][2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int d = 0; d < 2; ++d)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) o[j][d][r] = 0.f;
+  float m[2] = {-INFINITY, -INFINITY}, l[2] = {0.f, 0.f};
+
+  const int nt = (Lk + 63) / 64;
+  int koff[2], voff[2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    const int row = 8 * (2 * wave + t) + (lane >> 3);
+    const int f = (((row >> 1) & 1) << 2) | ((row >> 3) & 3);
+    koff[t] = (int)(row * ldk * 2 + (((lane & 7) ^ f) << 4));
+    voff[t] = (int)(row * ldv * 2 + (((lane & 7) ^ f) << 4));
+  }
+  // loop-invariant buffer resources over the whole head (rows past Lk fall outside num_records and read as zero); a
+  // tile's row offset rides in the per-lane voffset
+  const uint4_t rk = buf_rsrc(Kb, (long)(Lk - 1) * ldk * 2 + 128);
+  const uint4_t rv = buf_rsrc(Vb, (long)(Lk - 1) * ldv * 2 + 128);
+  const unsigned la0 = lds_addr(smem + 2 * wave * 1024);
+  auto issue = [&](int kt, int slot) __attribute__((always_inline)) {   // 4 DMA per wave
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      async_dma16(rk, la0 + slot * TB + t * 1024, koff[t] + kt * 64 * (int)ldk * 2);
+      async_dma16(rv, la0 + slot * TB + 8192 + t * 1024, voff[t] + kt * 64 * (int)ldv * 2);
+    }
+  };
+  issue(0, 0);
+  if (nt > 1) issue(1, 1);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+
+  // Sᵀ = K·Qᵀ of key half kb of a slot for both query blocks (query on the lane; ragged keys masked to −inf)
+  auto scores = [&](const char* ks, int kb, int kbase, floatx16 (&s)[2]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) s[j][r] = 0.f;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const bf16x8 kf = row_frag(ks, kb * 32, t, lane);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) s[j] = mma32<E>(kf, qf[j][t], s[j]);
+    }
+    if (kbase + kb * 32 + 32 > Lk) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          if (kbase + kb * 32 + acc_row(r, h) >= Lk) s[j][r] = -INFINITY;
+    }
+  };
+  // online softmax of one half (lazy rescale, as attn_fwd_bf16) then O += Vᵀ·Pᵀ
+  auto softpv = [&](const char* vs, int kb, floatx16 (&s)[2]) __attribute__((always_inline)) {
+    bf16x8 pb[2][2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      float mt = -INFINITY;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) mt = fmaxf(mt, s[j][r]);
+      mt = fmaxf(mt, xhalf(mt)) * c;
+      if (__builtin_amdgcn_ballot_w64(mt > m[j] + 8.f) != 0) {
+        const float mn = fmaxf(m[j], mt);
+        const float alpha = fexp2(m[j] - mn);
+        m[j] = mn;
+        l[j] *= alpha;
+#pragma unroll
+        for (int d = 0; d < 2; ++d)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) o[j][d][r] *= alpha;
+      }
+      const float mn = m[j];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float p = fexp2(fmaf(s[j][r], c, -mn));
+        s[j][r] = p;
+        l[j] += p;
+      }
+#pragma unroll
+      for (int ss = 0; ss < 2; ++ss) pb[j][ss] = pack8<E>(s[j], ss);
+    }
+#pragma unroll
+    for (int ss = 0; ss < 2; ++ss)
+#pragma unroll
+      for (int d = 0; d < 2; ++d) {
+        const bf16x8 vf = tr_frag(vs, kb * 32, ss, d * 32, lane);
+#pragma unroll
+        for (int j = 0; j < 2; ++j) o[j][d] = mma32<E>(vf, pb[j][ss], o[j][d]);
+      }
+  };
+  floatx16 sA[2], sB[2];                        // A: half (t, 0); B: half (t, 1), carried into the next iteration
+  auto iter = [&](auto CUR, int t) __attribute__((always_inline)) {
+    constexpr int cur = decltype(CUR)::value, prv = (cur + 3) & 3, nx2 = (cur + 2) & 3;
+    const bool more2 = t + 2 < nt;
+    if (more2) issue(t + 2, nx2);
+    scores(KS(cur), 0, t * 64, sA);
+    if (t > 0) softpv(VS(prv), 1, sB);
+    scores(KS(cur), 1, t * 64, sB);
+    softpv(VS(cur), 0, sA);
+    if (more2) asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  };
+  for (int t = 0; t < nt; t += 4) {
+    iter(std::integral_constant<int, 0>{}, t);
+    if (t + 1 < nt) iter(std::integral_constant<int, 1>{}, t + 1);
+    if (t + 2 < nt) iter(std::integral_constant<int, 2>{}, t + 2);
+    if (t + 3 < nt) iter(std::integral_constant<int, 3>{}, t + 3);
+  }
+  softpv(VS((nt - 1) & 3), 1, sB);
+#undef KS
+#undef VS
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const float lj = l[j] + xhalf(l[j]);
+    const float inv = 1.f / lj;
+    const int q = q0 + 32 * j + (lane & 31);
+    if (q < Lq) {
+      E* orow = O + ((long)b * Lq + q) * ldo + hd * 64;
+#pragma unroll
+      for (int d = 0; d < 2; ++d)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          typedef E __attribute__((ext_vector_type(4))) e4;
+          e4 v;
+#pragma unroll
+          for (int jj = 0; jj < 4; ++jj) v[jj] = (E)(o[j][d][4 * g + jj] * inv);
+          *(e4*)(orow + d * 32 + 8 * g + 4 * h) = v;
+        }
+      if (h == 0) lse[((long)b * H + hd) * Lq + q] = m[j] + log2f(lj);
+    }
+  }
+}
+
 // dK, dV: one wave = 32 keys (K, V fragments in registers as B operands), q tiles of 64 staged in LDS.
 // Three waves per SIMD for the dK/dV kernel (168 VGPRs, 12 B/lane spilled): its LDS-DMA staging freed the 64
 // register-staged tile VGPRs; measured 4-7 % faster than two waves per SIMD (tools/debug/attn_ab.py)
@@ -631,27 +822,6 @@ __global__ __launch_bounds__(256, CMHAR_DKDV_OCC) void attn_bwd_dkdv_bf16(int H,
 #ifndef CMHAR_DKDV_K64
 #define CMHAR_DKDV_K64 0
 #endif
-// one 1-KiB LDS-DMA piece (lane-linear 16 B per lane) / one 256-B row piece (4 B per lane) by inline asm; rs = the
-// buffer resource (wave-uniform), la = the piece's LDS byte address (wave-uniform)
-__device__ __forceinline__ void async_dma16(uint4_t rs, unsigned la, int voff) {
-  asm volatile("s_mov_b32 m0, %0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds" :: "s"(la), "v"(voff), "s"(rs) : "memory");
-}
-__device__ __forceinline__ void async_dma4(uint4_t rs, unsigned la, int voff) {
-  asm volatile("s_mov_b32 m0, %0\n\tbuffer_load_dword %1, %2, 0 offen lds" :: "s"(la), "v"(voff), "s"(rs) : "memory");
-}
-__device__ __forceinline__ uint4_t buf_rsrc(const void* p, long bytes) {
-  const unsigned long long a = (unsigned long long)p;
-  uint4_t rs;
-  rs[0] = __builtin_amdgcn_readfirstlane((unsigned)a);
-  rs[1] = __builtin_amdgcn_readfirstlane((unsigned)(a >> 32)) & 0xffffu;
-  rs[2] = __builtin_amdgcn_readfirstlane((unsigned)(bytes > 0 ? (bytes < 0x7fffffff ? bytes : 0x7fffffff) : 0));
-  rs[3] = 0x00020000u;
-  return rs;
-}
-__device__ __forceinline__ unsigned lds_addr(const char* p) {
-  return __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(att_lds_ptr)(p));
-}
-
 __global__ __launch_bounds__(256, 1) void attn_bwd_dkdv_k64(int H, int Lq, int Lk, const bf16* __restrict__ Q,
                                                             long ldq, const bf16* __restrict__ K, long ldk,
                                                             const bf16* __restrict__ V, long ldv,
@@ -706,20 +876,21 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dkdv_k64(int H, int Lq, int L
   }
   // one tile: 2 Q pieces + 2 dO pieces + this wave's 256-B row piece (waves 0 / 2 lse, 1 / 3 δ: each row piece is
   // staged twice, identically) = 5 DMA per wave
-  auto issue = [&](int qt, char* slot) __attribute__((always_inline)) {
-    const long r0 = (long)qt * 64;
-    const uint4_t rq = buf_rsrc(Qb + r0 * ldq * 2, (long)(Lq - 1 - r0) * ldq * 2 + 128);
-    const uint4_t rg = buf_rsrc(Gb + r0 * lddo * 2, (long)(Lq - 1 - r0) * lddo * 2 + 128);
-    const uint4_t rr = buf_rsrc(rowb + r0, (long)(Lq - r0) * 4);
+  const uint4_t rq = buf_rsrc(Qb, (long)(Lq - 1) * ldq * 2 + 128);     // loop-invariant (see attn_fwd_p2)
+  const uint4_t rg = buf_rsrc(Gb, (long)(Lq - 1) * lddo * 2 + 128);
+  const uint4_t rr = buf_rsrc(rowb, (long)Lq * 4);
+  const unsigned la0 = lds_addr(smem + 2 * wave * 1024);
+  const unsigned lr0 = lds_addr(smem + 16384 + (wave & 1) * 256);
+  auto issue = [&](int qt, int slot) __attribute__((always_inline)) {
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
-      async_dma16(rq, lds_addr(slot + (2 * wave + t) * 1024), qoff[t]);
-      async_dma16(rg, lds_addr(slot + 8192 + (2 * wave + t) * 1024), goff[t]);
+      async_dma16(rq, la0 + slot * TB + t * 1024, qoff[t] + qt * 64 * (int)ldq * 2);
+      async_dma16(rg, la0 + slot * TB + 8192 + t * 1024, goff[t] + qt * 64 * (int)lddo * 2);
     }
-    async_dma4(rr, lds_addr(slot + 16384 + (wave & 1) * 256), lane * 4);
+    async_dma4(rr, lr0 + slot * TB, (qt * 64 + lane) * 4);
   };
-  issue(0, QS(0));
-  if (nt > 1) issue(1, QS(1));
+  issue(0, 0);
+  if (nt > 1) issue(1, 1);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
 
@@ -791,7 +962,7 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dkdv_k64(int H, int Lq, int L
   auto iter = [&](auto CUR, int t) __attribute__((always_inline)) {
     constexpr int cur = decltype(CUR)::value, prv = (cur + 3) & 3, nx2 = (cur + 2) & 3;
     const bool more2 = t + 2 < nt;
-    if (more2) issue(t + 2, QS(nx2));
+    if (more2) issue(t + 2, nx2);
     sdp(QS(cur), GS(cur), LS(cur), DS(cur), 0, sA, dpA);
     if (t > 0) {
       soft(sB, dpB, pb, db);
@@ -1096,18 +1267,20 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dq_q64(int H, int Lq, int Lk,
     koff[t] = (int)(row * ldk * 2 + (((lane & 7) ^ f) << 4));
     voff[t] = (int)(row * ldv * 2 + (((lane & 7) ^ f) << 4));
   }
-  auto issue = [&](int kt, char* slot) __attribute__((always_inline)) {   // 4 DMA per wave
-    const long r0 = (long)kt * 64;
-    const uint4_t rk = buf_rsrc(Kb + r0 * ldk * 2, (long)(Lk - 1 - r0) * ldk * 2 + 128);
-    const uint4_t rv = buf_rsrc(Vb + r0 * ldv * 2, (long)(Lk - 1 - r0) * ldv * 2 + 128);
+  // loop-invariant buffer resources over the whole head (rows past Lk fall outside num_records and read as zero); a
+  // tile's row offset rides in the per-lane voffset
+  const uint4_t rk = buf_rsrc(Kb, (long)(Lk - 1) * ldk * 2 + 128);
+  const uint4_t rv = buf_rsrc(Vb, (long)(Lk - 1) * ldv * 2 + 128);
+  const unsigned la0 = lds_addr(smem + 2 * wave * 1024);
+  auto issue = [&](int kt, int slot) __attribute__((always_inline)) {   // 4 DMA per wave
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
-      async_dma16(rk, lds_addr(slot + (2 * wave + t) * 1024), koff[t]);
-      async_dma16(rv, lds_addr(slot + 8192 + (2 * wave + t) * 1024), voff[t]);
+      async_dma16(rk, la0 + slot * TB + t * 1024, koff[t] + kt * 64 * (int)ldk * 2);
+      async_dma16(rv, la0 + slot * TB + 8192 + t * 1024, voff[t] + kt * 64 * (int)ldv * 2);
     }
   };
-  issue(0, KS(0));
-  if (nt > 1) issue(1, KS(1));
+  issue(0, 0);
+  if (nt > 1) issue(1, 1);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
 
@@ -1166,7 +1339,7 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dq_q64(int H, int Lq, int Lk,
   auto iter = [&](auto CUR, int t) __attribute__((always_inline)) {
     constexpr int cur = decltype(CUR)::value, prv = (cur + 3) & 3, nx2 = (cur + 2) & 3;
     const bool more2 = t + 2 < nt;
-    if (more2) issue(t + 2, KS(nx2));
+    if (more2) issue(t + 2, nx2);
     sdp(KS(cur), VS(cur), 0, t * 64, sA, dpA);
     if (t > 0) {
       soft(sB, dpB, db);
@@ -1758,7 +1931,10 @@ extern "C" int cmhar_attention_fwd(int dtype, int B, int H, int Lq, int Lk, int 
     const int bulk = CMHAR_ATTN_FWD_ONE_LAUNCH ? cdiv(Lq, 256) * 256 : (Lq / 256) * 256;
 #define FL(E)                                                                                                    \
   do {                                                                                                           \
-    if (bulk > 0)                                                                                                \
+    if (bulk > 0 && CMHAR_ATTN_FWD_P2 && !CMHAR_ATTN_FWD_ONE_LAUNCH)                                            \
+      attn_fwd_p2<E><<<dim3(bulk / 256, H, B), 256, 0, st>>>(H, Lq, Lk, (const bf16*)Q, ldq, (const bf16*)K, ldk,  \
+                                                             (const bf16*)V, ldv, (E*)O, ldo, lse, scale);        \
+    else if (bulk > 0)                                                                                           \
       attn_fwd_bf16<E, 2><<<dim3(bulk / 256, H, B), 256, 0, st>>>(H, Lq, Lk, 0, (const bf16*)Q, ldq, (const bf16*)K, \
                                                                   ldk, (const bf16*)V, ldv, (E*)O, ldo, lse, scale); \
     if (Lq > bulk && Lq - bulk <= CMHAR_ATTN_TAIL)                                                             \

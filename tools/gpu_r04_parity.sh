@@ -11,7 +11,7 @@ timeout -k 10 240 python -u tools/debug/dgrad_layout_ab.py > gpurun_out/${TAG}_d
 cat gpurun_out/${TAG}_dgrad_ab.log
 if [ -f var/libA.so ] && [ -f var/libB.so ]; then
   echo "== attention A/B (var/libA.so vs var/libB.so)"
-  timeout -k 10 300 python -u tools/debug/attn_ab.py var/libA.so var/libB.so var/libC.so var/libD.so var/libE.so --prescaled > gpurun_out/${TAG}_attn_ab.log 2>&1 || exit $?
+  timeout -k 10 300 python -u tools/debug/attn_ab.py var/libA.so var/libB.so var/libC.so var/libD.so var/libE.so var/libF.so --prescaled > gpurun_out/${TAG}_attn_ab.log 2>&1 || exit $?
   cat gpurun_out/${TAG}_attn_ab.log
 fi
 echo "== r3d layers"
