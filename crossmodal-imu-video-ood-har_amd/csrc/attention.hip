@@ -1920,6 +1920,16 @@ static bool f32m_ok(int dtype, int D, float pdrop, std::initializer_list<std::pa
 // C ABI.  Tensors are [B*L, ld] row-major with head h at columns h*D .. h*D+D-1.
 // lse / delta: fp32 [B*H*Lq] workspaces owned by the caller.
 // ----------------------------------------------------------------------------------------------------------------
+// Round-4 kernel forms (attn_fwd_p2, attn_bwd_dq_q64, attn_bwd_dkdv_k64): on by the build default, switchable per
+// process with CMHAR_ATTN_FWD_P2 / CMHAR_DQ_Q64 / CMHAR_DKDV_K64 = 0 / 1 (A/B measurements and the bit-identity tests)
+static bool attn_knob(const char* name, int dflt) {
+  const char* v = getenv(name);
+  return v ? atoi(v) != 0 : dflt != 0;
+}
+static bool use_fwd_p2() { static const bool v = attn_knob("CMHAR_ATTN_FWD_P2", CMHAR_ATTN_FWD_P2); return v; }
+static bool use_dq_q64() { static const bool v = attn_knob("CMHAR_DQ_Q64", CMHAR_DQ_Q64); return v; }
+static bool use_dkdv_k64() { static const bool v = attn_knob("CMHAR_DKDV_K64", CMHAR_DKDV_K64); return v; }
+
 extern "C" int cmhar_attention_fwd(int dtype, int B, int H, int Lq, int Lk, int D, const void* Q, long ldq,
                                    const void* K, long ldk, const void* V, long ldv, void* O, long ldo, float* lse,
                                    float scale, float pdrop, unsigned long long seed, hipStream_t st) {
@@ -1931,7 +1941,7 @@ extern "C" int cmhar_attention_fwd(int dtype, int B, int H, int Lq, int Lk, int 
     const int bulk = CMHAR_ATTN_FWD_ONE_LAUNCH ? cdiv(Lq, 256) * 256 : (Lq / 256) * 256;
 #define FL(E)                                                                                                    \
   do {                                                                                                           \
-    if (bulk > 0 && CMHAR_ATTN_FWD_P2 && !CMHAR_ATTN_FWD_ONE_LAUNCH)                                            \
+    if (bulk > 0 && use_fwd_p2() && !CMHAR_ATTN_FWD_ONE_LAUNCH)                                               \
       attn_fwd_p2<E><<<dim3(bulk / 256, H, B), 256, 0, st>>>(H, Lq, Lk, (const bf16*)Q, ldq, (const bf16*)K, ldk,  \
                                                              (const bf16*)V, ldv, (E*)O, ldo, lse, scale);        \
     else if (bulk > 0)                                                                                           \
@@ -1977,7 +1987,7 @@ static void flash_bwd_bf16(int B, int H, int Lq, int Lk, const void* Q, long ldq
                            long lddv, float scale, hipStream_t st) {
   const float s_in = PS ? 1.f / LOG2E : scale;   // c = s_in·log2e (1 when PS) and the dQ output factor
   // 256-query workgroups (QB = 2) over the bulk, 128-query workgroups for the rest (as the forward)
-  const bool q64 = PS && CMHAR_DQ_Q64;
+  const bool q64 = PS && use_dq_q64();
   const int bulk = (CMHAR_ATTN_DQ_QB == 2 || q64) ? (Lq / 256) * 256 : 0;
   if (bulk > 0 && q64)
     attn_bwd_dq_q64<<<dim3(bulk / 256, H, B), 256, 0, st>>>(H, Lq, Lk, (const bf16*)Q, ldq, (const bf16*)K, ldk,
@@ -2007,7 +2017,7 @@ static void flash_bwd_bf16(int B, int H, int Lq, int Lk, const void* Q, long ldq
   const int kfull = (Lk / 128) * 128;
   const bool ktail = Lk > kfull && Lk - kfull <= CMHAR_ATTN_TAIL;
   // 256-key workgroups of the 64-keys-per-wave kernel over the bulk (round 4), 128-key ones for the rest
-  const int k256 = (PS && CMHAR_DKDV_K64) ? (Lk / 256) * 256 : 0;
+  const int k256 = (PS && use_dkdv_k64()) ? (Lk / 256) * 256 : 0;
   if (k256 > 0)
     attn_bwd_dkdv_k64<<<dim3(k256 / 256, H, B), 256, 0, st>>>(H, Lq, Lk, (const bf16*)Q, ldq, (const bf16*)K, ldk,
                                                               (const bf16*)V, ldv, (const bf16*)dO, lddo, lse, delta,
