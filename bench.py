@@ -42,8 +42,8 @@ PEAK_F32_TFLOPS = 157.3        # f32-input MFMA (= the f32 vector rate; no xf32 
 PEAK_HBM_GBS = 8000.0
 
 
-TRAFFIC_JSON = os.path.join(REPO, 'profiles', 'r03_pmc_traffic.json')
-MFMA_JSON = os.path.join(REPO, 'profiles', 'r03_pmc_mfma.json')
+TRAFFIC_JSON = os.path.join(REPO, 'profiles', 'r04_pmc_traffic.json')
+MFMA_JSON = os.path.join(REPO, 'profiles', 'r04_pmc_mfma.json')
 
 # per-workload defaults of --batch / --frames / --image / --imu-len / --dtype (BASELINE.json configs)
 WORKLOADS = {
@@ -606,6 +606,7 @@ def main():
            'roofline': roof,
            'whole_step_model_tflops': round(whole_tflops, 1),
            'whole_step_mfma_frac': round(whole_tflops / peak, 4),
+           'whole_step_frac_of_measured_peak': round(whole_tflops / peak_meas, 4) if peak_meas else None,
            'executed_gflop_per_clip': round(exec_flops / 1e9, 2),
            'reference_algorithmic_gflop_per_clip': round(W.flops_per_clip / 1e9, 2),
            'first_warmup_loss': first_loss,

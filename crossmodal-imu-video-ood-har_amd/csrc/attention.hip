@@ -34,9 +34,6 @@ __device__ __forceinline__ int att_off(int row, int chunk) {
 }
 
 typedef __attribute__((address_space(3))) void* att_lds_ptr;
-#ifndef CMHAR_ATTN_DMA_ASM
-#define CMHAR_ATTN_DMA_ASM 0
-#endif
 typedef __attribute__((ext_vector_type(2))) float float2_t;
 typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2_t;
 
@@ -64,53 +61,12 @@ struct TileDma {
     const long off = (long)r0 * row_bytes;
     const long left = valid - off;
     const int nrec = (int)(left > 0 ? (left < 0x7fffffff ? left : 0x7fffffff) : 0);
-#if CMHAR_ATTN_DMA_ASM
-    // the same buffer_load_dwordx4 … lds, issued by inline asm: hipcc then does not see an LDS write in flight, so it
-    // no longer drains it (`s_waitcnt vmcnt(0)`) before the first transposed LDS read of the tile being computed —
-    // it did so in all three flash kernels, which serialised the next tile's prefetch with the current tile's work.
-    // The kernels order every DMA with explicit counted vmcnt waits + barriers (as before).  M0 is written here; no
-    // compiler-generated code in these kernels uses M0 (checked in the .s), so nothing relies on it across the asm.
-    const unsigned long long a = (unsigned long long)(base + off);
-    uint4_t rs;
-    rs[0] = __builtin_amdgcn_readfirstlane((unsigned)a);
-    rs[1] = __builtin_amdgcn_readfirstlane((unsigned)(a >> 32)) & 0xffffu;
-    rs[2] = __builtin_amdgcn_readfirstlane((unsigned)nrec);
-    rs[3] = 0x00020000u;
-#pragma unroll
-    for (int t = 0; t < 2; ++t) {
-      const unsigned la = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(att_lds_ptr)(lds + (2 * wave + t) * 1024));
-      asm volatile("s_mov_b32 m0, %0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds" :: "s"(la), "v"(voff[t]), "s"(rs)
-                   : "memory");
-    }
-#else
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)(base + off), (short)0, nrec, 0x00020000);
 #pragma unroll
     for (int t = 0; t < 2; ++t)
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (att_lds_ptr)(lds + (2 * wave + t) * 1024), 16, voff[t], 0, 0, 0);
-#endif
   }
 };
-
-// one 1-KiB LDS-DMA piece (lane-linear 16 B per lane) / one 256-B row piece (4 B per lane) by inline asm; rs = the
-// buffer resource (wave-uniform), la = the piece's LDS byte address (wave-uniform)
-__device__ __forceinline__ void async_dma16(uint4_t rs, unsigned la, int voff) {
-  asm volatile("s_mov_b32 m0, %0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds" :: "s"(la), "v"(voff), "s"(rs) : "memory");
-}
-__device__ __forceinline__ void async_dma4(uint4_t rs, unsigned la, int voff) {
-  asm volatile("s_mov_b32 m0, %0\n\tbuffer_load_dword %1, %2, 0 offen lds" :: "s"(la), "v"(voff), "s"(rs) : "memory");
-}
-__device__ __forceinline__ uint4_t buf_rsrc(const void* p, long bytes) {
-  const unsigned long long a = (unsigned long long)p;
-  uint4_t rs;
-  rs[0] = __builtin_amdgcn_readfirstlane((unsigned)a);
-  rs[1] = __builtin_amdgcn_readfirstlane((unsigned)(a >> 32)) & 0xffffu;
-  rs[2] = __builtin_amdgcn_readfirstlane((unsigned)(bytes > 0 ? (bytes < 0x7fffffff ? bytes : 0x7fffffff) : 0));
-  rs[3] = 0x00020000u;
-  return rs;
-}
-__device__ __forceinline__ unsigned lds_addr(const char* p) {
-  return __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(att_lds_ptr)(p));
-}
 
 // Row fragment for a 32x32x16 A operand: lane holds row (r0 + lane&31), cols 16t + 8(lane>>5) .. +8.
 __device__ __forceinline__ bf16x8 row_frag(const char* lds, int r0, int t, int lane) {
@@ -128,43 +84,6 @@ __device__ __forceinline__ bf16x8 tr_frag(const char* lds, int r0, int s, int c0
   short4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(short4_t, lds + att_off(ra + 8, ch) + hb));
   short8_t v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
   return __builtin_bit_cast(bf16x8, v);
-}
-
-// The same transposed fragment read by inline asm.  hipcc (ROCm 7.2) cannot tell a ds_read_tr16 builtin from an
-// access to the LDS-DMA destination, so it puts an `s_waitcnt vmcnt(0)` in front of the first one after any DMA
-// issue — which drains the NEXT tile's prefetch in the middle of the current tile (seen in the .s of all three flash
-// kernels).  The asm reads are invisible to its LDS-DMA tracking; their results are consumed only behind
-// `tr_wait()` (lgkmcnt(0) + a scheduling fence, so no consumer is hoisted above the wait).  The compiler's own
-// counted lgkmcnt waits stay correct beside them: LDS returns in order, so extra reads in flight only make a count
-// conservative.  CMHAR_ATTN_TRASM=0 restores the builtin (A/B).
-#ifndef CMHAR_ATTN_TRASM
-#define CMHAR_ATTN_TRASM 0
-#endif
-__device__ __forceinline__ short4_t ds_tr16_asm(const char* p) {
-  short4_t v;
-  const unsigned a = (unsigned)(uintptr_t)(att_lds_ptr)(p);
-  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(v) : "v"(a) : "memory");
-  return v;
-}
-__device__ __forceinline__ bf16x8 tr_frag_a(const char* lds, int r0, int s, int c0, int lane) {
-#if CMHAR_ATTN_TRASM
-  const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3, h = g >> 1;
-  const int col = c0 + 16 * (g & 1) + 4 * p;
-  const int ch = col >> 3, hb = (col & 7) * 2;
-  const int ra = r0 + 16 * s + 4 * h + q;
-  const short4_t lo = ds_tr16_asm(lds + att_off(ra, ch) + hb);
-  const short4_t hi = ds_tr16_asm(lds + att_off(ra + 8, ch) + hb);
-  short8_t v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-  return __builtin_bit_cast(bf16x8, v);
-#else
-  return tr_frag(lds, r0, s, c0, lane);
-#endif
-}
-__device__ __forceinline__ void tr_wait() {
-#if CMHAR_ATTN_TRASM
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_sched_barrier(0);
-#endif
 }
 
 // Accumulator registers 8s..8s+7 → 16-bit operand fragment in format E (bf16, or fp16 on the inference path).
@@ -272,13 +191,6 @@ __global__ __launch_bounds__(256, CMHAR_ATTN_FWD_PERKB ? 3 : 2) void attn_fwd_bf
 #pragma unroll
           for (int j = 0; j < QB; ++j) s[j] = mma32<E>(kf, qf[j][t], s[j]);
         }
-#if CMHAR_ATTN_TRASM
-        bf16x8 vtr[2][2];                  // V transposed fragments in flight under the softmax
-#pragma unroll
-        for (int ss = 0; ss < 2; ++ss)
-#pragma unroll
-          for (int d = 0; d < 2; ++d) vtr[ss][d] = tr_frag_a(Vs(cur), kb * 32, ss, d * 32, lane);
-#endif
         if (kbase + kb * 32 + 32 > Lk) {   // ragged last half-tile only (wave-uniform branch)
 #pragma unroll
           for (int j = 0; j < QB; ++j)
@@ -314,15 +226,6 @@ __global__ __launch_bounds__(256, CMHAR_ATTN_FWD_PERKB ? 3 : 2) void attn_fwd_bf
 #pragma unroll
           for (int ss = 0; ss < 2; ++ss) pb[j][ss] = pack8<E>(s[j], ss);
         }
-#if CMHAR_ATTN_TRASM
-        tr_wait();
-#pragma unroll
-        for (int ss = 0; ss < 2; ++ss)
-#pragma unroll
-          for (int d = 0; d < 2; ++d)
-#pragma unroll
-            for (int j = 0; j < QB; ++j) o[j][d] = mma32<E>(vtr[ss][d], pb[j][ss], o[j][d]);
-#else
 #pragma unroll
         for (int ss = 0; ss < 2; ++ss)
 #pragma unroll
@@ -331,7 +234,6 @@ __global__ __launch_bounds__(256, CMHAR_ATTN_FWD_PERKB ? 3 : 2) void attn_fwd_bf
 #pragma unroll
             for (int j = 0; j < QB; ++j) o[j][d] = mma32<E>(vf, pb[j][ss], o[j][d]);
           }
-#endif
       }
     }
 #else
@@ -447,191 +349,15 @@ __global__ __launch_bounds__(256, CMHAR_ATTN_FWD_PERKB ? 3 : 2) void attn_fwd_bf
   }
 }
 
-// Forward, round-4 form: 64 queries per wave (two 32-query blocks), 4 waves = 256 queries, two workgroups per CU; K / V
-// tiles of 64 keys arrive by inline-asm LDS-DMA (see attn_bwd_dkdv_k64) into a four-slot ring two tiles ahead, so no
-// compiler-inserted `vmcnt(0)` drains the prefetch before the V transposed reads; and the loop is software-pipelined
-// over 32-key halves: the S products of a half issue beside the previous half's softmax and P·V.  Halves are consumed
-// in key order, so the online softmax (lazy rescale, running max / sum) and every accumulation are those of
-// attn_fwd_bf16<E, 2>: bit-identical O and LSE.
-#ifndef CMHAR_ATTN_FWD_P2
-#define CMHAR_ATTN_FWD_P2 0
-#endif
-template <typename E>
-__global__ __launch_bounds__(256, 2) void attn_fwd_p2(int H, int Lq, int Lk, const bf16* __restrict__ Q, long ldq,
-                                                      const bf16* __restrict__ K, long ldk,
-                                                      const bf16* __restrict__ V, long ldv, E* __restrict__ O,
-                                                      long ldo, float* __restrict__ lse, float scale) {
-  constexpr int TB = 16384;                     // one ring slot: K [64][64] | V [64][64]
-  __shared__ __attribute__((aligned(16))) char smem[4 * TB];
-#define KS(i) (smem + TB * (i))
-#define VS(i) (smem + TB * (i) + 8192)
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5;
-  const BlkIdx bi = flash_block(H);
-  const int hd = bi.hd, b = bi.b;
-  const int q0 = bi.blk * 256 + wave * 64;
-  const bf16* Qb = Q + (long)b * Lq * ldq + hd * 64;
-  const char* Kb = (const char*)(K + (long)b * Lk * ldk + hd * 64);
-  const char* Vb = (const char*)(V + (long)b * Lk * ldv + hd * 64);
-  const float c = scale * LOG2E;
-  bf16x8 qf[2][4];
-#pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int myq = min(q0 + 32 * j + (lane & 31), Lq - 1);
-#pragma unroll
-    for (int t = 0; t < 4; ++t) qf[j][t] = *(const bf16x8*)(Qb + (long)myq * ldq + 16 * t + 8 * h);
-  }
-  floatx16 o[2][2];
-#pragma unroll
-  for (int j = 0; j < 2; ++j)
-#pragma unroll
-    for (int d = 0; d < 2; ++d)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) o[j][d][r] = 0.f;
-  float m[2] = {-INFINITY, -INFINITY}, l[2] = {0.f, 0.f};
-
-  const int nt = (Lk + 63) / 64;
-  int koff[2], voff[2];
-#pragma unroll
-  for (int t = 0; t < 2; ++t) {
-    const int row = 8 * (2 * wave + t) + (lane >> 3);
-    const int f = (((row >> 1) & 1) << 2) | ((row >> 3) & 3);
-    koff[t] = (int)(row * ldk * 2 + (((lane & 7) ^ f) << 4));
-    voff[t] = (int)(row * ldv * 2 + (((lane & 7) ^ f) << 4));
-  }
-  // loop-invariant buffer resources over the whole head (rows past Lk fall outside num_records and read as zero); a
-  // tile's row offset rides in the per-lane voffset
-  const uint4_t rk = buf_rsrc(Kb, (long)(Lk - 1) * ldk * 2 + 128);
-  const uint4_t rv = buf_rsrc(Vb, (long)(Lk - 1) * ldv * 2 + 128);
-  const unsigned la0 = lds_addr(smem + 2 * wave * 1024);
-  auto issue = [&](int kt, int slot) __attribute__((always_inline)) {   // 4 DMA per wave
-#pragma unroll
-    for (int t = 0; t < 2; ++t) {
-      async_dma16(rk, la0 + slot * TB + t * 1024, koff[t] + kt * 64 * (int)ldk * 2);
-      async_dma16(rv, la0 + slot * TB + 8192 + t * 1024, voff[t] + kt * 64 * (int)ldv * 2);
-    }
-  };
-  issue(0, 0);
-  if (nt > 1) issue(1, 1);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-
-  // Sᵀ = K·Qᵀ of key half kb of a slot for both query blocks (query on the lane; ragged keys masked to −inf)
-  auto scores = [&](const char* ks, int kb, int kbase, floatx16 (&s)[2]) __attribute__((always_inline)) {
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) s[j][r] = 0.f;
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      const bf16x8 kf = row_frag(ks, kb * 32, t, lane);
-#pragma unroll
-      for (int j = 0; j < 2; ++j) s[j] = mma32<E>(kf, qf[j][t], s[j]);
-    }
-    if (kbase + kb * 32 + 32 > Lk) {
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-#pragma unroll
-        for (int r = 0; r < 16; ++r)
-          if (kbase + kb * 32 + acc_row(r, h) >= Lk) s[j][r] = -INFINITY;
-    }
-  };
-  // online softmax of one half (lazy rescale, as attn_fwd_bf16) then O += Vᵀ·Pᵀ
-  auto softpv = [&](const char* vs, int kb, floatx16 (&s)[2]) __attribute__((always_inline)) {
-    bf16x8 pb[2][2];
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      float mt = -INFINITY;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) mt = fmaxf(mt, s[j][r]);
-      mt = fmaxf(mt, xhalf(mt)) * c;
-      if (__builtin_amdgcn_ballot_w64(mt > m[j] + 8.f) != 0) {
-        const float mn = fmaxf(m[j], mt);
-        const float alpha = fexp2(m[j] - mn);
-        m[j] = mn;
-        l[j] *= alpha;
-#pragma unroll
-        for (int d = 0; d < 2; ++d)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) o[j][d][r] *= alpha;
-      }
-      const float mn = m[j];
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const float p = fexp2(fmaf(s[j][r], c, -mn));
-        s[j][r] = p;
-        l[j] += p;
-      }
-#pragma unroll
-      for (int ss = 0; ss < 2; ++ss) pb[j][ss] = pack8<E>(s[j], ss);
-    }
-#pragma unroll
-    for (int ss = 0; ss < 2; ++ss)
-#pragma unroll
-      for (int d = 0; d < 2; ++d) {
-        const bf16x8 vf = tr_frag(vs, kb * 32, ss, d * 32, lane);
-#pragma unroll
-        for (int j = 0; j < 2; ++j) o[j][d] = mma32<E>(vf, pb[j][ss], o[j][d]);
-      }
-  };
-  floatx16 sA[2], sB[2];                        // A: half (t, 0); B: half (t, 1), carried into the next iteration
-  auto iter = [&](auto CUR, int t) __attribute__((always_inline)) {
-    constexpr int cur = decltype(CUR)::value, prv = (cur + 3) & 3, nx2 = (cur + 2) & 3;
-    const bool more2 = t + 2 < nt;
-    if (more2) issue(t + 2, nx2);
-    scores(KS(cur), 0, t * 64, sA);
-    if (t > 0) softpv(VS(prv), 1, sB);
-    scores(KS(cur), 1, t * 64, sB);
-    softpv(VS(cur), 0, sA);
-    if (more2) asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-  };
-  for (int t = 0; t < nt; t += 4) {
-    iter(std::integral_constant<int, 0>{}, t);
-    if (t + 1 < nt) iter(std::integral_constant<int, 1>{}, t + 1);
-    if (t + 2 < nt) iter(std::integral_constant<int, 2>{}, t + 2);
-    if (t + 3 < nt) iter(std::integral_constant<int, 3>{}, t + 3);
-  }
-  softpv(VS((nt - 1) & 3), 1, sB);
-#undef KS
-#undef VS
-#pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const float lj = l[j] + xhalf(l[j]);
-    const float inv = 1.f / lj;
-    const int q = q0 + 32 * j + (lane & 31);
-    if (q < Lq) {
-      E* orow = O + ((long)b * Lq + q) * ldo + hd * 64;
-#pragma unroll
-      for (int d = 0; d < 2; ++d)
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          typedef E __attribute__((ext_vector_type(4))) e4;
-          e4 v;
-#pragma unroll
-          for (int jj = 0; jj < 4; ++jj) v[jj] = (E)(o[j][d][4 * g + jj] * inv);
-          *(e4*)(orow + d * 32 + 8 * g + 4 * h) = v;
-        }
-      if (h == 0) lse[((long)b * H + hd) * Lq + q] = m[j] + log2f(lj);
-    }
-  }
-}
-
 // dK, dV: one wave = 32 keys (K, V fragments in registers as B operands), q tiles of 64 staged in LDS.
 // Three waves per SIMD for the dK/dV kernel (168 VGPRs, 12 B/lane spilled): its LDS-DMA staging freed the 64
 // register-staged tile VGPRs; measured 4-7 % faster than two waves per SIMD (tools/debug/attn_ab.py)
-#ifndef CMHAR_DKDV_V2
-#define CMHAR_DKDV_V2 0
-#endif
-#ifndef CMHAR_DKDV_OCC
-#define CMHAR_DKDV_OCC (CMHAR_DKDV_V2 ? 2 : 3)
-#endif
 // PS (pre-scaled keys): K holds bf16(scale·log2e·K) written by the QKV GEMM's epilogue (CmharEpilogue.colscale) and
 // the launch passes scale = 1/log2e, so c = 1 and p = exp2(acc) needs no multiply per score (−6 % backward time:
 // the kernels are VALU-issue bound beside their MFMAs); kscale is the dK output factor (the true softmax scale, so
 // dK is the gradient of the unscaled key and the QKV backward is unchanged).
 template <bool PS = false>
-__global__ __launch_bounds__(256, CMHAR_DKDV_OCC) void attn_bwd_dkdv_bf16(int H, int Lq, int Lk, int k_base,
+__global__ __launch_bounds__(256, 3) void attn_bwd_dkdv_bf16(int H, int Lq, int Lk, int k_base,
                                                              const bf16* __restrict__ Q,
                                                              long ldq, const bf16* __restrict__ K, long ldk,
                                                              const bf16* __restrict__ V, long ldv,
@@ -714,41 +440,15 @@ __global__ __launch_bounds__(256, CMHAR_DKDV_OCC) void attn_bwd_dkdv_bf16(int H,
         s[r] = L_[q];
         dp[r] = D_[q];
       }
-#if CMHAR_DKDV_V2
-      // all eight row fragments issued before the two MFMA chains (32 VGPRs at 2 waves per SIMD): one LDS latency
-      // exposed per block instead of one per MFMA
-      bf16x8 qr[4], gr[4];
-#pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        qr[t] = row_frag(Qs(cur), qb * 32, t, lane);
-        gr[t] = row_frag(Gs(cur), qb * 32, t, lane);
-      }
-#pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qr[t], kf[t], s, 0, 0, 0);
-        dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(gr[t], vf[t], dp, 0, 0, 0);
-      }
-#else
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
         s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag(Qs(cur), qb * 32, t, lane), kf[t], s, 0, 0, 0);
         dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag(Gs(cur), qb * 32, t, lane), vf[t], dp, 0, 0, 0);
       }
-#endif
       // p = exp2(c·s), dS = P ∘ (dP − δ), then both packed to bf16 — written in aligned register pairs (one
       // v_pk_mul_f32 + one v_cvt_pk_bf16_f32 per pair; element-wise, the compiler paired (1,2),(3,4),... and spent
       // v_mov / v_alignbit / v_perm re-pairing them for the packs; the backward got 3 % faster, bit-identical.  The
       // same rewrite of the forward's softmax measured 5 % slower and is not used)
-#if CMHAR_ATTN_TRASM
-      bf16x8 gtr[2][2], qtr[2][2];         // dOᵀ / Qᵀ fragments in flight under the softmax
-#pragma unroll
-      for (int ss = 0; ss < 2; ++ss)
-#pragma unroll
-        for (int d = 0; d < 2; ++d) {
-          gtr[ss][d] = tr_frag_a(Gs(cur), qb * 32, ss, d * 32, lane);
-          qtr[ss][d] = tr_frag_a(Qs(cur), qb * 32, ss, d * 32, lane);
-        }
-#endif
       bf16x8 pbv[2], dbv[2];
 #pragma unroll
       for (int r = 0; r < 16; r += 2) {
@@ -761,21 +461,13 @@ __global__ __launch_bounds__(256, CMHAR_DKDV_OCC) void attn_bwd_dkdv_bf16(int H,
         dbv[r >> 3][r & 7] = dd[0];
         dbv[r >> 3][(r & 7) + 1] = dd[1];
       }
-#if CMHAR_ATTN_TRASM
-      tr_wait();
-#endif
 #pragma unroll
       for (int ss = 0; ss < 2; ++ss) {
         const bf16x8 pb = pbv[ss], db = dbv[ss];
 #pragma unroll
         for (int d = 0; d < 2; ++d) {
-#if CMHAR_ATTN_TRASM
-          dv[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(gtr[ss][d], pb, dv[d], 0, 0, 0);
-          dk[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qtr[ss][d], db, dk[d], 0, 0, 0);
-#else
           dv[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_frag(Gs(cur), qb * 32, ss, d * 32, lane), pb, dv[d], 0, 0, 0);
           dk[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_frag(Qs(cur), qb * 32, ss, d * 32, lane), db, dk[d], 0, 0, 0);
-#endif
         }
       }
     }
@@ -806,212 +498,6 @@ __global__ __launch_bounds__(256, CMHAR_DKDV_OCC) void attn_bwd_dkdv_bf16(int H,
   }
 }
 
-// dK, dV with 64 keys per wave at ONE wave per SIMD (a workgroup = 4 waves = 256 keys; round 4), for the pre-scaled
-// bf16 training path.  The 32-key form above reads every Q / dO fragment from LDS for one 32-key MFMA block — its
-// LDS traffic is half its MFMA time — and its waves stall on per-MFMA read latency (PMC: MFMA pipes 49 % busy).  Here
-// each fragment feeds the wave's two 32-key blocks (half the LDS bytes per MFMA) and the 512-register file holds two
-// query blocks of S / dP: the loop is software-pipelined so a block's S and dP products issue beside the previous
-// block's softmax VALU and its dV / dK products beside the next block's.  Q / dO tiles of 64 queries AND their lse /
-// δ rows arrive by LDS-DMA into a ring of four slots two tiles ahead, every DMA issued by inline asm (async_dma16 /
-// async_dma4): hipcc then sees no LDS write in flight and emits no `vmcnt(0)` before the LDS reads of the current
-// tile (the builtin form drained the prefetch in the middle of every tile); the kernel orders the DMA itself with a
-// counted vmcnt + barrier per tile.  The rows arrive RAW: the key and value fragments are negated once at entry, so
-// the S / dP accumulators seeded with +lse / +δ hold −(Q·Kᵀ − lse) and −(dO·Vᵀ − δ) — exactly the negations of the
-// 32-key kernel's seeded sums (IEEE rounding is sign-symmetric) — p = exp2(−acc) takes the sign as a source modifier,
-// dS comes out negated and the final dK factor is −kscale: dK / dV are bit-identical to attn_bwd_dkdv_bf16<true>.
-#ifndef CMHAR_DKDV_K64
-#define CMHAR_DKDV_K64 0
-#endif
-__global__ __launch_bounds__(256, 1) void attn_bwd_dkdv_k64(int H, int Lq, int Lk, const bf16* __restrict__ Q,
-                                                            long ldq, const bf16* __restrict__ K, long ldk,
-                                                            const bf16* __restrict__ V, long ldv,
-                                                            const bf16* __restrict__ dO, long lddo,
-                                                            const float* __restrict__ lse,
-                                                            const float* __restrict__ delta, bf16* __restrict__ dK,
-                                                            long lddk, bf16* __restrict__ dV, long lddv, float kscale) {
-  constexpr int TB = 16384 + 512;               // one ring slot: Q [64][64] | dO [64][64] | lse [64] | δ [64]
-  __shared__ __attribute__((aligned(16))) char smem[4 * TB];
-#define QS(i) (smem + TB * (i))
-#define GS(i) (smem + TB * (i) + 8192)
-#define LS(i) ((const float*)(smem + TB * (i) + 16384))
-#define DS(i) ((const float*)(smem + TB * (i) + 16384 + 256))
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5;
-  const BlkIdx bi = flash_block(H);
-  const int hd = bi.hd, b = bi.b;
-  const int k0 = bi.blk * 256 + wave * 64;
-  const char* Qb = (const char*)(Q + (long)b * Lq * ldq + hd * 64);
-  const char* Gb = (const char*)(dO + (long)b * Lq * lddo + hd * 64);
-  const float* rowb = ((wave & 1) ? delta : lse) + ((long)b * H + hd) * Lq;   // wave w stages lse (even) / δ (odd)
-
-  // −K, −V fragments (bf16 sign flips: exact)
-  bf16x8 kf[2][4], vf[2][4];
-#pragma unroll
-  for (int kb = 0; kb < 2; ++kb) {
-    const int myk = min(k0 + 32 * kb + (lane & 31), Lk - 1);
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      const uint4_t kk = *(const uint4_t*)(K + ((long)b * Lk + myk) * ldk + hd * 64 + 16 * t + 8 * h);
-      const uint4_t vv = *(const uint4_t*)(V + ((long)b * Lk + myk) * ldv + hd * 64 + 16 * t + 8 * h);
-      kf[kb][t] = __builtin_bit_cast(bf16x8, kk ^ 0x80008000u);
-      vf[kb][t] = __builtin_bit_cast(bf16x8, vv ^ 0x80008000u);
-    }
-  }
-  floatx16 dk[2][2], dv[2][2];
-#pragma unroll
-  for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-    for (int d = 0; d < 2; ++d)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) { dk[kb][d][r] = 0.f; dv[kb][d][r] = 0.f; }
-
-  const int nt = (Lq + 63) / 64;
-  // per-lane DMA offsets: Q / dO piece t of this wave = rows 8(2·wave + t) .. +7, the att_off swizzle on the SOURCE
-  int qoff[2], goff[2];
-#pragma unroll
-  for (int t = 0; t < 2; ++t) {
-    const int row = 8 * (2 * wave + t) + (lane >> 3);
-    const int f = (((row >> 1) & 1) << 2) | ((row >> 3) & 3);
-    qoff[t] = (int)(row * ldq * 2 + (((lane & 7) ^ f) << 4));
-    goff[t] = (int)(row * lddo * 2 + (((lane & 7) ^ f) << 4));
-  }
-  // one tile: 2 Q pieces + 2 dO pieces + this wave's 256-B row piece (waves 0 / 2 lse, 1 / 3 δ: each row piece is
-  // staged twice, identically) = 5 DMA per wave
-  const uint4_t rq = buf_rsrc(Qb, (long)(Lq - 1) * ldq * 2 + 128);     // loop-invariant (see attn_fwd_p2)
-  const uint4_t rg = buf_rsrc(Gb, (long)(Lq - 1) * lddo * 2 + 128);
-  const uint4_t rr = buf_rsrc(rowb, (long)Lq * 4);
-  const unsigned la0 = lds_addr(smem + 2 * wave * 1024);
-  const unsigned lr0 = lds_addr(smem + 16384 + (wave & 1) * 256);
-  auto issue = [&](int qt, int slot) __attribute__((always_inline)) {
-#pragma unroll
-    for (int t = 0; t < 2; ++t) {
-      async_dma16(rq, la0 + slot * TB + t * 1024, qoff[t] + qt * 64 * (int)ldq * 2);
-      async_dma16(rg, la0 + slot * TB + 8192 + t * 1024, goff[t] + qt * 64 * (int)lddo * 2);
-    }
-    async_dma4(rr, lr0 + slot * TB, (qt * 64 + lane) * 4);
-  };
-  issue(0, 0);
-  if (nt > 1) issue(1, 1);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-
-  // S / dP of query block qb of a slot (key on the lane), seeded with +lse / +δ over −K / −V: acc = −(true − seed)
-  auto sdp = [&](const char* qs, const char* gs, const float* L_, const float* D_, int qb, floatx16 (&s)[2],
-                 floatx16 (&dp)[2]) __attribute__((always_inline)) {
-    bf16x8 qr[4], gr[4];
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      qr[t] = row_frag(qs, qb * 32, t, lane);
-      gr[t] = row_frag(gs, qb * 32, t, lane);
-    }
-#pragma unroll
-    for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int q = qb * 32 + acc_row(r, h);
-        s[kb][r] = L_[q];
-        dp[kb][r] = D_[q];
-      }
-#pragma unroll
-    for (int t = 0; t < 4; ++t)
-#pragma unroll
-      for (int kb = 0; kb < 2; ++kb) {
-        s[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qr[t], kf[kb][t], s[kb], 0, 0, 0);
-        dp[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(gr[t], vf[kb][t], dp[kb], 0, 0, 0);
-      }
-  };
-  // p = exp2(−acc_s), −dS = p ∘ acc_dp: bf16 packs in aligned register pairs
-  auto soft = [&](const floatx16 (&s)[2], const floatx16 (&dp)[2], bf16x8 (&pb)[2][2], bf16x8 (&db)[2][2])
-      __attribute__((always_inline)) {
-#pragma unroll
-    for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-      for (int r = 0; r < 16; r += 2) {
-        const float2_t pv = float2_t{fexp2(-s[kb][r]), fexp2(-s[kb][r + 1])};
-        const float2_t dv2 = pv * float2_t{dp[kb][r], dp[kb][r + 1]};
-        const bf16x2_t pp = __builtin_convertvector(pv, bf16x2_t);
-        const bf16x2_t dd = __builtin_convertvector(dv2, bf16x2_t);
-        pb[kb][r >> 3][r & 7] = pp[0];
-        pb[kb][r >> 3][(r & 7) + 1] = pp[1];
-        db[kb][r >> 3][r & 7] = dd[0];
-        db[kb][r >> 3][(r & 7) + 1] = dd[1];
-      }
-  };
-  // dVᵀ += dOᵀ·P, −dKᵀ += Qᵀ·(−dS) for both key blocks; each transposed fragment feeds two MFMAs
-  auto dvdk = [&](const char* qs, const char* gs, int qb, const bf16x8 (&pb)[2][2], const bf16x8 (&db)[2][2])
-      __attribute__((always_inline)) {
-#pragma unroll
-    for (int ss = 0; ss < 2; ++ss)
-#pragma unroll
-      for (int d = 0; d < 2; ++d) {
-        const bf16x8 gt = tr_frag(gs, qb * 32, ss, d * 32, lane);
-        const bf16x8 qt = tr_frag(qs, qb * 32, ss, d * 32, lane);
-#pragma unroll
-        for (int kb = 0; kb < 2; ++kb) {
-          dv[kb][d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(gt, pb[kb][ss], dv[kb][d], 0, 0, 0);
-          dk[kb][d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(qt, db[kb][ss], dk[kb][d], 0, 0, 0);
-        }
-      }
-  };
-
-  // Software pipeline over the 2·nt query blocks (block (t, qb) = rows 32qb.. of tile t).  Iteration t: S/dP of (t, 0)
-  // beside the softmax of (t−1, 1); dV/dK of (t−1, 1); S/dP of (t, 1) beside the softmax of (t, 0); dV/dK of (t, 0).
-  // Ring slot of tile t = t % 4; the DMA of tile t + 2 goes to the slot tile t − 2 used (last read in iteration
-  // t − 1, behind its closing barrier) and is waited for at the end of iteration t + 1.
-  floatx16 sA[2], dpA[2], sB[2], dpB[2];       // A: (t, 0); B: (t, 1) — B carries into the next iteration
-  bf16x8 pb[2][2], db[2][2];
-  auto iter = [&](auto CUR, int t) __attribute__((always_inline)) {
-    constexpr int cur = decltype(CUR)::value, prv = (cur + 3) & 3, nx2 = (cur + 2) & 3;
-    const bool more2 = t + 2 < nt;
-    if (more2) issue(t + 2, nx2);
-    sdp(QS(cur), GS(cur), LS(cur), DS(cur), 0, sA, dpA);
-    if (t > 0) {
-      soft(sB, dpB, pb, db);
-      dvdk(QS(prv), GS(prv), 1, pb, db);
-    }
-    sdp(QS(cur), GS(cur), LS(cur), DS(cur), 1, sB, dpB);
-    soft(sA, dpA, pb, db);
-    dvdk(QS(cur), GS(cur), 0, pb, db);
-    // tile t + 1 landed (issued one iteration earlier): leave only tile t + 2's 5 pieces in flight
-    if (more2) asm volatile("s_waitcnt vmcnt(5) lgkmcnt(0)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-  };
-  for (int t = 0; t < nt; t += 4) {
-    iter(std::integral_constant<int, 0>{}, t);
-    if (t + 1 < nt) iter(std::integral_constant<int, 1>{}, t + 1);
-    if (t + 2 < nt) iter(std::integral_constant<int, 2>{}, t + 2);
-    if (t + 3 < nt) iter(std::integral_constant<int, 3>{}, t + 3);
-  }
-  {   // the last block (nt − 1, 1): its S/dP were issued in the last iteration
-    const int lb = (nt - 1) & 3;
-    soft(sB, dpB, pb, db);
-    dvdk(QS(lb), GS(lb), 1, pb, db);
-  }
-#undef QS
-#undef GS
-#undef LS
-#undef DS
-  const float nks = -kscale;
-#pragma unroll
-  for (int kb = 0; kb < 2; ++kb) {
-    const int key = k0 + 32 * kb + (lane & 31);
-    if (key < Lk) {
-      bf16* krow = dK + ((long)b * Lk + key) * lddk + hd * 64;
-      bf16* vrow = dV + ((long)b * Lk + key) * lddv + hd * 64;
-#pragma unroll
-      for (int d = 0; d < 2; ++d)
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          bf16x4 a, v;
-#pragma unroll
-          for (int j = 0; j < 4; ++j) { a[j] = (bf16)(dk[kb][d][4 * g + j] * nks); v[j] = (bf16)dv[kb][d][4 * g + j]; }
-          *(bf16x4*)(krow + d * 32 + 8 * g + 4 * h) = a;
-          *(bf16x4*)(vrow + d * 32 + 8 * g + 4 * h) = v;
-        }
-    }
-  }
-}
-
 // dQ: one wave = QB blocks of 32 queries (Q, dO fragments in registers), K/V tiles of 64 keys in LDS.  With QB = 2
 // every K / V row fragment and K transposed fragment read from LDS feeds two MFMA chains: the kernel's LDS read
 // traffic per MFMA halves (at QB = 1 the 4 waves' reads of the shared K/V tiles took as many LDS cycles as the MFMAs
@@ -1020,14 +506,8 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dkdv_k64(int H, int Lq, int L
 // and written for the dK/dV kernel, which runs after this one on the same stream.
 // Three waves per SIMD for dQ: with the fragments read just before their MFMAs (not hoisted per key block) the
 // kernel fits 168 VGPRs without spilling; measured 7 % faster than two waves per SIMD
-#ifndef CMHAR_DQ_V2
-#define CMHAR_DQ_V2 0
-#endif
-#ifndef CMHAR_DQ_OCC
-#define CMHAR_DQ_OCC (CMHAR_DQ_V2 ? 2 : 3)
-#endif
 template <int QB, bool PS = false>
-__global__ __launch_bounds__(256, QB == 1 ? CMHAR_DQ_OCC : 2) void attn_bwd_dq_bf16(int H, int Lq, int Lk, int q_base,
+__global__ __launch_bounds__(256, QB == 1 ? 3 : 2) void attn_bwd_dq_bf16(int H, int Lq, int Lk, int q_base,
                                                            const bf16* __restrict__ Q, long ldq,
                                                            const bf16* __restrict__ K, long ldk,
                                                            const bf16* __restrict__ V, long ldv,
@@ -1102,21 +582,6 @@ __global__ __launch_bounds__(256, QB == 1 ? CMHAR_DQ_OCC : 2) void attn_bwd_dq_b
       for (int j = 0; j < QB; ++j)
 #pragma unroll
         for (int r = 0; r < 16; ++r) { s[j][r] = sL[j]; dp[j][r] = -Dl[j]; }
-#if CMHAR_DQ_V2
-      bf16x8 kfr[4], vfr[4];             // all eight row fragments before the two chains (2 waves per SIMD)
-#pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        kfr[t] = row_frag(Ks(cur), kb * 32, t, lane);
-        vfr[t] = row_frag(Vs(cur), kb * 32, t, lane);
-      }
-#pragma unroll
-      for (int t = 0; t < 4; ++t)
-#pragma unroll
-        for (int j = 0; j < QB; ++j) {
-          s[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kfr[t], qf[j][t], s[j], 0, 0, 0);
-          dp[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vfr[t], gf[j][t], dp[j], 0, 0, 0);
-        }
-#else
 #pragma unroll
       for (int t = 0; t < 4; ++t) {    // each K / V row fragment read once, used by all QB q-blocks
         const bf16x8 kfr = row_frag(Ks(cur), kb * 32, t, lane);
@@ -1127,14 +592,6 @@ __global__ __launch_bounds__(256, QB == 1 ? CMHAR_DQ_OCC : 2) void attn_bwd_dq_b
           dp[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vfr, gf[j][t], dp[j], 0, 0, 0);
         }
       }
-#endif
-#if CMHAR_ATTN_TRASM
-      bf16x8 ktrs[2][2];                   // Kᵀ fragments in flight under the dS arithmetic
-#pragma unroll
-      for (int ss = 0; ss < 2; ++ss)
-#pragma unroll
-        for (int d = 0; d < 2; ++d) ktrs[ss][d] = tr_frag_a(Ks(cur), kb * 32, ss, d * 32, lane);
-#endif
       if (kbase + 64 > Lk) {   // ragged last tile only (wave-uniform branch)
 #pragma unroll
         for (int j = 0; j < QB; ++j)
@@ -1154,16 +611,6 @@ __global__ __launch_bounds__(256, QB == 1 ? CMHAR_DQ_OCC : 2) void attn_bwd_dq_b
           db[j][r >> 3][(r & 7) + 1] = dd[1];
         }
       }
-#if CMHAR_ATTN_TRASM
-      tr_wait();
-#pragma unroll
-      for (int ss = 0; ss < 2; ++ss)
-#pragma unroll
-        for (int d = 0; d < 2; ++d)
-#pragma unroll
-          for (int j = 0; j < QB; ++j)
-            dq[j][d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ktrs[ss][d], db[j][ss], dq[j][d], 0, 0, 0);
-#else
 #pragma unroll
       for (int ss = 0; ss < 2; ++ss)
 #pragma unroll
@@ -1173,7 +620,6 @@ __global__ __launch_bounds__(256, QB == 1 ? CMHAR_DQ_OCC : 2) void attn_bwd_dq_b
           for (int j = 0; j < QB; ++j)
             dq[j][d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ktr, db[j][ss], dq[j][d], 0, 0, 0);
         }
-#endif
     }
     if (more) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // own pieces of the next tile landed
     __syncthreads();
@@ -1202,197 +648,6 @@ __global__ __launch_bounds__(256, QB == 1 ? CMHAR_DQ_OCC : 2) void attn_bwd_dq_b
 #undef Ks
 #undef Vs
 
-// dQ with 64 queries per wave at ONE wave per SIMD (a workgroup = 4 waves = 256 queries; round 4), pre-scaled bf16
-// training path — the counterpart of attn_bwd_dkdv_k64: every K / V fragment read from LDS feeds both of the wave's
-// 32-query blocks, K / V tiles of 64 keys arrive by inline-asm LDS-DMA into a four-slot ring two tiles ahead, and the
-// loop is software-pipelined over 32-key halves (S / dP of a half beside the previous half's dS arithmetic, dQ of a
-// half beside the next one's).  Per-element arithmetic and accumulation order are those of attn_bwd_dq_bf16<QB, true>
-// (seeds −lse and −δ, p = exp2(acc), dS packs, dQ over the key halves in order): bit-identical dQ and δ.
-#ifndef CMHAR_DQ_Q64
-#define CMHAR_DQ_Q64 0
-#endif
-__global__ __launch_bounds__(256, 1) void attn_bwd_dq_q64(int H, int Lq, int Lk, const bf16* __restrict__ Q, long ldq,
-                                                          const bf16* __restrict__ K, long ldk,
-                                                          const bf16* __restrict__ V, long ldv,
-                                                          const bf16* __restrict__ O, long ldo,
-                                                          const bf16* __restrict__ dO, long lddo,
-                                                          const float* __restrict__ lse, float* __restrict__ delta,
-                                                          bf16* __restrict__ dQ, long lddq, float scale) {
-  constexpr int TB = 16384;                     // one ring slot: K [64][64] | V [64][64]
-  __shared__ __attribute__((aligned(16))) char smem[4 * TB];
-#define KS(i) (smem + TB * (i))
-#define VS(i) (smem + TB * (i) + 8192)
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5;
-  const BlkIdx bi = flash_block(H);
-  const int hd = bi.hd, b = bi.b;
-  const int q0 = bi.blk * 256 + wave * 64;
-  const char* Kb = (const char*)(K + (long)b * Lk * ldk + hd * 64);
-  const char* Vb = (const char*)(V + (long)b * Lk * ldv + hd * 64);
-  bf16x8 qf[2][4], gf[2][4];
-  float sL[2], Dl[2];
-#pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int myq = min(q0 + 32 * j + (lane & 31), Lq - 1);
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      qf[j][t] = *(const bf16x8*)(Q + ((long)b * Lq + myq) * ldq + hd * 64 + 16 * t + 8 * h);
-      gf[j][t] = *(const bf16x8*)(dO + ((long)b * Lq + myq) * lddo + hd * 64 + 16 * t + 8 * h);
-    }
-    sL[j] = -lse[((long)b * H + hd) * Lq + myq];      // c = 1 (pre-scaled keys): p = exp2(acc)
-    float d_ = 0.f;
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      const bf16x8 ov = *(const bf16x8*)(O + ((long)b * Lq + myq) * ldo + hd * 64 + 16 * t + 8 * h);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) d_ = fmaf((float)gf[j][t][e], (float)ov[e], d_);
-    }
-    d_ += xhalf(d_);
-    Dl[j] = d_;
-    if (h == 0 && q0 + 32 * j + (lane & 31) < Lq) delta[((long)b * H + hd) * Lq + myq] = d_;
-  }
-  floatx16 dq[2][2];
-#pragma unroll
-  for (int j = 0; j < 2; ++j)
-#pragma unroll
-    for (int d = 0; d < 2; ++d)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) dq[j][d][r] = 0.f;
-
-  const int nt = (Lk + 63) / 64;
-  int koff[2], voff[2];
-#pragma unroll
-  for (int t = 0; t < 2; ++t) {
-    const int row = 8 * (2 * wave + t) + (lane >> 3);
-    const int f = (((row >> 1) & 1) << 2) | ((row >> 3) & 3);
-    koff[t] = (int)(row * ldk * 2 + (((lane & 7) ^ f) << 4));
-    voff[t] = (int)(row * ldv * 2 + (((lane & 7) ^ f) << 4));
-  }
-  // loop-invariant buffer resources over the whole head (rows past Lk fall outside num_records and read as zero); a
-  // tile's row offset rides in the per-lane voffset
-  const uint4_t rk = buf_rsrc(Kb, (long)(Lk - 1) * ldk * 2 + 128);
-  const uint4_t rv = buf_rsrc(Vb, (long)(Lk - 1) * ldv * 2 + 128);
-  const unsigned la0 = lds_addr(smem + 2 * wave * 1024);
-  auto issue = [&](int kt, int slot) __attribute__((always_inline)) {   // 4 DMA per wave
-#pragma unroll
-    for (int t = 0; t < 2; ++t) {
-      async_dma16(rk, la0 + slot * TB + t * 1024, koff[t] + kt * 64 * (int)ldk * 2);
-      async_dma16(rv, la0 + slot * TB + 8192 + t * 1024, voff[t] + kt * 64 * (int)ldv * 2);
-    }
-  };
-  issue(0, 0);
-  if (nt > 1) issue(1, 1);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-
-  // Sᵀ / dPᵀ of key half kb of a slot for both query blocks (query on the lane), seeded with −lse / −δ
-  auto sdp = [&](const char* ks, const char* vs, int kb, int kbase, floatx16 (&s)[2], floatx16 (&dp)[2])
-      __attribute__((always_inline)) {
-    bf16x8 kr[4], vr[4];
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      kr[t] = row_frag(ks, kb * 32, t, lane);
-      vr[t] = row_frag(vs, kb * 32, t, lane);
-    }
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) { s[j][r] = sL[j]; dp[j][r] = -Dl[j]; }
-#pragma unroll
-    for (int t = 0; t < 4; ++t)
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        s[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kr[t], qf[j][t], s[j], 0, 0, 0);
-        dp[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vr[t], gf[j][t], dp[j], 0, 0, 0);
-      }
-    if (kbase + kb * 32 + 32 > Lk) {         // ragged last half only (wave-uniform branch)
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-#pragma unroll
-        for (int r = 0; r < 16; ++r)
-          if (kbase + kb * 32 + acc_row(r, h) >= Lk) s[j][r] = -INFINITY;
-    }
-  };
-  auto soft = [&](const floatx16 (&s)[2], const floatx16 (&dp)[2], bf16x8 (&db)[2][2]) __attribute__((always_inline)) {
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; r += 2) {
-        const float2_t pv = float2_t{fexp2(s[j][r]), fexp2(s[j][r + 1])};
-        const bf16x2_t dd = __builtin_convertvector(pv * float2_t{dp[j][r], dp[j][r + 1]}, bf16x2_t);
-        db[j][r >> 3][r & 7] = dd[0];
-        db[j][r >> 3][(r & 7) + 1] = dd[1];
-      }
-  };
-  auto dqs = [&](const char* ks, int kb, const bf16x8 (&db)[2][2]) __attribute__((always_inline)) {
-#pragma unroll
-    for (int ss = 0; ss < 2; ++ss)
-#pragma unroll
-      for (int d = 0; d < 2; ++d) {
-        const bf16x8 ktr = tr_frag(ks, kb * 32, ss, d * 32, lane);
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-          dq[j][d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ktr, db[j][ss], dq[j][d], 0, 0, 0);
-      }
-  };
-  floatx16 sA[2], dpA[2], sB[2], dpB[2];
-  bf16x8 db[2][2];
-  auto iter = [&](auto CUR, int t) __attribute__((always_inline)) {
-    constexpr int cur = decltype(CUR)::value, prv = (cur + 3) & 3, nx2 = (cur + 2) & 3;
-    const bool more2 = t + 2 < nt;
-    if (more2) issue(t + 2, nx2);
-    sdp(KS(cur), VS(cur), 0, t * 64, sA, dpA);
-    if (t > 0) {
-      soft(sB, dpB, db);
-      dqs(KS(prv), 1, db);
-    }
-    sdp(KS(cur), VS(cur), 1, t * 64, sB, dpB);
-    soft(sA, dpA, db);
-    dqs(KS(cur), 0, db);
-    if (more2) asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-  };
-  for (int t = 0; t < nt; t += 4) {
-    iter(std::integral_constant<int, 0>{}, t);
-    if (t + 1 < nt) iter(std::integral_constant<int, 1>{}, t + 1);
-    if (t + 2 < nt) iter(std::integral_constant<int, 2>{}, t + 2);
-    if (t + 3 < nt) iter(std::integral_constant<int, 3>{}, t + 3);
-  }
-  {
-    const int lb = (nt - 1) & 3;
-    soft(sB, dpB, db);
-    dqs(KS(lb), 1, db);
-  }
-#undef KS
-#undef VS
-#pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int q = q0 + 32 * j + (lane & 31);
-    if (q < Lq) {
-      bf16* row = dQ + ((long)b * Lq + q) * lddq + hd * 64;
-#pragma unroll
-      for (int d = 0; d < 2; ++d)
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          bf16x4 v;
-#pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] = (bf16)(dq[j][d][4 * g + e] * scale);
-          *(bf16x4*)(row + d * 32 + 8 * g + 4 * h) = v;
-        }
-    }
-  }
-}
-
-// ---------------------------------------------------------------------------------------------------------------
-// Ragged tails.  At 16×224² L = 1568 = 12·128 + 32: each head leaves ≤ 32 queries (forward, dQ) or keys (dK/dV)
-// beyond the last full block.  As a block of the kernels above, such a tail runs ONE active wave over the whole other
-// sequence (1/4 of its workgroup's slots).  The tail kernels below give the tail a workgroup of its own per
-// (batch, head) whose 4 waves take the SAME ≤ 32 rows and split the OTHER sequence: per step the workgroup stages
-// 128 rows of it (two [64][64] att_off images per operand, LDS-DMA, double-buffered), each wave works on its own
-// 32, and the 4 partial results are merged through LDS at the end — (m, l, O) flash-decoding merge for the forward,
-// plain sums for dQ and dK/dV.  Deterministic (fixed merge order); the same per-element arithmetic as the kernels
-// above except the order in which the four key (query) quarters are summed.
-// ---------------------------------------------------------------------------------------------------------------
 __device__ __forceinline__ void stage128(const TileDma& t, int r0, char* lds, int wave) {
   t.tile(r0, lds, wave);
   t.tile(r0 + 64, lds + 8192, wave);
@@ -1920,16 +1175,6 @@ static bool f32m_ok(int dtype, int D, float pdrop, std::initializer_list<std::pa
 // C ABI.  Tensors are [B*L, ld] row-major with head h at columns h*D .. h*D+D-1.
 // lse / delta: fp32 [B*H*Lq] workspaces owned by the caller.
 // ----------------------------------------------------------------------------------------------------------------
-// Round-4 kernel forms (attn_fwd_p2, attn_bwd_dq_q64, attn_bwd_dkdv_k64): on by the build default, switchable per
-// process with CMHAR_ATTN_FWD_P2 / CMHAR_DQ_Q64 / CMHAR_DKDV_K64 = 0 / 1 (A/B measurements and the bit-identity tests)
-static bool attn_knob(const char* name, int dflt) {
-  const char* v = getenv(name);
-  return v ? atoi(v) != 0 : dflt != 0;
-}
-static bool use_fwd_p2() { static const bool v = attn_knob("CMHAR_ATTN_FWD_P2", CMHAR_ATTN_FWD_P2); return v; }
-static bool use_dq_q64() { static const bool v = attn_knob("CMHAR_DQ_Q64", CMHAR_DQ_Q64); return v; }
-static bool use_dkdv_k64() { static const bool v = attn_knob("CMHAR_DKDV_K64", CMHAR_DKDV_K64); return v; }
-
 extern "C" int cmhar_attention_fwd(int dtype, int B, int H, int Lq, int Lk, int D, const void* Q, long ldq,
                                    const void* K, long ldk, const void* V, long ldv, void* O, long ldo, float* lse,
                                    float scale, float pdrop, unsigned long long seed, hipStream_t st) {
@@ -1941,10 +1186,7 @@ extern "C" int cmhar_attention_fwd(int dtype, int B, int H, int Lq, int Lk, int 
     const int bulk = CMHAR_ATTN_FWD_ONE_LAUNCH ? cdiv(Lq, 256) * 256 : (Lq / 256) * 256;
 #define FL(E)                                                                                                    \
   do {                                                                                                           \
-    if (bulk > 0 && use_fwd_p2() && !CMHAR_ATTN_FWD_ONE_LAUNCH)                                               \
-      attn_fwd_p2<E><<<dim3(bulk / 256, H, B), 256, 0, st>>>(H, Lq, Lk, (const bf16*)Q, ldq, (const bf16*)K, ldk,  \
-                                                             (const bf16*)V, ldv, (E*)O, ldo, lse, scale);        \
-    else if (bulk > 0)                                                                                           \
+    if (bulk > 0)                                                                                                \
       attn_fwd_bf16<E, 2><<<dim3(bulk / 256, H, B), 256, 0, st>>>(H, Lq, Lk, 0, (const bf16*)Q, ldq, (const bf16*)K, \
                                                                   ldk, (const bf16*)V, ldv, (E*)O, ldo, lse, scale); \
     if (Lq > bulk && Lq - bulk <= CMHAR_ATTN_TAIL)                                                             \
@@ -1987,13 +1229,8 @@ static void flash_bwd_bf16(int B, int H, int Lq, int Lk, const void* Q, long ldq
                            long lddv, float scale, hipStream_t st) {
   const float s_in = PS ? 1.f / LOG2E : scale;   // c = s_in·log2e (1 when PS) and the dQ output factor
   // 256-query workgroups (QB = 2) over the bulk, 128-query workgroups for the rest (as the forward)
-  const bool q64 = PS && use_dq_q64();
-  const int bulk = (CMHAR_ATTN_DQ_QB == 2 || q64) ? (Lq / 256) * 256 : 0;
-  if (bulk > 0 && q64)
-    attn_bwd_dq_q64<<<dim3(bulk / 256, H, B), 256, 0, st>>>(H, Lq, Lk, (const bf16*)Q, ldq, (const bf16*)K, ldk,
-                                                            (const bf16*)V, ldv, (const bf16*)O, ldo, (const bf16*)dO,
-                                                            lddo, lse, delta, (bf16*)dQ, lddq, s_in);
-  else if (bulk > 0)
+  const int bulk = CMHAR_ATTN_DQ_QB == 2 ? (Lq / 256) * 256 : 0;
+  if (bulk > 0)
     attn_bwd_dq_bf16<2, PS><<<dim3(bulk / 256, H, B), 256, 0, st>>>(H, Lq, Lk, 0, (const bf16*)Q, ldq, (const bf16*)K,
                                                                     ldk, (const bf16*)V, ldv, (const bf16*)O, ldo,
                                                                     (const bf16*)dO, lddo, lse, delta, (bf16*)dQ,
@@ -2016,15 +1253,9 @@ static void flash_bwd_bf16(int B, int H, int Lq, int Lk, const void* Q, long ldq
                                                              (const bf16*)dO, lddo, lse, delta, (bf16*)dQ, lddq, s_in);
   const int kfull = (Lk / 128) * 128;
   const bool ktail = Lk > kfull && Lk - kfull <= CMHAR_ATTN_TAIL;
-  // 256-key workgroups of the 64-keys-per-wave kernel over the bulk (round 4), 128-key ones for the rest
-  const int k256 = (PS && use_dkdv_k64()) ? (Lk / 256) * 256 : 0;
-  if (k256 > 0)
-    attn_bwd_dkdv_k64<<<dim3(k256 / 256, H, B), 256, 0, st>>>(H, Lq, Lk, (const bf16*)Q, ldq, (const bf16*)K, ldk,
-                                                              (const bf16*)V, ldv, (const bf16*)dO, lddo, lse, delta,
-                                                              (bf16*)dK, lddk, (bf16*)dV, lddv, scale);
-  const int kblocks = (ktail ? kfull : cdiv(Lk, 128) * 128) / 128 - k256 / 128;
+  const int kblocks = (ktail ? kfull : cdiv(Lk, 128) * 128) / 128;
   if (kblocks > 0)
-    attn_bwd_dkdv_bf16<PS><<<dim3(kblocks, H, B), 256, 0, st>>>(H, Lq, Lk, k256, (const bf16*)Q, ldq, (const bf16*)K,
+    attn_bwd_dkdv_bf16<PS><<<dim3(kblocks, H, B), 256, 0, st>>>(H, Lq, Lk, 0, (const bf16*)Q, ldq, (const bf16*)K,
                                                                 ldk, (const bf16*)V, ldv, (const bf16*)dO, lddo, lse,
                                                                 delta, (bf16*)dK, lddk, (bf16*)dV, lddv, s_in, scale);
   if (ktail)

@@ -7,7 +7,7 @@ Kernels: MaxPool2d(3, 2, 1) forward and gather backward are exact (max / sums of
 maxima (torch's first-maximum rule, checked against torch's CPU kernel); depthwise conv forward / input gradient /
 weight gradient ≤ 1e-5 rel in fp32 (stride 1 and 2, 32..960 channels); channels-last BatchNorm with channel counts
 that are not 8·2^j and ReLU6 ≤ 1e-5; weight packs bit-exact.  Backbones: fp32 features ≤ 1e-4 rel, every parameter
-gradient ≤ 2e-3 rel, running statistics ≤ 1e-5; bf16 within 3× (+1e-2) of the error bf16 storage alone causes per
+gradient ≤ 2e-3 rel, running statistics ≤ 1e-5; bf16 within 3× (+2e-3) of the error bf16 storage alone causes per
 parameter (oracle re-run with bf16 rounding at the storage points); VideoEncoder output (per-frame projection + temporal
 mean) ≤ 1e-4."""
 import pytest
@@ -204,7 +204,7 @@ def test_backbone_bf16_error_is_bf16_storage(backbone):
     from test_r3d_gpu import bf16_storage_bound
     m, sd_p, _, ref, feat, (sd_q, _, ref_q) = _case(backbone, 'bf16', B=2, T=2, S=128, emulate=True)
     e_feat = rel(ref_q, ref)
-    assert rel(feat, ref) < 3 * e_feat + 1e-2, (rel(feat, ref), e_feat)
+    assert rel(feat, ref) < 3 * e_feat + 2e-3, (rel(feat, ref), e_feat)
     grads = {k: p.grad for k, p in m.named_parameters()}
     rows = bf16_storage_bound(grads, {k: sd_p[k].grad for k in grads}, {k: sd_q[k].grad for k in grads})
     print(backbone, 'worst (gpu err, bf16-storage err, param):', rows[:4])

@@ -28,7 +28,7 @@ def _free_port():
 # fp32: the HIP kernels and the oracle sum in different orders; the IMU encoder's post-LN backward amplifies that to
 # ~1.2e-4 on a few of its bias gradients (measured; g1 / g2 bound fp32 gradients at 1e-4 / 1e-3 the same way)
 TOL_FP32 = {'videomae': 5e-4, 'r3d_18': 5e-4}
-FLOOR_BF16 = {'videomae': 2e-3, 'r3d_18': 1e-2}
+FLOOR_BF16 = {'videomae': 2e-3, 'r3d_18': 2e-3}
 
 
 def _run(tmp_path, backbone, dtype='fp32', world=2, backend='gloo', force_reduce=False):
@@ -141,9 +141,9 @@ def test_dataparallel_rccl_single_rank(tmp_path, backbone):
     assert r0['sink']                 # every cmhar video backbone writes into the reducer's flat bucket buffer
     if backbone not in ('videomae', 'r3d_18'):
         return                        # (the CNN backbones' gradients vs their oracle: tests/test_cnn2d_gpu.py)
-    # against the oracle with the bounds of the two-rank test's gradients (one 4-clip shard: R3D-18's train-mode
-    # BatchNorm over 4 clips puts the bf16 loss 2.9e-3 from the fp32 oracle, 6.7x the storage emulation's error)
-    lt = 3 * abs(r0['emul_loss'] - r0['oracle_loss']) / abs(r0['oracle_loss']) + FLOOR_BF16[backbone]
+    # against the oracle with the bounds of the two-rank test's gradients; the loss floor is 1e-4 for both backbones
+    # (round 3's R3D-18 excess was the emulation's missing conv-weight rounding, oracle/r3d_cpu.py bf16_weight)
+    lt = 3 * abs(r0['emul_loss'] - r0['oracle_loss']) / abs(r0['oracle_loss']) + 1e-4
     assert abs(r0['loss'] - r0['oracle_loss']) <= lt * abs(r0['oracle_loss'])
 
 

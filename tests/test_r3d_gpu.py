@@ -5,7 +5,7 @@ Kernel level (fp32, exact-fp32 GEMM): conv3d = im2col + GEMM vs F.conv3d (≤ 1e
 vectorised (C % 8 == 0) paths with stride/padding; col2im is the adjoint of im2col (<im2col x, c> = <x, col2im c>);
 channels-last BatchNorm3d (+ residual + ReLU) forward / backward vs torch autograd (≤ 1e-5).
 Backbone: fp32 mode features ≤ 1e-4 rel, running stats ≤ 1e-5, every parameter gradient ≤ 2e-3 rel; bf16 mode
-(throughput): every parameter gradient within 3× (+1e-2) of the error bf16 storage alone causes for that parameter
+(throughput): every parameter gradient within 3× (+2e-3) of the error bf16 storage alone causes for that parameter
 (the fp32 oracle re-run with bf16 rounding at the HIP path's storage points — `bf16_storage_bound` documents why the
 stem / early-BN gradients are the ill-conditioned ones); eval mode (running statistics) ≤ 1e-4 rel.  The stem
 weight gradient's ~1024-way split-K at production row counts ≤ 1e-4 vs the fp32 product of the same operands."""
@@ -147,7 +147,7 @@ def test_r3d18_fp32_matches_oracle():
         assert int(bufs[pre + 'num_batches_tracked']) == 1
 
 
-def bf16_storage_bound(gpu_grads, fp32_grads, emul_grads, slack=3.0, floor=1e-2):
+def bf16_storage_bound(gpu_grads, fp32_grads, emul_grads, slack=3.0, floor=2e-3):
     """Per-parameter check of a bf16-storage path against the fp32 oracle, with the bound set by the error that bf16
     STORAGE ITSELF causes for that parameter: the fp32 restatement run with bf16 rounding at the HIP path's storage
     points (oracle q = bf16_storage) shows e_p = rel(emulated, fp32).  Root cause of the large stem / early-BN errors
@@ -167,7 +167,7 @@ def bf16_storage_bound(gpu_grads, fp32_grads, emul_grads, slack=3.0, floor=1e-2)
 def test_r3d18_bf16_error_is_bf16_storage():
     m, sd_p, _, ref, feat, (sd_q, _, ref_q) = _backbone_case('bf16', B=4, T=4, S=48, emulate=True)
     e_feat = rel(ref_q, ref)
-    assert rel(feat, ref) < 3 * e_feat + 1e-2, (rel(feat, ref), e_feat)
+    assert rel(feat, ref) < 3 * e_feat + 2e-3, (rel(feat, ref), e_feat)
     grads = {k: p.grad for k, p in m.named_parameters()}
     rows = bf16_storage_bound(grads, {k: sd_p[k].grad for k in grads}, {k: sd_q[k].grad for k in grads})
     print('worst (gpu err, bf16-storage err, param):', rows[:4])

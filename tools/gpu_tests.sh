@@ -1,7 +1,7 @@
 #!/bin/bash
-# Round-3 GPU session: full GPU test suite (-s: the bf16 tests print their worst per-parameter errors), smoke, and a
-# short bench.  usage: tools/gpu_r03.sh TAG [pytest -k expression]
-TAG=${1:-r03}
+# GPU test session: full GPU test suite (-s: the bf16 tests print their worst per-parameter errors), smoke, and a
+# short bench.  usage: tools/gpu_tests.sh TAG [pytest -k expression]
+TAG=${1:-r04}
 KEXPR=${2:-}
 mkdir -p gpurun_out
 export TMPDIR=/tmp
