@@ -111,14 +111,11 @@ __device__ __forceinline__ float xhalf(float v) { return __shfl_xor(v, 32); }
 // Forward per 32-key half at 3 waves per SIMD (168 VGPRs): 4 % faster than scoring whole 64-key tiles at 2 waves
 // per SIMD (tools/debug/attn_ab.py; the lazy-rescale points move, so not bit-identical to that form).  One launch
 // with the last 256-query workgroup of each head partly idle instead of the 128-query tail launch: 1 % slower.
-#ifndef CMHAR_ATTN_FWD_PERKB
-#define CMHAR_ATTN_FWD_PERKB 1
-#endif
 #ifndef CMHAR_ATTN_FWD_ONE_LAUNCH
 #define CMHAR_ATTN_FWD_ONE_LAUNCH 0
 #endif
 template <typename E, int QB>
-__global__ __launch_bounds__(256, CMHAR_ATTN_FWD_PERKB ? 3 : 2) void attn_fwd_bf16(int H, int Lq, int Lk, int q_base, const bf16* __restrict__ Q,
+__global__ __launch_bounds__(256, 3) void attn_fwd_bf16(int H, int Lq, int Lk, int q_base, const bf16* __restrict__ Q,
                                                         long ldq, const bf16* __restrict__ K, long ldk,
                                                         const bf16* __restrict__ V, long ldv, E* __restrict__ O,
                                                         long ldo, float* __restrict__ lse, float scale) {
@@ -168,7 +165,6 @@ __global__ __launch_bounds__(256, CMHAR_ATTN_FWD_PERKB ? 3 : 2) void attn_fwd_bf
   auto tile = [&](auto CUR, int kt) __attribute__((always_inline)) {
     constexpr int cur = decltype(CUR)::value;
     const bool more = kt + 1 < nt;
-#if CMHAR_ATTN_FWD_PERKB
     // Per 32-key half (kb): Sᵀ for every q-block (each K fragment read once, used QB times), its softmax, then
     // Oᵀ += Vᵀ·Pᵀ for that half — only one half's scores are live (32 fewer VGPRs than scoring the whole 64-key
     // tile first), which lets QB = 2 run at 3 waves per SIMD.
@@ -205,7 +201,10 @@ __global__ __launch_bounds__(256, CMHAR_ATTN_FWD_PERKB ? 3 : 2) void attn_fwd_bf
 #pragma unroll
           for (int r = 0; r < 16; ++r) mt = fmaxf(mt, s[j][r]);
           mt = fmaxf(mt, xhalf(mt)) * c;
-          // lazy rescale (see below): the running max moves only when a row's half-tile max exceeds it by > 8
+          // Lazy rescale: the running max m only moves (and O, l are rescaled) when some row's half-tile max
+          // exceeds it by more than 8 (log2 units), so p = exp2(c·s − m) ≤ 2^8 stays well inside fp32/bf16 range;
+          // with the row maxima settling after the first key tiles this skips ~all rescales.  (Seeding the S
+          // accumulators with −m instead of the fma below: the seed costs 16 v_mov per block, the same issue slots.)
           if (__builtin_amdgcn_ballot_w64(mt > m[j] + 8.f) != 0) {
             const float mn = fmaxf(m[j], mt);
             const float alpha = fexp2(m[j] - mn);
@@ -236,90 +235,6 @@ __global__ __launch_bounds__(256, CMHAR_ATTN_FWD_PERKB ? 3 : 2) void attn_fwd_bf
           }
       }
     }
-#else
-    // Sᵀ = K·Qᵀ for every q-block; each K fragment is read once and used QB times
-    floatx16 s[QB][2];
-    if (active) {
-#pragma unroll
-    for (int kb = 0; kb < 2; ++kb) {
-#pragma unroll
-      for (int j = 0; j < QB; ++j)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) s[j][kb][r] = 0.f;
-#pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        const bf16x8 kf = row_frag(Ks(cur), kb * 32, t, lane);
-#pragma unroll
-        for (int j = 0; j < QB; ++j)
-          s[j][kb] = mma32<E>(kf, qf[j][t], s[j][kb]);
-      }
-    }
-    }
-    if (more) {   // next tile DMA'd into the other buffer under the softmax and P·V
-      tk.tile((kt + 1) * 64, Ks(cur ^ 1), wave);
-      tv.tile((kt + 1) * 64, Vs(cur ^ 1), wave);
-    }
-    if (active) {
-    const int kbase = kt * 64;
-    if (kbase + 64 > Lk) {   // ragged last tile only (wave-uniform branch)
-#pragma unroll
-      for (int j = 0; j < QB; ++j)
-#pragma unroll
-        for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-          for (int r = 0; r < 16; ++r)
-            if (kbase + kb * 32 + acc_row(r, h) >= Lk) s[j][kb][r] = -INFINITY;
-    }
-    bf16x8 pb[QB][2][2];
-#pragma unroll
-    for (int j = 0; j < QB; ++j) {
-      // row max on the raw scores (c > 0), then p = exp2(c·s − m) as one fma + v_exp per element
-      float mt = -INFINITY;
-#pragma unroll
-      for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) mt = fmaxf(mt, s[j][kb][r]);
-      mt = fmaxf(mt, xhalf(mt)) * c;
-      // Lazy rescale: the running max m only moves (and O, l are rescaled) when some row's tile max exceeds it by
-      // more than 8 (log2 units), so p = exp2(c·s − m) ≤ 2^8 stays well inside fp32/bf16 range; with the row
-      // maxima settling after the first key tiles this skips ~all rescales (64 v_mul per tile per wave).
-      if (__builtin_amdgcn_ballot_w64(mt > m[j] + 8.f) != 0) {
-        const float mn = fmaxf(m[j], mt);
-        const float alpha = fexp2(m[j] - mn);
-        m[j] = mn;
-        l[j] *= alpha;
-#pragma unroll
-        for (int d = 0; d < 2; ++d)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) o[j][d][r] *= alpha;
-      }
-      const float mn = m[j];
-#pragma unroll
-      for (int kb = 0; kb < 2; ++kb) {
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const float p = fexp2(fmaf(s[j][kb][r], c, -mn));
-          s[j][kb][r] = p;
-          l[j] += p;
-        }
-#pragma unroll
-        for (int ss = 0; ss < 2; ++ss) pb[j][kb][ss] = pack8<E>(s[j][kb], ss);   // P leaves fp32 registers here
-      }
-    }
-    // Oᵀ += Vᵀ·Pᵀ; each V transposed fragment is read once and used QB times
-#pragma unroll
-    for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-      for (int ss = 0; ss < 2; ++ss)
-#pragma unroll
-        for (int d = 0; d < 2; ++d) {
-          const bf16x8 vf = tr_frag(Vs(cur), kb * 32, ss, d * 32, lane);
-#pragma unroll
-          for (int j = 0; j < QB; ++j)
-            o[j][d] = mma32<E>(vf, pb[j][kb][ss], o[j][d]);
-        }
-    }
-#endif
     if (more) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // own pieces of the next tile landed
     __syncthreads();
   };
