@@ -132,28 +132,35 @@ def parse():
     return args
 
 
-def measure_mfma_peak(dev, blocks=2048, iters=20000, reps=3):
-    """The on-box dense bf16 MFMA rate: csrc/probe.hip's back-to-back v_mfma_f32_32x32x16_bf16 on random
-    fragments over every SIMD (2048 workgroups × 4 waves), one launch ≈ 20 ms, timed with HIP events on the launch
-    stream; the best of `reps` after one warm launch.  Returns TFLOP/s."""
+def measure_mfma_peak(dev, blocks=2048, iters=10000, reps=3, per_shape=None):
+    """The on-box dense bf16 MFMA rate: csrc/probe.hip's back-to-back bf16 MFMAs (8 chains per wave) on
+    random fragments over every SIMD (2048 workgroups × 4 waves), both shapes — v_mfma_f32_32x32x16_bf16 (attention)
+    and v_mfma_f32_16x16x32_bf16 (GEMMs), which the chip runs at different clocks on random data — one launch each
+    ≈ 10–20 ms, timed with HIP events on the launch stream; the best of `reps` after one warm launch per shape.
+    Returns the larger rate in TFLOP/s; `per_shape` (a dict) receives both."""
     from cmhar import _lib as L
     g = torch.Generator(device=dev).manual_seed(77)
     ops = torch.randn(512 * 8, device=dev, generator=g).bfloat16()
     out = torch.empty(blocks * 256, device=dev)
-    flops = L.lib().cmhar_mfma_peak_probe_flops(blocks, iters)
     st = torch.cuda.current_stream(dev)
-    best = 0.0
-    for r in range(reps + 1):
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record(st)
-        L.call('cmhar_mfma_peak_probe', blocks, iters, ops.data_ptr(), 512, out.data_ptr(), L.stream(dev))
-        e1.record(st)
-        e1.synchronize()
-        if r:
-            best = max(best, flops / (e0.elapsed_time(e1) / 1e3) / 1e12)
-    if not torch.isfinite(out).all():
-        raise RuntimeError('MFMA peak probe produced non-finite sums')
-    return best
+    rates = {}
+    for shape, name in ((0, '32x32x16'), (1, '16x16x32')):
+        flops = L.lib().cmhar_mfma_peak_probe_flops(shape, blocks, iters)
+        best = 0.0
+        for r in range(reps + 1):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(st)
+            L.call('cmhar_mfma_peak_probe', shape, blocks, iters, ops.data_ptr(), 512, out.data_ptr(), L.stream(dev))
+            e1.record(st)
+            e1.synchronize()
+            if r:
+                best = max(best, flops / (e0.elapsed_time(e1) / 1e3) / 1e12)
+        if not torch.isfinite(out).all():
+            raise RuntimeError('MFMA peak probe produced non-finite sums')
+        rates[name] = round(best, 1)
+    if per_shape is not None:
+        per_shape.update(rates)
+    return max(rates.values())
 
 
 def videomae_flops_per_clip(T, H, W, hd=768, layers=12, inter=3072, P=16, tub=2, C=3):
@@ -564,8 +571,9 @@ def main():
     # kernel in the serial traced warm-up step.
     roof = None
     peak_meas = None
+    peak_shapes = {}
     if headline and rank == 0 and os.environ.get('CMHAR_BENCH_PEAK_PROBE', '1') == '1':
-        peak_meas = measure_mfma_peak(dev)      # after the timed region: it does not perturb the measurement
+        peak_meas = measure_mfma_peak(dev, per_shape=peak_shapes)   # after the timed region: no perturbation
         log(f'on-box MFMA peak probe: {peak_meas:.1f} TFLOP/s')
     summ = K.TRACE.summary() if trace else {}
     if dominant in summ:
@@ -577,8 +585,10 @@ def main():
                 'frac': round(achieved / PEAK_BF16_TFLOPS, 4),
                 'peak_measured': round(peak_meas, 1) if peak_meas else None,
                 'frac_of_measured_peak': round(achieved / peak_meas, 4) if peak_meas else None,
+                'peak_measured_per_shape': peak_shapes or None,
                 'peak_note': 'frac divides by the vendor dense bf16 peak (2.5 PF); peak_measured = csrc/probe.hip '
-                             'back-to-back 32x32x16 bf16 MFMAs on random fragments, every SIMD, this box',
+                             'back-to-back bf16 MFMAs on random fragments (the faster of the 32x32x16 and 16x16x32 '
+                             'shapes), every SIMD, this box',
                 'traffic': traffic, 'traffic_source': tsrc,
                 'kernel': name,
                 'launches': n, 'avg_launch_ms': round(tot_ms / n, 4),

@@ -125,8 +125,8 @@ _SIGS = {
     'cmhar_dwconv2d_cl_wgrad_ws': (i64, [i32, i32, i32, i32, i32, i32, i32]),
     'cmhar_dwconv2d_cl_wgrad': (i32, [i32, i32, i32, i32, i32, i32, i32, i32, vp, vp, vp, vp, vp]),
     'cmhar_mt_transpose_bf16': (i32, [vp, i32, i32, vp]),
-    'cmhar_mfma_peak_probe_flops': (i64, [i32, i32]),
-    'cmhar_mfma_peak_probe': (i32, [i32, i32, vp, i32, vp, vp]),
+    'cmhar_mfma_peak_probe_flops': (i64, [i32, i32, i32]),
+    'cmhar_mfma_peak_probe': (i32, [i32, i32, i32, vp, i32, vp, vp]),
 }
 
 EXPORTED = tuple(_SIGS)

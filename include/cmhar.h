@@ -368,11 +368,13 @@ int cmhar_dwconv2d_cl_wgrad(int dtype, int N, int H, int W, int C, int k, int s,
 int cmhar_video_to_ndhwc(int out_dtype, int B, int T, int C, int H, int W, const float* video, void* out,
                          hipStream_t stream);
 
-/* ---- measurement (the on-box MFMA peak).  Back-to-back v_mfma_f32_32x32x16_bf16 on random bf16
- * fragments, 4 independent chains per wave: `blocks` workgroups of 256 threads, `iters` iterations of 8 MFMAs per
- * wave; ops = nops 16-B bf16 fragments (random), out = blocks·256 floats.  _flops = the FLOPs one launch executes. */
-long cmhar_mfma_peak_probe_flops(int blocks, int iters);
-int cmhar_mfma_peak_probe(int blocks, int iters, const void* ops, int nops, float* out, hipStream_t stream);
+/* ---- measurement (the on-box MFMA peak).  Back-to-back bf16 MFMAs on random bf16 fragments, 8
+ * independent chains per wave — shape 0: v_mfma_f32_32x32x16_bf16, 1: v_mfma_f32_16x16x32_bf16 (-1 otherwise):
+ * `blocks` workgroups of 256 threads, `iters` iterations of 8 MFMAs per wave; ops = nops 16-B bf16 fragments
+ * (random), out = blocks·256 floats.  _flops = the FLOPs one launch executes. */
+long cmhar_mfma_peak_probe_flops(int shape, int blocks, int iters);
+int cmhar_mfma_peak_probe(int shape, int blocks, int iters, const void* ops, int nops, float* out,
+                          hipStream_t stream);
 
 #ifdef __cplusplus
 }

@@ -626,9 +626,12 @@ def test_mfma_peak_probe():
     above 900 TF/s (the chip lowers its clock under dense MFMA load on random data: r04 measured 1414) and below
     2.6 PF — and finite accumulator sums."""
     import bench
-    tf = bench.measure_mfma_peak(torch.device(DEV), blocks=1024, iters=4000, reps=2)
-    print(f'MFMA peak probe: {tf:.1f} TFLOP/s')
-    assert 900.0 < tf < 2600.0, tf     # DVFS: random-data MFMA loops hold ≈1.9-2.0 GHz (MICROARCH DVFS give-back)
+    shapes = {}
+    tf = bench.measure_mfma_peak(torch.device(DEV), blocks=1024, iters=4000, reps=2, per_shape=shapes)
+    print(f'MFMA peak probe: {tf:.1f} TFLOP/s', shapes)
+    assert set(shapes) == {'32x32x16', '16x16x32'} and tf == max(shapes.values())
+    for v in shapes.values():       # DVFS: random-data MFMA loops hold ≈1.9 GHz (MICROARCH DVFS give-back)
+        assert 900.0 < v < 2600.0, shapes
 
 
 def test_packed_weights_transposed_copies():
