@@ -1070,63 +1070,6 @@ __global__ __launch_bounds__(64) void attn_bwd_dkdv_f32(int H, int Lq, int Lk, c
 #define CMHAR_ATTN_TAIL 64
 #endif
 
-// The ragged-tail kernels run on a second stream, concurrently with the bulk kernel of the same call (they write
-// disjoint rows): launched after the bulk on one stream, a tail (one workgroup per (batch, head), 32 rows against the
-// whole other sequence) is a latency-bound launch of its own — 30 µs (forward) / 40 µs (dK/dV) per layer at
-// L = 1568 — where beside the bulk its workgroups take CU slots the bulk's last round leaves free.  Per host thread
-// (thread_local: concurrent callers on their own streams never share the fork / join events) and per device.
-// CMHAR_ATTN_TAIL_STREAM=0 (read once per process) keeps the tails on the caller's stream (A/B).
-#ifndef CMHAR_ATTN_TAIL_STREAM_DEFAULT
-#define CMHAR_ATTN_TAIL_STREAM_DEFAULT 1
-#endif
-static bool tail_stream_on() {
-  static const bool v = [] {
-    const char* s = getenv("CMHAR_ATTN_TAIL_STREAM");
-    return s ? atoi(s) != 0 : CMHAR_ATTN_TAIL_STREAM_DEFAULT != 0;
-  }();
-  return v;
-}
-struct SideStream {
-  hipStream_t st = nullptr;      // the caller's stream
-  hipStream_t side = nullptr;
-  hipEvent_t fork_ev = nullptr, join_ev = nullptr;
-  bool forked = false;
-  explicit SideStream(hipStream_t s) : st(s) {
-    if (!tail_stream_on()) return;
-    struct PerDev { hipStream_t s = nullptr; hipEvent_t f = nullptr, j = nullptr; };
-    thread_local PerDev per[64];
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return;
-    PerDev& p = per[dev];
-    if (!p.s) {
-      if (hipStreamCreateWithFlags(&p.s, hipStreamNonBlocking) != hipSuccess ||
-          hipEventCreateWithFlags(&p.f, hipEventDisableTiming) != hipSuccess ||
-          hipEventCreateWithFlags(&p.j, hipEventDisableTiming) != hipSuccess) {
-        p.s = nullptr;
-        return;
-      }
-    }
-    side = p.s;
-    fork_ev = p.f;
-    join_ev = p.j;
-  }
-  // the stream a tail launches on: the side stream, ordered after everything already enqueued on the caller's
-  hipStream_t fork() {
-    if (!side) return st;
-    if (!forked && hipEventRecord(fork_ev, st) == hipSuccess && hipStreamWaitEvent(side, fork_ev, 0) == hipSuccess)
-      forked = true;
-    return forked ? side : st;
-  }
-  // the caller's stream waits for the tail (every later use of the outputs is ordered after it)
-  void join() {
-    if (forked) {
-      hipEventRecord(join_ev, side);
-      hipStreamWaitEvent(st, join_ev, 0);
-      forked = false;
-    }
-  }
-};
-
 // f32-MFMA flash kernels (csrc/attention_f32.hip) for fp32 storage, D = 64, no dropout
 void cmhar_attn_f32m_fwd(int B, int H, int Lq, int Lk, const float* Q, long ldq, const float* K, long ldk,
                          const float* V, long ldv, float* O, long ldo, float* lse, float scale, hipStream_t st);
@@ -1157,17 +1100,15 @@ extern "C" int cmhar_attention_fwd(int dtype, int B, int H, int Lq, int Lk, int 
     // (CMHAR_ATTN_FWD_ONE_LAUNCH: 256-query workgroups everywhere, the last one per head partly idle)
     const int bulk = CMHAR_ATTN_FWD_ONE_LAUNCH ? cdiv(Lq, 256) * 256 : (Lq / 256) * 256;
     const bool tail = Lq > bulk && Lq - bulk <= CMHAR_ATTN_TAIL;
-    SideStream ss(st);
-    hipStream_t tst = tail && bulk > 0 ? ss.fork() : st;   // the tail beside the bulk (see SideStream)
 #define FL(E)                                                                                                    \
   do {                                                                                                           \
     if (bulk > 0)                                                                                                \
       attn_fwd_bf16<E, 2><<<dim3(bulk / 256, H, B), 256, 0, st>>>(H, Lq, Lk, 0, (const bf16*)Q, ldq, (const bf16*)K, \
                                                                   ldk, (const bf16*)V, ldv, (E*)O, ldo, lse, scale); \
     if (tail)                                                                                                    \
-      attn_fwd_tail_bf16<E><<<dim3(cdiv(Lq - bulk, 32), H, B), 256, 0, tst>>>(H, Lq, Lk, bulk, (const bf16*)Q, ldq,  \
-                                                                              (const bf16*)K, ldk,               \
-                                                            (const bf16*)V, ldv, (E*)O, ldo, lse, scale);       \
+      attn_fwd_tail_bf16<E><<<dim3(cdiv(Lq - bulk, 32), H, B), 256, 0, st>>>(H, Lq, Lk, bulk, (const bf16*)Q, ldq,   \
+                                                                             (const bf16*)K, ldk,                \
+                                                           (const bf16*)V, ldv, (E*)O, ldo, lse, scale);        \
     else if (Lq > bulk)                                                                                          \
       attn_fwd_bf16<E, 1><<<dim3(cdiv(Lq - bulk, 128), H, B), 256, 0, st>>>(H, Lq, Lk, bulk, (const bf16*)Q, ldq,   \
                                                                             (const bf16*)K, ldk, (const bf16*)V, ldv, \
@@ -1175,7 +1116,6 @@ extern "C" int cmhar_attention_fwd(int dtype, int B, int H, int Lq, int Lk, int 
   } while (0)
     if (dtype == CMHAR_F16) FL(f16); else FL(bf16);
 #undef FL
-    ss.join();
   } else if (f32m_ok(dtype, D, pdrop, {{Q, ldq}, {K, ldk}, {V, ldv}, {O, ldo}})) {
     cmhar_attn_f32m_fwd(B, H, Lq, Lk, (const float*)Q, ldq, (const float*)K, ldk, (const float*)V, ldv, (float*)O, ldo,
                         lse, scale, st);
@@ -1230,18 +1170,15 @@ static void flash_bwd_bf16(int B, int H, int Lq, int Lk, const void* Q, long ldq
   const int kfull = (Lk / 128) * 128;
   const bool ktail = Lk > kfull && Lk - kfull <= CMHAR_ATTN_TAIL;
   const int kblocks = (ktail ? kfull : cdiv(Lk, 128) * 128) / 128;
-  SideStream ss(st);   // the dK/dV tail beside the bulk, after the dQ kernel that writes δ (see SideStream)
-  const hipStream_t tst = ktail && kblocks > 0 ? ss.fork() : st;
   if (kblocks > 0)
     attn_bwd_dkdv_bf16<PS><<<dim3(kblocks, H, B), 256, 0, st>>>(H, Lq, Lk, 0, (const bf16*)Q, ldq, (const bf16*)K,
                                                                 ldk, (const bf16*)V, ldv, (const bf16*)dO, lddo, lse,
                                                                 delta, (bf16*)dK, lddk, (bf16*)dV, lddv, s_in, scale);
   if (ktail)
-    attn_bwd_dkdv_tail_bf16<PS><<<dim3(cdiv(Lk - kfull, 32), H, B), 256, 0, tst>>>(H, Lq, Lk, kfull, (const bf16*)Q,
+    attn_bwd_dkdv_tail_bf16<PS><<<dim3(cdiv(Lk - kfull, 32), H, B), 256, 0, st>>>(H, Lq, Lk, kfull, (const bf16*)Q,
                                                                                   ldq, (const bf16*)K,
                                                                ldk, (const bf16*)V, ldv, (const bf16*)dO, lddo, lse,
                                                                delta, (bf16*)dK, lddk, (bf16*)dV, lddv, s_in, scale);
-  ss.join();
 }
 
 extern "C" int cmhar_attention_bwd_prescaled(int B, int H, int Lq, int Lk, const void* Q, long ldq, const void* K,

@@ -880,12 +880,18 @@ __device__ __forceinline__ bf16x8 frag8p_a(const char* lds, int r0, int kk, int 
 // K-split of klen (fp32 partial slabs at split_stride when raw_out, reduced by splitk_reduce_kernel), with the bias
 // gradient Σ_k A(m,k) (Epilogue::rowsum) on the same MFMA operand fragments as gemm256_kernel; the per-output
 // accumulation order (K-tile, then kk) is gemm256_kernel's, so the two kernels give identical bits.
-template <typename E, bool A_KC, bool B_KC, typename OutT, bool PFS = false>
+// NA = 3: the A operand triple-buffered (three 32 KiB A images + two B images = the whole 160 KiB): A of K-tile t+2
+// is staged during K-tile t (half 1 in phase 2, half 0 in phase 4) and B of t+1 in phase 1, so phase 4 waits with
+// vmcnt(4) for B(t+1) and A(t+1) only — the activation stream (the HBM / MALL-bound operand) gets a whole K-tile more
+// lead than the 2–4 barrier intervals (~0.3 µs) of the two-buffer schedule.  Same fragments, same MFMA order:
+// identical bits.
+template <typename E, bool A_KC, bool B_KC, typename OutT, bool PFS = false, int NA = 2>
 __global__ __launch_bounds__(NT2, 2) void gemm8p_kernel(int M, int N, int K, const bf16* __restrict__ A, long lda,
                                                         const bf16* __restrict__ B, long ldb, OutT* __restrict__ C,
                                                         long ldc, Epilogue e, int klen, long split_stride,
                                                         int raw_out) {
-  __shared__ __attribute__((aligned(16))) char smem[SMEM2];
+  static_assert(NA == 2 || NA == 3, "two or three A buffers");
+  __shared__ __attribute__((aligned(16))) char smem[NA == 3 ? 163840 : SMEM2];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = wave >> 2, wc = wave & 3;
@@ -907,9 +913,10 @@ __global__ __launch_bounds__(NT2, 2) void gemm8p_kernel(int M, int N, int K, con
   DmaHalf<B_KC> db;
   da.init(A, lda, bm, wave, lane);
   db.init(B, ldb, bn, wave, lane);
-  // buffer b: A image [256][64] at b*64 KiB, B image at b*64 KiB + 32 KiB
-  auto abuf = [&](int t) -> char* { return smem + (t & 1) * 65536; };
-  auto bbuf = [&](int t) -> char* { return smem + (t & 1) * 65536 + 32768; };
+  // NA = 2: buffer b = A image [256][64] at b*64 KiB, B image at b*64 KiB + 32 KiB; NA = 3: A images at (t % 3) *
+  // 32 KiB, B images at 96 KiB + (t & 1) * 32 KiB
+  auto abuf = [&](int t) -> char* { return NA == 3 ? smem + (t % 3) * 32768 : smem + (t & 1) * 65536; };
+  auto bbuf = [&](int t) -> char* { return NA == 3 ? smem + 98304 + (t & 1) * 32768 : smem + (t & 1) * 65536 + 32768; };
 
   floatx4 acc[8][4];
 #pragma unroll
@@ -918,13 +925,18 @@ __global__ __launch_bounds__(NT2, 2) void gemm8p_kernel(int M, int N, int K, con
     for (int j = 0; j < 4; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
   bf16x8 af[2][4], b0[2][2], b1[2][2];
 
-  // prologue: K-tile 0 whole + K-tile 1's A upper half; wait for tile 0
+  // prologue: K-tile 0 whole + K-tile 1's A half 0 (NA = 3: K-tile 1's whole A); wait for tile 0
   da.half(kbeg, abuf(0), 0, wave);
   da.half(kbeg, abuf(0), 1, wave);
   db.half(kbeg, bbuf(0), 0, wave);
   db.half(kbeg, bbuf(0), 1, wave);
   da.half(kbeg + TK2, abuf(1), 0, wave);
-  asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+  if constexpr (NA == 3) {
+    da.half(kbeg + TK2, abuf(1), 1, wave);
+    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+  }
   __builtin_amdgcn_s_barrier();
   if (wr == 1) __builtin_amdgcn_s_barrier();   // group 1 runs one interval behind
   __builtin_amdgcn_sched_barrier(0);
@@ -960,7 +972,7 @@ __global__ __launch_bounds__(NT2, 2) void gemm8p_kernel(int M, int N, int K, con
     const char* bs = bbuf(t);
     const bool n1 = t + 1 < nk, n2 = t + 2 < nk;
     const int k1 = kbeg + (t + 1) * TK2, k2 = kbeg + (t + 2) * TK2;
-    // phase 1: A0 + B0, stage A lower half of t+1; MFMA quadrant (0,0)
+    // phase 1: A0 + B0, stage A lower half of t+1 (NA = 3: both B halves of t+1); MFMA quadrant (0,0)
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
 #pragma unroll
@@ -968,20 +980,31 @@ __global__ __launch_bounds__(NT2, 2) void gemm8p_kernel(int M, int N, int K, con
 #pragma unroll
       for (int i = 0; i < 4; ++i) af[kk][i] = frag8p_a<A_KC>(as, wr * 128 + i * 16, kk, lane);
     }
-    if (n1) da.half(k1, abuf(t + 1), 1, wave);
+    if constexpr (NA == 3) {
+      if (n1) {
+        db.half(k1, bbuf(t + 1), 0, wave);
+        db.half(k1, bbuf(t + 1), 1, wave);
+      }
+    } else {
+      if (n1) da.half(k1, abuf(t + 1), 1, wave);
+    }
     END_LOADS();
     {
       constexpr int qn_ = 0;
       MFMA_Q(0, b0);
     }
-    // phase 2: B1, stage both B halves of t+1; quadrant (0,1)
+    // phase 2: B1, stage both B halves of t+1 (NA = 3: A half 1 of t+2); quadrant (0,1)
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
       for (int j = 0; j < 2; ++j) b1[kk][j] = frag256<B_KC>(bs, wc * 64 + 32 + j * 16, kk, lane);
-    if (n1) {
-      db.half(k1, bbuf(t + 1), 0, wave);
-      db.half(k1, bbuf(t + 1), 1, wave);
+    if constexpr (NA == 3) {
+      if (n2) da.half(k2, abuf(t + 2), 1, wave);
+    } else {
+      if (n1) {
+        db.half(k1, bbuf(t + 1), 0, wave);
+        db.half(k1, bbuf(t + 1), 1, wave);
+      }
     }
     END_LOADS();
     {
@@ -998,9 +1021,19 @@ __global__ __launch_bounds__(NT2, 2) void gemm8p_kernel(int M, int N, int K, con
       constexpr int qn_ = 1;
       MFMA_Q(1, b1);
     }
-    // phase 4: no reads; all of t+1 landed (own pieces), then A upper half of t+2; quadrant (1,0)
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (n2) da.half(k2, abuf(t + 2), 0, wave);
+    // phase 4: no reads; all of t+1 landed (own pieces), then A upper half of t+2; quadrant (1,0).  NA = 3: A half 0
+    // of t+2 first, then a wait that leaves t+2's four A pieces in flight
+    if constexpr (NA == 3) {
+      if (n2) {
+        da.half(k2, abuf(t + 2), 0, wave);
+        asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (n2) da.half(k2, abuf(t + 2), 0, wave);
+    }
     END_LOADS();
     {
       constexpr int qn_ = 0;
@@ -1178,6 +1211,26 @@ static bool use_8p_wgrad() {
   return v;
 }
 
+// A-operand buffers of the 8-phase kernel (gemm8p_kernel NA): forward / dgrad layouts and the weight-gradient
+// layout separately; CMHAR_GEMM8P_NA / CMHAR_GEMM8P_WGRAD_NA = 2 / 3 override the build defaults (A/B measurements;
+// identical bits either way).
+#ifndef CMHAR_GEMM8P_NA_DEFAULT
+#define CMHAR_GEMM8P_NA_DEFAULT 3
+#endif
+#ifndef CMHAR_GEMM8P_WGRAD_NA_DEFAULT
+#define CMHAR_GEMM8P_WGRAD_NA_DEFAULT 2
+#endif
+static int na_knob(const char* name, int dflt) {
+  const char* s = getenv(name);
+  const int v = s ? atoi(s) : dflt;
+  return v == 3 ? 3 : 2;
+}
+static int gemm8p_na(bool ak) {
+  static const int fwd = na_knob("CMHAR_GEMM8P_NA", CMHAR_GEMM8P_NA_DEFAULT);
+  static const int wg = na_knob("CMHAR_GEMM8P_WGRAD_NA", CMHAR_GEMM8P_WGRAD_NA_DEFAULT);
+  return ak ? fwd : wg;
+}
+
 // Which kernel(s) a cmhar_gemm_bf16 call launches (also exported for trace labels: cmhar_gemm_bf16_plan).
 enum GemmPlan {
   PLAN_128 = 0, PLAN_256 = 1, PLAN_256_TAIL = 2, PLAN_256_SPLITK = 3, PLAN_8P = 4, PLAN_128_SPLITK = 5, PLAN_8P_SPLITK = 6
@@ -1235,12 +1288,19 @@ int launch(int M, int N, int K, const bf16* A, long lda, const bf16* B, long ldb
         splitk_reduce_kernel<OutT><<<reduce_blocks(tail_rows, N), 256, 0, st>>>(
             tail_rows, N, ts.nsplit, ws, (long)tail_rows * N, C, ldc, e, ts.tail_m0);
     } else if (plan == PLAN_8P) {
-      if (ph_gemm && pfs)
+      const bool na3 = gemm8p_na(AK) == 3;
+      if (ph_gemm && pfs && na3)
+        gemm8p_kernel<E, AK, BKc, OutT, true, 3><<<grid, NT2, 0, st>>>(M, N, K, A, lda, B, ldb, C, ldc, e, K, 0, 0);
+      else if (ph_gemm && pfs)
         gemm8p_kernel<E, AK, BKc, OutT, true><<<grid, NT2, 0, st>>>(M, N, K, A, lda, B, ldb, C, ldc, e, K, 0, 0);
+      else if (ph_gemm && na3)
+        gemm8p_kernel<E, AK, BKc, OutT, false, 3><<<grid, NT2, 0, st>>>(M, N, K, A, lda, B, ldb, C, ldc, e, K, 0, 0);
       else if (ph_gemm)
         gemm8p_kernel<E, AK, BKc, OutT><<<grid, NT2, 0, st>>>(M, N, K, A, lda, B, ldb, C, ldc, e, K, 0, 0);
     } else if (plan == PLAN_8P_SPLITK) {
-      if (ph_gemm)
+      if (ph_gemm && gemm8p_na(AK) == 3)
+        gemm8p_kernel<E, AK, BKc, float, false, 3><<<grid, NT2, 0, st>>>(M, N, K, A, lda, B, ldb, ws, N, e, klen, ss, 1);
+      else if (ph_gemm)
         gemm8p_kernel<E, AK, BKc, float><<<grid, NT2, 0, st>>>(M, N, K, A, lda, B, ldb, ws, N, e, klen, ss, 1);
       if (ph_red) splitk_reduce_kernel<OutT><<<reduce_blocks(M, N), 256, 0, st>>>(M, N, nsplit, ws, ss, C, ldc, e);
     } else if (plan == PLAN_256) {
