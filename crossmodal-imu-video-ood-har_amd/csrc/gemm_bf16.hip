@@ -791,6 +791,26 @@ __global__ __launch_bounds__(NT2, 2) void gemm256_kernel(int M, int N, int K, co
 // read and read >= 1 interval after the wait that retires it.  (Measured against gemm256_kernel in one process,
 // tools/debug/gemm_ab.py: forward 5-6 % faster at K = 768-1536; bit-identical — each output's k order is unchanged.)
 // ---------------------------------------------------------------------------------------------------------------
+// One 1-KiB LDS-DMA piece (`buffer_load_dwordx4 … lds`, 16 B per lane) issued by inline asm: hipcc then does not see
+// an LDS write in flight, so it no longer puts `s_waitcnt vmcnt(0)` in front of every transposed LDS read
+// (ds_read_b64_tr_b16) that follows a DMA issue — in the weight-gradient instantiation it did so at every phase,
+// draining the next K-tile's prefetch three times per K-tile.  The kernel orders every DMA itself (counted vmcnt +
+// barriers, as with the builtin).  src: the tile origin at this K-slice (wave-uniform); M0 is written here and no
+// compiler-generated code in these kernels uses M0 (no builtin DMA left in an ASM instantiation; checked in the .s).
+__device__ __forceinline__ void dma_asm(const char* src, char* lds, int voff) {
+  const unsigned long long a = (unsigned long long)src;
+  uint4_t rs;
+  rs[0] = __builtin_amdgcn_readfirstlane((unsigned)a);
+  rs[1] = __builtin_amdgcn_readfirstlane((unsigned)(a >> 32)) & 0xffffu;
+  rs[2] = 0x7fffffffu;
+  rs[3] = 0x00020000u;
+  const unsigned la = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(lds_void_ptr)lds);
+  // (s_nop: the SALU write of M0 needs one wait state before the LDS-DMA reads it — hipcc puts the same nop after
+  // its own M0 writes; inside inline asm its hazard recognizer cannot)
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds" :: "s"(la), "v"(voff), "s"(rs)
+               : "memory");
+}
+
 // Per-lane offsets of this wave's 2 pieces of each half of an operand tile.  K-contiguous [256 rows][64 k]: half h =
 // rows 128h..128h+127.  Row-contraction [64 k][256 cols] (the dgrad weight operand): half h = k rows 32h..32h+31.
 template <bool KC>
@@ -817,18 +837,27 @@ struct DmaHalf {
     base = (const char*)(KC ? P + (long)r0 * ld : P + r0);
     kstride = KC ? 2 : ld * 2;
   }
+  template <bool ASM = false>
   __device__ __forceinline__ void half(int k0, char* lds, int h, int wave) const {
-    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void*)(base + (long)k0 * kstride), (short)0,
-                                                                       0x7fffffff, 0x00020000);
+    if constexpr (ASM) {
 #pragma unroll
-    for (int t = 0; t < 2; ++t)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void_ptr)(lds + (16 * h + 2 * wave + t) * 1024), 16,
-                                               voff[h][t], 0, 0, 0);
+      for (int t = 0; t < 2; ++t) dma_asm(base + (long)k0 * kstride, lds + (16 * h + 2 * wave + t) * 1024, voff[h][t]);
+    } else {
+      const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void*)(base + (long)k0 * kstride), (short)0,
+                                                                         0x7fffffff, 0x00020000);
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void_ptr)(lds + (16 * h + 2 * wave + t) * 1024), 16,
+                                                 voff[h][t], 0, 0, 0);
+    }
   }
 };
 
 #ifndef CMHAR_GEMM8P_ABLATE
 #define CMHAR_GEMM8P_ABLATE 0
+#endif
+#ifndef CMHAR_GEMM8P_ASM_DMA
+#define CMHAR_GEMM8P_ASM_DMA 1
 #endif
 
 // The weight-gradient A operand (dYᵀ: [k][m], m contiguous) on the 8-phase schedule, staged in COLUMN halves: the
@@ -851,13 +880,19 @@ struct DmaHalfM {
     base = (const char*)(P + c0);
     kstride = ld * 2;
   }
+  template <bool ASM = false>
   __device__ __forceinline__ void half(int k0, char* lds, int h, int wave) const {
-    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void*)(base + (long)k0 * kstride), (short)0,
-                                                                       0x7fffffff, 0x00020000);
+    if constexpr (ASM) {
 #pragma unroll
-    for (int t = 0; t < 2; ++t)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void_ptr)(lds + h * 16384 + (2 * wave + t) * 1024), 16,
-                                               voff[h][t], 0, 0, 0);
+      for (int t = 0; t < 2; ++t) dma_asm(base + (long)k0 * kstride, lds + h * 16384 + (2 * wave + t) * 1024, voff[h][t]);
+    } else {
+      const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void*)(base + (long)k0 * kstride), (short)0,
+                                                                         0x7fffffff, 0x00020000);
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void_ptr)(lds + h * 16384 + (2 * wave + t) * 1024), 16,
+                                                 voff[h][t], 0, 0, 0);
+    }
   }
 };
 
@@ -891,6 +926,8 @@ __global__ __launch_bounds__(NT2, 2) void gemm8p_kernel(int M, int N, int K, con
                                                         long ldc, Epilogue e, int klen, long split_stride,
                                                         int raw_out) {
   static_assert(NA == 2 || NA == 3, "two or three A buffers");
+  // transposed-read instantiations issue their DMA by inline asm (see dma_asm)
+  constexpr bool kAD = CMHAR_GEMM8P_ASM_DMA && (!A_KC || !B_KC);
   __shared__ __attribute__((aligned(16))) char smem[NA == 3 ? 163840 : SMEM2];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -926,13 +963,13 @@ __global__ __launch_bounds__(NT2, 2) void gemm8p_kernel(int M, int N, int K, con
   bf16x8 af[2][4], b0[2][2], b1[2][2];
 
   // prologue: K-tile 0 whole + K-tile 1's A half 0 (NA = 3: K-tile 1's whole A); wait for tile 0
-  da.half(kbeg, abuf(0), 0, wave);
-  da.half(kbeg, abuf(0), 1, wave);
-  db.half(kbeg, bbuf(0), 0, wave);
-  db.half(kbeg, bbuf(0), 1, wave);
-  da.half(kbeg + TK2, abuf(1), 0, wave);
+  da.template half<kAD>(kbeg, abuf(0), 0, wave);
+  da.template half<kAD>(kbeg, abuf(0), 1, wave);
+  db.template half<kAD>(kbeg, bbuf(0), 0, wave);
+  db.template half<kAD>(kbeg, bbuf(0), 1, wave);
+  da.template half<kAD>(kbeg + TK2, abuf(1), 0, wave);
   if constexpr (NA == 3) {
-    da.half(kbeg + TK2, abuf(1), 1, wave);
+    da.template half<kAD>(kbeg + TK2, abuf(1), 1, wave);
     asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
   } else {
     asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
@@ -982,11 +1019,11 @@ __global__ __launch_bounds__(NT2, 2) void gemm8p_kernel(int M, int N, int K, con
     }
     if constexpr (NA == 3) {
       if (n1) {
-        db.half(k1, bbuf(t + 1), 0, wave);
-        db.half(k1, bbuf(t + 1), 1, wave);
+        db.template half<kAD>(k1, bbuf(t + 1), 0, wave);
+        db.template half<kAD>(k1, bbuf(t + 1), 1, wave);
       }
     } else {
-      if (n1) da.half(k1, abuf(t + 1), 1, wave);
+      if (n1) da.template half<kAD>(k1, abuf(t + 1), 1, wave);
     }
     END_LOADS();
     {
@@ -999,11 +1036,11 @@ __global__ __launch_bounds__(NT2, 2) void gemm8p_kernel(int M, int N, int K, con
 #pragma unroll
       for (int j = 0; j < 2; ++j) b1[kk][j] = frag256<B_KC>(bs, wc * 64 + 32 + j * 16, kk, lane);
     if constexpr (NA == 3) {
-      if (n2) da.half(k2, abuf(t + 2), 1, wave);
+      if (n2) da.template half<kAD>(k2, abuf(t + 2), 1, wave);
     } else {
       if (n1) {
-        db.half(k1, bbuf(t + 1), 0, wave);
-        db.half(k1, bbuf(t + 1), 1, wave);
+        db.template half<kAD>(k1, bbuf(t + 1), 0, wave);
+        db.template half<kAD>(k1, bbuf(t + 1), 1, wave);
       }
     }
     END_LOADS();
@@ -1025,14 +1062,14 @@ __global__ __launch_bounds__(NT2, 2) void gemm8p_kernel(int M, int N, int K, con
     // of t+2 first, then a wait that leaves t+2's four A pieces in flight
     if constexpr (NA == 3) {
       if (n2) {
-        da.half(k2, abuf(t + 2), 0, wave);
+        da.template half<kAD>(k2, abuf(t + 2), 0, wave);
         asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
       } else {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
     } else {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      if (n2) da.half(k2, abuf(t + 2), 0, wave);
+      if (n2) da.template half<kAD>(k2, abuf(t + 2), 0, wave);
     }
     END_LOADS();
     {
@@ -1215,7 +1252,7 @@ static bool use_8p_wgrad() {
 // layout separately; CMHAR_GEMM8P_NA / CMHAR_GEMM8P_WGRAD_NA = 2 / 3 override the build defaults (A/B measurements;
 // identical bits either way).
 #ifndef CMHAR_GEMM8P_NA_DEFAULT
-#define CMHAR_GEMM8P_NA_DEFAULT 3
+#define CMHAR_GEMM8P_NA_DEFAULT 2
 #endif
 #ifndef CMHAR_GEMM8P_WGRAD_NA_DEFAULT
 #define CMHAR_GEMM8P_WGRAD_NA_DEFAULT 2
