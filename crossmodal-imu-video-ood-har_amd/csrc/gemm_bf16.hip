@@ -434,6 +434,32 @@ __device__ __forceinline__ int mc_off512(int k, int chunk) { return k * 512 + ((
 
 typedef __attribute__((address_space(3))) void* lds_void_ptr;
 
+#ifndef CMHAR_GEMM8P_ASM_DMA
+#define CMHAR_GEMM8P_ASM_DMA 1
+#endif
+// One 1-KiB LDS-DMA piece (`buffer_load_dwordx4 … lds`, 16 B per lane) issued by inline asm: hipcc then does not see
+// an LDS write in flight, so it no longer puts `s_waitcnt vmcnt(0)` in front of every transposed LDS read
+// (ds_read_b64_tr_b16) that follows a DMA issue — in the 8-phase weight-gradient instantiation it did so at every
+// phase, draining the next K-tile's prefetch three times per K-tile (asm issue: weight gradients 14–19 % faster,
+// `gpurun_out/r04w_gemm_ab.log`).  Used by the instantiations with transposed reads (CMHAR_GEMM8P_ASM_DMA = 0: the
+// builtin everywhere).  The kernel orders every DMA itself (counted vmcnt +
+// barriers, as with the builtin).  src: the tile origin at this K-slice (wave-uniform); M0 is written here and no
+// compiler-generated code in these kernels uses M0 (no builtin DMA left in an ASM instantiation; checked in the .s).
+__device__ __forceinline__ void dma_asm(const char* src, char* lds, int voff) {
+  const unsigned long long a = (unsigned long long)src;
+  uint4_t rs;
+  rs[0] = __builtin_amdgcn_readfirstlane((unsigned)a);
+  rs[1] = __builtin_amdgcn_readfirstlane((unsigned)(a >> 32)) & 0xffffu;
+  rs[2] = 0x7fffffffu;
+  rs[3] = 0x00020000u;
+  const unsigned la = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(lds_void_ptr)lds);
+  // (s_nop: the SALU write of M0 needs one wait state before the LDS-DMA reads it — hipcc puts the same nop after
+  // its own M0 writes; inside inline asm its hazard recognizer cannot)
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds" :: "s"(la), "v"(voff), "s"(rs)
+               : "memory");
+}
+
+
 // LDS-DMA source of one operand (256 rows/cols x 64 k per tile) as a BUFFER load: the scalar resource holds the
 // tile's K-slice origin (advanced per K-tile with two SALU ops), the per-lane byte offsets of this wave's 4 pieces
 // (swizzle included) are computed once, so issuing a piece costs no VALU at all (`buffer_load_dwordx4 … lds`).
@@ -473,10 +499,16 @@ struct DmaSrc {
   __device__ __forceinline__ void piece(__amdgpu_buffer_rsrc_t r, char* lds, int wave, int t) const {
     __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void_ptr)(lds + (wave * 4 + t) * 1024), 16, voff[t], 0, 0, 0);
   }
+  template <bool ASM = false>
   __device__ __forceinline__ void tile(int k0, char* lds, int wave) const {
-    const __amdgpu_buffer_rsrc_t r = rsrc(k0);
+    if constexpr (ASM) {
 #pragma unroll
-    for (int t = 0; t < 4; ++t) piece(r, lds, wave, t);
+      for (int t = 0; t < 4; ++t) dma_asm(base + (long)k0 * kstride, lds + (wave * 4 + t) * 1024, voff[t]);
+    } else {
+      const __amdgpu_buffer_rsrc_t r = rsrc(k0);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) piece(r, lds, wave, t);
+    }
   }
   // Touch every 128-B line of the tile at k0 (256 lines, one per lane of 4 waves) with a 4-byte LDS-DMA into a junk
   // LDS slot: the lines are pulled into this XCD's L2 a tile ahead of the DMA that stages them, so that DMA hits L2.
@@ -521,6 +553,7 @@ __global__ __launch_bounds__(NT2, 2) void gemm256_kernel(int M, int N, int K, co
                                                          int raw_out, float* __restrict__ sk_ws, int n_dp,
                                                          int sk_klen) {
   constexpr bool PF = CMHAR_GEMM_L2PF && NA == 2 && MODE == 0;
+  constexpr bool kAD = CMHAR_GEMM8P_ASM_DMA && (!A_KC || !B_KC);   // see dma_asm
   __shared__ __attribute__((aligned(16))) char smem[NA == 3 ? 163840 : SMEM2 + (PF ? 2048 : 0)];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -602,9 +635,9 @@ __global__ __launch_bounds__(NT2, 2) void gemm256_kernel(int M, int N, int K, co
   db.init(B, ldb, bn, wave, lane);
   if (nk > 0) {
     if (MODE != 7) {
-      da.tile(kbeg, a_buf(0), wave);
-      db.tile(kbeg, b_buf(0), wave);
-      if (NA == 3 && nk > 1) da.tile(kbeg + TK2, a_buf(1), wave);
+      da.template tile<kAD>(kbeg, a_buf(0), wave);
+      db.template tile<kAD>(kbeg, b_buf(0), wave);
+      if (NA == 3 && nk > 1) da.template tile<kAD>(kbeg + TK2, a_buf(1), wave);
     }
     if (NA == 3 && nk > 1) asm volatile("s_waitcnt vmcnt(4)\n\ts_barrier" ::: "memory");   // tile 0 landed
     else __syncthreads();
@@ -625,11 +658,11 @@ __global__ __launch_bounds__(NT2, 2) void gemm256_kernel(int M, int N, int K, co
     const bool pf = PF && kt + 2 < nk;
     if (MODE != 7) {
       if (NA == 3) {
-        if (more) db.tile(kbeg + (kt + 1) * TK2, nxt_b, wave);
-        if (more2) da.tile(kbeg + (kt + 2) * TK2, a_buf(kt + 2), wave);
+        if (more) db.template tile<kAD>(kbeg + (kt + 1) * TK2, nxt_b, wave);
+        if (more2) da.template tile<kAD>(kbeg + (kt + 2) * TK2, a_buf(kt + 2), wave);
       } else if (more) {
-        da.tile(kbeg + (kt + 1) * TK2, nxt, wave);
-        db.tile(kbeg + (kt + 1) * TK2, nxt_b, wave);
+        da.template tile<kAD>(kbeg + (kt + 1) * TK2, nxt, wave);
+        db.template tile<kAD>(kbeg + (kt + 1) * TK2, nxt_b, wave);
         if (pf) {       // after the DMA pieces: the vmcnt(1) below leaves this one in flight
           if (wave < 4) da.l2_prefetch(kbeg + (kt + 2) * TK2, smem + SMEM2 + wave * 256);
           else db.l2_prefetch(kbeg + (kt + 2) * TK2, smem + SMEM2 + wave * 256);
@@ -791,26 +824,6 @@ __global__ __launch_bounds__(NT2, 2) void gemm256_kernel(int M, int N, int K, co
 // read and read >= 1 interval after the wait that retires it.  (Measured against gemm256_kernel in one process,
 // tools/debug/gemm_ab.py: forward 5-6 % faster at K = 768-1536; bit-identical — each output's k order is unchanged.)
 // ---------------------------------------------------------------------------------------------------------------
-// One 1-KiB LDS-DMA piece (`buffer_load_dwordx4 … lds`, 16 B per lane) issued by inline asm: hipcc then does not see
-// an LDS write in flight, so it no longer puts `s_waitcnt vmcnt(0)` in front of every transposed LDS read
-// (ds_read_b64_tr_b16) that follows a DMA issue — in the weight-gradient instantiation it did so at every phase,
-// draining the next K-tile's prefetch three times per K-tile.  The kernel orders every DMA itself (counted vmcnt +
-// barriers, as with the builtin).  src: the tile origin at this K-slice (wave-uniform); M0 is written here and no
-// compiler-generated code in these kernels uses M0 (no builtin DMA left in an ASM instantiation; checked in the .s).
-__device__ __forceinline__ void dma_asm(const char* src, char* lds, int voff) {
-  const unsigned long long a = (unsigned long long)src;
-  uint4_t rs;
-  rs[0] = __builtin_amdgcn_readfirstlane((unsigned)a);
-  rs[1] = __builtin_amdgcn_readfirstlane((unsigned)(a >> 32)) & 0xffffu;
-  rs[2] = 0x7fffffffu;
-  rs[3] = 0x00020000u;
-  const unsigned la = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(lds_void_ptr)lds);
-  // (s_nop: the SALU write of M0 needs one wait state before the LDS-DMA reads it — hipcc puts the same nop after
-  // its own M0 writes; inside inline asm its hazard recognizer cannot)
-  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds" :: "s"(la), "v"(voff), "s"(rs)
-               : "memory");
-}
-
 // Per-lane offsets of this wave's 2 pieces of each half of an operand tile.  K-contiguous [256 rows][64 k]: half h =
 // rows 128h..128h+127.  Row-contraction [64 k][256 cols] (the dgrad weight operand): half h = k rows 32h..32h+31.
 template <bool KC>
@@ -856,9 +869,7 @@ struct DmaHalf {
 #ifndef CMHAR_GEMM8P_ABLATE
 #define CMHAR_GEMM8P_ABLATE 0
 #endif
-#ifndef CMHAR_GEMM8P_ASM_DMA
-#define CMHAR_GEMM8P_ASM_DMA 1
-#endif
+
 
 // The weight-gradient A operand (dYᵀ: [k][m], m contiguous) on the 8-phase schedule, staged in COLUMN halves: the
 // schedule hands A's half h (rows 128h.. of the output tile) to wave group h only, so each half is its own
