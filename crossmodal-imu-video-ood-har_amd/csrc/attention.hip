@@ -40,15 +40,7 @@ typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2_t;
 // The same [64][64] tile image written by LDS-DMA (buffer_load_dwordx4 ... lds: global → LDS without a VGPR round
 // trip, no ds_write): each wave issues 2 of the tile's 8 pieces of 1 KiB (8 rows × 128 B); the DMA's LDS destination
 // is lane-linear, so the att_off XOR swizzle is applied to each lane's SOURCE chunk (an involution).  Rows at or past
-// `rows_total` fall outside the buffer resource's num_records and read as zero.  Per-lane offsets are computed once.
-// CMHAR_ATTN_DMA_ASM (default): the pieces are issued by inline asm (the resource from the same builtin), so hipcc
-// sees no LDS write in flight and no longer puts `s_waitcnt vmcnt(0)` in front of the transposed LDS reads
-// (ds_read_b64_tr_b16) that follow a DMA issue — in all three flash kernels it did, draining the next tile's prefetch
-// in the middle of the current tile.  The kernels order every DMA themselves (vmcnt(0) + barrier per tile).  M0 is
-// written by the asm only (no builtin DMA is left in these kernels; checked in the .s).
-#ifndef CMHAR_ATTN_DMA_ASM
-#define CMHAR_ATTN_DMA_ASM 1
-#endif
+// `rows_total` fall outside the buffer resource's num_records and read as zero.  Per-lane offsets are computed once; a tile costs two scalar resource updates and 2 DMA instructions.
 struct TileDma {
   const char* base;   // row 0 of the head slice
   long row_bytes;     // ld * 2
@@ -67,25 +59,12 @@ struct TileDma {
   }
   __device__ __forceinline__ void tile(int r0, char* lds, int wave) const {
     const long off = (long)r0 * row_bytes;
-    if (CMHAR_ATTN_DMA_ASM) {
-      const long left = valid - off;
-      const int nrec = (int)(left > 0 ? (left < 0x7fffffff ? left : 0x7fffffff) : 0);
-      const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void*)(base + off), (short)0, nrec, 0x00020000);
+    const long left = valid - off;
+    const int nrec = (int)(left > 0 ? (left < 0x7fffffff ? left : 0x7fffffff) : 0);
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)(base + off), (short)0, nrec, 0x00020000);
 #pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        const unsigned la = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(att_lds_ptr)(lds + (2 * wave + t) * 1024));
-        // (s_nop: one wait state between the SALU write of M0 and the LDS-DMA reading it)
-        asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds"
-                     :: "s"(la), "v"(voff[t]), "s"(r));
-      }
-    } else {
-      const long left = valid - off;
-      const int nrec = (int)(left > 0 ? (left < 0x7fffffff ? left : 0x7fffffff) : 0);
-      const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void*)(base + off), (short)0, nrec, 0x00020000);
-#pragma unroll
-      for (int t = 0; t < 2; ++t)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (att_lds_ptr)(lds + (2 * wave + t) * 1024), 16, voff[t], 0, 0, 0);
-    }
+    for (int t = 0; t < 2; ++t)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (att_lds_ptr)(lds + (2 * wave + t) * 1024), 16, voff[t], 0, 0, 0);
   }
 };
 
@@ -246,7 +225,6 @@ __global__ __launch_bounds__(256, 3) void attn_fwd_bf16(int H, int Lq, int Lk, i
 #pragma unroll
           for (int ss = 0; ss < 2; ++ss) pb[j][ss] = pack8<E>(s[j], ss);
         }
-        if (CMHAR_ATTN_DMA_ASM) __builtin_amdgcn_sched_barrier(0);   // the transposed reads stay here (see TileDma)
 #pragma unroll
         for (int ss = 0; ss < 2; ++ss)
 #pragma unroll
@@ -398,7 +376,6 @@ __global__ __launch_bounds__(256, 3) void attn_bwd_dkdv_bf16(int H, int Lq, int 
         dbv[r >> 3][r & 7] = dd[0];
         dbv[r >> 3][(r & 7) + 1] = dd[1];
       }
-      if (CMHAR_ATTN_DMA_ASM) __builtin_amdgcn_sched_barrier(0);   // the transposed reads stay here (see TileDma)
 #pragma unroll
       for (int ss = 0; ss < 2; ++ss) {
         const bf16x8 pb = pbv[ss], db = dbv[ss];
@@ -549,7 +526,6 @@ __global__ __launch_bounds__(256, QB == 1 ? 3 : 2) void attn_bwd_dq_bf16(int H, 
           db[j][r >> 3][(r & 7) + 1] = dd[1];
         }
       }
-      if (CMHAR_ATTN_DMA_ASM) __builtin_amdgcn_sched_barrier(0);   // the transposed reads stay here (see TileDma)
 #pragma unroll
       for (int ss = 0; ss < 2; ++ss)
 #pragma unroll
