@@ -639,8 +639,10 @@ __global__ __launch_bounds__(NT2, 2) void gemm256_kernel(int M, int N, int K, co
       db.template tile<kAD>(kbeg, b_buf(0), wave);
       if (NA == 3 && nk > 1) da.template tile<kAD>(kbeg + TK2, a_buf(1), wave);
     }
-    if (NA == 3 && nk > 1) asm volatile("s_waitcnt vmcnt(4)\n\ts_barrier" ::: "memory");   // tile 0 landed
-    else __syncthreads();
+    // tile 0 landed (own pieces) before the barrier — explicitly: with the asm-issued DMA (kAD) hipcc no longer adds
+    // the vmcnt(0) it used to put in front of the first transposed read
+    if (NA == 3 && nk > 1) asm volatile("s_waitcnt vmcnt(4)\n\ts_barrier" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
     load_k0(a_buf(0), b_buf(0), 0, 8, true);
 #pragma unroll
     for (int j = 0; j < 4; ++j) bf1[j] = frag256<B_KC>(b_buf(0), wc * 64 + j * 16, 1, lane);
