@@ -113,6 +113,7 @@ _SIGS = {
     'cmhar_bn_cl_ws': (i64, [i64, i32]),
     'cmhar_bn_cl_fwd': (i32, [i32, i64, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, i32, f32, f32, i32, vp, vp, vp]),
     'cmhar_bn_cl_bwd': (i32, [i32, i64, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, vp, vp]),
+    'cmhar_bn_cl_bwd_nores': (i32, [i32, i64, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, vp, vp]),
     'cmhar_avgpool_cl': (i32, [i32, i32, i64, i32, vp, vp, vp]),
     'cmhar_avgpool_cl_bwd': (i32, [i32, i32, i64, i32, vp, vp, vp]),
     'cmhar_video_to_ndhwc': (i32, [i32, i32, i32, i32, i32, i32, vp, vp, vp]),

@@ -23,7 +23,7 @@ import torch.nn as nn
 from . import _lib as L
 from . import kernels as K
 from ._lib import call, ptr
-from .r3d import _bn_fwd, _dgrad_igemm_ok, _grad_acc, _grad_dest, _pack, _stem_ok, _unit_bwd, _unit_fwd
+from .r3d import _bn_bwd, _bn_fwd, _dgrad_igemm_ok, _grad_acc, _grad_dest, _pack, _stem_ok, _unit_bwd, _unit_fwd
 
 RELU, RELU6 = 1, 2
 
@@ -140,7 +140,7 @@ class MobileNetV2Features(L.NoReplicate, nn.Sequential):
 # units: dense conv (+BN, act, residual) via r3d's unit, depthwise conv (+BN, act), max pool
 # ---------------------------------------------------------------------------------------------------------------
 class _DwUnit:
-    __slots__ = ('conv', 'bn', 'relu', 'shape', 'oshape', 'x', 'z', 'y', 'sm', 'sr')
+    __slots__ = ('conv', 'bn', 'relu', 'shape', 'oshape', 'x', 'z', 'y', 'sm', 'sr', 'res')
 
 
 def _geom(shape, conv):
@@ -164,6 +164,7 @@ def _dw_fwd(x, shape, conv, bn, relu, training, save):
         u = _DwUnit()
         u.conv, u.bn, u.relu, u.shape, u.oshape, u.x, u.z, u.y, u.sm, u.sr = conv, bn, relu, shape, oshape, x, z, y, \
             sm, sr
+        u.res = False
     return y, oshape, u
 
 
@@ -174,10 +175,7 @@ def _dw_bwd(u, dy, grads, training):
     dz = torch.empty(M, C, dtype=dt, device=dev)
     dw_bn, acc_w = _grad_dest(grads, u.bn.weight, dev)
     db_bn, acc_b = _grad_dest(grads, u.bn.bias, dev)
-    ws = K.workspace(L.lib().cmhar_bn_cl_ws(M, C), dev)
-    call('cmhar_bn_cl_bwd', L.dtype_code(dt), M, C, ptr(u.z), ptr(u.y), ptr(dy), ptr(u.bn.weight), ptr(u.sm),
-         ptr(u.sr), ptr(dz), None, ptr(dw_bn), ptr(db_bn), int(training or not u.bn.track_running_stats), u.relu,
-         ptr(ws), L.stream(dev))
+    _bn_bwd(u, dy, dz, None, dw_bn, db_bn, training)
     _grad_acc(dw_bn, acc_w)
     _grad_acc(db_bn, acc_b)
     N, H, W, C_, k, s, p, _, _ = _geom(u.shape, u.conv)

@@ -206,7 +206,7 @@ def _bn_fwd_tiles(z, bn, res, relu, tstats, ntile):
 class _Unit:
     """Forward state of one conv+BN unit (input, pre-BN output, BN output, batch statistics)."""
     __slots__ = ('conv', 'bn', 'relu', 'shape', 'oshape', 'x', 'z', 'y', 'sm', 'sr', 'Kp', 'rows', 'wp', 'col',
-                 'igemm', 'wf', 'stem')
+                 'igemm', 'wf', 'stem', 'res')
 
 
 def _pointwise(conv, shape, Kp, M, rows):
@@ -265,6 +265,7 @@ def _unit_fwd(x, shape, conv, bn, relu, training, save, res=None, wp=None, keep_
         u.igemm = igemm
         u.wf = wf
         u.stem = stem
+        u.res = res is not None
     return y, oshape, u
 
 
@@ -342,6 +343,23 @@ def unit_param_order(m: 'R3D18'):
     return order
 
 
+def _bn_bwd(u, dy, dz, dres, dw_bn, db_bn, training):
+    """BatchNorm(+residual)+activation backward of a unit into dz (and dres).  Without a residual input the
+    activation mask is recomputed from z in the forward's arithmetic (`cmhar_bn_cl_bwd_nores`: y not re-read)."""
+    M, Cc = u.z.shape
+    dt = u.z.dtype
+    ws = K.workspace(L.lib().cmhar_bn_cl_ws(M, Cc), dy.device)
+    use_batch = int(training or not u.bn.track_running_stats)
+    if u.relu and not u.res and dres is None:
+        call('cmhar_bn_cl_bwd_nores', L.dtype_code(dt), M, Cc, ptr(u.z), ptr(dy), ptr(u.bn.weight), ptr(u.bn.bias),
+             ptr(u.sm), ptr(u.sr), ptr(dz), ptr(dw_bn), ptr(db_bn), use_batch, int(u.relu), ptr(ws),
+             L.stream(dy.device))
+    else:
+        call('cmhar_bn_cl_bwd', L.dtype_code(dt), M, Cc, ptr(u.z), ptr(u.y), ptr(dy), ptr(u.bn.weight), ptr(u.sm),
+             ptr(u.sr), ptr(dz), ptr(dres), ptr(dw_bn), ptr(db_bn), use_batch, int(u.relu), ptr(ws),
+             L.stream(dy.device))
+
+
 def _unit_bwd(u, dy, grads, training, need_dx, want_dres, dx_acc=None):
     """Returns (dx or None, dres or None); dx accumulates into dx_acc when given."""
     M, Cc = u.z.shape
@@ -352,10 +370,7 @@ def _unit_bwd(u, dy, grads, training, need_dx, want_dres, dx_acc=None):
     dres = torch.empty(M, Cc, dtype=dt, device=dy.device) if want_dres else None
     dw_bn, acc_w = _grad_dest(grads, u.bn.weight, dy.device)
     db_bn, acc_b = _grad_dest(grads, u.bn.bias, dy.device)
-    ws = K.workspace(L.lib().cmhar_bn_cl_ws(M, Cc), dy.device)
-    call('cmhar_bn_cl_bwd', L.dtype_code(dt), M, Cc, ptr(u.z), ptr(u.y), ptr(dy), ptr(u.bn.weight), ptr(u.sm),
-         ptr(u.sr), ptr(dz), ptr(dres), ptr(dw_bn), ptr(db_bn), int(training or not u.bn.track_running_stats), int(u.relu), ptr(ws),
-         L.stream(dy.device))
+    _bn_bwd(u, dy, dz, dres, dw_bn, db_bn, training)
     _grad_acc(dw_bn, acc_w)
     _grad_acc(db_bn, acc_b)
     w = u.conv.weight

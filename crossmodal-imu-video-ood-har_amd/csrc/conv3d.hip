@@ -172,11 +172,23 @@ __global__ __launch_bounds__(256) void col2im3d_kernel(Geom g, const T* __restri
 // vector), TPR = C/8 threads cover a row and the block's RPI = 256/TPR row slots are combined in a fixed order.
 // mode 0: Σx; mode 1: Σ(x−mean)²; mode 2: Σg, Σg·x̂ with g = dy·act'(y) (relu 1: [y > 0]; relu 2 = ReLU6:
 // [0 < y < 6]).  part: [2][nchunk][C].  C/8 need not divide 256: the 256 % TPR spare threads only add zeros.
+// relu | BN_ZMASK: the unit had no residual input, so y = act(x̂·w + b) is recomputed from x in bn_cl_apply's exact
+// arithmetic and rounding (bit-identical mask) instead of read: one M×C tensor less per pass.
+constexpr int BN_ZMASK = 4;
+template <typename T>
+__device__ __forceinline__ float bn_round(float v) { return (float)(T)v; }
+template <typename T>
+__device__ __forceinline__ bool bn_act_zero(float x, float mu, float rs, float w, float b, int relu) {
+  const float lo = (relu & 3) ? 0.f : -INFINITY, hi = (relu & 3) == 2 ? 6.f : INFINITY;
+  const float t = bn_round<T>(fminf(fmaxf(fmaf((x - mu) * rs, w, b), lo), hi));
+  return !(t > lo && t < hi);
+}
 template <typename T>
 __global__ __launch_bounds__(256) void bn_cl_partial(int mode, int M, int C, int rows_per_chunk,
                                                      const T* __restrict__ x, const T* __restrict__ y,
                                                      const T* __restrict__ dy, const float* __restrict__ mean,
-                                                     const float* __restrict__ rstd, int relu,
+                                                     const float* __restrict__ rstd, const float* __restrict__ w,
+                                                     const float* __restrict__ b, int relu,
                                                      float* __restrict__ part) {
   __shared__ float s0[256][9], s1[256][9];
   const int tid = threadIdx.x;
@@ -185,11 +197,14 @@ __global__ __launch_bounds__(256) void bn_cl_partial(int mode, int M, int C, int
   const int r0 = blockIdx.x * rows_per_chunk;
   const int r1 = min(r0 + rows_per_chunk, M);
   const int rs0 = slot < RPI ? r0 + slot : r1;
-  float mu[8], rs[8], a0[8], a1[8];
+  const bool zm = mode == 2 && (relu & BN_ZMASK), ry = mode == 2 && relu && !zm;
+  float mu[8], rs[8], a0[8], a1[8], ww[8], bb[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     mu[j] = mode ? mean[c0 + j] : 0.f;
     rs[j] = mode == 2 ? rstd[c0 + j] : 0.f;
+    ww[j] = zm ? w[c0 + j] : 0.f;
+    bb[j] = zm ? b[c0 + j] : 0.f;
     a0[j] = a1[j] = 0.f;
   }
   auto accum = [&](const float* v, const float* gv, const float* yv) {
@@ -201,7 +216,9 @@ __global__ __launch_bounds__(256) void bn_cl_partial(int mode, int M, int C, int
         const float d = v[j] - mu[j];
         a0[j] = fmaf(d, d, a0[j]);
       } else {
-        const float gj = (relu && yv[j] <= 0.f) || (relu == 2 && yv[j] >= 6.f) ? 0.f : gv[j];
+        const bool off = zm ? bn_act_zero<T>(v[j], mu[j], rs[j], ww[j], bb[j], relu)
+                            : (relu && yv[j] <= 0.f) || (relu == 2 && yv[j] >= 6.f);
+        const float gj = off ? 0.f : gv[j];
         a0[j] += gj;
         a1[j] = fmaf(gj, (v[j] - mu[j]) * rs[j], a1[j]);
       }
@@ -219,7 +236,7 @@ __global__ __launch_bounds__(256) void bn_cl_partial(int mode, int M, int C, int
       Vec8<T>::load(x + off, v[u]);
       if (mode == 2) {
         Vec8<T>::load(dy + off, gv[u]);
-        if (relu) Vec8<T>::load(y + off, yv[u]);
+        if (ry) Vec8<T>::load(y + off, yv[u]);
       }
     }
 #pragma unroll
@@ -231,7 +248,7 @@ __global__ __launch_bounds__(256) void bn_cl_partial(int mode, int M, int C, int
     Vec8<T>::load(x + off, v);
     if (mode == 2) {
       Vec8<T>::load(dy + off, gv);
-      if (relu) Vec8<T>::load(y + off, yv);
+      if (ry) Vec8<T>::load(y + off, yv);
     }
     accum(v, gv, yv);
   }
@@ -403,26 +420,34 @@ __global__ void bn_cl_eval_stats(int C, const float* __restrict__ rmean, const f
   if (c < C) { mean[c] = rmean[c]; rstd[c] = rsqrtf(rvar[c] + eps); }
 }
 
-// y = act((x − mean)·rstd·w + b + res), act = identity / ReLU (relu 1) / ReLU6 (relu 2), 8 channels per thread
-template <typename T>
+// y = act((x − mean)·rstd·w + b + res), act = identity / ReLU (relu 1) / ReLU6 (relu 2), 8 channels per thread.
+// HOIST (C/8 divides 256, so a thread's channels never change along the grid-stride loop): the per-channel
+// constants are loaded once per thread instead of once per vector (8 of the 10 loads of an iteration).
+template <typename T, bool HOIST>
 __global__ __launch_bounds__(256) void bn_cl_apply(unsigned nvec, int C, const T* __restrict__ x,
                                                    const T* __restrict__ res, const float* __restrict__ mean,
                                                    const float* __restrict__ rstd, const float* __restrict__ w,
                                                    const float* __restrict__ b, int relu, T* __restrict__ y) {
   const unsigned cv = C / 8;
-  for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < nvec; i += gridDim.x * blockDim.x) {
+  float mu[8], rs[8], ww[8], bb[8];
+  // per-channel constants as explicit 16-B loads (c0 % 8 == 0; the per-element form lost its vectorisation
+  // once the activation became a two-way choice: 34 vs 10 loads per 8 channels, 4x slower)
+  auto consts = [&](unsigned i) {
     const int c0 = (int)(i % cv) * 8;
-    const long off = (long)i * 8;
-    float v[8], rv[8], mu[8], rs[8], ww[8], bb[8];
-    Vec8<T>::load(x + off, v);
-    if (res) Vec8<T>::load(res + off, rv);
-    // per-channel constants as explicit 16-B loads (c0 % 8 == 0; the per-element form lost its vectorisation
-    // once the activation became a two-way choice: 34 vs 10 loads per 8 channels, 4x slower)
     Vec8<float>::load(mean + c0, mu);
     Vec8<float>::load(rstd + c0, rs);
     Vec8<float>::load(w + c0, ww);
     Vec8<float>::load(b + c0, bb);
-    const float lo = relu ? 0.f : -INFINITY, hi = relu == 2 ? 6.f : INFINITY;
+  };
+  const unsigned i0 = blockIdx.x * blockDim.x + threadIdx.x;
+  if (HOIST) consts(i0);
+  const float lo = relu ? 0.f : -INFINITY, hi = relu == 2 ? 6.f : INFINITY;
+  for (unsigned i = i0; i < nvec; i += gridDim.x * blockDim.x) {
+    const long off = (long)i * 8;
+    float v[8], rv[8];
+    Vec8<T>::load(x + off, v);
+    if (res) Vec8<T>::load(res + off, rv);
+    if (!HOIST) consts(i);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       v[j] = fmaf((v[j] - mu[j]) * rs[j], ww[j], bb[j]);
@@ -433,35 +458,46 @@ __global__ __launch_bounds__(256) void bn_cl_apply(unsigned nvec, int C, const T
   }
 }
 
-// g = dy·[y > 0];  dres = g (optional);  dx = w·rstd·(g − Σg/M − x̂·Σgx̂/M) (training) or w·rstd·g (eval).
-template <typename T>
+// g = dy·act'(y);  dres = g (optional);  dx = w·rstd·(g − Σg/M − x̂·Σgx̂/M) (training) or w·rstd·g (eval).
+// relu | BN_ZMASK: act'(y) recomputed from x (no residual; see bn_cl_partial), y not read.  HOIST: as bn_cl_apply.
+template <typename T, bool HOIST>
 __global__ __launch_bounds__(256) void bn_cl_bwd_apply(unsigned nvec, int M, int C, const T* __restrict__ x,
                                                        const T* __restrict__ y, const T* __restrict__ dy,
                                                        const float* __restrict__ mean, const float* __restrict__ rstd,
-                                                       const float* __restrict__ w, const float* __restrict__ dw,
-                                                       const float* __restrict__ db, int training, int relu,
-                                                       T* __restrict__ dx, T* __restrict__ dres) {
+                                                       const float* __restrict__ w, const float* __restrict__ b,
+                                                       const float* __restrict__ dw, const float* __restrict__ db,
+                                                       int training, int relu, T* __restrict__ dx,
+                                                       T* __restrict__ dres) {
   const float inv = 1.f / (float)M;
   const unsigned cv = C / 8;
-  for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < nvec; i += gridDim.x * blockDim.x) {
+  const bool zm = relu & BN_ZMASK, ry = relu && !zm, needx = training || zm;
+  float rs[8], ww[8], mu[8], sw[8], sb[8], bb[8];
+  // per-channel constants as explicit 16-B loads (c0 % 8 == 0): per element they compiled to 40 scalar loads
+  auto consts = [&](unsigned i) {
     const int c0 = (int)(i % cv) * 8;
-    const long off = (long)i * 8;
-    float gv[8], yv[8], xv[8], out[8], rs[8], ww[8], mu[8], sw[8], sb[8];
-    Vec8<T>::load(dy + off, gv);
-    if (relu) Vec8<T>::load(y + off, yv);
-    if (training) Vec8<T>::load(x + off, xv);
-    // per-channel constants as explicit 16-B loads (c0 % 8 == 0): per element they compiled to 40 scalar loads
     Vec8<float>::load(rstd + c0, rs);
     Vec8<float>::load(w + c0, ww);
+    if (needx) Vec8<float>::load(mean + c0, mu);
     if (training) {
-      Vec8<float>::load(mean + c0, mu);
       Vec8<float>::load(dw + c0, sw);
       Vec8<float>::load(db + c0, sb);
     }
-    const float lo = relu ? 0.f : -INFINITY, hi = relu == 2 ? 6.f : INFINITY;
+    if (zm) Vec8<float>::load(b + c0, bb);
+  };
+  const unsigned i0 = blockIdx.x * blockDim.x + threadIdx.x;
+  if (HOIST) consts(i0);
+  const float lo = relu ? 0.f : -INFINITY, hi = (relu & 3) == 2 ? 6.f : INFINITY;
+  for (unsigned i = i0; i < nvec; i += gridDim.x * blockDim.x) {
+    const long off = (long)i * 8;
+    float gv[8], yv[8], xv[8], out[8];
+    Vec8<T>::load(dy + off, gv);
+    if (ry) Vec8<T>::load(y + off, yv);
+    if (needx) Vec8<T>::load(x + off, xv);
+    if (!HOIST) consts(i);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      if (relu && !(yv[j] > lo && yv[j] < hi)) gv[j] = 0.f;
+      if (zm ? bn_act_zero<T>(xv[j], mu[j], rs[j], ww[j], bb[j], relu) : ry && !(yv[j] > lo && yv[j] < hi))
+        gv[j] = 0.f;
       if (training) {
         const float xh = (xv[j] - mu[j]) * rs[j];
         out[j] = ww[j] * rs[j] * (gv[j] - sb[j] * inv - xh * sw[j] * inv);
@@ -1712,6 +1748,46 @@ extern "C" int cmhar_conv3d_col2im(int dtype, const int* dims, const void* dcol,
   return 0;
 }
 
+// A thread's 8 channels are fixed along the grid-stride loop when C/8 divides 256 (grid_for's blocks are 256 wide)
+inline bool bn_hoist(int C) { return 256 % (C / 8) == 0; }
+
+template <typename T>
+void bn_apply_launch(long M, int C, const void* x, const void* res, const float* smean, const float* srstd,
+                     const float* w, const float* b, int relu, void* y, hipStream_t stream) {
+  const unsigned nvec = (unsigned)(M * C / 8);
+  if (bn_hoist(C))
+    bn_cl_apply<T, true><<<grid_for(nvec), 256, 0, stream>>>(nvec, C, (const T*)x, (const T*)res, smean, srstd, w,
+                                                              b, relu, (T*)y);
+  else
+    bn_cl_apply<T, false><<<grid_for(nvec), 256, 0, stream>>>(nvec, C, (const T*)x, (const T*)res, smean, srstd, w,
+                                                               b, relu, (T*)y);
+}
+
+// BatchNorm backward: column partials (Σg, Σg·x̂), their combination into db / dw, then dx (and dres).
+// y == nullptr with relu != 0: no residual entered the unit, the activation mask is recomputed from x (BN_ZMASK).
+template <typename T>
+int bn_bwd_launch(long M, int C, const void* x, const void* y, const void* dy, const float* w, const float* b,
+                  const float* smean, const float* srstd, void* dx, void* dres, float* dw, float* db, int training,
+                  int relu, float* ws, hipStream_t stream) {
+  const int nch = bn_chunks(M, C);
+  const int rpc = (int)((M + nch - 1) / nch);
+  const int act = relu && !y ? relu | BN_ZMASK : relu;
+  bn_cl_partial<T><<<nch, 256, 0, stream>>>(2, (int)M, C, rpc, (const T*)x, (const T*)y, (const T*)dy, smean, srstd,
+                                             w, b, act, ws);
+  bn_cl_final<<<(C + BN_FC - 1) / BN_FC, 256, 0, stream>>>(2, M, C, nch, ws, nullptr, nullptr, nullptr, nullptr,
+                                                           nullptr, 0.f, 0.f, dw, db);
+  const unsigned nvec = (unsigned)(M * C / 8);
+  if (bn_hoist(C))
+    bn_cl_bwd_apply<T, true><<<grid_for(nvec), 256, 0, stream>>>(nvec, (int)M, C, (const T*)x, (const T*)y,
+                                                                  (const T*)dy, smean, srstd, w, b, dw, db, training,
+                                                                  act, (T*)dx, (T*)dres);
+  else
+    bn_cl_bwd_apply<T, false><<<grid_for(nvec), 256, 0, stream>>>(nvec, (int)M, C, (const T*)x, (const T*)y,
+                                                                   (const T*)dy, smean, srstd, w, b, dw, db, training,
+                                                                   act, (T*)dx, (T*)dres);
+  return 0;
+}
+
 extern "C" long cmhar_bn_cl_ws(long M, int C) { return 2L * bn_chunks(M, C) * C; }
 
 extern "C" int cmhar_bn_cl_fwd(int dtype, long M, int C, const void* x, const void* res, void* y, const float* w,
@@ -1727,10 +1803,10 @@ extern "C" int cmhar_bn_cl_fwd(int dtype, long M, int C, const void* x, const vo
     for (int mode = 0; mode < 2; ++mode) {
       if (dtype == CMHAR_BF16)
         bn_cl_partial<bf16><<<nch, 256, 0, stream>>>(mode, (int)M, C, rpc, (const bf16*)x, nullptr, nullptr, smean,
-                                                     nullptr, 0, ws);
+                                                     nullptr, nullptr, nullptr, 0, ws);
       else if (dtype == CMHAR_F32)
         bn_cl_partial<float><<<nch, 256, 0, stream>>>(mode, (int)M, C, rpc, (const float*)x, nullptr, nullptr, smean,
-                                                      nullptr, 0, ws);
+                                                      nullptr, nullptr, nullptr, 0, ws);
       else return -1;
       bn_cl_final<<<fgrid, 256, 0, stream>>>(mode, M, C, nch, ws, smean, srstd, rmean, rvar, num_batches_tracked,
                                              momentum, eps, nullptr, nullptr);
@@ -1739,13 +1815,8 @@ extern "C" int cmhar_bn_cl_fwd(int dtype, long M, int C, const void* x, const vo
     if (!rmean || !rvar) return -2;
     bn_cl_eval_stats<<<(C + 255) / 256, 256, 0, stream>>>(C, rmean, rvar, eps, smean, srstd);
   }
-  const unsigned nvec = (unsigned)(M * C / 8);
-  if (dtype == CMHAR_BF16)
-    bn_cl_apply<bf16><<<grid_for(nvec), 256, 0, stream>>>(nvec, C, (const bf16*)x, (const bf16*)res, smean, srstd,
-                                                           w, b, relu, (bf16*)y);
-  else
-    bn_cl_apply<float><<<grid_for(nvec), 256, 0, stream>>>(nvec, C, (const float*)x, (const float*)res, smean,
-                                                            srstd, w, b, relu, (float*)y);
+  if (dtype == CMHAR_BF16) bn_apply_launch<bf16>(M, C, x, res, smean, srstd, w, b, relu, y, stream);
+  else bn_apply_launch<float>(M, C, x, res, smean, srstd, w, b, relu, y, stream);
   CMHAR_CHECK_LAUNCH();
   return 0;
 }
@@ -1763,9 +1834,7 @@ extern "C" int cmhar_bn_cl_fwd_tiles(long M, int C, int ntile, float* tile_stats
   bn_tile_group<<<cdiv((long)ngroup * C, 256), 256, 0, stream>>>(C, ntile, tile_stats, cnt, groups, gcnt);
   bn_tile_final<<<(C + 15) / 16, 256, 0, stream>>>(M, C, ngroup, groups, gcnt, smean, srstd, rmean, rvar,
                                                    num_batches_tracked, momentum, eps);
-  const unsigned nvec = (unsigned)(M * C / 8);
-  bn_cl_apply<bf16><<<grid_for(nvec), 256, 0, stream>>>(nvec, C, (const bf16*)x, (const bf16*)res, smean, srstd, w,
-                                                        b, relu, (bf16*)y);
+  bn_apply_launch<bf16>(M, C, x, res, smean, srstd, w, b, relu, y, stream);
   CMHAR_CHECK_LAUNCH();
   return 0;
 }
@@ -1773,28 +1842,27 @@ extern "C" int cmhar_bn_cl_fwd_tiles(long M, int C, int ntile, float* tile_stats
 extern "C" int cmhar_bn_cl_bwd(int dtype, long M, int C, const void* x, const void* y, const void* dy,
                                const float* w, const float* smean, const float* srstd, void* dx, void* dres,
                                float* dw, float* db, int training, int relu, float* ws, hipStream_t stream) {
-  if (M <= 0 || !bn_channels_ok(C) || !ws || !dw || !db) return -1;
+  if (M <= 0 || !bn_channels_ok(C) || !ws || !dw || !db || (relu && !y)) return -1;
   if (M >= (1L << 31) || M * C / 8 >= (1L << 31)) return -2;   // unsigned grid-stride loops never wrap
-  const int nch = bn_chunks(M, C);
-  const int rpc = (int)((M + nch - 1) / nch);
   if (dtype == CMHAR_BF16)
-    bn_cl_partial<bf16><<<nch, 256, 0, stream>>>(2, (int)M, C, rpc, (const bf16*)x, (const bf16*)y, (const bf16*)dy,
-                                                 smean, srstd, relu, ws);
+    bn_bwd_launch<bf16>(M, C, x, y, dy, w, nullptr, smean, srstd, dx, dres, dw, db, training, relu, ws, stream);
   else if (dtype == CMHAR_F32)
-    bn_cl_partial<float><<<nch, 256, 0, stream>>>(2, (int)M, C, rpc, (const float*)x, (const float*)y, (const float*)dy,
-                                                  smean, srstd, relu, ws);
+    bn_bwd_launch<float>(M, C, x, y, dy, w, nullptr, smean, srstd, dx, dres, dw, db, training, relu, ws, stream);
   else return -1;
-  bn_cl_final<<<(C + BN_FC - 1) / BN_FC, 256, 0, stream>>>(2, M, C, nch, ws, nullptr, nullptr, nullptr, nullptr, nullptr, 0.f,
-                                                 0.f, dw, db);
-  const unsigned nvec = (unsigned)(M * C / 8);
+  CMHAR_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int cmhar_bn_cl_bwd_nores(int dtype, long M, int C, const void* x, const void* dy, const float* w,
+                                     const float* b, const float* smean, const float* srstd, void* dx, float* dw,
+                                     float* db, int training, int relu, float* ws, hipStream_t stream) {
+  if (M <= 0 || !bn_channels_ok(C) || !ws || !dw || !db || relu < 0 || relu > 2 || (relu && !b)) return -1;
+  if (M >= (1L << 31) || M * C / 8 >= (1L << 31)) return -2;   // unsigned grid-stride loops never wrap
   if (dtype == CMHAR_BF16)
-    bn_cl_bwd_apply<bf16><<<grid_for(nvec), 256, 0, stream>>>(nvec, (int)M, C, (const bf16*)x, (const bf16*)y,
-                                                               (const bf16*)dy, smean, srstd, w, dw, db, training,
-                                                               relu, (bf16*)dx, (bf16*)dres);
-  else
-    bn_cl_bwd_apply<float><<<grid_for(nvec), 256, 0, stream>>>(nvec, (int)M, C, (const float*)x, (const float*)y,
-                                                                (const float*)dy, smean, srstd, w, dw, db, training,
-                                                                relu, (float*)dx, (float*)dres);
+    bn_bwd_launch<bf16>(M, C, x, nullptr, dy, w, b, smean, srstd, dx, nullptr, dw, db, training, relu, ws, stream);
+  else if (dtype == CMHAR_F32)
+    bn_bwd_launch<float>(M, C, x, nullptr, dy, w, b, smean, srstd, dx, nullptr, dw, db, training, relu, ws, stream);
+  else return -1;
   CMHAR_CHECK_LAUNCH();
   return 0;
 }

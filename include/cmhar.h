@@ -329,6 +329,11 @@ int cmhar_bn_cl_fwd(int dtype, long M, int C, const void* x, const void* res, vo
 int cmhar_bn_cl_bwd(int dtype, long M, int C, const void* x, const void* y, const void* dy, const float* w,
                     const float* smean, const float* srstd, void* dx, void* dres, float* dw, float* db, int training,
                     int relu, float* ws, hipStream_t stream);
+/* The same for a unit whose forward added no residual (y = act(bn(x))): act'(y) is recomputed from x with b in the
+ * forward's exact arithmetic and rounding (the same mask bit for bit), so y is not read; no dres. */
+int cmhar_bn_cl_bwd_nores(int dtype, long M, int C, const void* x, const void* dy, const float* w, const float* b,
+                          const float* smean, const float* srstd, void* dx, float* dw, float* db, int training,
+                          int relu, float* ws, hipStream_t stream);
 /* AdaptiveAvgPool3d(1): [N, S, C] → fp32 [N, C], and its backward (dx = dout / S broadcast). */
 int cmhar_avgpool_cl(int dtype, int N, long S, int C, const void* x, float* out, hipStream_t stream);
 int cmhar_avgpool_cl_bwd(int dtype, int N, long S, int C, const float* dout, void* dx, hipStream_t stream);

@@ -100,6 +100,49 @@ def test_bn_channels_last_fwd_bwd(C, relu, res):
         assert rel(dres, rr.grad) < 1e-6
 
 
+@pytest.mark.parametrize('dtype', [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize('C,relu', [(64, 1), (96, 2), (192, 1), (512, 1)])
+@pytest.mark.parametrize('training', [1, 0])
+def test_bn_bwd_nores_matches_y_mask(dtype, C, relu, training):
+    """cmhar_bn_cl_bwd_nores recomputes the activation mask from z in bn_cl_apply's arithmetic: dx / dw / db must
+    equal cmhar_bn_cl_bwd's (which reads the stored y) bit for bit.  C = 96 / 192: C/8 does not divide 256 (the
+    per-vector constant loads); 64 / 512 the hoisted ones.  z is offset so that many pre-activations sit near 0."""
+    from cmhar import _lib as L
+    from cmhar import kernels as K
+    from cmhar import r3d
+    torch.manual_seed(3)
+    M = 4099
+    z = (torch.randn(M, C) * 2 + 0.3).to(DEV).to(dtype)
+    bn = torch.nn.BatchNorm3d(C).to(DEV)
+    with torch.no_grad():
+        bn.weight.uniform_(0.5, 3.5)
+        bn.bias.uniform_(-0.5, 3.0)
+        bn.running_mean.uniform_(-0.2, 0.2)
+        bn.running_var.uniform_(0.5, 1.5)
+    y, sm, sr = r3d._bn_fwd(z, bn, None, relu, bool(training))
+    frac_off = float(((y.float() <= 0) | (y.float() >= 6)).float().mean()) if relu == 2 else float((y <= 0).float().mean())
+    assert 0.05 < frac_off < 0.95
+    dy = torch.randn(M, C, device=DEV).to(dtype)
+    ws = K.workspace(L.lib().cmhar_bn_cl_ws(M, C), z.device)
+    outs = []
+    for nores in (False, True):
+        dx = torch.empty_like(z)
+        dw = torch.empty(C, device=DEV)
+        db = torch.empty(C, device=DEV)
+        if nores:
+            L.call('cmhar_bn_cl_bwd_nores', L.dtype_code(dtype), M, C, z.data_ptr(), dy.data_ptr(),
+                   bn.weight.data_ptr(), bn.bias.data_ptr(), sm.data_ptr(), sr.data_ptr(), dx.data_ptr(),
+                   dw.data_ptr(), db.data_ptr(), training, relu, ws.data_ptr(), L.stream(z.device))
+        else:
+            L.call('cmhar_bn_cl_bwd', L.dtype_code(dtype), M, C, z.data_ptr(), y.data_ptr(), dy.data_ptr(),
+                   bn.weight.data_ptr(), sm.data_ptr(), sr.data_ptr(), dx.data_ptr(), None, dw.data_ptr(),
+                   db.data_ptr(), training, relu, ws.data_ptr(), L.stream(z.device))
+        torch.cuda.synchronize()
+        outs.append((dx, dw, db))
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+
+
 def _backbone_case(dtype, training=True, B=2, T=4, S=32, emulate=False):
     from cmhar.r3d import R3D18, run_r3d
     from oracle.r3d_cpu import BF16, r3d18_features
