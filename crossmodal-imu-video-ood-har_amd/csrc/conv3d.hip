@@ -183,7 +183,7 @@ __device__ __forceinline__ bool bn_act_zero(float x, float mu, float rs, float w
   const float t = bn_round<T>(fminf(fmaxf(fmaf((x - mu) * rs, w, b), lo), hi));
   return !(t > lo && t < hi);
 }
-template <typename T>
+template <typename T, bool ZM = false>
 __global__ __launch_bounds__(256) void bn_cl_partial(int mode, int M, int C, int rows_per_chunk,
                                                      const T* __restrict__ x, const T* __restrict__ y,
                                                      const T* __restrict__ dy, const float* __restrict__ mean,
@@ -197,7 +197,9 @@ __global__ __launch_bounds__(256) void bn_cl_partial(int mode, int M, int C, int
   const int r0 = blockIdx.x * rows_per_chunk;
   const int r1 = min(r0 + rows_per_chunk, M);
   const int rs0 = slot < RPI ? r0 + slot : r1;
-  const bool zm = mode == 2 && (relu & BN_ZMASK), ry = mode == 2 && relu && !zm;
+  // ZM: relu carries BN_ZMASK (a separate instantiation: the mask's w / b and the y loads never share registers —
+  // together they took the kernel past 128 VGPRs, 3 waves per SIMD for the 4 the chunk count assumes)
+  const bool zm = ZM && mode == 2, ry = !ZM && mode == 2 && relu;
   float mu[8], rs[8], a0[8], a1[8], ww[8], bb[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
@@ -265,7 +267,10 @@ __global__ __launch_bounds__(256) void bn_cl_partial(int mode, int M, int C, int
 
 // Combine the chunk partials (BN_FC columns per block, 256 / BN_FC chunk slots, fixed order) and finish the statistic.
 // mode 0: mean;  mode 1: rstd (+ running stats, num_batches_tracked);  mode 2: db = Σg, dw = Σg·x̂.
-constexpr int BN_FC = 8, BN_FS = 256 / BN_FC;
+// Each slot keeps BN_FU independent partial sums (BN_FU chunk loads in flight instead of one dependent chain; the
+// kernel is load-latency bound: ≤ 512 KiB of partials), combined in a fixed order.
+constexpr int BN_FC = 4, BN_FS = 256 / BN_FC, BN_FU = 4;
+static_assert(BN_FU == 4, "the fixed-order combine below adds four partial sums");
 __global__ __launch_bounds__(256) void bn_cl_final(int mode, long M, int C, int nchunk, const float* __restrict__ part,
                                                    float* __restrict__ mean, float* __restrict__ rstd,
                                                    float* __restrict__ rmean, float* __restrict__ rvar,
@@ -274,14 +279,23 @@ __global__ __launch_bounds__(256) void bn_cl_final(int mode, long M, int C, int 
   __shared__ float s0[256], s1[256];
   const int tid = threadIdx.x, cl = tid % BN_FC, slot = tid / BN_FC;
   const int c = blockIdx.x * BN_FC + cl;
-  float a0 = 0.f, a1 = 0.f;
-  if (c < C)
-    for (int k = slot; k < nchunk; k += BN_FS) {
-      a0 += part[(long)k * C + c];
-      if (mode == 2) a1 += part[((long)nchunk + k) * C + c];
+  float a0[BN_FU] = {}, a1[BN_FU] = {};
+  if (c < C) {
+    int k = slot;
+    for (; k + (BN_FU - 1) * BN_FS < nchunk; k += BN_FU * BN_FS) {
+#pragma unroll
+      for (int u = 0; u < BN_FU; ++u) {
+        a0[u] += part[(long)(k + u * BN_FS) * C + c];
+        if (mode == 2) a1[u] += part[((long)nchunk + k + u * BN_FS) * C + c];
+      }
     }
-  s0[tid] = a0;
-  s1[tid] = a1;
+    for (; k < nchunk; k += BN_FS) {
+      a0[0] += part[(long)k * C + c];
+      if (mode == 2) a1[0] += part[((long)nchunk + k) * C + c];
+    }
+  }
+  s0[tid] = (a0[0] + a0[1]) + (a0[2] + a0[3]);
+  s1[tid] = (a1[0] + a1[1]) + (a1[2] + a1[3]);
   __syncthreads();
   if (slot || c >= C) return;
   float b0 = 0.f, b1 = 0.f;
@@ -311,7 +325,8 @@ __global__ __launch_bounds__(256) void bn_cl_final(int mode, long M, int C, int 
 // running statistics as bn_cl_final.  Statistics buffer: [2][ntile][C] tile (mean, M2) | [2][ngroup][C] group
 // partials | [ntile] tile counts | [ngroup] group counts (ngroup = ⌈ntile / BN_TG⌉).
 // Level 1: one thread per (group of BN_TG tiles, channel) merges its tiles sequentially (Chan's update) into the
-// group's (mean, M2); channel 0's thread also writes the group's row count.
+// group's (mean, M2); channel 0's thread also writes the group's row count.  The group's loads are issued up front
+// (clamped tile index, count 0 past the end) so the sequential merge is not a chain of dependent load latencies.
 constexpr int BN_TG = 16;   // tiles per level-1 group: short sequential chains, enough threads (64 measured 35 us/call)
 __global__ __launch_bounds__(256) void bn_tile_group(int C, int ntile, const float* __restrict__ ts,
                                                      const float* __restrict__ cnt, float* __restrict__ out,
@@ -320,13 +335,22 @@ __global__ __launch_bounds__(256) void bn_tile_group(int C, int ntile, const flo
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= (long)ngroup * C) return;
   const int g = (int)(i / C), c = (int)(i % C);
+  float nv[BN_TG], mv[BN_TG], qv[BN_TG];
+#pragma unroll
+  for (int j = 0; j < BN_TG; ++j) {
+    const int t = min(g * BN_TG + j, ntile - 1);
+    nv[j] = g * BN_TG + j < ntile ? cnt[t] : 0.f;
+    mv[j] = ts[(long)t * C + c];
+    qv[j] = ts[((long)ntile + t) * C + c];
+  }
   float n = 0.f, mu = 0.f, m2 = 0.f;
-  for (int t = g * BN_TG; t < min(ntile, (g + 1) * BN_TG); ++t) {
-    const float nt = cnt[t], mt = ts[(long)t * C + c];
+#pragma unroll
+  for (int j = 0; j < BN_TG; ++j) {
+    const float nt = nv[j];
     if (nt <= 0.f) continue;
-    const float d = mt - mu, n2 = n + nt;
+    const float d = mv[j] - mu, n2 = n + nt;
     mu = fmaf(d, nt / n2, mu);
-    m2 += ts[((long)ntile + t) * C + c] + d * d * (n * nt / n2);
+    m2 += qv[j] + d * d * (n * nt / n2);
     n = n2;
   }
   out[(long)g * C + c] = mu;
@@ -334,40 +358,64 @@ __global__ __launch_bounds__(256) void bn_tile_group(int C, int ntile, const flo
   if (c == 0) gcnt[g] = n;
 }
 
-// Level 2 over the groups (their row counts in gcnt).
+// Level 2 over the groups (their row counts in gcnt): BN_GC channels per block, BN_GS group slots, each slot with
+// BN_FU independent partial sums (fixed-order combine).
+constexpr int BN_GC = 4, BN_GS = 256 / BN_GC;
 __global__ __launch_bounds__(256) void bn_tile_final(long M, int C, int ngroup, const float* __restrict__ ts,
                                                      const float* __restrict__ gcnt, float* __restrict__ mean,
                                                      float* __restrict__ rstd, float* __restrict__ rmean,
                                                      float* __restrict__ rvar, long long* __restrict__ nbt,
                                                      float momentum, float eps) {
   __shared__ float sh[256];
-  __shared__ float smu[16];
-  const int tid = threadIdx.x, cl = tid & 15, slot = tid >> 4;
-  const int c = blockIdx.x * 16 + cl;
-  float a = 0.f;
-  if (c < C)
-    for (int t = slot; t < ngroup; t += 16) a = fmaf(gcnt[t], ts[(long)t * C + c], a);
-  sh[tid] = a;
+  __shared__ float smu[BN_GC];
+  const int tid = threadIdx.x, cl = tid % BN_GC, slot = tid / BN_GC;
+  const int c = blockIdx.x * BN_GC + cl;
+  // pass 1: Σ n_g·mean_g;  pass 2: Σ M2_g + n_g·(mean_g − mean)²
+  auto sweep = [&](bool second, float mu) {
+    float a[BN_FU] = {};
+    if (c < C) {
+      int t = slot;
+      for (; t + (BN_FU - 1) * BN_GS < ngroup; t += BN_FU * BN_GS) {
+#pragma unroll
+        for (int u = 0; u < BN_FU; ++u) {
+          const int tt = t + u * BN_GS;
+          const float m = ts[(long)tt * C + c], n = gcnt[tt];
+          if (second) {
+            const float d = m - mu;
+            a[u] += ts[((long)ngroup + tt) * C + c] + n * d * d;
+          } else {
+            a[u] = fmaf(n, m, a[u]);
+          }
+        }
+      }
+      for (; t < ngroup; t += BN_GS) {
+        const float m = ts[(long)t * C + c], n = gcnt[t];
+        if (second) {
+          const float d = m - mu;
+          a[0] += ts[((long)ngroup + t) * C + c] + n * d * d;
+        } else {
+          a[0] = fmaf(n, m, a[0]);
+        }
+      }
+    }
+    return (a[0] + a[1]) + (a[2] + a[3]);
+  };
+  sh[tid] = sweep(false, 0.f);
   __syncthreads();
   if (slot == 0) {
     float b = 0.f;
-    for (int k = 0; k < 16; ++k) b += sh[k * 16 + cl];
+    for (int k = 0; k < BN_GS; ++k) b += sh[k * BN_GC + cl];
     smu[cl] = b / (float)M;
   }
   __syncthreads();
   const float mu = smu[cl];
-  float q = 0.f;
-  if (c < C)
-    for (int t = slot; t < ngroup; t += 16) {
-      const float d = ts[(long)t * C + c] - mu;
-      q += ts[((long)ngroup + t) * C + c] + gcnt[t] * d * d;
-    }
+  const float q = sweep(true, mu);
   __syncthreads();
   sh[tid] = q;
   __syncthreads();
   if (slot || c >= C) return;
   float m2 = 0.f;
-  for (int k = 0; k < 16; ++k) m2 += sh[k * 16 + cl];
+  for (int k = 0; k < BN_GS; ++k) m2 += sh[k * BN_GC + cl];
   const float var = m2 / (float)M;
   mean[c] = mu;
   rstd[c] = rsqrtf(var + eps);
@@ -1772,8 +1820,12 @@ int bn_bwd_launch(long M, int C, const void* x, const void* y, const void* dy, c
   const int nch = bn_chunks(M, C);
   const int rpc = (int)((M + nch - 1) / nch);
   const int act = relu && !y ? relu | BN_ZMASK : relu;
-  bn_cl_partial<T><<<nch, 256, 0, stream>>>(2, (int)M, C, rpc, (const T*)x, (const T*)y, (const T*)dy, smean, srstd,
-                                             w, b, act, ws);
+  if (act & BN_ZMASK)
+    bn_cl_partial<T, true><<<nch, 256, 0, stream>>>(2, (int)M, C, rpc, (const T*)x, (const T*)y, (const T*)dy, smean,
+                                                     srstd, w, b, act, ws);
+  else
+    bn_cl_partial<T, false><<<nch, 256, 0, stream>>>(2, (int)M, C, rpc, (const T*)x, (const T*)y, (const T*)dy,
+                                                      smean, srstd, w, b, act, ws);
   bn_cl_final<<<(C + BN_FC - 1) / BN_FC, 256, 0, stream>>>(2, M, C, nch, ws, nullptr, nullptr, nullptr, nullptr,
                                                            nullptr, 0.f, 0.f, dw, db);
   const unsigned nvec = (unsigned)(M * C / 8);
@@ -1832,7 +1884,7 @@ extern "C" int cmhar_bn_cl_fwd_tiles(long M, int C, int ntile, float* tile_stats
   const float* cnt = (float*)tile_stats + 2L * (ntile + ngroup) * C;
   float* gcnt = (float*)cnt + ntile;
   bn_tile_group<<<cdiv((long)ngroup * C, 256), 256, 0, stream>>>(C, ntile, tile_stats, cnt, groups, gcnt);
-  bn_tile_final<<<(C + 15) / 16, 256, 0, stream>>>(M, C, ngroup, groups, gcnt, smean, srstd, rmean, rvar,
+  bn_tile_final<<<(C + BN_GC - 1) / BN_GC, 256, 0, stream>>>(M, C, ngroup, groups, gcnt, smean, srstd, rmean, rvar,
                                                    num_batches_tracked, momentum, eps);
   bn_apply_launch<bf16>(M, C, x, res, smean, srstd, w, b, relu, y, stream);
   CMHAR_CHECK_LAUNCH();
