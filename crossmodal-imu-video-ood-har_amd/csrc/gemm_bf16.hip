@@ -385,8 +385,7 @@ __global__ void splitk_reduce_kernel(int M, int N, int splits, const float* __re
     if (e0 >= (long)M * N) return;
     const int m = (int)(e0 / N) + m_base, n0 = (int)(e0 % N);
     float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    for (int z = 0; z < splits; ++z) {
-      floatx4 a, b;
+    auto ld = [&](int z, floatx4& a, floatx4& b) {
       if (CMHAR_NT_REDUCE_LOAD) {   // the slabs are dead after this pass
         a = __builtin_nontemporal_load((const floatx4*)(P + z * split_stride + e0));
         b = __builtin_nontemporal_load((const floatx4*)(P + z * split_stride + e0 + 4));
@@ -394,8 +393,25 @@ __global__ void splitk_reduce_kernel(int M, int N, int splits, const float* __re
         a = *(const floatx4*)(P + z * split_stride + e0);
         b = *(const floatx4*)(P + z * split_stride + e0 + 4);
       }
+    };
+    auto add = [&](const floatx4& a, const floatx4& b) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) { s[j] += a[j]; s[4 + j] += b[j]; }
+    };
+    // four slabs' loads in flight before they are added in slab order (one pair per iteration left the reduce
+    // latency-bound); same order of additions, same bits
+    int z = 0;
+    for (; z + 3 < splits; z += 4) {
+      floatx4 a[4], b[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) ld(z + u, a[u], b[u]);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) add(a[u], b[u]);
+    }
+    for (; z < splits; ++z) {
+      floatx4 a, b;
+      ld(z, a, b);
+      add(a, b);
     }
     if (e.rowsum && idx < M) {                       // bias-gradient slabs follow the C slabs
       float r = 0.f;
