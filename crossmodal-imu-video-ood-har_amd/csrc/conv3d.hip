@@ -175,21 +175,24 @@ __global__ __launch_bounds__(256) void col2im3d_kernel(Geom g, const T* __restri
 // relu | BN_ZMASK: the unit had no residual input, so y = act(x̂·w + b) is recomputed from x in bn_cl_apply's exact
 // arithmetic and rounding (bit-identical mask) instead of read: one M×C tensor less per pass.
 constexpr int BN_ZMASK = 4;
+// act'(y) ≠ 0 for y = T(clamp(v, lo, hi)), v = fmaf((x − mean)·rstd, w, b) (bn_cl_apply's arithmetic), without the
+// round trip: for bf16 storage, T(v) of 0 < v < 2^-134 is +0 (round to nearest even) and ReLU6's T(v) reaches 6 from
+// v = 6 − 2^-6 on (the tie rounds to the even 6.0), ReLU's T(v) overflows to +inf from 0x1.fep127 on; fp32 storage
+// keeps v.  NaN: every comparison false → 0, as act(NaN) = clamp → 0 in the forward.
 template <typename T>
-__device__ __forceinline__ float bn_round(float v) { return (float)(T)v; }
-template <typename T>
-__device__ __forceinline__ bool bn_act_zero(float x, float mu, float rs, float w, float b, int relu) {
-  const float lo = (relu & 3) ? 0.f : -INFINITY, hi = (relu & 3) == 2 ? 6.f : INFINITY;
-  const float t = bn_round<T>(fminf(fmaxf(fmaf((x - mu) * rs, w, b), lo), hi));
-  return !(t > lo && t < hi);
+__device__ __forceinline__ bool bn_act_on(float v, int relu) {
+  constexpr bool B16 = sizeof(T) == 2;
+  const float lo = B16 ? 0x1p-134f : 0.f;
+  const float hi = (relu & 3) == 2 ? (B16 ? 5.984375f : 6.f) : (B16 ? 0x1.fep127f : INFINITY);
+  return v > lo && v < hi;
 }
-template <typename T, bool ZM = false>
-__global__ __launch_bounds__(256) void bn_cl_partial(int mode, int M, int C, int rows_per_chunk,
-                                                     const T* __restrict__ x, const T* __restrict__ y,
-                                                     const T* __restrict__ dy, const float* __restrict__ mean,
-                                                     const float* __restrict__ rstd, const float* __restrict__ w,
-                                                     const float* __restrict__ b, int relu,
-                                                     float* __restrict__ part) {
+template <typename T, int MODE, bool ZM = false>
+__global__ __launch_bounds__(256, sizeof(T) == 2 ? 4 : 3) void bn_cl_partial(int M, int C, int rows_per_chunk, const T* __restrict__ x,
+                                                     const T* __restrict__ y, const T* __restrict__ dy,
+                                                     const float* __restrict__ mean, const float* __restrict__ rstd,
+                                                     const float* __restrict__ w, const float* __restrict__ b,
+                                                     int relu, float* __restrict__ part) {
+  static_assert(MODE >= 0 && MODE <= 2 && (!ZM || MODE == 2), "modes 0 / 1 / 2; the z-mask in mode 2 only");
   __shared__ float s0[256][9], s1[256][9];
   const int tid = threadIdx.x;
   const int TPR = C / 8, RPI = 256 / TPR;
@@ -197,32 +200,33 @@ __global__ __launch_bounds__(256) void bn_cl_partial(int mode, int M, int C, int
   const int r0 = blockIdx.x * rows_per_chunk;
   const int r1 = min(r0 + rows_per_chunk, M);
   const int rs0 = slot < RPI ? r0 + slot : r1;
-  // ZM: relu carries BN_ZMASK (a separate instantiation: the mask's w / b and the y loads never share registers —
-  // together they took the kernel past 128 VGPRs, 3 waves per SIMD for the 4 the chunk count assumes)
-  const bool zm = ZM && mode == 2, ry = !ZM && mode == 2 && relu;
+  // ZM: a separate instantiation (the mask's w / b and the y loads never share registers); bf16: ≤ 128 VGPRs (launch
+  // bounds), 4 waves per SIMD, the 1024 chunks of bn_chunks in one round; MODE compile-time: one loop body
+  const bool ry = !ZM && MODE == 2 && relu;
   float mu[8], rs[8], a0[8], a1[8], ww[8], bb[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
-    mu[j] = mode ? mean[c0 + j] : 0.f;
-    rs[j] = mode == 2 ? rstd[c0 + j] : 0.f;
-    ww[j] = zm ? w[c0 + j] : 0.f;
-    bb[j] = zm ? b[c0 + j] : 0.f;
+    mu[j] = MODE ? mean[c0 + j] : 0.f;
+    rs[j] = MODE == 2 ? rstd[c0 + j] : 0.f;
+    ww[j] = ZM ? w[c0 + j] : 0.f;
+    bb[j] = ZM ? b[c0 + j] : 0.f;
     a0[j] = a1[j] = 0.f;
   }
   auto accum = [&](const float* v, const float* gv, const float* yv) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      if (mode == 0) {
+      if (MODE == 0) {
         a0[j] += v[j];
-      } else if (mode == 1) {
+      } else if (MODE == 1) {
         const float d = v[j] - mu[j];
         a0[j] = fmaf(d, d, a0[j]);
       } else {
-        const bool off = zm ? bn_act_zero<T>(v[j], mu[j], rs[j], ww[j], bb[j], relu)
+        const float xh = (v[j] - mu[j]) * rs[j];
+        const bool off = ZM ? !bn_act_on<T>(fmaf(xh, ww[j], bb[j]), relu)
                             : (relu && yv[j] <= 0.f) || (relu == 2 && yv[j] >= 6.f);
         const float gj = off ? 0.f : gv[j];
         a0[j] += gj;
-        a1[j] = fmaf(gj, (v[j] - mu[j]) * rs[j], a1[j]);
+        a1[j] = fmaf(gj, xh, a1[j]);
       }
     }
   };
@@ -236,7 +240,7 @@ __global__ __launch_bounds__(256) void bn_cl_partial(int mode, int M, int C, int
     for (int u = 0; u < UR; ++u) {
       const long off = (long)(r + u * RPI) * C + c0;
       Vec8<T>::load(x + off, v[u]);
-      if (mode == 2) {
+      if (MODE == 2) {
         Vec8<T>::load(dy + off, gv[u]);
         if (ry) Vec8<T>::load(y + off, yv[u]);
       }
@@ -248,7 +252,7 @@ __global__ __launch_bounds__(256) void bn_cl_partial(int mode, int M, int C, int
     const long off = (long)r * C + c0;
     float v[8], gv[8], yv[8];
     Vec8<T>::load(x + off, v);
-    if (mode == 2) {
+    if (MODE == 2) {
       Vec8<T>::load(dy + off, gv);
       if (ry) Vec8<T>::load(y + off, yv);
     }
@@ -261,7 +265,7 @@ __global__ __launch_bounds__(256) void bn_cl_partial(int mode, int M, int C, int
     float b0 = 0.f, b1 = 0.f;
     for (int sl = 0; sl < RPI; ++sl) { b0 += s0[sl * TPR + c / 8][c % 8]; b1 += s1[sl * TPR + c / 8][c % 8]; }
     part[(long)blockIdx.x * C + c] = b0;
-    if (mode == 2) part[((long)gridDim.x + blockIdx.x) * C + c] = b1;
+    if (MODE == 2) part[((long)gridDim.x + blockIdx.x) * C + c] = b1;
   }
 }
 
@@ -544,7 +548,7 @@ __global__ __launch_bounds__(256) void bn_cl_bwd_apply(unsigned nvec, int M, int
     if (!HOIST) consts(i);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      if (zm ? bn_act_zero<T>(xv[j], mu[j], rs[j], ww[j], bb[j], relu) : ry && !(yv[j] > lo && yv[j] < hi))
+      if (zm ? !bn_act_on<T>(fmaf((xv[j] - mu[j]) * rs[j], ww[j], bb[j]), relu) : ry && !(yv[j] > lo && yv[j] < hi))
         gv[j] = 0.f;
       if (training) {
         const float xh = (xv[j] - mu[j]) * rs[j];
@@ -1830,10 +1834,10 @@ int bn_bwd_launch(long M, int C, const void* x, const void* y, const void* dy, c
   const int rpc = (int)((M + nch - 1) / nch);
   const int act = relu && !y ? relu | BN_ZMASK : relu;
   if (act & BN_ZMASK)
-    bn_cl_partial<T, true><<<nch, 256, 0, stream>>>(2, (int)M, C, rpc, (const T*)x, (const T*)y, (const T*)dy, smean,
+    bn_cl_partial<T, 2, true><<<nch, 256, 0, stream>>>((int)M, C, rpc, (const T*)x, (const T*)y, (const T*)dy, smean,
                                                      srstd, w, b, act, ws);
   else
-    bn_cl_partial<T, false><<<nch, 256, 0, stream>>>(2, (int)M, C, rpc, (const T*)x, (const T*)y, (const T*)dy,
+    bn_cl_partial<T, 2, false><<<nch, 256, 0, stream>>>((int)M, C, rpc, (const T*)x, (const T*)y, (const T*)dy,
                                                       smean, srstd, w, b, act, ws);
   bn_cl_final<<<(C + BN_FC - 1) / BN_FC, 256, 0, stream>>>(2, M, C, nch, ws, nullptr, nullptr, nullptr, nullptr,
                                                            nullptr, 0.f, 0.f, dw, db);
@@ -1862,13 +1866,17 @@ extern "C" int cmhar_bn_cl_fwd(int dtype, long M, int C, const void* x, const vo
   const int fgrid = (C + BN_FC - 1) / BN_FC;
   if (training) {
     for (int mode = 0; mode < 2; ++mode) {
-      if (dtype == CMHAR_BF16)
-        bn_cl_partial<bf16><<<nch, 256, 0, stream>>>(mode, (int)M, C, rpc, (const bf16*)x, nullptr, nullptr, smean,
-                                                     nullptr, nullptr, nullptr, 0, ws);
-      else if (dtype == CMHAR_F32)
-        bn_cl_partial<float><<<nch, 256, 0, stream>>>(mode, (int)M, C, rpc, (const float*)x, nullptr, nullptr, smean,
-                                                      nullptr, nullptr, nullptr, 0, ws);
-      else return -1;
+#define BNP(T, MODE)                                                                                            \
+  bn_cl_partial<T, MODE><<<nch, 256, 0, stream>>>((int)M, C, rpc, (const T*)x, nullptr, nullptr, smean, nullptr,  \
+                                                  nullptr, nullptr, 0, ws)
+      if (dtype == CMHAR_BF16) {
+        if (mode == 0) BNP(bf16, 0);
+        else BNP(bf16, 1);
+      } else if (dtype == CMHAR_F32) {
+        if (mode == 0) BNP(float, 0);
+        else BNP(float, 1);
+      } else return -1;
+#undef BNP
       bn_cl_final<<<fgrid, 256, 0, stream>>>(mode, M, C, nch, ws, smean, srstd, rmean, rvar, num_batches_tracked,
                                              momentum, eps, nullptr, nullptr);
     }
