@@ -19,6 +19,10 @@ is over the gathered global batch (DataParallel semantics).  Rank 0 prints one J
             per GPU (global 64 on 8 GPUs), CE loss, bf16;
   ood_fp16  config 5: the OOD evaluation stream, fp16 inference: forward → SigLIP logits → energy score, one step =
             one batch of 32 clips from a ring of 8 distinct resident batches; default 313 steps = 10 016 clips.
+  imu       config 1 on the HIP path (the reference runs it on the CPU): IMU-only classifier (IMUEncoder + the
+            256-128 MLP head, models.py:296-348) fine-tune step of ClassificationTrainer (CE, clip 1.0, AdamW over
+            encoder + head), 6x200 windows, batch 8; `clips/sec` = windows/s.  Its CPU counterpart is the headline
+            line's `cpu_baseline.imu_only_b8_train_windows_per_sec`.
 For the non-headline workloads `roofline` is the whole step's algorithmic FLOP rate against the bf16 / fp16 peak
 (`kernel`: "whole step"); the headline's is the dominant single kernel's (HIP events) with PMC traffic.
 """
@@ -51,6 +55,7 @@ WORKLOADS = {
     'r3d': dict(batch=32, frames=16, image=112, imu_len=200, dtype='bf16'),
     'fusion': dict(batch=8, frames=32, image=224, imu_len=400, dtype='bf16'),
     'ood_fp16': dict(batch=32, frames=16, image=224, imu_len=200, dtype='fp16'),
+    'imu': dict(batch=8, frames=16, image=224, imu_len=200, dtype='fp32'),
 }
 
 
@@ -360,6 +365,44 @@ class Workload:
     step's algorithmic FLOPs per clip (the whole-step roofline numerator)."""
 
 
+def imu_flops_per_window(T, d=128, layers=4, ff=512, patch=16, hidden=(256, 128), classes=32):
+    """Algorithmic FLOPs of one IMU window's forward: patch embedding, `layers` post-LN encoder layers over
+    n = (T - patch) // patch + 2 tokens (patches + CLS), the MLP head."""
+    n = (T - patch) // patch + 2
+    embed = 2 * (n - 1) * patch * d
+    layer = 2 * n * (4 * d * d + 2 * d * ff) + 4 * n * n * d
+    dims = (d,) + tuple(hidden) + (classes,)
+    head = sum(2 * a * b for a, b in zip(dims, dims[1:]))
+    return embed + layers * layer + head
+
+
+def _imu_workload(args, W, dev, rank, world):
+    """BASELINE config 1: ClassificationTrainer.train_step (finetune) of the IMU-only classifier."""
+    from cmhar import dist as cdist
+    from cmhar.models import IMUClassifier, IMUEncoder
+    from cmhar.trainer import ClassificationTrainer
+    cfg = W.make_cfg()
+    model = IMUClassifier(IMUEncoder(cfg), cfg).to(dev).train()
+    cdist.broadcast_parameters(model)
+    reducer = cdist.GradReducer(model) if world > 1 else None
+    tr = ClassificationTrainer(model, cfg, device=dev, mode='finetune', grad_reducer=reducer)
+    g = torch.Generator(device=dev).manual_seed(1000 + rank)
+    B = args.batch
+    imu = torch.randn(B, 6, args.imu_len, device=dev, generator=g)
+    labels = torch.randint(0, cfg.model.num_classes, (B,), device=dev, generator=g)
+
+    def step():
+        return tr.train_step(imu, labels)[1]
+    W.model, W.B, W.step, W.training = model, B, step, True
+    W.flops_per_clip = 3 * imu_flops_per_window(args.imu_len, ff=4 * cfg.model.imu_d_model,
+                                                hidden=tuple(cfg.model.classifier_hidden_dims),
+                                                classes=cfg.model.num_classes)
+    W.metric = f'windows/sec IMU-only classifier train step (BASELINE config 1), 6x{args.imu_len}, batch {B}'
+    W.workload = (f'IMUClassifier fine-tune step (ClassificationTrainer.train_step): PatchTST IMU encoder 6x'
+                  f'{args.imu_len} + 256-128 MLP head, CE, clip 1.0, AdamW; fp32')
+    return W
+
+
 def build_workload(args, dev, rank, world):
     import warnings
     from cmhar import dist as cdist
@@ -383,6 +426,8 @@ def build_workload(args, dev, rank, world):
     W = Workload()
     W.make_cfg = make_cfg
     torch.manual_seed(0)
+    if args.workload == 'imu':
+        return _imu_workload(args, W, dev, rank, world)
     with warnings.catch_warnings():
         warnings.simplefilter('ignore')          # hub checkpoint not fetchable offline → random init
         if args.workload == 'fusion':

@@ -262,3 +262,13 @@ def test_multi_device_dataparallel_refused_with_pointer(backbone):
             assert 'cmhar.dist' in str(e) and 'GradReducer' in str(e)
             refused.append(name)
     assert {'imu_encoder', 'video_encoder.backbone', 'imu_proj', 'video_proj'} <= set(refused), refused
+
+
+def test_bench_imu_flops_count():
+    """bench.imu_flops_per_window (the config-1 workload's roofline numerator) at the reference geometry: 200-sample
+    windows → 12 patches + CLS = 13 tokens of d 128, FF 512, 4 layers, 128-256-128-32 head."""
+    import bench
+    n, d, ff = 13, 128, 512
+    want = 2 * 12 * 16 * d + 4 * (2 * n * (4 * d * d + 2 * d * ff) + 4 * n * n * d) + \
+        2 * (128 * 256 + 256 * 128 + 128 * 32)
+    assert bench.imu_flops_per_window(200) == want

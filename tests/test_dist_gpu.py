@@ -9,6 +9,7 @@ The ranks are separate processes started with subprocess from this pytest proces
 (`tests/conftest.py`) does not initialise HIP.
 """
 import json
+import math
 import os
 import socket
 import subprocess
@@ -182,3 +183,18 @@ def test_bench_two_rank_rehearsal(tmp_path):
     losses = rec['last_loss_per_rank']
     assert len(losses) == 2 and losses[0] == losses[1], losses
     assert abs(rec['value'] - 64 * 2 / (rec['ms_per_step'] * 2 / 1000)) <= 1e-3 * rec['value']
+
+
+@pytest.mark.gpu
+def test_bench_imu_workload(tmp_path):
+    """BASELINE config 1 on the HIP path (`bench.py --workload imu`): the IMU-only classifier's ClassificationTrainer
+    fine-tune step at batch 8 — one JSON line, windows/s from the timed region, a finite loss."""
+    p = subprocess.run([sys.executable, '-u', os.path.join(REPO, 'bench.py'), '--workload', 'imu', '--steps', '20',
+                        '--warmup', '3'], capture_output=True, timeout=240, cwd=str(tmp_path))
+    assert p.returncode == 0, p.stderr.decode(errors='replace')[-3000:]
+    lines = [ln for ln in p.stdout.decode(errors='replace').splitlines() if ln.startswith('{')]
+    assert len(lines) == 1
+    rec = json.loads(lines[0])
+    assert rec['config']['per_gpu_batch'] == 8 and rec['dtype'] == 'fp32' and rec['n_gpus'] == 1
+    assert rec['value'] > 0 and abs(rec['value'] - 8 * 1000 / rec['ms_per_step']) <= 1e-3 * rec['value']
+    assert math.isfinite(rec['first_warmup_loss'])
