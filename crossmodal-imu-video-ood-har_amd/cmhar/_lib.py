@@ -118,6 +118,7 @@ _SIGS = {
     'cmhar_avgpool_cl_bwd': (i32, [i32, i32, i64, i32, vp, vp, vp]),
     'cmhar_video_to_ndhwc': (i32, [i32, i32, i32, i32, i32, i32, vp, vp, vp]),
     'cmhar_conv_pack_weight': (i32, [i32, i32, i32, i32, i32, i32, i32, vp, vp, vp, vp]),
+    'cmhar_conv_pack_weights': (i32, [i32, i32, vp, vp, vp]),
     'cmhar_conv_grad_unpack': (i32, [i32, i32, i32, i32, i32, i32, i32, vp, vp, vp]),
     'cmhar_maxpool2d_cl_fwd': (i32, [i32, i32, i32, i32, i32, i32, i32, i32, vp, vp, vp, vp]),
     'cmhar_maxpool2d_cl_bwd': (i32, [i32, i32, i32, i32, i32, i32, i32, i32, vp, vp, vp, vp]),

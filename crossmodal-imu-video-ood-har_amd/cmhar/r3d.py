@@ -129,6 +129,30 @@ def _pack(conv, dt, flip=False):
     return (wp, wf) if flip else wp
 
 
+def _pack_all(jobs, dt, dev):
+    """[(conv, flip)] → {conv: wp, or (wp, wf) when flip}: every pack of `_pack` from ONE cmhar_conv_pack_weights
+    launch (R3D-18's 19 block convs were 19 serial launches of a few blocks each)."""
+    n = len(jobs)
+    dims = (ctypes.c_int * (6 * n))()
+    ptrs = (ctypes.c_void_p * (3 * n))()
+    out, keep = {}, []
+    for i, (conv, flip) in enumerate(jobs):
+        w = conv.weight.detach()
+        if not w.is_contiguous():
+            w = w.contiguous()
+            keep.append(w)
+        co, ci, kt, kh, kw = w.shape
+        kp = _r8(w[0].numel())
+        wp = torch.empty(co, kp, dtype=dt, device=dev)
+        wf = torch.empty(ci, kt * kh * kw * co, dtype=dt, device=dev) if flip else None
+        dims[6 * i:6 * i + 6] = [co, ci, kt, kh, kw, kp]
+        ptrs[3 * i:3 * i + 3] = [w.data_ptr(), wp.data_ptr(), ptr(wf)]
+        out[conv] = (wp, wf) if flip else wp
+    if n:
+        call('cmhar_conv_pack_weights', L.dtype_code(dt), n, dims, ptrs, L.stream(dev))
+    return out
+
+
 def _stem_ok(x, shape, conv):
     """Implicit stem kernel (cmhar_conv3d_stem_*): bf16, <= 4 input channels, kw <= 8 taps at w-stride 2, 64 outputs
     (R3D-18's 3x7x7 (1,2,2) stem, ResNet-18's 7x7/2 stem run as (1, 7, 7))."""
@@ -436,18 +460,24 @@ def _forward_impl(m: R3D18, video, training, save):
     call('cmhar_video_to_ndhwc', L.dtype_code(dt), B, T, Cc, H, W, ptr(video), ptr(x), L.stream(video.device))
     shape = (B, T, H, W, Cc)
     units = []
-    packs = {}
+    # every block conv's pack from one launch; the backward's flipped weight (stride-1 input gradient on the
+    # implicit-GEMM kernels) from the same pass
+    seqs = [sq for blk in m.blocks() for sq in ([blk.conv1] + ([blk.downsample] if blk.downsample is not None else [])
+                                                 + [blk.conv2])]
+    packs = _pack_all([(sq[0], save and dt == torch.bfloat16 and _dgrad_igemm_ok(sq[0]) and
+                        sq[0].in_channels % 64 == 0) for sq in seqs], dt, video.device)
 
     def unit(xin, shp, seq, relu, res=None):
         conv, bn = seq[0], seq[1]
         wf = None
         if _stem_ok(xin, shp, conv):
             wp = None                                # _unit_fwd packs the stem's own layout
-        elif save and dt == torch.bfloat16 and _dgrad_igemm_ok(conv) and shp[4] % 64 == 0:
-            wp, wf = _pack(conv, dt, flip=True)      # the backward's flipped weight from the same pass
+        elif conv in packs:
+            wp = packs[conv]
+            if isinstance(wp, tuple):
+                wp, wf = wp
         else:
             wp = _pack(conv, dt)
-        packs[conv] = wp
         y, osh, u = _unit_fwd(xin, shp, conv, bn, relu, training, save, res=res, wp=wp, keep_col=m.keep_cols, wf=wf)
         units.append(u)
         return y, osh

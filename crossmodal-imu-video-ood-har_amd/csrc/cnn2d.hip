@@ -296,11 +296,10 @@ inline PackDiv pack_div(int d) { return PackDiv{(unsigned)d, d == 1 ? 0u : (unsi
 // V8 (Cin, Cout, Kp and ci_t multiples of 8): each thread gathers 8 channels from the brick and writes them as one
 // 16-B vector (2-B scalar stores left the kernel store-issue bound).
 template <typename T, bool V8>
-__global__ __launch_bounds__(256) void conv_pack_kernel(int Cout, int Cin, int taps, int Kp, int ci_t, PackDiv d_taps,
-                                                        const float* __restrict__ w, T* __restrict__ out,
-                                                        T* __restrict__ outf) {
-  __shared__ float brick[PACK_LDS];
-  const int co0 = blockIdx.x * PACK_CO, ci0 = blockIdx.y * ci_t;
+__device__ __forceinline__ void conv_pack_block(int bx, int by, float* brick, int Cout, int Cin, int taps, int Kp,
+                                                int ci_t, PackDiv d_taps, const float* __restrict__ w,
+                                                T* __restrict__ out, T* __restrict__ outf) {
+  const int co0 = bx * PACK_CO, ci0 = by * ci_t;
   const int nco = min(PACK_CO, Cout - co0), nci = min(ci_t, Cin - ci0);
   const int run = nci * taps;                      // contiguous floats per co
   const PackDiv d_run{(unsigned)run, run == 1 ? 0u : (unsigned)((0x100000000ull + run - 1) / run)};
@@ -329,7 +328,7 @@ __global__ __launch_bounds__(256) void conv_pack_kernel(int Cout, int Cin, int t
     }
   }
   if (out) {
-    if (blockIdx.y == 0) {                          // zero padding k in [K, Kp)
+    if (by == 0) {                                  // zero padding k in [K, Kp)
       const int K = taps * Cin, pad = Kp - K;
       for (int i = threadIdx.x; i < nco * pad; i += 256)
         out[(long)(co0 + i / pad) * Kp + K + i % pad] = from_f<T>(0.f);
@@ -353,6 +352,45 @@ __global__ __launch_bounds__(256) void conv_pack_kernel(int Cout, int Cin, int t
           from_f<T>(brick[c * run + ci * taps + tap]);
     }
   }
+}
+
+template <typename T, bool V8>
+__global__ __launch_bounds__(256) void conv_pack_kernel(int Cout, int Cin, int taps, int Kp, int ci_t, PackDiv d_taps,
+                                                        const float* __restrict__ w, T* __restrict__ out,
+                                                        T* __restrict__ outf) {
+  __shared__ float brick[PACK_LDS];
+  conv_pack_block<T, V8>(blockIdx.x, blockIdx.y, brick, Cout, Cin, taps, Kp, ci_t, d_taps, w, out, outf);
+}
+
+// All of a network's weight packs in one launch (the per-conv launches were 19 serial small kernels per R3D-18
+// step, most of them a few blocks): job k owns the blocks [blk0_k, blk0_{k+1}) of a 1-D grid, laid out as its own
+// (gx × gy) pack grid.  Jobs passed by value (≤ PACK_JOBS per launch).
+constexpr int PACK_JOBS = 24;
+struct PackJob {
+  const float* w;
+  void* out;
+  void* outf;
+  int Cout, Cin, taps, Kp, ci_t, gx, blk0, v8;
+  PackDiv d_taps;
+};
+struct PackJobs {
+  int n;
+  PackJob j[PACK_JOBS];
+};
+template <typename T>
+__global__ __launch_bounds__(256) void conv_pack_multi_kernel(PackJobs jobs) {
+  __shared__ float brick[PACK_LDS];
+  const int b = blockIdx.x;
+  int k = 0;
+  while (k + 1 < jobs.n && b >= jobs.j[k + 1].blk0) ++k;
+  const PackJob& J = jobs.j[k];
+  const int local = b - J.blk0, bx = local % J.gx, by = local / J.gx;
+  if (J.v8)
+    conv_pack_block<T, true>(bx, by, brick, J.Cout, J.Cin, J.taps, J.Kp, J.ci_t, J.d_taps, J.w, (T*)J.out,
+                             (T*)J.outf);
+  else
+    conv_pack_block<T, false>(bx, by, brick, J.Cout, J.Cin, J.taps, J.Kp, J.ci_t, J.d_taps, J.w, (T*)J.out,
+                              (T*)J.outf);
 }
 
 // Weight gradient [Cout][Kp] fp32 in a packed k order → the parameter layout [Cout][Cin][R][kw] (R = kt·kh tap rows):
@@ -467,16 +505,53 @@ extern "C" int cmhar_dwconv2d_cl_wgrad(int dtype, int N, int H, int W, int C, in
   return 0;
 }
 
+// One pack's plan: channel tile ci_t, 8-channel vector form, grid; false on invalid arguments
+static bool pack_plan(int Cout, int Cin, int kt, int kh, int kw, int Kp, const float* w, const void* out,
+                      const void* out_flip, int& taps, int& ci_t, bool& v8, dim3& grid) {
+  if (Cout <= 0 || Cin <= 0 || kt <= 0 || kh <= 0 || kw <= 0 || !w || (!out && !out_flip)) return false;
+  taps = kt * kh * kw;
+  if (out && Kp < taps * Cin) return false;
+  if (PACK_CO * taps > PACK_LDS) return false;
+  ci_t = max(1, min(Cin, min(32, PACK_LDS / (PACK_CO * taps))));
+  v8 = Cin % 8 == 0 && Cout % 8 == 0 && (!out || Kp % 8 == 0) && ci_t >= 8;
+  if (v8) ci_t &= ~7;
+  grid = dim3(cdiv(Cout, PACK_CO), cdiv(Cin, ci_t));
+  return true;
+}
+
+extern "C" int cmhar_conv_pack_weights(int out_dtype, int n, const int* dims, const void* const* ptrs,
+                                       hipStream_t stream) {
+  if (n < 0 || (n > 0 && (!dims || !ptrs))) return -1;
+  if (out_dtype != CMHAR_BF16 && out_dtype != CMHAR_F32) return -1;
+  for (int i0 = 0; i0 < n; i0 += PACK_JOBS) {
+    PackJobs jobs{};
+    jobs.n = min(PACK_JOBS, n - i0);
+    int blocks = 0;
+    for (int k = 0; k < jobs.n; ++k) {
+      const int* d = dims + 6 * (i0 + k);
+      const void* const* pp = ptrs + 3 * (i0 + k);
+      int taps, ci_t;
+      bool v8;
+      dim3 g;
+      if (!pack_plan(d[0], d[1], d[2], d[3], d[4], d[5], (const float*)pp[0], pp[1], pp[2], taps, ci_t, v8, g))
+        return -1;
+      jobs.j[k] = PackJob{(const float*)pp[0], const_cast<void*>(pp[1]), const_cast<void*>(pp[2]), d[0], d[1], taps,
+                          d[5], ci_t, (int)g.x, blocks, (int)v8, pack_div(taps)};
+      blocks += (int)(g.x * g.y);
+    }
+    if (out_dtype == CMHAR_BF16) conv_pack_multi_kernel<bf16><<<blocks, 256, 0, stream>>>(jobs);
+    else conv_pack_multi_kernel<float><<<blocks, 256, 0, stream>>>(jobs);
+  }
+  CMHAR_CHECK_LAUNCH();
+  return 0;
+}
+
 extern "C" int cmhar_conv_pack_weight(int out_dtype, int Cout, int Cin, int kt, int kh, int kw, int Kp, const float* w,
                                       void* out, void* out_flip, hipStream_t stream) {
-  if (Cout <= 0 || Cin <= 0 || kt <= 0 || kh <= 0 || kw <= 0 || !w || (!out && !out_flip)) return -1;
-  const int taps = kt * kh * kw;
-  if (out && Kp < taps * Cin) return -1;
-  if (PACK_CO * taps > PACK_LDS) return -1;
-  int ci_t = max(1, min(Cin, min(32, PACK_LDS / (PACK_CO * taps))));
-  const bool v8 = Cin % 8 == 0 && Cout % 8 == 0 && (!out || Kp % 8 == 0) && ci_t >= 8;
-  if (v8) ci_t &= ~7;
-  dim3 grid(cdiv(Cout, PACK_CO), cdiv(Cin, ci_t));
+  int taps, ci_t;
+  bool v8;
+  dim3 grid;
+  if (!pack_plan(Cout, Cin, kt, kh, kw, Kp, w, out, out_flip, taps, ci_t, v8, grid)) return -1;
 #define F(T)                                                                                                       \
   if (v8)                                                                                                          \
     conv_pack_kernel<T, true><<<grid, 256, 0, stream>>>(Cout, Cin, taps, Kp, ci_t, pack_div(taps), w, (T*)out,     \

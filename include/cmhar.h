@@ -343,6 +343,9 @@ int cmhar_avgpool_cl_bwd(int dtype, int N, long S, int C, const float* dout, voi
  * gradient convolves dz with.  taps = kt·kh·kw ≤ 384. */
 int cmhar_conv_pack_weight(int out_dtype, int Cout, int Cin, int kt, int kh, int kw, int Kp, const float* w,
                            void* out, void* out_flip, hipStream_t stream);
+/* n such packs in one launch: dims host [n][6] = (Cout, Cin, kt, kh, kw, Kp), ptrs host [n][3] = (w, out, out_flip),
+ * the same arguments and outputs as n cmhar_conv_pack_weight calls. */
+int cmhar_conv_pack_weights(int out_dtype, int n, const int* dims, const void* const* ptrs, hipStream_t stream);
 /* Weight gradient from a packed k order back to the parameter layout (replaces the strided-view copy autograd's
  * gradient accumulation made of the conv weight gradient, torchvision conv weights [Cout, Cin, kt, kh, kw]):
  * dst [Cout, Cin, R, kw] fp32 (R = kt·kh) from src [Cout, Kp] fp32 at co·Kp + r·rs + iw·cs + ci — im2col order

@@ -277,3 +277,36 @@ def test_conv_pack_weight_both_forms(co, ci, k, dt):
     assert torch.equal(wp, ref.to(dt))
     reff = w.flip(2, 3, 4).permute(1, 2, 3, 4, 0).reshape(ci, -1)
     assert torch.equal(wf, reff.to(dt))
+
+
+@pytest.mark.parametrize('dt', [torch.float32, torch.bfloat16])
+def test_conv_pack_weights_multi_launch(dt):
+    """cmhar_conv_pack_weights: 30 packs (more than one launch's 24 jobs) of mixed geometry — vector and scalar forms,
+    with and without the flipped copy, the out-only form — equal to torch's permute / flip bit for bit."""
+    import ctypes
+    from cmhar import _lib as L
+    from cmhar import r3d
+    torch.manual_seed(7)
+    geo = [(64, 3, (3, 7, 7)), (512, 256, (3, 3, 3)), (96, 144, (1, 1, 1)), (40, 24, (1, 3, 3)), (64, 64, (3, 3, 3)),
+           (128, 64, (1, 1, 1))]
+    jobs = [(geo[i % len(geo)], i % 3 != 0) for i in range(30)]
+    dims = (ctypes.c_int * (6 * len(jobs)))()
+    ptrs = (ctypes.c_void_p * (3 * len(jobs)))()
+    bufs = []
+    for i, ((co, ci, k), flip) in enumerate(jobs):
+        w = torch.randn(co, ci, *k, device=DEV)
+        taps = k[0] * k[1] * k[2]
+        kp = r3d._r8(ci * taps)
+        wp = torch.full((co, kp), 7.0, dtype=dt, device=DEV)
+        wf = torch.empty(ci, taps * co, dtype=dt, device=DEV) if flip else None
+        dims[6 * i:6 * i + 6] = [co, ci, *k, kp]
+        ptrs[3 * i:3 * i + 3] = [w.data_ptr(), wp.data_ptr(), None if wf is None else wf.data_ptr()]
+        bufs.append((w, wp, wf, ci, taps))
+    L.call('cmhar_conv_pack_weights', L.dtype_code(dt), len(jobs), dims, ptrs, L.stream(torch.device(DEV)))
+    torch.cuda.synchronize()
+    for w, wp, wf, ci, taps in bufs:
+        ref = torch.zeros(wp.shape, device=DEV)
+        ref[:, :ci * taps] = w.permute(0, 2, 3, 4, 1).reshape(w.shape[0], -1)
+        assert torch.equal(wp, ref.to(dt))
+        if wf is not None:
+            assert torch.equal(wf, w.flip(2, 3, 4).permute(1, 2, 3, 4, 0).reshape(ci, -1).to(dt))
