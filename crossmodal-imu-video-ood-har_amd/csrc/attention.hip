@@ -100,6 +100,14 @@ __device__ __forceinline__ int acc_row(int r, int h) { return (r & 3) + 8 * (r >
 
 __device__ __forceinline__ float xhalf(float v) { return __shfl_xor(v, 32); }
 
+// CMHAR_ATTN_PRIO = 1: raise the wave's issue priority over each MFMA chain (as the GEMM's MFMA_Q) so the co-resident
+// waves' softmax / exp VALU work fills the matrix pipe's gaps instead of delaying the chain (A/B knob)
+#ifndef CMHAR_ATTN_PRIO
+#define CMHAR_ATTN_PRIO 0
+#endif
+#define PRIO_HI() do { if (CMHAR_ATTN_PRIO) __builtin_amdgcn_s_setprio(1); } while (0)
+#define PRIO_LO() do { if (CMHAR_ATTN_PRIO) __builtin_amdgcn_s_setprio(0); } while (0)
+
 // ---------------------------------------------------------------------------------------------------------------
 // forward
 // ---------------------------------------------------------------------------------------------------------------
@@ -181,12 +189,14 @@ __global__ __launch_bounds__(256, 3) void attn_fwd_bf16(int H, int Lq, int Lk, i
         for (int j = 0; j < QB; ++j)
 #pragma unroll
           for (int r = 0; r < 16; ++r) s[j][r] = 0.f;
+        PRIO_HI();
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
           const bf16x8 kf = row_frag(Ks(cur), kb * 32, t, lane);
 #pragma unroll
           for (int j = 0; j < QB; ++j) s[j] = mma32<E>(kf, qf[j][t], s[j]);
         }
+        PRIO_LO();
         if (kbase + kb * 32 + 32 > Lk) {   // ragged last half-tile only (wave-uniform branch)
 #pragma unroll
           for (int j = 0; j < QB; ++j)
@@ -225,6 +235,7 @@ __global__ __launch_bounds__(256, 3) void attn_fwd_bf16(int H, int Lq, int Lk, i
 #pragma unroll
           for (int ss = 0; ss < 2; ++ss) pb[j][ss] = pack8<E>(s[j], ss);
         }
+        PRIO_HI();
 #pragma unroll
         for (int ss = 0; ss < 2; ++ss)
 #pragma unroll
@@ -233,6 +244,7 @@ __global__ __launch_bounds__(256, 3) void attn_fwd_bf16(int H, int Lq, int Lk, i
 #pragma unroll
             for (int j = 0; j < QB; ++j) o[j][d] = mma32<E>(vf, pb[j][ss], o[j][d]);
           }
+        PRIO_LO();
       }
     }
     if (more) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // own pieces of the next tile landed
@@ -355,11 +367,13 @@ __global__ __launch_bounds__(256, 3) void attn_bwd_dkdv_bf16(int H, int Lq, int 
         s[r] = L_[q];
         dp[r] = D_[q];
       }
+      PRIO_HI();
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
         s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag(Qs(cur), qb * 32, t, lane), kf[t], s, 0, 0, 0);
         dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag(Gs(cur), qb * 32, t, lane), vf[t], dp, 0, 0, 0);
       }
+      PRIO_LO();
       // p = exp2(c·s), dS = P ∘ (dP − δ), then both packed to bf16 — written in aligned register pairs (one
       // v_pk_mul_f32 + one v_cvt_pk_bf16_f32 per pair; element-wise, the compiler paired (1,2),(3,4),... and spent
       // v_mov / v_alignbit / v_perm re-pairing them for the packs; the backward got 3 % faster, bit-identical.  The
@@ -376,6 +390,7 @@ __global__ __launch_bounds__(256, 3) void attn_bwd_dkdv_bf16(int H, int Lq, int 
         dbv[r >> 3][r & 7] = dd[0];
         dbv[r >> 3][(r & 7) + 1] = dd[1];
       }
+      PRIO_HI();
 #pragma unroll
       for (int ss = 0; ss < 2; ++ss) {
         const bf16x8 pb = pbv[ss], db = dbv[ss];
@@ -385,6 +400,7 @@ __global__ __launch_bounds__(256, 3) void attn_bwd_dkdv_bf16(int H, int Lq, int 
           dk[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_frag(Qs(cur), qb * 32, ss, d * 32, lane), db, dk[d], 0, 0, 0);
         }
       }
+      PRIO_LO();
     }
     if (more) {
       store_rows(cur ^ 1);
@@ -497,6 +513,7 @@ __global__ __launch_bounds__(256, QB == 1 ? 3 : 2) void attn_bwd_dq_bf16(int H, 
       for (int j = 0; j < QB; ++j)
 #pragma unroll
         for (int r = 0; r < 16; ++r) { s[j][r] = sL[j]; dp[j][r] = -Dl[j]; }
+      PRIO_HI();
 #pragma unroll
       for (int t = 0; t < 4; ++t) {    // each K / V row fragment read once, used by all QB q-blocks
         const bf16x8 kfr = row_frag(Ks(cur), kb * 32, t, lane);
@@ -507,6 +524,7 @@ __global__ __launch_bounds__(256, QB == 1 ? 3 : 2) void attn_bwd_dq_bf16(int H, 
           dp[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vfr, gf[j][t], dp[j], 0, 0, 0);
         }
       }
+      PRIO_LO();
       if (kbase + 64 > Lk) {   // ragged last tile only (wave-uniform branch)
 #pragma unroll
         for (int j = 0; j < QB; ++j)
@@ -526,6 +544,7 @@ __global__ __launch_bounds__(256, QB == 1 ? 3 : 2) void attn_bwd_dq_bf16(int H, 
           db[j][r >> 3][(r & 7) + 1] = dd[1];
         }
       }
+      PRIO_HI();
 #pragma unroll
       for (int ss = 0; ss < 2; ++ss)
 #pragma unroll
@@ -535,6 +554,7 @@ __global__ __launch_bounds__(256, QB == 1 ? 3 : 2) void attn_bwd_dq_bf16(int H, 
           for (int j = 0; j < QB; ++j)
             dq[j][d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ktr, db[j][ss], dq[j][d], 0, 0, 0);
         }
+      PRIO_LO();
     }
     if (more) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // own pieces of the next tile landed
     __syncthreads();
