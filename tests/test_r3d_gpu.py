@@ -444,3 +444,50 @@ def test_conv3d_implicit_gemm_dgrad(cin, cout, shape, acc):
     dx = r3d._dgrad_igemm(dzc, conv, (N, T, H, W, cout), xc,
                           None if res is None else res.reshape(-1, cin).contiguous().to(DEV))
     assert rel(dx.float().reshape(N, T, H, W, cin), expect) < 5e-3
+
+
+@pytest.mark.parametrize('relu', [1, 2])
+def test_bn_bwd_nores_rounding_boundaries(relu):
+    """The z-mask's thresholds at the bf16 rounding boundaries of y = bf16(act(v)): with mean 0, rstd 1 (eval, eps 0)
+    and z = 1 the pre-activation v is the channel's weight, chosen at each boundary and one fp32 ulp inside it —
+    ReLU6's tie at 6 − 2^-6 (rounds to the even 6.0), the denormal 2^-134 (rounds to +0), ReLU's overflow at 0x1.fep127
+    — plus ordinary values.  The no-residual entry must give the y-reading entry's dx / dw / db bit for bit (whatever
+    rsqrt(1) rounds to, both entries use the same saved statistics)."""
+    from cmhar import _lib as L
+    from cmhar import kernels as K
+    from cmhar import r3d
+    below = lambda v: math.nextafter(v, 0.0)      # noqa: E731
+    ws = [5.984375, below(5.984375), 2.0 ** -134, 1.5 * 2.0 ** -134, float.fromhex('0x1.fep127'),
+          below(float.fromhex('0x1.fep127')), -1.0, 2.0 ** -133, 6.0, 0.75, 3.0, 2.0 ** -126, 1e-3, -2.0 ** -140,
+          5.96875, 0.0]
+    C = len(ws)
+    M = 257
+    bn = torch.nn.BatchNorm3d(C, eps=0.0).to(DEV)
+    with torch.no_grad():
+        bn.weight.copy_(torch.tensor(ws, dtype=torch.float64).float())
+        bn.bias.zero_()
+        bn.running_mean.zero_()
+        bn.running_var.fill_(1.0)
+    z = torch.ones(M, C, device=DEV, dtype=torch.bfloat16)
+    z[M // 2:] = torch.randn(M - M // 2, C, device=DEV).to(torch.bfloat16)
+    y, sm, sr = r3d._bn_fwd(z, bn, None, relu, False)
+    dy = torch.randn(M, C, device=DEV).to(torch.bfloat16)
+    wsp = K.workspace(L.lib().cmhar_bn_cl_ws(M, C), z.device)
+    outs = []
+    for nores in (False, True):
+        dx = torch.empty_like(z)
+        dw = torch.empty(C, device=DEV)
+        db = torch.empty(C, device=DEV)
+        if nores:
+            L.call('cmhar_bn_cl_bwd_nores', L.BF16, M, C, z.data_ptr(), dy.data_ptr(), bn.weight.data_ptr(),
+                   bn.bias.data_ptr(), sm.data_ptr(), sr.data_ptr(), dx.data_ptr(), dw.data_ptr(), db.data_ptr(), 0,
+                   relu, wsp.data_ptr(), L.stream(z.device))
+        else:
+            L.call('cmhar_bn_cl_bwd', L.BF16, M, C, z.data_ptr(), y.data_ptr(), dy.data_ptr(), bn.weight.data_ptr(),
+                   sm.data_ptr(), sr.data_ptr(), dx.data_ptr(), None, dw.data_ptr(), db.data_ptr(), 0, relu,
+                   wsp.data_ptr(), L.stream(z.device))
+        torch.cuda.synchronize()
+        outs.append((dx, dw, db))
+    for a, b in zip(*outs):      # bitwise (±0 and inf included)
+        assert torch.equal(a.view(torch.int16) if a.dtype == torch.bfloat16 else a.view(torch.int32),
+                           b.view(torch.int16) if b.dtype == torch.bfloat16 else b.view(torch.int32))
