@@ -177,13 +177,14 @@ __global__ __launch_bounds__(256) void col2im3d_kernel(Geom g, const T* __restri
 constexpr int BN_ZMASK = 4;
 // act'(y) ≠ 0 for y = T(clamp(v, lo, hi)), v = fmaf((x − mean)·rstd, w, b) (bn_cl_apply's arithmetic), without the
 // round trip: for bf16 storage, T(v) of 0 < v < 2^-134 is +0 (round to nearest even) and ReLU6's T(v) reaches 6 from
-// v = 6 − 2^-6 on (the tie rounds to the even 6.0), ReLU's T(v) overflows to +inf from 0x1.fep127 on; fp32 storage
+// v = 6 − 2^-6 on (the tie rounds to the even 6.0), ReLU's T(v) overflows to +inf from 0x1.ffp127 on (the tie between the largest finite bf16, 0x1.fep127,
+// and 2^128 rounds to the even +inf); fp32 storage
 // keeps v.  NaN: every comparison false → 0, as act(NaN) = clamp → 0 in the forward.
 template <typename T>
 __device__ __forceinline__ bool bn_act_on(float v, int relu) {
   constexpr bool B16 = sizeof(T) == 2;
   const float lo = B16 ? 0x1p-134f : 0.f;
-  const float hi = (relu & 3) == 2 ? (B16 ? 5.984375f : 6.f) : (B16 ? 0x1.fep127f : INFINITY);
+  const float hi = (relu & 3) == 2 ? (B16 ? 5.984375f : 6.f) : (B16 ? 0x1.ffp127f : INFINITY);
   return v > lo && v < hi;
 }
 template <typename T, int MODE, bool ZM = false>

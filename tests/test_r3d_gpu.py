@@ -450,16 +450,17 @@ def test_conv3d_implicit_gemm_dgrad(cin, cout, shape, acc):
 def test_bn_bwd_nores_rounding_boundaries(relu):
     """The z-mask's thresholds at the bf16 rounding boundaries of y = bf16(act(v)): with mean 0, rstd 1 (eval, eps 0)
     and z = 1 the pre-activation v is the channel's weight, chosen at each boundary and one fp32 ulp inside it —
-    ReLU6's tie at 6 − 2^-6 (rounds to the even 6.0), the denormal 2^-134 (rounds to +0), ReLU's overflow at 0x1.fep127
+    ReLU6's tie at 6 − 2^-6 (rounds to the even 6.0), the denormal 2^-134 (rounds to +0), ReLU's overflow at 0x1.ffp127
     — plus ordinary values.  The no-residual entry must give the y-reading entry's dx / dw / db bit for bit (whatever
     rsqrt(1) rounds to, both entries use the same saved statistics)."""
     from cmhar import _lib as L
     from cmhar import kernels as K
     from cmhar import r3d
-    below = lambda v: math.nextafter(v, 0.0)      # noqa: E731
-    ws = [5.984375, below(5.984375), 2.0 ** -134, 1.5 * 2.0 ** -134, float.fromhex('0x1.fep127'),
-          below(float.fromhex('0x1.fep127')), -1.0, 2.0 ** -133, 6.0, 0.75, 3.0, 2.0 ** -126, 1e-3, -2.0 ** -140,
-          5.96875, 0.0]
+    import numpy as np
+    below = lambda v: float(np.nextafter(np.float32(v), np.float32(0)))      # one fp32 ulp toward 0  # noqa: E731
+    ws = [5.984375, below(5.984375), 2.0 ** -134, 1.5 * 2.0 ** -134, float.fromhex('0x1.ffp127'),
+          below(float.fromhex('0x1.ffp127')), float.fromhex('0x1.fep127'), 2.0 ** -133, 6.0, 0.75, 3.0, 2.0 ** -126,
+          1e-3, -2.0 ** -140, 5.96875, -1.0]
     C = len(ws)
     M = 257
     bn = torch.nn.BatchNorm3d(C, eps=0.0).to(DEV)
