@@ -175,17 +175,17 @@ __global__ __launch_bounds__(256) void col2im3d_kernel(Geom g, const T* __restri
 // relu | BN_ZMASK: the unit had no residual input, so y = act(x̂·w + b) is recomputed from x in bn_cl_apply's exact
 // arithmetic and rounding (bit-identical mask) instead of read: one M×C tensor less per pass.
 constexpr int BN_ZMASK = 4;
-// act'(y) ≠ 0 for y = T(clamp(v, lo, hi)), v = fmaf((x − mean)·rstd, w, b) (bn_cl_apply's arithmetic), without the
-// round trip: for bf16 storage, T(v) of 0 < v < 2^-134 is +0 (round to nearest even) and ReLU6's T(v) reaches 6 from
-// v = 6 − 2^-6 on (the tie rounds to the even 6.0), ReLU's T(v) overflows to +inf from 0x1.ffp127 on (the tie between the largest finite bf16, 0x1.fep127,
-// and 2^128 rounds to the even +inf); fp32 storage
-// keeps v.  NaN: every comparison false → 0, as act(NaN) = clamp → 0 in the forward.
+// act'(y) ≠ 0 from the stored y: ReLU [y > 0] (+inf included, as torch's threshold_backward on the result), ReLU6
+// [0 < y < 6]; NaN → 0.
+__device__ __forceinline__ bool bn_y_on(float y, int relu) { return y > 0.f && ((relu & 3) != 2 || y < 6.f); }
+// The same mask from the pre-activation v = fmaf((x − mean)·rstd, w, b) (bn_cl_apply's arithmetic), without the
+// round trip y = T(clamp(v)): for bf16 storage T(v) of 0 < v ≤ 2^-134 is +0 (round to nearest even: 2^-134 is the
+// tie between +0 and the smallest denormal 2^-133) and ReLU6's T(v) reaches 6 from v = 6 − 2^-6 on (the tie rounds
+// to the even 6.0); fp32 storage keeps v.  NaN: the forward's clamp gives 0 → off, as here.
 template <typename T>
 __device__ __forceinline__ bool bn_act_on(float v, int relu) {
   constexpr bool B16 = sizeof(T) == 2;
-  const float lo = B16 ? 0x1p-134f : 0.f;
-  const float hi = (relu & 3) == 2 ? (B16 ? 5.984375f : 6.f) : (B16 ? 0x1.ffp127f : INFINITY);
-  return v > lo && v < hi;
+  return v > (B16 ? 0x1p-134f : 0.f) && ((relu & 3) != 2 || v < (B16 ? 5.984375f : 6.f));
 }
 template <typename T, int MODE, bool ZM = false>
 __global__ __launch_bounds__(256, sizeof(T) == 2 ? 4 : 3) void bn_cl_partial(int M, int C, int rows_per_chunk, const T* __restrict__ x,
@@ -223,8 +223,7 @@ __global__ __launch_bounds__(256, sizeof(T) == 2 ? 4 : 3) void bn_cl_partial(int
         a0[j] = fmaf(d, d, a0[j]);
       } else {
         const float xh = (v[j] - mu[j]) * rs[j];
-        const bool off = ZM ? !bn_act_on<T>(fmaf(xh, ww[j], bb[j]), relu)
-                            : (relu && yv[j] <= 0.f) || (relu == 2 && yv[j] >= 6.f);
+        const bool off = ZM ? !bn_act_on<T>(fmaf(xh, ww[j], bb[j]), relu) : relu && !bn_y_on(yv[j], relu);
         const float gj = off ? 0.f : gv[j];
         a0[j] += gj;
         a1[j] = fmaf(gj, xh, a1[j]);
@@ -539,7 +538,6 @@ __global__ __launch_bounds__(256) void bn_cl_bwd_apply(unsigned nvec, int M, int
   };
   const unsigned i0 = blockIdx.x * blockDim.x + threadIdx.x;
   if (HOIST) consts(i0);
-  const float lo = relu ? 0.f : -INFINITY, hi = (relu & 3) == 2 ? 6.f : INFINITY;
   for (unsigned i = i0; i < nvec; i += gridDim.x * blockDim.x) {
     const long off = (long)i * 8;
     float gv[8], yv[8], xv[8], out[8];
@@ -549,7 +547,7 @@ __global__ __launch_bounds__(256) void bn_cl_bwd_apply(unsigned nvec, int M, int
     if (!HOIST) consts(i);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      if (zm ? !bn_act_on<T>(fmaf((xv[j] - mu[j]) * rs[j], ww[j], bb[j]), relu) : ry && !(yv[j] > lo && yv[j] < hi))
+      if (zm ? !bn_act_on<T>(fmaf((xv[j] - mu[j]) * rs[j], ww[j], bb[j]), relu) : ry && !bn_y_on(yv[j], relu))
         gv[j] = 0.f;
       if (training) {
         const float xh = (xv[j] - mu[j]) * rs[j];

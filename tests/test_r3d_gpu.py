@@ -450,7 +450,7 @@ def test_conv3d_implicit_gemm_dgrad(cin, cout, shape, acc):
 def test_bn_bwd_nores_rounding_boundaries(relu):
     """The z-mask's thresholds at the bf16 rounding boundaries of y = bf16(act(v)): with mean 0, rstd 1 (eval, eps 0)
     and z = 1 the pre-activation v is the channel's weight, chosen at each boundary and one fp32 ulp inside it —
-    ReLU6's tie at 6 − 2^-6 (rounds to the even 6.0), the denormal 2^-134 (rounds to +0), ReLU's overflow at 0x1.ffp127
+    ReLU6's tie at 6 − 2^-6 (rounds to the even 6.0), the denormal 2^-134 (rounds to +0), ReLU's overflow to +inf at 0x1.ffp127 (active: [y > 0], as torch)
     — plus ordinary values.  The no-residual entry must give the y-reading entry's dx / dw / db bit for bit (whatever
     rsqrt(1) rounds to, both entries use the same saved statistics)."""
     from cmhar import _lib as L
@@ -490,5 +490,9 @@ def test_bn_bwd_nores_rounding_boundaries(relu):
         torch.cuda.synchronize()
         outs.append((dx, dw, db))
     for a, b in zip(*outs):      # bitwise (±0 and inf included)
-        assert torch.equal(a.view(torch.int16) if a.dtype == torch.bfloat16 else a.view(torch.int32),
-                           b.view(torch.int16) if b.dtype == torch.bfloat16 else b.view(torch.int32))
+        ai = a.view(torch.int16) if a.dtype == torch.bfloat16 else a.view(torch.int32)
+        bi = b.view(torch.int16) if b.dtype == torch.bfloat16 else b.view(torch.int32)
+        bad = (ai != bi).nonzero()
+        assert bad.numel() == 0, [(tuple(i), ws[int(i[-1])], float(y.view(-1, C)[int(i[0]), int(i[-1])])
+                                   if a.dim() == 2 else None, float(a[tuple(i)]), float(b[tuple(i)]))
+                                  for i in bad[:6].tolist()]
