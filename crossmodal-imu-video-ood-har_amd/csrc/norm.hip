@@ -50,43 +50,58 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(int M, int N, const T* __re
 }
 
 // Vectorised forward for N % 256 == 0 without the add/dropout input: one wave per row, 4 consecutive columns per
-// lane per 256-column group (8-B bf16 / 16-B fp32 accesses), two-pass statistics in registers.
+// lane per 256-column group (8-B bf16 / 16-B fp32 accesses), two-pass statistics in registers.  Rows grid-strided
+// over LNF_WAVES-wave blocks with the next row's loads issued under the current row's math (one short-lived wave
+// per row left the loads of a single row in flight per wave); γ / β loaded once per lane.  Per-row arithmetic as
+// before: the same bits.
+constexpr int LNF_WAVES = 8;
 template <typename T, int G>
-__global__ __launch_bounds__(256) void ln_fwd_vec_kernel(int M, const T* __restrict__ a, long lda, T* __restrict__ y,
-                                                         long ldy, const float* __restrict__ gamma,
-                                                         const float* __restrict__ beta, float* __restrict__ mean,
-                                                         float* __restrict__ rstd, float eps) {
+__global__ __launch_bounds__(64 * LNF_WAVES) void ln_fwd_vec_kernel(int M, const T* __restrict__ a, long lda,
+                                                                    T* __restrict__ y, long ldy,
+                                                                    const float* __restrict__ gamma,
+                                                                    const float* __restrict__ beta,
+                                                                    float* __restrict__ mean, float* __restrict__ rstd,
+                                                                    float eps) {
   constexpr int N = 256 * G;
   typedef __attribute__((ext_vector_type(4))) T vec4;
-  const int lane = threadIdx.x & 63;
-  const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (row >= M) return;
-  float v[G][4];
-  float s = 0.f;
-#pragma unroll
-  for (int i = 0; i < G; ++i) {
-    const vec4 x = *(const vec4*)(a + row * lda + 256 * i + 4 * lane);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) { v[i][j] = to_f<T>(x[j]); s += v[i][j]; }
-  }
-  const float mu = wave_sum(s) * (1.f / N);
-  float q = 0.f;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  float gm[G][4], bt[G][4];
 #pragma unroll
   for (int i = 0; i < G; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) { const float d = v[i][j] - mu; q += d * d; }
-  const float r = rsqrtf(wave_sum(q) * (1.f / N) + eps);
+    for (int j = 0; j < 4; ++j) { gm[i][j] = gamma[256 * i + 4 * lane + j]; bt[i][j] = beta[256 * i + 4 * lane + j]; }
+  const long wstride = (long)gridDim.x * LNF_WAVES;
+  const long row0 = (long)blockIdx.x * LNF_WAVES + wave;
+  vec4 vx[G];
+  auto load = [&](long row) {
 #pragma unroll
-  for (int i = 0; i < G; ++i) {
-    vec4 o;
+    for (int i = 0; i < G; ++i) vx[i] = *(const vec4*)(a + row * lda + 256 * i + 4 * lane);
+  };
+  if (row0 < M) load(row0);
+  for (long row = row0; row < M; row += wstride) {
+    float v[G][4];
+    float s = 0.f;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int c = 256 * i + 4 * lane + j;
-      o[j] = from_f<T>((v[i][j] - mu) * r * gamma[c] + beta[c]);
+    for (int i = 0; i < G; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) { v[i][j] = to_f<T>(vx[i][j]); s += v[i][j]; }
+    if (row + wstride < M) load(row + wstride);     // prefetch the next row under this row's math
+    const float mu = wave_sum(s) * (1.f / N);
+    float q = 0.f;
+#pragma unroll
+    for (int i = 0; i < G; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) { const float d = v[i][j] - mu; q += d * d; }
+    const float r = rsqrtf(wave_sum(q) * (1.f / N) + eps);
+#pragma unroll
+    for (int i = 0; i < G; ++i) {
+      vec4 o;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) o[j] = from_f<T>((v[i][j] - mu) * r * gm[i][j] + bt[i][j]);
+      *(vec4*)(y + row * ldy + 256 * i + 4 * lane) = o;
     }
-    *(vec4*)(y + row * ldy + 256 * i + 4 * lane) = o;
+    if (lane == 0) { mean[row] = mu; rstd[row] = r; }
   }
-  if (lane == 0) { mean[row] = mu; rstd[row] = r; }
 }
 
 // dh = LN_bwd(dy) (+ dres); db_out (optional) = dh * dropmask(b); dgamma/dbeta partial slabs per block.
@@ -335,7 +350,10 @@ extern "C" int cmhar_layernorm_fwd(int dtype, int M, int N, const void* a, long 
   if (N > 64 * MAXPER) return -1;
   const int grid = cdiv(M, 4);
   if (!b && !h_out && ln_vec_ok(N, lda, ldy, ldy)) {
-#define LF(TT, G) ln_fwd_vec_kernel<TT, G><<<grid, 256, 0, st>>>(M, (const TT*)a, lda, (TT*)y, ldy, gamma, beta, mean, rstd, eps)
+    // 512-thread blocks, rows grid-strided: three per CU (256 CUs) for N <= 768 (72 VGPRs: 7 waves per SIMD), two
+    // above
+    const int vgrid = std::min(N <= 768 ? 768 : 512, cdiv(M, LNF_WAVES));
+#define LF(TT, G) ln_fwd_vec_kernel<TT, G><<<vgrid, 64 * LNF_WAVES, 0, st>>>(M, (const TT*)a, lda, (TT*)y, ldy, gamma, beta, mean, rstd, eps)
     const int G = N / 256;
     if (dtype == CMHAR_BF16) {
       switch (G) { case 1: LF(bf16, 1); break; case 2: LF(bf16, 2); break; case 3: LF(bf16, 3); break; default: LF(bf16, 4); }
