@@ -249,6 +249,38 @@ __global__ __launch_bounds__(256) void colsum_final2_kernel(int chunks, int N2, 
   }
 }
 
+// One-launch form of colsum_partial + colsum_final2 for up to RR1_MAX partial rows (the LayerNorm backward's 512
+// per-block rows): 16 columns × 16 row slots per block, each slot summing its rows with 8 independent partial sums
+// (8 loads in flight), then the 16 slots combined through LDS — fixed order throughout.  (The two launches of ~5 µs
+// each were mostly launch and dependent-load latency.)
+constexpr int RR1_MAX = 1024;
+__global__ __launch_bounds__(256) void colsum_rows2_kernel(int rows, int N2, const float* __restrict__ part,
+                                                           float* __restrict__ out0, float* __restrict__ out1,
+                                                           float beta) {
+  __shared__ float red[16][17];
+  const int N = 2 * N2;
+  const int cl = threadIdx.x & 15, slot = threadIdx.x >> 4;
+  const int col = blockIdx.x * 16 + cl;
+  float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (col < N) {
+    int r = slot;
+    for (; r + 7 * 16 < rows; r += 8 * 16) {
+#pragma unroll
+      for (int u = 0; u < 8; ++u) a[u] += part[(long)(r + 16 * u) * N + col];
+    }
+    for (; r < rows; r += 16) a[0] += part[(long)r * N + col];
+  }
+  red[slot][cl] = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
+  __syncthreads();
+  if (slot == 0 && col < N) {
+    float t = 0.f;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) t += red[k][cl];
+    float* o = col < N2 ? out0 + col : out1 + (col - N2);
+    *o = t + (beta != 0.f ? beta * *o : 0.f);
+  }
+}
+
 // BatchNorm1d (+ optional ReLU) over x [B][C] fp32: one thread per channel.
 __global__ void bn_fwd_kernel(int B, int C, const float* __restrict__ x, float* __restrict__ y,
                               const float* __restrict__ w, const float* __restrict__ bias,
@@ -397,7 +429,9 @@ static void reduce_rows(const float* part, int rows, int N, float* out, float al
 // dγ and dβ from interleaved partial rows [rows][dγ(N) | dβ(N)] in one (or two, for many rows) launches.
 static void reduce_rows_gb(const float* part, int rows, int N, float* dgamma, float* dbeta, float beta,
                            float* scratch, hipStream_t st) {
-  if (rows > 32) {
+  if (rows > 32 && rows <= RR1_MAX) {
+    colsum_rows2_kernel<<<cdiv(2 * N, 16), 256, 0, st>>>(rows, N, part, dgamma, dbeta, beta);
+  } else if (rows > 32) {
     const int chunks = rr_chunks(rows), rpc = cdiv(rows, chunks);
     colsum_partial_kernel<float><<<dim3(cdiv(2 * N, 64 * CS_VEC), chunks), 256, 0, st>>>(rows, 2 * N, part, 2 * N,
                                                                                          rpc, scratch);

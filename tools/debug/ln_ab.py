@@ -56,6 +56,35 @@ def main():
     print('ln_fwd ' + ' | '.join(f'{chr(65 + k)} {m:7.1f} us {b:6.0f} GB/s' for k, (m, b) in enumerate(zip(med, gbs)))
           + f' | bitwise-equal-to-A={same}')
 
+    # backward (dy, h, residual gradient in; dh out; dγ / dβ through the partial-row reduction)
+    dy = torch.randn(M, N, device='cuda', generator=g).bfloat16()
+    dres = torch.randn(M, N, device='cuda', generator=g).bfloat16()
+    mu, rs = outs[0][1], outs[0][2]
+    nws = int(libs[0].cmhar_layernorm_bwd_ws(M, N))
+    bouts = []
+    for L in libs:
+        bouts.append((torch.empty(M, N, device='cuda', dtype=torch.bfloat16), torch.empty(N, device='cuda'),
+                      torch.empty(N, device='cuda'), torch.empty(nws, device='cuda')))
+
+    def runb(k):
+        dh, dg, db, ws = bouts[k]
+        rc = libs[k].cmhar_layernorm_bwd(_lib.BF16, M, N, dy.data_ptr(), N, x.data_ptr(), N, gamma.data_ptr(),
+                                         mu.data_ptr(), rs.data_ptr(), dres.data_ptr(), N, dh.data_ptr(), N, None, 0,
+                                         0.0, 0, dg.data_ptr(), db.data_ptr(), 0.0, ws.data_ptr(), st)
+        assert rc == 0
+    bt = [[] for _ in libs]
+    for k in range(len(libs)):
+        runb(k)
+    torch.cuda.synchronize()
+    for _ in range(rounds):
+        for k in range(len(libs)):
+            bt[k].append(timed(lambda: runb(k), reps=20) * 1e3)
+    bmed = [statistics.median(t) for t in bt]
+    dh_same = [torch.equal(bouts[0][0].view(torch.int16), o[0].view(torch.int16)) for o in bouts[1:]]
+    rel = [max(float((o[i] - bouts[0][i]).abs().max() / bouts[0][i].abs().max()) for i in (1, 2)) for o in bouts[1:]]
+    print('ln_bwd ' + ' | '.join(f'{chr(65 + k)} {m:7.1f} us' for k, m in enumerate(bmed))
+          + f' | dh bitwise-equal-to-A={dh_same} | dgamma/dbeta max rel diff to A={rel}')
+
 
 if __name__ == '__main__':
     main()
