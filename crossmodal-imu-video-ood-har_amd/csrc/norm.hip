@@ -291,11 +291,15 @@ __global__ void bn_fwd_kernel(int B, int C, const float* __restrict__ x, float* 
   if (c >= C) return;
   float mu, r;
   if (training && nbt && c == 0) *nbt += 1;   // num_batches_tracked
+  // (the b loops unrolled: their loads issue together instead of one dependent-latency round trip per row — one
+  // thread per channel, a few hundred threads in all; the summation order is unchanged)
   if (training) {
     float s = 0.f;
+#pragma unroll 8
     for (int b = 0; b < B; ++b) s += x[(long)b * C + c];
     mu = s / B;
     float q = 0.f;
+#pragma unroll 8
     for (int b = 0; b < B; ++b) { const float d = x[(long)b * C + c] - mu; q += d * d; }
     const float var = q / B;
     r = rsqrtf(var + eps);
@@ -309,8 +313,10 @@ __global__ void bn_fwd_kernel(int B, int C, const float* __restrict__ x, float* 
   }
   smean[c] = mu;
   srstd[c] = r;
+  const float wc = w[c], bc = bias[c];
+#pragma unroll 8
   for (int b = 0; b < B; ++b) {
-    float v = (x[(long)b * C + c] - mu) * r * w[c] + bias[c];
+    float v = (x[(long)b * C + c] - mu) * r * wc + bc;
     if (relu) v = fmaxf(v, 0.f);
     y[(long)b * C + c] = v;
   }
@@ -325,6 +331,7 @@ __global__ void bn_bwd_kernel(int B, int C, const float* __restrict__ x, const f
   if (c >= C) return;
   const float mu = smean[c], r = srstd[c];
   float sg = 0.f, sgx = 0.f;
+#pragma unroll 8
   for (int b = 0; b < B; ++b) {
     float g = dy[(long)b * C + c];
     if (relu && y[(long)b * C + c] <= 0.f) g = 0.f;
@@ -334,11 +341,13 @@ __global__ void bn_bwd_kernel(int B, int C, const float* __restrict__ x, const f
   }
   dw[c] = sgx + (beta != 0.f ? beta * dw[c] : 0.f);
   db[c] = sg + (beta != 0.f ? beta * db[c] : 0.f);
+  const float wc = w[c];
+#pragma unroll 8
   for (int b = 0; b < B; ++b) {
     float g = dy[(long)b * C + c];
     if (relu && y[(long)b * C + c] <= 0.f) g = 0.f;
     const float xh = (x[(long)b * C + c] - mu) * r;
-    dx[(long)b * C + c] = training ? w[c] * r * (g - sg / B - xh * sgx / B) : w[c] * r * g;
+    dx[(long)b * C + c] = training ? wc * r * (g - sg / B - xh * sgx / B) : wc * r * g;
   }
 }
 
