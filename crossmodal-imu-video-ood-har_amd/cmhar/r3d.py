@@ -265,11 +265,12 @@ def _unit_fwd(x, shape, conv, bn, relu, training, save, res=None, wp=None, keep_
     elif igemm:
         col = None
         dims = _dims(shape, conv, Kp)
-        if training and bn.track_running_stats:      # BN statistics from the conv epilogue (no statistics pass)
-            ntile = L.lib().cmhar_conv3d_fwd_tiles(dims, conv.out_channels)
-            tstats = K.workspace(L.lib().cmhar_conv3d_fwd_stats_floats(dims, conv.out_channels), x.device)
-        call('cmhar_conv3d_fwd', dims, conv.out_channels, ptr(x), ptr(wp), None, ptr(z), ptr(tstats),
-             L.stream(x.device))
+        if not _conv_fwd_split(dims, conv.out_channels, x, wp, None, z):
+            if training and bn.track_running_stats:      # BN statistics from the conv epilogue (no statistics pass)
+                ntile = L.lib().cmhar_conv3d_fwd_tiles(dims, conv.out_channels)
+                tstats = K.workspace(L.lib().cmhar_conv3d_fwd_stats_floats(dims, conv.out_channels), x.device)
+            call('cmhar_conv3d_fwd', dims, conv.out_channels, ptr(x), ptr(wp), None, ptr(z), ptr(tstats),
+                 L.stream(x.device))
     elif _pointwise(conv, shape, Kp, M, rows):
         col = x.reshape(M, Kp)
         K.gemm(0, col, wp, z)
@@ -310,8 +311,20 @@ def _dgrad_igemm(dz, conv, oshape, x, dx_acc=None, wf=None):
     pt, ph, pw = conv.padding
     dims = (ctypes.c_int * 15)(N, To, Ho, Wo, cout, kt, kh, kw, 1, 1, 1, pt, ph, pw, wf.shape[1])
     dx = torch.empty_like(x)
-    call('cmhar_conv3d_fwd', dims, cin, ptr(dz), ptr(wf), ptr(dx_acc), ptr(dx), None, L.stream(dz.device))
+    if not _conv_fwd_split(dims, cin, dz, wf, dx_acc, dx):
+        call('cmhar_conv3d_fwd', dims, cin, ptr(dz), ptr(wf), ptr(dx_acc), ptr(dx), None, L.stream(dz.device))
     return dx
+
+
+def _conv_fwd_split(dims, cout, x, w, res, z):
+    """The split-K implicit-GEMM forward when the library plans one for this geometry (the small-M layer-4 convs:
+    `cmhar_conv3d_fwd_split_ws` > 0); False otherwise.  No BatchNorm tile statistics come with it."""
+    n = L.lib().cmhar_conv3d_fwd_split_ws(dims, cout)
+    if n <= 0:
+        return False
+    ws = K.workspace(n, x.device)
+    call('cmhar_conv3d_fwd_split', dims, cout, ptr(x), ptr(w), ptr(res), ptr(z), ptr(ws), L.stream(x.device))
+    return True
 
 
 def _grad_dest(grads, p, dev):

@@ -1205,10 +1205,13 @@ template <int TM> struct Cfg {
 };
 }  // namespace fr
 
+// raw (split-K over the (it, ih, 64-channel) K-steps, blockIdx.y = split of gridDim.y): this split's fp32 partial
+// tile goes to raw[split][M][Cout] (no residual, rounding or statistics: conv_split_reduce finishes it).
 template <int TM>
 __global__ __launch_bounds__(256, 2) void conv3d_fwd_rows(Geom g, int M, int Cout, int Ls, const bf16* __restrict__ x,
                                                           const bf16* __restrict__ Wt, const bf16* __restrict__ res,
-                                                          bf16* __restrict__ z, float* __restrict__ tstats) {
+                                                          bf16* __restrict__ z, float* __restrict__ tstats,
+                                                          float* __restrict__ raw = nullptr) {
   using namespace fr;
   typedef Cfg<TM> CF;
   constexpr int SQ = CF::SQ, SLAB = CF::SLAB, WB = CF::WB, SL_PER = CF::SL_PER, W_PER = CF::W_PER, ELD = CF::ELD;
@@ -1251,7 +1254,9 @@ __global__ __launch_bounds__(256, 2) void conv3d_fwd_rows(Geom g, int M, int Cou
     a_off[i] = row * RS + (lane >> 4) * 16;
   }
   const int b_off = (lane & 15) * RS + (lane >> 4) * 16;
-  const int ncc = g.C / 64, nks = g.kt * g.kh * ncc;
+  const int ncc = g.C / 64, nks_all = g.kt * g.kh * ncc;
+  const int split = blockIdx.y, nsp = gridDim.y;
+  const int ks0 = (int)((long)nks_all * split / nsp), nks = (int)((long)nks_all * (split + 1) / nsp);
   uint4_t rsl[SL_PER], rw[W_PER];
   __syncthreads();   // the row table
   auto load = [&](int ks) {
@@ -1292,10 +1297,10 @@ __global__ __launch_bounds__(256, 2) void conv3d_fwd_rows(Geom g, int M, int Cou
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 0; j < JB; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
-  load(0);
+  load(ks0);
   store();
   __syncthreads();
-  for (int ks = 0; ks < nks; ++ks) {
+  for (int ks = ks0; ks < nks; ++ks) {
     const bool more = ks + 1 < nks;
     if (more) load(ks + 1);
 #pragma unroll
@@ -1323,7 +1328,8 @@ __global__ __launch_bounds__(256, 2) void conv3d_fwd_rows(Geom g, int M, int Cou
 #pragma unroll
   for (int k = 0; k < TM / 32; ++k) {
     const int m = bm + (tid >> 3) + 32 * k;
-    rq[k] = res && m < M ? *(const uint4_t*)(res + (long)m * Cout + bn + (tid & 7) * 8) : uint4_t{0u, 0u, 0u, 0u};
+    rq[k] = res && !raw && m < M ? *(const uint4_t*)(res + (long)m * Cout + bn + (tid & 7) * 8)
+                                  : uint4_t{0u, 0u, 0u, 0u};
   }
   float* T = (float*)smem;
 #pragma unroll
@@ -1343,6 +1349,12 @@ __global__ __launch_bounds__(256, 2) void conv3d_fwd_rows(Geom g, int M, int Cou
     float v[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) v[j] = T[rr * ELD + cg + j];
+    if (raw) {
+      float* dst = raw + ((long)split * M + m) * Cout + bn + cg;
+      *(floatx4*)dst = floatx4{v[0], v[1], v[2], v[3]};
+      *(floatx4*)(dst + 4) = floatx4{v[4], v[5], v[6], v[7]};
+      continue;
+    }
     if (res) {
       const bf16x8 q = __builtin_bit_cast(bf16x8, rq[k]);
 #pragma unroll
@@ -1350,7 +1362,7 @@ __global__ __launch_bounds__(256, 2) void conv3d_fwd_rows(Geom g, int M, int Cou
     }
     zstore8(z + (long)m * Cout + bn + cg, v);
   }
-  if (tstats) {
+  if (tstats && !raw) {
     // one statistics column per (128-row half, Cout column)
     const int ntm = (M + 127) / 128;
     tile_col_stats<NT>(
@@ -1363,6 +1375,31 @@ __global__ __launch_bounds__(256, 2) void conv3d_fwd_rows(Geom g, int M, int Cou
           tstats[((long)ntm + tm) * Cout + bn + c] = m2;
           if (c == 0 && bn == 0) tile_counts(tstats, ntm, Cout)[tm] = (float)min(128, M - (bm + half * 128));
         });
+  }
+}
+
+// Split-K forward: z = Σ_split raw[split] (+ res), in split order, rounded once (conv3d_fwd_rows' epilogue
+// arithmetic on the summed tile); 8 columns per thread.
+__global__ __launch_bounds__(256) void conv_split_reduce(int M, int Cout, int nsplit, const float* __restrict__ raw,
+                                                         const bf16* __restrict__ res, bf16* __restrict__ z) {
+  const long n8 = (long)M * Cout / 8;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += (long)gridDim.x * blockDim.x) {
+    const long off = i * 8;
+    float v[8];
+    Vec8<float>::load(raw + off, v);
+    for (int sp = 1; sp < nsplit; ++sp) {
+      float w[8];
+      Vec8<float>::load(raw + (long)sp * M * Cout + off, w);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] += w[j];
+    }
+    if (res) {
+      float r[8];
+      Vec8<bf16>::load(res + off, r);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] += r[j];
+    }
+    zstore8(z + off, v);
   }
 }
 
@@ -2012,6 +2049,49 @@ extern "C" long cmhar_conv3d_fwd_stats_floats(const int* dims, int Cout) {
   if (nt <= 0) return -1;
   const int ng = (nt + BN_TG - 1) / BN_TG;
   return 2L * (nt + ng) * Cout + nt + ng;
+}
+
+// Split-K plan for the forward convs whose 128-row tile grid leaves most of the chip idle (R3D-18 layer 4: 3136 rows
+// × 512 outputs = 200 tiles for 512 workgroup slots): the (it, ih, channel-slice) K-steps split over nsplit workgroups
+// per tile, fp32 partials in the caller's workspace, conv_split_reduce sums them in order (+ residual) and rounds
+// once.  No BatchNorm tile statistics (the caller takes the statistics passes over z: small at these sizes).
+// 0 = not this plan.  CMHAR_FWD_SPLIT=0 turns it off (A/B runs).
+static int fwd_split_count(const Geom& g, int Cout) {
+  static const bool on = [] {
+    const char* v = getenv("CMHAR_FWD_SPLIT");
+    return !(v && v[0] == '0');
+  }();
+  if (!on || !igemm_ok(g, Cout)) return 0;
+  Fwd3Plan p3;
+  if (fwd3_plan(g, Cout, p3)) return 0;
+  const int M = g.N * g.To * g.Ho * g.Wo;
+  const int Ls = (g.Wo - 1) * g.sw + g.kw;
+  if (g.kw != 3 || Cout % fr::TN || g.Wo > 255 || Ls > 255 || (long)g.N * g.T * g.H * g.W >= (1L << 30)) return 0;
+  if ((long)((128 + g.Wo - 2) / g.Wo + 1) * Ls > fr::Cfg<128>::SQ) return 0;
+  const long t128 = (long)((M + 127) / 128) * (Cout / fr::TN);
+  if (t128 >= 256) return 0;
+  const int nks = g.kt * g.kh * (g.C / 64);
+  const int s = (int)std::min<long>(4, (512 + t128 - 1) / t128);
+  return s >= 2 && nks >= 2 * s ? s : 0;
+}
+extern "C" long cmhar_conv3d_fwd_split_ws(const int* dims, int Cout) {
+  const Geom g = make_geom(dims);
+  const int s = fwd_split_count(g, Cout);
+  return s ? (long)s * g.N * g.To * g.Ho * g.Wo * Cout : 0;
+}
+extern "C" int cmhar_conv3d_fwd_split(const int* dims, int Cout, const void* x, const void* w, const void* res,
+                                      void* z, float* ws, hipStream_t stream) {
+  const Geom g = make_geom(dims);
+  const int s = fwd_split_count(g, Cout);
+  if (!s || !ws) return -1;
+  const int M = g.N * g.To * g.Ho * g.Wo;
+  const int Ls = (g.Wo - 1) * g.sw + g.kw;
+  const int t128 = ((M + 127) / 128) * (Cout / fr::TN);
+  conv3d_fwd_rows<128><<<dim3(t128, s), 256, 0, stream>>>(g, M, Cout, Ls, (const bf16*)x, (const bf16*)w, nullptr,
+                                                         nullptr, nullptr, ws);
+  conv_split_reduce<<<grid_for((long)M * Cout / 8), 256, 0, stream>>>(M, Cout, s, ws, (const bf16*)res, (bf16*)z);
+  CMHAR_CHECK_LAUNCH();
+  return 0;
 }
 
 extern "C" int cmhar_conv3d_fwd(const int* dims, int Cout, const void* x, const void* w, const void* res, void* z,

@@ -288,6 +288,12 @@ int cmhar_conv3d_im2col(int in_dtype, int out_dtype, const int* dims, const void
  * dzᵀ · col(x), split over M into ws (cmhar_conv3d_wgrad_ws floats; 0 = no workspace), reduced in a fixed order. */
 int cmhar_conv3d_fwd(const int* dims, int Cout, const void* x, const void* w, const void* res, void* z,
                      float* tile_stats, hipStream_t stream);
+/* Split-K forward for the convs whose output tile grid leaves most of the chip idle (R3D-18 layer 4): ws fp32
+ * floats = cmhar_conv3d_fwd_split_ws(dims, Cout) (0: not this plan — call cmhar_conv3d_fwd); z = conv(x) (+ res),
+ * no BatchNorm tile statistics (the caller's BatchNorm takes its own statistics passes). */
+long cmhar_conv3d_fwd_split_ws(const int* dims, int Cout);
+int cmhar_conv3d_fwd_split(const int* dims, int Cout, const void* x, const void* w, const void* res, void* z, float* ws,
+                           hipStream_t stream);
 /* tile_stats (nullable): per row tile of z and channel, the mean and Σ(v − mean)² of the bf16 outputs and each
  * tile's row count, consumed by cmhar_bn_cl_fwd_tiles (training-mode BatchNorm3d of z without a statistics pass).
  * cmhar_conv3d_fwd_tiles gives the tile count ntile of the forward's plan (-1: not an implicit-GEMM conv) and

@@ -496,3 +496,43 @@ def test_bn_bwd_nores_rounding_boundaries(relu):
         assert bad.numel() == 0, [(tuple(i), ws[int(i[-1])], float(y.view(-1, C)[int(i[0]), int(i[-1])])
                                    if a.dim() == 2 else None, float(a[tuple(i)]), float(b[tuple(i)]))
                                   for i in bad[:6].tolist()]
+
+
+@pytest.mark.parametrize('res', [False, True])
+def test_conv3d_fwd_split_layer4(res):
+    """The split-K implicit-GEMM forward at R3D-18 layer 4's geometry (batch 32: 32×2×7×7 = 3136 output rows, 512 → 512,
+    3×3×3 'same'): planned (`cmhar_conv3d_fwd_split_ws` > 0), against the fp32 conv of the same bf16 operands (+ the
+    residual, as the dgrad call adds dx_acc) within the bf16 output rounding, and within one bf16 ulp (of the value or of
+    the output's rms near zero) of the unsplit kernel (`cmhar_conv3d_fwd`, the same products summed in a different order)."""
+    from cmhar import _lib as L
+    from cmhar import kernels as K
+    from cmhar import r3d
+    torch.manual_seed(9)
+    N, C, T, S = 32, 512, 2, 7
+    conv = torch.nn.Conv3d(C, C, 3, 1, 1, bias=False)
+    x = torch.randn(N, C, T, S, S).bfloat16().float()
+    wq = conv.weight.detach().bfloat16().float()
+    ref = F.conv3d(x.to(DEV), wq.to(DEV), padding=1)
+    conv = conv.to(DEV)
+    xc = x.permute(0, 2, 3, 4, 1).contiguous().to(DEV).bfloat16()
+    shp = tuple(xc.shape)
+    Kp = r3d._r8(conv.weight[0].numel())
+    wp = r3d._pack(conv, torch.bfloat16)
+    M = N * T * S * S
+    dims = r3d._dims(shp, conv, Kp)
+    n = L.lib().cmhar_conv3d_fwd_split_ws(dims, C)
+    assert n > 0 and n % (M * C) == 0
+    rr = torch.randn(M, C, device=DEV).bfloat16() if res else None
+    z = torch.empty(M, C, dtype=torch.bfloat16, device=DEV)
+    ws = K.workspace(n, xc.device)
+    L.call('cmhar_conv3d_fwd_split', dims, C, xc.data_ptr(), wp.data_ptr(), None if rr is None else rr.data_ptr(),
+           z.data_ptr(), ws.data_ptr(), L.stream(xc.device))
+    z1 = torch.empty_like(z)
+    L.call('cmhar_conv3d_fwd', dims, C, xc.data_ptr(), wp.data_ptr(), None if rr is None else rr.data_ptr(),
+           z1.data_ptr(), None, L.stream(xc.device))
+    torch.cuda.synchronize()
+    want = ref.permute(0, 2, 3, 4, 1).reshape(M, C) + (rr.float() if res else 0.)
+    assert rel(z.float(), want) < 5e-3
+    # (near-zero outputs: the summation-order difference is absolute, ~1e-6 of the accumulated magnitude)
+    tol = torch.maximum(z1.float().abs(), z1.float().pow(2).mean().sqrt()) * 2.0 ** -7
+    assert bool(((z.float() - z1.float()).abs() <= tol).all())
