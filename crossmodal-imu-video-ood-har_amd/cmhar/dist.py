@@ -21,8 +21,12 @@ collective sequence whatever order its hooks fire in:
   bucket is flattened into its persistent buffer on a communication stream that waits on every stream that
   produced its gradients, and launched; `finish()` scatters the reduced values back into `.grad`.
 Parameters whose gradient stays None on every rank (unused parameters such as `CrossModalModel.temperature`)
-are skipped consistently: after the first step they sit in one trailing bucket, reduced in `finish()` over its
-non-None gradients (every rank must agree on which gradients are None, as under DataParallel).
+sit, after the first step, in one trailing bucket reduced in `finish()`.  Every hook bucket is all-reduced at its
+full size on every rank (a gradient that is None on this rank contributes zeros), so ranks that disagree on which
+gradients are None in a later step still issue identical collectives: a parameter that received gradients in the
+first step gets the sum of the other ranks' even where its own is None (DataParallel's reduce-add over replicas);
+one of the trailing bucket's keeps None where it had none locally (the first step's agreement check covers that
+step only).
 """
 from __future__ import annotations
 
@@ -115,11 +119,12 @@ def sink_param_order(backbone) -> List[torch.nn.Parameter]:
 
 
 class _Bucket:
-    __slots__ = ('params', 'kind', 'start', 'end', 'ready', 'launched', 'flat', 'live', 'streams')
+    __slots__ = ('params', 'kind', 'start', 'end', 'ready', 'launched', 'flat', 'live', 'streams', 'fill')
 
-    def __init__(self, params, kind, start=0, end=0):
+    def __init__(self, params, kind, start=0, end=0, fill=False):
         self.params, self.kind, self.start, self.end = params, kind, start, end
         self.ready, self.launched, self.flat, self.live, self.streams = set(), False, None, None, {}
+        self.fill = fill      # hook bucket: a parameter with no local gradient gets the reduced sum as its .grad
 
 
 def _cut(params, limit):
@@ -201,8 +206,8 @@ class GradReducer:
             for p in self.rest:
                 self._hooks.append(p.register_post_accumulate_grad_hook(self._on_hook))
 
-    def _set_hook_buckets(self, groups):
-        self.buckets = self.buckets[:self.n_sink] + [_Bucket(g, 'hook') for g in groups]
+    def _set_hook_buckets(self, groups, n_fill=0):
+        self.buckets = self.buckets[:self.n_sink] + [_Bucket(g, 'hook', fill=i < n_fill) for i, g in enumerate(groups)]
         self._bucket_of = {p: i for i, b in enumerate(self.buckets) for p in b.params}
 
     def _comm_stream(self, device):
@@ -260,29 +265,37 @@ class GradReducer:
             self.pending.append(dist.all_reduce(self.sink.flat[b.start:b.end], group=self.group, async_op=True))
             self.n_collectives += 1
         else:
-            live = [p for p in b.params if p.grad is not None]
-            b.live = live
-            if live:
-                dev = live[0].grad.device
-                comm = self._comm_stream(dev)
-                if comm is None:
-                    self._flatten_and_reduce(b, live)
-                else:
-                    cur = torch.cuda.current_stream(dev)
-                    comm.wait_stream(cur)
-                    for s in b.streams.values():
-                        if s.cuda_stream != comm.cuda_stream:
-                            comm.wait_stream(s)
-                    with torch.cuda.stream(comm):
-                        self._flatten_and_reduce(b, live)
+            # every rank reduces the bucket at its full size (zeros for gradients that are None here), so the
+            # collective is the same on every rank whichever gradients each produced
+            b.live = [p for p in b.params if p.grad is not None]
+            dev = b.params[0].device
+            comm = self._comm_stream(dev)
+            if comm is None:
+                self._flatten_and_reduce(b)
+            else:
+                cur = torch.cuda.current_stream(dev)
+                comm.wait_stream(cur)
+                for s in b.streams.values():
+                    if s.cuda_stream != comm.cuda_stream:
+                        comm.wait_stream(s)
+                with torch.cuda.stream(comm):
+                    self._flatten_and_reduce(b)
         b.launched = True
 
-    def _flatten_and_reduce(self, b, live):
-        n = sum(p.numel() for p in live)
-        dev = live[0].grad.device
+    def _flatten_and_reduce(self, b):
+        n = sum(p.numel() for p in b.params)
+        dev = b.params[0].device
         if b.flat is None or b.flat.numel() != n or b.flat.device != dev:
             b.flat = torch.empty(n, dtype=torch.float32, device=dev)
-        torch.cat([p.grad.reshape(-1).float() for p in live], out=b.flat)
+        if len(b.live) == len(b.params):
+            torch.cat([p.grad.reshape(-1).float() for p in b.params], out=b.flat)
+        else:
+            b.flat.zero_()
+            off = 0
+            for p in b.params:
+                if p.grad is not None:
+                    b.flat[off:off + p.numel()].copy_(p.grad.reshape(-1))
+                off += p.numel()
         self.pending.append(dist.all_reduce(b.flat, group=self.group, async_op=True))
         self.n_collectives += 1
 
@@ -312,12 +325,16 @@ class GradReducer:
         self.pending = []
         dst, src = [], []
         for b in self.buckets:
-            if b.kind == 'hook' and b.live:
+            if b.kind == 'hook' and b.launched and b.flat is not None:
                 off = 0
-                for p in b.live:
+                for p in b.params:
                     n = p.numel()
-                    dst.append(p.grad)
-                    src.append(b.flat[off:off + n].view_as(p.grad))
+                    red = b.flat[off:off + n].view_as(p)
+                    if p.grad is not None:
+                        dst.append(p.grad)
+                        src.append(red)
+                    elif b.fill:           # used in the first step on every rank, no gradient here this step
+                        p.grad = red.clone()
                     off += n
         if dst:
             torch._foreach_copy_(dst, src)     # the reduced values back into .grad: one multi-tensor launch
@@ -355,9 +372,10 @@ class GradReducer:
         fired_set = set(fired)
         never = [p for p in reversed(self.rest) if p not in fired_set]
         groups = _cut(fired, self.limit)
+        n_fill = len(groups)
         if never:
             groups.append(never)   # unused parameters: one trailing bucket, reduced in finish()
-        self._set_hook_buckets(groups)
+        self._set_hook_buckets(groups, n_fill)
         self._fired = []
         self.learned = True
 

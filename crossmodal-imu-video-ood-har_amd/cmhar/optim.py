@@ -86,8 +86,9 @@ class FusedAdamW(torch.optim.Optimizer):
     `write_clipped_grad=True` (default) the AdamW pass also stores the clipped gradient back, so `.grad` after the
     step is exactly what `clip_grad_norm_` leaves; `False` leaves `.grad` unclipped (saves that write too).  The
     total norm of the last step is `last_grad_norm` (0-dim device tensor, as `clip_grad_norm_` returns).
-    Gradients in `clip_params` that the optimizer does not own enter the norm and are scaled in place by the clip
-    coefficient (one multi-tensor multiply), exactly as `clip_grad_norm_` would leave them."""
+    Gradients in `clip_params` that the optimizer does not own enter the norm; with `write_clipped_grad=True` they are
+    scaled in place by the clip coefficient (one multi-tensor multiply), exactly as `clip_grad_norm_` would leave them,
+    with `False` they are left unclipped like the owned ones (every `.grad` then holds the unclipped gradient)."""
 
     def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-2, shadow_sources=(),
                  max_grad_norm=None, write_clipped_grad=True, clip_params=None):
@@ -130,7 +131,7 @@ class FusedAdamW(torch.optim.Optimizer):
                 norm_out = _grad_norm(allp, float(self.max_grad_norm), apply_clip=False)
                 self.last_grad_norm = norm_out[0]
                 gscale = norm_out
-                if extra:      # clipped like clip_grad_norm_ leaves them; the owned ones inside the AdamW pass
+                if extra and self.write_clipped_grad:   # as clip_grad_norm_ leaves them (owned: in the AdamW pass)
                     torch._foreach_mul_(extra, norm_out[1])
         for gi, group in enumerate(self.param_groups):
             b1, b2 = group['betas']

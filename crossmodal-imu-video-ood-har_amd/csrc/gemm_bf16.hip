@@ -459,8 +459,11 @@ typedef __attribute__((address_space(3))) void* lds_void_ptr;
 // phase, draining the next K-tile's prefetch three times per K-tile (asm issue: weight gradients 14–19 % faster,
 // `gpurun_out/r04w_gemm_ab.log`).  Used by the instantiations with transposed reads (CMHAR_GEMM8P_ASM_DMA = 0: the
 // builtin everywhere).  The kernel orders every DMA itself (counted vmcnt +
-// barriers, as with the builtin).  src: the tile origin at this K-slice (wave-uniform); M0 is written here and no
-// compiler-generated code in these kernels uses M0 (no builtin DMA left in an ASM instantiation; checked in the .s).
+// barriers, as with the builtin).  src: the tile origin at this K-slice (wave-uniform).  M0 is written here without
+// the compiler knowing (M0 is a reserved register: clang accepts it on a clobber list only with a warning that the
+// clobber may not be honoured), so an instantiation that issues its DMA this way must contain NO compiler-generated
+// M0 use: both operands of a kernel take the same kAD choice, and the one builtin LDS-DMA that could share a K loop
+// with it (gemm256's L2 prefetch, CMHAR_GEMM_L2PF) is compiled out of kAD instantiations (static_assert there).
 __device__ __forceinline__ void dma_asm(const char* src, char* lds, int voff) {
   const unsigned long long a = (unsigned long long)src;
   uint4_t rs;
@@ -568,8 +571,10 @@ __global__ __launch_bounds__(NT2, 2) void gemm256_kernel(int M, int N, int K, co
                                                          long ldc, Epilogue e, int klen, long split_stride,
                                                          int raw_out, float* __restrict__ sk_ws, int n_dp,
                                                          int sk_klen) {
-  constexpr bool PF = CMHAR_GEMM_L2PF && NA == 2 && MODE == 0;
   constexpr bool kAD = CMHAR_GEMM8P_ASM_DMA && (!A_KC || !B_KC);   // see dma_asm
+  // the L2 prefetch is a builtin LDS-DMA (compiler-managed M0): never in a K loop whose DMA the asm issues
+  constexpr bool PF = CMHAR_GEMM_L2PF && NA == 2 && MODE == 0 && !kAD;
+  static_assert(!(PF && kAD), "builtin LDS-DMA (L2 prefetch) beside asm-issued DMA: M0 is not tracked across dma_asm");
   __shared__ __attribute__((aligned(16))) char smem[NA == 3 ? 163840 : SMEM2 + (PF ? 2048 : 0)];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);

@@ -131,9 +131,10 @@ def test_dataparallel_rccl_single_rank(tmp_path, backbone):
     res, sums = _run(tmp_path, backbone, 'bf16', world=1, backend='nccl', force_reduce=True)
     r0 = res[0]
     assert r0['backend'] == 'nccl'
-    # one all-reduce per bucket, except the trailing bucket of never-used parameters (no gradients to reduce)
+    # one all-reduce per bucket — the trailing bucket of never-used parameters too (full-size hook buckets on every
+    # rank, zeros for gradients that are None: the collective never depends on which gradients a rank produced)
     assert sorted(r0['trailing_unused']) == ['bias', 'temperature'], r0['trailing_unused']
-    assert r0['n_collectives'] == r0['n_buckets'] - 1 and r0['n_collectives'] >= 2, r0
+    assert r0['n_collectives'] == r0['n_buckets'] and r0['n_collectives'] >= 3, r0
     assert r0['learned'] and r0['launched_before_finish'] == r0['n_buckets'] - 1, r0
     assert r0['missing'] == []
     bad = {n: e for n, (e, norm) in r0['grad_errs'].items() if e != 0.0}

@@ -279,6 +279,9 @@ def _attn_ref(q, k, v, B, H, Lq, Lk, D, scale):
 
 @pytest.mark.parametrize('L_', [64, 200, 1568])
 def test_flash_attention_bf16_fwd_bwd(L_):
+    """O, dQ, dK, dV vs torch fp32 autograd, each within 3x the error of the same algorithm with the kernel's bf16
+    roundings emulated + 1e-3 (tests/flash_ref.py)."""
+    from flash_ref import check_flash
     torch.manual_seed(2)
     B, H, D = 2, 3, 64
     scale = D ** -0.5
@@ -287,17 +290,12 @@ def test_flash_attention_bf16_fwd_bwd(L_):
     o = torch.empty(B * L_, H * D, dtype=torch.bfloat16, device=DEV)
     lse = torch.empty(B * H * L_, device=DEV)
     K().attention_fwd(q, k, v, o, lse, B=B, H=H, Lq=L_, Lk=L_, D=D, scale=scale)
-    qr, kr, vr = (t.float().clone().requires_grad_(True) for t in (q, k, v))
-    ref = _attn_ref(qr, kr, vr, B, H, L_, L_, D, scale)
-    assert rel(o, ref) < 1e-2
     do = torch.randn(B * L_, H * D, device=DEV).bfloat16()
-    gq, gk, gv = torch.autograd.grad(ref, (qr, kr, vr), do.float())
     dqkv = torch.empty_like(qkv)
     K().attention_bwd(q, k, v, o, do, lse, dqkv[:, :H * D], dqkv[:, H * D:2 * H * D], dqkv[:, 2 * H * D:],
                       B=B, H=H, Lq=L_, Lk=L_, D=D, scale=scale)
-    assert rel(dqkv[:, :H * D], gq) < 2e-2
-    assert rel(dqkv[:, H * D:2 * H * D], gk) < 2e-2
-    assert rel(dqkv[:, 2 * H * D:], gv) < 2e-2
+    got = {'o': o, 'dq': dqkv[:, :H * D], 'dk': dqkv[:, H * D:2 * H * D], 'dv': dqkv[:, 2 * H * D:]}
+    check_flash(got, q, k, v, do, B=B, H=H, Lq=L_, Lk=L_, D=D, scale=scale)
 
 
 @pytest.mark.parametrize('Lq,Lk', [(1568, 1568), (129, 257), (32, 200), (1, 64), (300, 33), (26, 3136), (13, 392),
@@ -305,8 +303,10 @@ def test_flash_attention_bf16_fwd_bwd(L_):
 def test_flash_attention_ragged_tails(Lq, Lk):
     """The split-sequence tail kernels (csrc/attention.hip, tails of <= 64 queries / keys past the last full block, in
     workgroups of 32 rows — 3136 = 12·256 + 64 is the 32-frame geometry):
-    forward O, dQ, dK, dV vs torch fp32 autograd, with the TAIL rows checked on their own (a tail bug would hide in a
-    whole-tensor norm), at cross-attention shapes (Lq != Lk) including a whole-tail-only sequence (Lq <= 32)."""
+    forward O, dQ, dK, dV vs torch fp32 autograd within 3x the emulated bf16-rounding error + 1e-3, with the TAIL rows
+    checked on their own (a tail bug would hide in a whole-tensor norm), at cross-attention shapes (Lq != Lk)
+    including a whole-tail-only sequence (Lq <= 32)."""
+    from flash_ref import check_flash
     torch.manual_seed(13)
     B, H, D = 2, 2, 64
     scale = D ** -0.5
@@ -316,29 +316,24 @@ def test_flash_attention_ragged_tails(Lq, Lk):
     o = torch.empty(B * Lq, H * D, dtype=torch.bfloat16, device=DEV)
     lse = torch.empty(B * H * Lq, device=DEV)
     K().attention_fwd(q, k, v, o, lse, B=B, H=H, Lq=Lq, Lk=Lk, D=D, scale=scale)
-    qr, kr, vr = (t.float().clone().requires_grad_(True) for t in (q, k, v))
-    ref = _attn_ref(qr, kr, vr, B, H, Lq, Lk, D, scale)
     do = torch.randn(B * Lq, H * D, device=DEV).bfloat16()
-    gq, gk, gv = torch.autograd.grad(ref, (qr, kr, vr), do.float())
     dq = torch.empty_like(q)
     dkv = torch.empty_like(kv)
     K().attention_bwd(q, k, v, o, do, lse, dq, dkv[:, :H * D], dkv[:, H * D:], B=B, H=H, Lq=Lq, Lk=Lk, D=D,
                       scale=scale)
     qt = (Lq // 128) * 128 if Lq % 128 else max(Lq - 128, 0)      # first row of the query tail region
     kt = (Lk // 128) * 128 if Lk % 128 else max(Lk - 128, 0)
-    rows_q = lambda t, r0: t.view(B, -1, t.shape[-1])[:, r0:]     # noqa: E731
-    for got, want, r0, tol in ((o, ref, qt, 1e-2), (dq, gq, qt, 2e-2), (dkv[:, :H * D], gk, kt, 2e-2),
-                               (dkv[:, H * D:], gv, kt, 2e-2)):
-        assert rel(got, want) < tol
-        assert rel(rows_q(got, r0), rows_q(want, r0)) < tol
+    got = {'o': o, 'dq': dq, 'dk': dkv[:, :H * D], 'dv': dkv[:, H * D:]}
+    check_flash(got, q, k, v, do, B=B, H=H, Lq=Lq, Lk=Lk, D=D, scale=scale, row_ranges={'q': qt, 'k': kt})
 
 
 @pytest.mark.parametrize('L_', [200, 1568])
 def test_flash_attention_prescaled_keys(L_):
     """The VideoMAE bf16 training form: the QKV GEMM's epilogue writes K pre-scaled by scale·log2(e) (colscale), the
     forward runs with scale = 1/log2(e) and cmhar_attention_bwd_prescaled returns dQ, dV and the gradient of the
-    UNSCALED key — vs torch fp32 autograd on the unscaled operands, at the plain flash kernels' bounds; and the
-    colscale epilogue itself against the unscaled GEMM (same fp32 product, one rounding)."""
+    UNSCALED key — vs torch fp32 autograd on the unscaled operands within 3x the emulated bf16-rounding error + 1e-3;
+    and the colscale epilogue itself against the unscaled GEMM (same fp32 product, one rounding)."""
+    from flash_ref import check_flash
     torch.manual_seed(12)
     B, H, D = 2, 3, 64
     Hd, scale = H * D, D ** -0.5
@@ -354,18 +349,12 @@ def test_flash_attention_prescaled_keys(L_):
     o = torch.empty(B * L_, Hd, dtype=torch.bfloat16, device=DEV)
     lse = torch.empty(B * H * L_, device=DEV)
     K().attention_fwd(q, kp, v, o, lse, B=B, H=H, Lq=L_, Lk=L_, D=D, scale=1.0 / K().LOG2E)
-    qr, vr = q.float().clone().requires_grad_(True), v.float().clone().requires_grad_(True)
-    kr = (kp.float() / c).requires_grad_(True)                # the unscaled key the model means
-    ref = _attn_ref(qr, kr, vr, B, H, L_, L_, D, scale)
-    assert rel(o, ref) < 1e-2
     do = torch.randn(B * L_, Hd, device=DEV).bfloat16()
-    gq, gk, gv = torch.autograd.grad(ref, (qr, kr, vr), do.float())
     dqkv = torch.empty_like(qkv)
     K().attention_bwd_prescaled(q, kp, v, o, do, lse, dqkv[:, :Hd], dqkv[:, Hd:2 * Hd], dqkv[:, 2 * Hd:],
                                 B=B, H=H, Lq=L_, Lk=L_, D=D, scale=scale)
-    assert rel(dqkv[:, :Hd], gq) < 2e-2
-    assert rel(dqkv[:, Hd:2 * Hd], gk) < 2e-2
-    assert rel(dqkv[:, 2 * Hd:], gv) < 2e-2
+    got = {'o': o, 'dq': dqkv[:, :Hd], 'dk': dqkv[:, Hd:2 * Hd], 'dv': dqkv[:, 2 * Hd:]}
+    check_flash(got, q, kp.float() / c, v, do, B=B, H=H, Lq=L_, Lk=L_, D=D, scale=scale)
 
 
 @pytest.mark.parametrize('D', [16, 64])
@@ -622,16 +611,17 @@ def test_fused_adamw_clip_params_beyond_owned():
 
 
 def test_mfma_peak_probe():
-    """csrc/probe.hip (the on-box MFMA peak bench.py reports as roofline.peak_measured): a plausible dense bf16 rate —
-    above 900 TF/s (the chip lowers its clock under dense MFMA load on random data: r04 measured 1414) and below
-    2.6 PF — and finite accumulator sums."""
+    """csrc/probe.hip (the on-box MFMA peak bench.py reports as roofline.peak_measured): a plausible dense bf16 rate
+    per shape — above 1400 TF/s (the chip lowers its clock under dense MFMA load on random data; the 8-chain probe read
+    1480-1832 TF/s on 32x32x16 and 1736-1971 on 16x16x32 across the round-4 boxes, so 1400 is ~0.8x the lowest) and
+    below the 2.5 PF vendor peak."""
     import bench
     shapes = {}
     tf = bench.measure_mfma_peak(torch.device(DEV), blocks=1024, iters=4000, reps=2, per_shape=shapes)
     print(f'MFMA peak probe: {tf:.1f} TFLOP/s', shapes)
     assert set(shapes) == {'32x32x16', '16x16x32'} and tf == max(shapes.values())
     for v in shapes.values():       # DVFS: random-data MFMA loops hold ≈1.9 GHz (MICROARCH DVFS give-back)
-        assert 900.0 < v < 2600.0, shapes
+        assert 1400.0 < v < 2500.0, shapes
 
 
 def test_packed_weights_transposed_copies():
