@@ -102,6 +102,8 @@ _SIGS = {
     'cmhar_bn_cl_fwd_tiles': (i32, [i64, i32, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, f32, f32, i32, vp, vp]),
     'cmhar_conv3d_fwd_tiles': (i32, [vp, i32]),
     'cmhar_conv3d_fwd_split_ws': (i64, [vp, i32]),
+    'cmhar_conv3d_fwd_plan': (i32, [vp, i32]),
+    'cmhar_conv3d_wgrad_plan': (i32, [vp, i32]),
     'cmhar_conv3d_fwd_split': (i32, [vp, i32, vp, vp, vp, vp, vp, vp]),
     'cmhar_conv3d_stem_tiles': (i32, [vp, i32]),
     'cmhar_conv3d_stem_stats_floats': (i64, [vp, i32]),

@@ -244,7 +244,12 @@ def _igemm_ok(x, shape, conv, Kp):
     return x.dtype == torch.bfloat16 and shape[4] % 64 == 0 and Kp == conv.weight[0].numel()
 
 
-def _unit_fwd(x, shape, conv, bn, relu, training, save, res=None, wp=None, keep_col=True, wf=None):
+def _conv_fwd(x, shape, conv, wp, stats):
+    """The convolution of a unit, as the step launches it: z [M, Cout] (compute dtype) = conv(x) on the implicit stem
+    (C <= 4), the split-K implicit GEMM (layer-4 geometries), the implicit GEMM (C % 64 == 0), the pointwise GEMM, or
+    im2col + GEMM.  stats: also have the conv epilogue write BatchNorm tile statistics where the kernel can.
+    Returns (z, col, wp, stem, igemm, tstats, ntile); col is the im2col matrix when one was built (or x itself for a
+    pointwise conv), wp the weight pack the conv used (the stem packs its own layout)."""
     oshape = _out_shape(shape, conv)
     M = math.prod(oshape[:4])
     Kp = _r8(conv.weight[0].numel())
@@ -252,21 +257,19 @@ def _unit_fwd(x, shape, conv, bn, relu, training, save, res=None, wp=None, keep_
     z = torch.empty(M, conv.out_channels, dtype=x.dtype, device=x.device)
     stem = _stem_ok(x, shape, conv)
     igemm = not stem and _igemm_ok(x, shape, conv, Kp)
-    tstats = None
+    tstats, ntile, col = None, 0, None
     if stem:
         # implicit stem: no column matrix; the packed [64, kt·kh·32] weight replaces the im2col-order pack
-        col = None
         wp = _pack_stem(conv)
         dims = _dims(shape, conv, _stem_kp(conv))
-        if training and bn.track_running_stats:
+        if stats:
             ntile = L.lib().cmhar_conv3d_stem_tiles(dims, 64)
             tstats = K.workspace(L.lib().cmhar_conv3d_stem_stats_floats(dims, 64), x.device)
         call('cmhar_conv3d_stem_fwd', dims, 64, ptr(x), ptr(wp), ptr(z), ptr(tstats), L.stream(x.device))
     elif igemm:
-        col = None
         dims = _dims(shape, conv, Kp)
         if not _conv_fwd_split(dims, conv.out_channels, x, wp, None, z):
-            if training and bn.track_running_stats:      # BN statistics from the conv epilogue (no statistics pass)
+            if stats:      # BN statistics from the conv epilogue (no statistics pass)
                 ntile = L.lib().cmhar_conv3d_fwd_tiles(dims, conv.out_channels)
                 tstats = K.workspace(L.lib().cmhar_conv3d_fwd_stats_floats(dims, conv.out_channels), x.device)
             call('cmhar_conv3d_fwd', dims, conv.out_channels, ptr(x), ptr(wp), None, ptr(z), ptr(tstats),
@@ -277,6 +280,15 @@ def _unit_fwd(x, shape, conv, bn, relu, training, save, res=None, wp=None, keep_
     else:
         col = _im2col(x, shape, conv, Kp, rows)
         K.gemm(0, col[:M], wp, z)
+    return z, col, wp, stem, igemm, tstats, ntile
+
+
+def _unit_fwd(x, shape, conv, bn, relu, training, save, res=None, wp=None, keep_col=True, wf=None):
+    oshape = _out_shape(shape, conv)
+    M = math.prod(oshape[:4])
+    Kp = _r8(conv.weight[0].numel())
+    rows = _r8(M) if x.dtype == torch.bfloat16 else M
+    z, col, wp, stem, igemm, tstats, ntile = _conv_fwd(x, shape, conv, wp, training and bn.track_running_stats)
     if tstats is not None:
         y, sm, sr = _bn_fwd_tiles(z, bn, res, relu, tstats, ntile)
     else:
@@ -410,23 +422,37 @@ def _unit_bwd(u, dy, grads, training, need_dx, want_dres, dx_acc=None):
     _bn_bwd(u, dy, dz, dres, dw_bn, db_bn, training)
     _grad_acc(dw_bn, acc_w)
     _grad_acc(db_bn, acc_b)
+    if u.stem and need_dx:
+        raise RuntimeError('the implicit stem has no input gradient (its input is the video)')
+    dwp = _conv_wgrad(u, dz)
     w = u.conv.weight
     if u.stem:
+        _store_wgrad(u.conv, dwp, 32, 4, grads)
+    else:
+        _store_wgrad(u.conv, dwp, w.shape[4] * w.shape[1], w.shape[1], grads)
+    _unit_grads_done(grads, u)
+    dx = _conv_dgrad(u, dz, dx_acc) if need_dx else None
+    return dx, dres
+
+
+def _conv_wgrad(u, dz):
+    """Weight gradient of a unit's conv from dz ([rows, Cout], rows past M zero): fp32 in the packed layout the
+    forward used — [Cout, Kp] in the im2col k order, or [64, kt·kh·32] for the implicit stem.  Implicit stem / row
+    slab / nine-tap / gather kernels with their split reduces, or dzᵀ · col on the GEMM (split-K)."""
+    Cc = dz.shape[1]
+    dev = dz.device
+    if u.stem:
         dims = _dims(u.shape, u.conv, _stem_kp(u.conv))
-        dw4 = torch.empty(Cc, _stem_kp(u.conv), dtype=torch.float32, device=dy.device)
-        ws = K.workspace(L.lib().cmhar_conv3d_stem_wgrad_ws(dims, Cc), dy.device)
-        call('cmhar_conv3d_stem_wgrad', dims, Cc, ptr(u.x), ptr(dz), ptr(dw4), ptr(ws), L.stream(dy.device))
-        _store_wgrad(u.conv, dw4, 32, 4, grads)
-        _unit_grads_done(grads, u)
-        if need_dx:
-            raise RuntimeError('the implicit stem has no input gradient (its input is the video)')
-        return None, dres
-    dwp = torch.empty(Cc, u.Kp, dtype=torch.float32, device=dy.device)
+        dw4 = torch.empty(Cc, _stem_kp(u.conv), dtype=torch.float32, device=dev)
+        ws = K.workspace(L.lib().cmhar_conv3d_stem_wgrad_ws(dims, Cc), dev)
+        call('cmhar_conv3d_stem_wgrad', dims, Cc, ptr(u.x), ptr(dz), ptr(dw4), ptr(ws), L.stream(dev))
+        return dw4
+    dwp = torch.empty(Cc, u.Kp, dtype=torch.float32, device=dev)
     if u.igemm:
         dims = _dims(u.shape, u.conv, u.Kp)
         n = L.lib().cmhar_conv3d_wgrad_ws(dims, Cc)
-        ws = K.workspace(n, dy.device) if n > 0 else None
-        call('cmhar_conv3d_wgrad', dims, Cc, ptr(u.x), ptr(dz), ptr(dwp), ptr(ws), L.stream(dy.device))
+        ws = K.workspace(n, dev) if n > 0 else None
+        call('cmhar_conv3d_wgrad', dims, Cc, ptr(u.x), ptr(dz), ptr(dwp), ptr(ws), L.stream(dev))
     else:
         col = u.col if u.col is not None else _im2col(u.x, u.shape, u.conv, u.Kp, u.rows)
         u.col = None
@@ -438,28 +464,34 @@ def _unit_bwd(u, dy, grads, training, need_dx, want_dres, dx_acc=None):
             splits = max(1, min(1024 // tiles, u.rows // 4096))
         K.gemm(2, dz, col, dwp, splits=splits)
         del col
-    _store_wgrad(u.conv, dwp, w.shape[4] * w.shape[1], w.shape[1], grads)
-    _unit_grads_done(grads, u)
-    dx = None
-    if need_dx and u.igemm and _dgrad_igemm_ok(u.conv):
-        dx = _dgrad_igemm(dz, u.conv, u.oshape, u.x, dx_acc, u.wf)
-    elif need_dx and _pointwise(u.conv, u.shape, u.Kp, M, u.rows):
+    return dwp
+
+
+def _conv_dgrad(u, dz, dx_acc=None):
+    """Input gradient of a unit's conv (+ dx_acc, the residual-branch gradient, when given): the flipped-weight
+    implicit GEMM for stride-1 'same' convs (split-K where the forward plan splits), dz · W for a pointwise conv,
+    else dcol = dz · W on the GEMM + col2im.  Returns dx shaped like u.x (dx_acc itself when accumulating in place)."""
+    M = math.prod(u.oshape[:4])
+    dt = dz.dtype
+    dev = dz.device
+    if u.igemm and _dgrad_igemm_ok(u.conv):
+        return _dgrad_igemm(dz, u.conv, u.oshape, u.x, dx_acc, u.wf)
+    if _pointwise(u.conv, u.shape, u.Kp, M, u.rows):
         # 1×1 stride-1: dx = dz·W directly (the col2im of a pointwise conv is the identity); the residual-branch
         # gradient is added in the GEMM epilogue (element-wise read-then-write of the same buffer)
         if dx_acc is not None:
             dxv = dx_acc.reshape(M, u.Kp)
             K.gemm(1, dz[:M], u.wp, dxv, residual=dxv)
-            dx = dx_acc
-        else:
-            dx = torch.empty_like(u.x)
-            K.gemm(1, dz[:M], u.wp, dx.reshape(M, u.Kp))
-    elif need_dx:
-        dcol = torch.empty(M, u.Kp, dtype=dt, device=dy.device)
-        K.gemm(1, dz[:M], u.wp, dcol)
-        dx = dx_acc if dx_acc is not None else torch.empty_like(u.x)
-        call('cmhar_conv3d_col2im', L.dtype_code(dt), _dims(u.shape, u.conv, u.Kp), ptr(dcol), ptr(dx),
-             int(dx_acc is not None), L.stream(dy.device))
-    return dx, dres
+            return dx_acc
+        dx = torch.empty_like(u.x)
+        K.gemm(1, dz[:M], u.wp, dx.reshape(M, u.Kp))
+        return dx
+    dcol = torch.empty(M, u.Kp, dtype=dt, device=dev)
+    K.gemm(1, dz[:M], u.wp, dcol)
+    dx = dx_acc if dx_acc is not None else torch.empty_like(u.x)
+    call('cmhar_conv3d_col2im', L.dtype_code(dt), _dims(u.shape, u.conv, u.Kp), ptr(dcol), ptr(dx),
+         int(dx_acc is not None), L.stream(dev))
+    return dx
 
 
 # ------------------------------------------------------------------------------------------------------------

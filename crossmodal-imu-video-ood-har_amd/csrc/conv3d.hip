@@ -2094,24 +2094,20 @@ extern "C" int cmhar_conv3d_fwd_split(const int* dims, int Cout, const void* x, 
   return 0;
 }
 
-extern "C" int cmhar_conv3d_fwd(const int* dims, int Cout, const void* x, const void* w, const void* res, void* z,
-                                float* tile_stats, hipStream_t stream) {
-  const Geom g = make_geom(dims);
+// Launch plan of cmhar_conv3d_fwd (exported as cmhar_conv3d_fwd_plan so tests pin the kernel a geometry takes):
+// 1 = nine-tap conv3d_fwd_rows3 (Cout = 64, 3x3 taps at unit H/W stride), 2 = row-slab conv3d_fwd_rows<128>,
+// 3 = row-slab conv3d_fwd_rows<256>, 4 = generic conv3d_fwd_igemm 128x64, 5 = generic conv3d_fwd_igemm 128x128;
+// -1 = not an implicit-GEMM geometry.  (The split-K plan is the caller's choice: cmhar_conv3d_fwd_split_ws > 0.)
+// CMHAR_FWD_ROWS=0: the generic gather kernel instead of the row-slab ones (A/B runs).
+static int fwd_plan(const Geom& g, int Cout) {
   if (!igemm_ok(g, Cout)) return -1;
-  const int M = g.N * g.To * g.Ho * g.Wo;
   Fwd3Plan p3;
-  if (fwd3_plan(g, Cout, p3)) {
-    conv3d_fwd_rows3<<<p3.ntile, 256, 0, stream>>>(g, p3.R, p3.Ls, p3.cpf, (const bf16*)x, (const bf16*)w,
-                                                   (const bf16*)res, (bf16*)z, tile_stats);
-    CMHAR_CHECK_LAUNCH();
-    return 0;
-  }
-  // row-slab kernel: kw = 3, the input row segments of a 256-row tile's output rows within fr::SQ slab rows, whole
-  // 64-wide Cout tiles (CMHAR_FWD_ROWS=0: the generic gather kernel, A/B runs)
+  if (fwd3_plan(g, Cout, p3)) return 1;
   static const bool rows_on = [] {
     const char* v = getenv("CMHAR_FWD_ROWS");
     return !(v && v[0] == '0');
   }();
+  const int M = g.N * g.To * g.Ho * g.Wo;
   const int Ls = (g.Wo - 1) * g.sw + g.kw;
   auto fits = [&](int tm, int sq) { return (long)((tm + g.Wo - 2) / g.Wo + 1) * Ls <= sq; };   // rows a tile touches
   if (rows_on && g.kw == 3 && Cout % fr::TN == 0 && g.Wo <= 255 && Ls <= 255 &&
@@ -2120,26 +2116,44 @@ extern "C" int cmhar_conv3d_fwd(const int* dims, int Cout, const void* x, const 
     // at 392 256-row tiles measured 167 vs 199 us, so it keeps them)
     const long t256 = (long)((M + 255) / 256) * (Cout / fr::TN);
     const bool small = t256 < 256 && fits(128, fr::Cfg<128>::SQ);
-    if (small || fits(256, fr::Cfg<256>::SQ)) {
-      if (small)
-        conv3d_fwd_rows<128><<<((M + 127) / 128) * (Cout / fr::TN), 256, 0, stream>>>(
-            g, M, Cout, Ls, (const bf16*)x, (const bf16*)w, (const bf16*)res, (bf16*)z, tile_stats);
-      else
-        conv3d_fwd_rows<256><<<(int)t256, 256, 0, stream>>>(g, M, Cout, Ls, (const bf16*)x, (const bf16*)w,
-                                                            (const bf16*)res, (bf16*)z, tile_stats);
-      CMHAR_CHECK_LAUNCH();
-      return 0;
-    }
+    if (small) return 2;
+    if (fits(256, fr::Cfg<256>::SQ)) return 3;
   }
   // Cout <= 64: 128x64 tiles (a 128-wide tile would leave half its MFMA work on padding columns)
-  if (Cout <= 64) {
-    const int tiles = (M + 127) / 128;
-    conv3d_fwd_igemm<2><<<tiles, 256, 0, stream>>>(g, M, Cout, (const bf16*)x, (const bf16*)w, (const bf16*)res,
-                                                   (bf16*)z, tile_stats);
-  } else {
-    const int tiles = ((M + 127) / 128) * ((Cout + 127) / 128);
-    conv3d_fwd_igemm<4><<<tiles, 256, 0, stream>>>(g, M, Cout, (const bf16*)x, (const bf16*)w, (const bf16*)res,
-                                                   (bf16*)z, tile_stats);
+  return Cout <= 64 ? 4 : 5;
+}
+extern "C" int cmhar_conv3d_fwd_plan(const int* dims, int Cout) { return fwd_plan(make_geom(dims), Cout); }
+
+extern "C" int cmhar_conv3d_fwd(const int* dims, int Cout, const void* x, const void* w, const void* res, void* z,
+                                float* tile_stats, hipStream_t stream) {
+  const Geom g = make_geom(dims);
+  const int plan = fwd_plan(g, Cout);
+  if (plan < 0) return -1;
+  const int M = g.N * g.To * g.Ho * g.Wo;
+  const int Ls = (g.Wo - 1) * g.sw + g.kw;
+  switch (plan) {
+    case 1: {
+      Fwd3Plan p3;
+      fwd3_plan(g, Cout, p3);
+      conv3d_fwd_rows3<<<p3.ntile, 256, 0, stream>>>(g, p3.R, p3.Ls, p3.cpf, (const bf16*)x, (const bf16*)w,
+                                                     (const bf16*)res, (bf16*)z, tile_stats);
+      break;
+    }
+    case 2:
+      conv3d_fwd_rows<128><<<((M + 127) / 128) * (Cout / fr::TN), 256, 0, stream>>>(
+          g, M, Cout, Ls, (const bf16*)x, (const bf16*)w, (const bf16*)res, (bf16*)z, tile_stats);
+      break;
+    case 3:
+      conv3d_fwd_rows<256><<<((M + 255) / 256) * (Cout / fr::TN), 256, 0, stream>>>(
+          g, M, Cout, Ls, (const bf16*)x, (const bf16*)w, (const bf16*)res, (bf16*)z, tile_stats);
+      break;
+    case 4:
+      conv3d_fwd_igemm<2><<<(M + 127) / 128, 256, 0, stream>>>(g, M, Cout, (const bf16*)x, (const bf16*)w,
+                                                                (const bf16*)res, (bf16*)z, tile_stats);
+      break;
+    default:
+      conv3d_fwd_igemm<4><<<((M + 127) / 128) * ((Cout + 127) / 128), 256, 0, stream>>>(
+          g, M, Cout, (const bf16*)x, (const bf16*)w, (const bf16*)res, (bf16*)z, tile_stats);
   }
   CMHAR_CHECK_LAUNCH();
   return 0;
@@ -2282,6 +2296,17 @@ static bool rows_plan(const Geom& g, int Cout, RowsPlan& p) {
   p.cps = (nchunk + s - 1) / s;
   p.splits = (nchunk + p.cps - 1) / p.cps;
   return true;
+}
+
+// Launch plan of cmhar_conv3d_wgrad (exported for tests): 1 = nine-tap conv3d_wgrad_rows3, 2 = row-slab
+// conv3d_wgrad_rows with 128-wide Cout tiles, 3 = the same with 64-wide tiles, 4 = generic conv3d_wgrad_igemm; each
+// followed by conv3d_wgrad_reduce when cmhar_conv3d_wgrad_ws > 0 (split partials); -1 = not implicit-GEMM.
+extern "C" int cmhar_conv3d_wgrad_plan(const int* dims, int Cout) {
+  const Geom g = make_geom(dims);
+  if (!igemm_ok(g, Cout)) return -1;
+  RowsPlan rp;
+  if (rows_plan(g, Cout, rp)) return rp.grp == 9 ? 1 : rp.cot == 128 ? 2 : 3;
+  return 4;
 }
 
 extern "C" long cmhar_conv3d_wgrad_ws(const int* dims, int Cout) {

@@ -288,6 +288,12 @@ int cmhar_conv3d_im2col(int in_dtype, int out_dtype, const int* dims, const void
  * dzᵀ · col(x), split over M into ws (cmhar_conv3d_wgrad_ws floats; 0 = no workspace), reduced in a fixed order. */
 int cmhar_conv3d_fwd(const int* dims, int Cout, const void* x, const void* w, const void* res, void* z,
                      float* tile_stats, hipStream_t stream);
+/* The kernel cmhar_conv3d_fwd launches for a geometry (tests pin the production plans): 1 = nine-tap row slab
+ * (Cout = 64), 2 / 3 = row slab with 128- / 256-row tiles, 4 / 5 = generic gather with 128x64 / 128x128 tiles;
+ * -1 = not an implicit-GEMM geometry.  cmhar_conv3d_wgrad_plan likewise for cmhar_conv3d_wgrad: 1 = nine-tap row
+ * slab, 2 / 3 = row slab with 128- / 64-wide Cout tiles, 4 = generic gather (split reduce when its ws > 0). */
+int cmhar_conv3d_fwd_plan(const int* dims, int Cout);
+int cmhar_conv3d_wgrad_plan(const int* dims, int Cout);
 /* Split-K forward for the convs whose output tile grid leaves most of the chip idle (R3D-18 layer 4): ws fp32
  * floats = cmhar_conv3d_fwd_split_ws(dims, Cout) (0: not this plan — call cmhar_conv3d_fwd); z = conv(x) (+ res),
  * no BatchNorm tile statistics (the caller's BatchNorm takes its own statistics passes). */

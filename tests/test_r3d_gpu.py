@@ -499,20 +499,26 @@ def test_bn_bwd_nores_rounding_boundaries(relu):
 
 
 @pytest.mark.parametrize('res', [False, True])
-def test_conv3d_fwd_split_layer4(res):
+@pytest.mark.parametrize('geom', ['r3d_layer4', 'resnet18_layer4_kt1'])
+def test_conv3d_fwd_split_layer4(res, geom):
     """The split-K implicit-GEMM forward at R3D-18 layer 4's geometry (batch 32: 32×2×7×7 = 3136 output rows, 512 → 512,
-    3×3×3 'same'): planned (`cmhar_conv3d_fwd_split_ws` > 0), against the fp32 conv of the same bf16 operands (+ the
-    residual, as the dgrad call adds dx_acc) within the bf16 output rounding, and within one bf16 ulp (of the value or of
-    the output's rms near zero) of the unsplit kernel (`cmhar_conv3d_fwd`, the same products summed in a different order)."""
+    3×3×3 'same') and at a 2-D (kt = 1) ResNet-18 layer-4 conv run through the conv3d machinery (32 frames of 7×7,
+    (1,3,3) taps — ADVICE r04): planned (`cmhar_conv3d_fwd_split_ws` > 0), against the fp32 conv of the same bf16
+    operands (+ the residual, as the dgrad call adds dx_acc) within the bf16 output rounding, and within one bf16 ulp (of
+    the value or of the output's rms near zero) of the unsplit kernel (`cmhar_conv3d_fwd`, the same products summed in a
+    different order).  A stride-2 conv never takes the split plan (its slab does not fit the 128-row tile: asserted)."""
     from cmhar import _lib as L
     from cmhar import kernels as K
     from cmhar import r3d
     torch.manual_seed(9)
-    N, C, T, S = 32, 512, 2, 7
-    conv = torch.nn.Conv3d(C, C, 3, 1, 1, bias=False)
+    if geom == 'r3d_layer4':
+        N, C, T, S, k, pd = 32, 512, 2, 7, (3, 3, 3), (1, 1, 1)
+    else:
+        N, C, T, S, k, pd = 32, 512, 1, 7, (1, 3, 3), (0, 1, 1)
+    conv = torch.nn.Conv3d(C, C, k, 1, pd, bias=False)
     x = torch.randn(N, C, T, S, S).bfloat16().float()
     wq = conv.weight.detach().bfloat16().float()
-    ref = F.conv3d(x.to(DEV), wq.to(DEV), padding=1)
+    ref = F.conv3d(x.to(DEV), wq.to(DEV), padding=pd)
     conv = conv.to(DEV)
     xc = x.permute(0, 2, 3, 4, 1).contiguous().to(DEV).bfloat16()
     shp = tuple(xc.shape)
@@ -522,6 +528,9 @@ def test_conv3d_fwd_split_layer4(res):
     dims = r3d._dims(shp, conv, Kp)
     n = L.lib().cmhar_conv3d_fwd_split_ws(dims, C)
     assert n > 0 and n % (M * C) == 0
+    s2 = torch.nn.Conv3d(C // 2, C, k, 2, pd, bias=False)
+    assert L.lib().cmhar_conv3d_fwd_split_ws(r3d._dims((N, T * 2 if k[0] == 3 else 1, 2 * S, 2 * S, C // 2), s2,
+                                                       r3d._r8(s2.weight[0].numel())), C) == 0
     rr = torch.randn(M, C, device=DEV).bfloat16() if res else None
     z = torch.empty(M, C, dtype=torch.bfloat16, device=DEV)
     ws = K.workspace(n, xc.device)
