@@ -59,6 +59,16 @@ WORKLOADS = {
 }
 
 
+# rocprofv3 prints some instantiations half-demangled — the bf16 type as "bool _Accum", later template arguments
+# as "E" — so their PMC records carry no mangled codes to match.  The prefetching-epilogue (PFS = true)
+# instantiations of the forward-layout 256² kernels are such; they are launched under the same trace label as the
+# plain ones, so the label's traffic is the launch-weighted mean over both (the same launches its algorithmic bytes
+# average over).
+PMC_ALIASES = {
+    'gemm8p_kernel<true,true,bf16>': ('gemm8p_kernel<bool _Accum, bool, E, true, bool _Accum, bool, E, 2>',),
+}
+
+
 def _pmc_hits(label, path):
     """Per-kernel records of a committed PMC summary (tools/pmc_traffic.py / tools/pmc_mfma.py JSON) that belong to
     the traced kernel `label` (e.g. 'gemm256_kernel<false,false,float>'), and the file's provenance."""
@@ -73,7 +83,9 @@ def _pmc_hits(label, path):
         doc = json.load(f)
     ks = doc['kernels']
     demangled = base + '<' + ', '.join(a.strip() for a in args.rstrip('>').split(','))   # rocprof demangles some
-    hits = [v for k, v in ks.items() if any(mg in k for mg in mangled) or demangled in k]
+    aliases = PMC_ALIASES.get(label.replace(' ', ''), ())
+    hits = [v for k, v in ks.items() if any(mg in k for mg in mangled) or demangled in k or
+            any(a in k for a in aliases)]
     return hits, {'file': os.path.relpath(path, REPO), 'commit': doc.get('commit'), 'cmd': doc.get('cmd')}
 
 
@@ -637,7 +649,9 @@ def main():
                 'traffic': traffic, 'traffic_source': tsrc,
                 'kernel': name,
                 'launches': n, 'avg_launch_ms': round(tot_ms / n, 4),
-                'algorithmic_bytes_per_launch': int(nb / n)}
+                'algorithmic_bytes_per_launch': int(nb / n),
+                # both per launch over the same launches of the label (PMC: dispatch-weighted over its instantiations)
+                'traffic_over_algorithmic': round(traffic / (nb / n), 3) if traffic else None}
         if name in breakdown:
             bn_, btm, bfl, _ = breakdown[name]
             iso = bfl / (btm / 1e3) / 1e12
