@@ -100,6 +100,54 @@ __device__ __forceinline__ int acc_row(int r, int h) { return (r & 3) + 8 * (r >
 
 __device__ __forceinline__ float xhalf(float v) { return __shfl_xor(v, 32); }
 
+// v[lane] and v[lane ^ 32] in every lane from ONE v_permlane32_swap (a VALU half exchange: lanes 32-63 of the first
+// operand trade places with lanes 0-31 of the second) instead of a ds_bpermute round trip through the LDS
+__device__ __forceinline__ float2_t half_pair(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return float2_t{__uint_as_float(r[0]), __uint_as_float(r[1])};
+}
+// max / sum over the lane pair (lane, lane ^ 32); the max without the canonicalising v_max hipcc puts in front of an
+// fmaxf of a cross-lane value (the operands are finite scores or -inf, never NaN)
+__device__ __forceinline__ float pair_max(float v) {
+  const float2_t p = half_pair(v);
+  float m;
+  asm("v_max_f32 %0, %1, %2" : "=v"(m) : "v"(p[0]), "v"(p[1]));
+  return m;
+}
+__device__ __forceinline__ float pair_sum(float v) {
+  const float2_t p = half_pair(v);
+  return p[0] + p[1];
+}
+
+// Row-per-lane epilogue of a 64-column output held as two 32x32 accumulators (acc[0]: columns 0-31, acc[1]: 32-63;
+// row = lane & 31, half h = lane >> 5 holds columns 8k + 4h .. + 3 of each 8-column group k): the groups are paired
+// with v_permlane32_swap so that every lane holds 16 contiguous bytes — lanes 0-31 columns 8k..8k+7, lanes 32-63
+// 8k+8..8k+15 of groups (k, k+1) — and the row goes out in 4 16-B stores per lane instead of 8 of 8 B
+// (cdna_hip_programming.md T21: the store tail is issue-bound).  Values v·scale rounded as the 8-B form did.
+template <typename E>
+__device__ __forceinline__ void store_row64(E* __restrict__ row, const floatx16 (&acc)[2], float scale, int h) {
+  unsigned pk[8][2];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    typedef E __attribute__((ext_vector_type(2))) e2;
+#pragma unroll
+    for (int w = 0; w < 2; ++w) {
+      const e2 v = {(E)(acc[k >> 2][4 * (k & 3) + 2 * w] * scale), (E)(acc[k >> 2][4 * (k & 3) + 2 * w + 1] * scale)};
+      pk[k][w] = __builtin_bit_cast(unsigned, v);
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 8; k += 2) {
+#pragma unroll
+    for (int w = 0; w < 2; ++w) {
+      const auto r = __builtin_amdgcn_permlane32_swap(pk[k][w], pk[k + 1][w], false, false);
+      pk[k][w] = r[0];
+      pk[k + 1][w] = r[1];
+    }
+    *(uint4_t*)(row + 8 * k + 8 * h) = uint4_t{pk[k][0], pk[k][1], pk[k + 1][0], pk[k + 1][1]};
+  }
+}
+
 // CMHAR_ATTN_PRIO = 1: raise the wave's issue priority over each MFMA chain (as the GEMM's MFMA_Q) so the co-resident
 // waves' softmax / exp VALU work fills the matrix pipe's gaps instead of delaying the chain (A/B knob)
 #ifndef CMHAR_ATTN_PRIO
@@ -210,7 +258,7 @@ __global__ __launch_bounds__(256, 3) void attn_fwd_bf16(int H, int Lq, int Lk, i
           float mt = -INFINITY;
 #pragma unroll
           for (int r = 0; r < 16; ++r) mt = fmaxf(mt, s[j][r]);
-          mt = fmaxf(mt, xhalf(mt)) * c;
+          mt = pair_max(mt) * c;
           // Lazy rescale: the running max m only moves (and O, l are rescaled) when some row's half-tile max
           // exceeds it by more than 8 (log2 units), so p = exp2(c·s − m) ≤ 2^8 stays well inside fp32/bf16 range;
           // with the row maxima settling after the first key tiles this skips ~all rescales.  (Seeding the S
@@ -256,21 +304,11 @@ __global__ __launch_bounds__(256, 3) void attn_fwd_bf16(int H, int Lq, int Lk, i
   }
 #pragma unroll
   for (int j = 0; j < QB; ++j) {
-    const float lj = l[j] + xhalf(l[j]);
+    const float lj = pair_sum(l[j]);
     const float inv = 1.f / lj;
     const int q = q0 + 32 * j + (lane & 31);
     if (q < Lq) {
-      E* orow = O + ((long)b * Lq + q) * ldo + hd * 64;
-#pragma unroll
-      for (int d = 0; d < 2; ++d)
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          typedef E __attribute__((ext_vector_type(4))) e4;
-          e4 v;
-#pragma unroll
-          for (int jj = 0; jj < 4; ++jj) v[jj] = (E)(o[j][d][4 * g + jj] * inv);
-          *(e4*)(orow + d * 32 + 8 * g + 4 * h) = v;
-        }
+      store_row64<E>(O + ((long)b * Lq + q) * ldo + hd * 64, o[j], inv, h);
       if (h == 0) lse[((long)b * H + hd) * Lq + q] = m[j] + log2f(lj);   // log2-domain LSE of (scale*log2e)*s
     }
   }
@@ -414,18 +452,8 @@ __global__ __launch_bounds__(256, 3) void attn_bwd_dkdv_bf16(int H, int Lq, int 
   }
   const int key = k0 + (lane & 31);
   if (key < Lk) {
-    bf16* krow = dK + ((long)b * Lk + key) * lddk + hd * 64;
-    bf16* vrow = dV + ((long)b * Lk + key) * lddv + hd * 64;
-#pragma unroll
-    for (int d = 0; d < 2; ++d)
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        bf16x4 a, v;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) { a[j] = (bf16)(dk[d][4 * g + j] * kscale); v[j] = (bf16)dv[d][4 * g + j]; }
-        *(bf16x4*)(krow + d * 32 + 8 * g + 4 * h) = a;
-        *(bf16x4*)(vrow + d * 32 + 8 * g + 4 * h) = v;
-      }
+    store_row64<bf16>(dK + ((long)b * Lk + key) * lddk + hd * 64, dk, kscale, h);
+    store_row64<bf16>(dV + ((long)b * Lk + key) * lddv + hd * 64, dv, 1.f, h);
   }
 }
 
@@ -475,7 +503,7 @@ __global__ __launch_bounds__(256, QB == 1 ? 3 : 2) void attn_bwd_dq_bf16(int H, 
 #pragma unroll
       for (int e = 0; e < 8; ++e) d_ = fmaf((float)gf[j][t][e], (float)ov[e], d_);
     }
-    d_ += xhalf(d_);
+    d_ = pair_sum(d_);
     Dl[j] = d_;
     if (h == 0 && q0 + 32 * j + (lane & 31) < Lq) delta[((long)b * H + hd) * Lq + myq] = d_;
   }
@@ -566,18 +594,7 @@ __global__ __launch_bounds__(256, QB == 1 ? 3 : 2) void attn_bwd_dq_bf16(int H, 
 #pragma unroll
   for (int j = 0; j < QB; ++j) {
     const int q = q0 + 32 * j + (lane & 31);
-    if (q < Lq) {
-      bf16* row = dQ + ((long)b * Lq + q) * lddq + hd * 64;
-#pragma unroll
-      for (int d = 0; d < 2; ++d)
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          bf16x4 v;
-#pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] = (bf16)(dq[j][d][4 * g + e] * scale);
-          *(bf16x4*)(row + d * 32 + 8 * g + 4 * h) = v;
-        }
-    }
+    if (q < Lq) store_row64<bf16>(dQ + ((long)b * Lq + q) * lddq + hd * 64, dq[j], scale, h);
   }
 }
 #undef Ks

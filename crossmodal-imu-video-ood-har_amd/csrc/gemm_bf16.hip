@@ -954,11 +954,16 @@ __device__ __forceinline__ bf16x8 frag8p_a(const char* lds, int r0, int kk, int 
 // vmcnt(4) for B(t+1) and A(t+1) only — the activation stream (the HBM / MALL-bound operand) gets a whole K-tile more
 // lead than the 2–4 barrier intervals (~0.3 µs) of the two-buffer schedule.  Same fragments, same MFMA order:
 // identical bits.
+// ngroup > 1 (forward layout only): the output tiles are walked in ngroup column groups — every tile row of group 0,
+// then of group 1, … — so that the tiles an XCD runs (a contiguous band of this order, xcd_remap) share one group's
+// weight columns.  A group's weight panel (≤ ~2 MiB) then stays in the XCD's 4 MiB L2 across chip rounds while the
+// activation panels stream through; in row-major order every round needs the WHOLE weight (QKV 3.5 MiB, FC1 4.7 MiB),
+// which does not fit beside the round's activation panels and is re-fetched from the MALL every round.
 template <typename E, bool A_KC, bool B_KC, typename OutT, bool PFS = false, int NA = 2>
 __global__ __launch_bounds__(NT2, 2) void gemm8p_kernel(int M, int N, int K, const bf16* __restrict__ A, long lda,
                                                         const bf16* __restrict__ B, long ldb, OutT* __restrict__ C,
                                                         long ldc, Epilogue e, int klen, long split_stride,
-                                                        int raw_out) {
+                                                        int raw_out, int ngroup) {
   static_assert(NA == 2 || NA == 3, "two or three A buffers");
   // transposed-read instantiations issue their DMA by inline asm (see dma_asm)
   constexpr bool kAD = CMHAR_GEMM8P_ASM_DMA && (!A_KC || !B_KC);
@@ -971,7 +976,15 @@ __global__ __launch_bounds__(NT2, 2) void gemm8p_kernel(int M, int N, int K, con
   const int rlin = xcd_remap(blockIdx.x + ntile * blockIdx.z, ntile * gridDim.z);
   const int bid = rlin % ntile, split = rlin / ntile;
   const int kbeg = split * klen, kend = min(K, kbeg + klen);
-  const int tm = bid / tiles_n, tn = bid % tiles_n;
+  int tm = bid / tiles_n, tn = bid % tiles_n;
+  if (ngroup > 1) {
+    const int cw = (tiles_n + ngroup - 1) / ngroup;          // group width in tiles (the last group may be narrower)
+    const int gi = min(bid / (tiles_m * cw), ngroup - 1);
+    const int wg = min(cw, tiles_n - gi * cw);
+    const int loc = bid - gi * tiles_m * cw;
+    tm = loc / wg;
+    tn = gi * cw + loc % wg;
+  }
   const int bm = tm * TM2, bn = tn * TN2;
   const int nk = (kend - kbeg) / TK2;   // >= 2 (host-checked)
   float* const rs_slab = raw_out ? (float*)C + (long)gridDim.z * split_stride + (long)split * M : nullptr;
@@ -1323,6 +1336,23 @@ static int gemm_plan(bool ak, bool bkc, int M, int N, int K, int splits, bool ha
   return PLAN_256;
 }
 
+// Column groups of the 8-phase forward-layout kernel (see gemm8p_kernel): two when the weight panel (N·K bf16) exceeds
+// 3 MiB at K ≤ 1024 (QKV, FC1 forward, FC2's input gradient on W2ᵀ) — each activation panel is then fetched twice
+// (once per group) instead of the weight once per chip round; one otherwise.  CMHAR_GEMM_NGROUP=n forces n (A/B runs).
+#ifndef CMHAR_GEMM_NGROUP_DEFAULT
+#define CMHAR_GEMM_NGROUP_DEFAULT 0
+#endif
+static int gemm8p_groups(bool ak, bool bkc, int N, int K) {
+  static const int force = [] {
+    const char* v = getenv("CMHAR_GEMM_NGROUP");
+    return v ? atoi(v) : CMHAR_GEMM_NGROUP_DEFAULT;
+  }();
+  if (!ak || !bkc) return 1;
+  const int tiles_n = N / TN2;
+  if (force > 0) return min(force, tiles_n);
+  return (2L * N * K > (3L << 20) && K <= 1024 && tiles_n >= 4) ? 2 : 1;
+}
+
 template <typename E, bool AK, bool BKc, typename OutT>
 int launch(int M, int N, int K, const bf16* A, long lda, const bf16* B, long ldb, OutT* C, long ldc,
            const Epilogue& e, int splits, float* ws, hipStream_t st, int phases) {
@@ -1360,19 +1390,21 @@ int launch(int M, int N, int K, const bf16* A, long lda, const bf16* B, long ldb
             tail_rows, N, ts.nsplit, ws, (long)tail_rows * N, C, ldc, e, ts.tail_m0);
     } else if (plan == PLAN_8P) {
       const bool na3 = gemm8p_na(AK) == 3;
+      const int ng = gemm8p_groups(AK, BKc, N, K);
       if (ph_gemm && pfs && na3)
-        gemm8p_kernel<E, AK, BKc, OutT, true, 3><<<grid, NT2, 0, st>>>(M, N, K, A, lda, B, ldb, C, ldc, e, K, 0, 0);
+        gemm8p_kernel<E, AK, BKc, OutT, true, 3><<<grid, NT2, 0, st>>>(M, N, K, A, lda, B, ldb, C, ldc, e, K, 0, 0, ng);
       else if (ph_gemm && pfs)
-        gemm8p_kernel<E, AK, BKc, OutT, true><<<grid, NT2, 0, st>>>(M, N, K, A, lda, B, ldb, C, ldc, e, K, 0, 0);
+        gemm8p_kernel<E, AK, BKc, OutT, true><<<grid, NT2, 0, st>>>(M, N, K, A, lda, B, ldb, C, ldc, e, K, 0, 0, ng);
       else if (ph_gemm && na3)
-        gemm8p_kernel<E, AK, BKc, OutT, false, 3><<<grid, NT2, 0, st>>>(M, N, K, A, lda, B, ldb, C, ldc, e, K, 0, 0);
+        gemm8p_kernel<E, AK, BKc, OutT, false, 3><<<grid, NT2, 0, st>>>(M, N, K, A, lda, B, ldb, C, ldc, e, K, 0, 0, ng);
       else if (ph_gemm)
-        gemm8p_kernel<E, AK, BKc, OutT><<<grid, NT2, 0, st>>>(M, N, K, A, lda, B, ldb, C, ldc, e, K, 0, 0);
+        gemm8p_kernel<E, AK, BKc, OutT><<<grid, NT2, 0, st>>>(M, N, K, A, lda, B, ldb, C, ldc, e, K, 0, 0, ng);
     } else if (plan == PLAN_8P_SPLITK) {
       if (ph_gemm && gemm8p_na(AK) == 3)
-        gemm8p_kernel<E, AK, BKc, float, false, 3><<<grid, NT2, 0, st>>>(M, N, K, A, lda, B, ldb, ws, N, e, klen, ss, 1);
+        gemm8p_kernel<E, AK, BKc, float, false, 3><<<grid, NT2, 0, st>>>(M, N, K, A, lda, B, ldb, ws, N, e, klen, ss, 1,
+                                                                         1);
       else if (ph_gemm)
-        gemm8p_kernel<E, AK, BKc, float><<<grid, NT2, 0, st>>>(M, N, K, A, lda, B, ldb, ws, N, e, klen, ss, 1);
+        gemm8p_kernel<E, AK, BKc, float><<<grid, NT2, 0, st>>>(M, N, K, A, lda, B, ldb, ws, N, e, klen, ss, 1, 1);
       if (ph_red) splitk_reduce_kernel<OutT><<<reduce_blocks(M, N), 256, 0, st>>>(M, N, nsplit, ws, ss, C, ldc, e);
     } else if (plan == PLAN_256) {
       if (ph_gemm && pfs)

@@ -327,6 +327,41 @@ def test_flash_attention_ragged_tails(Lq, Lk):
     check_flash(got, q, k, v, do, B=B, H=H, Lq=Lq, Lk=Lk, D=D, scale=scale, row_ranges={'q': qt, 'k': kt})
 
 
+@pytest.mark.parametrize('pattern', ['ramp', 'spikes', 'flat_jump'])
+def test_flash_attention_running_max_moves(pattern):
+    """The forward's lazy rescale (the running row max moves only when a score exceeds it by 2^8 in p) at inputs that
+    make it fire mid-sequence: key norms ramping up along the sequence (the max grows every few tiles), isolated
+    large-score spikes late in the sequence, and a tile whose scores all jump by ~4.5 (log2) above the running max
+    (many moderate p whose lane sum exceeds 2^8 without any single one doing so).  O, dQ, dK, dV within 3x the
+    emulated bf16-rounding error + 1e-3 of fp32 autograd."""
+    from flash_ref import check_flash
+    torch.manual_seed(21)
+    B, H, D, L_ = 2, 2, 64, 700
+    scale = D ** -0.5
+    q = torch.randn(B * L_, H * D, device=DEV)
+    k = torch.randn(B * L_, H * D, device=DEV)
+    pos = torch.arange(L_, device=DEV).repeat(B).float()[:, None]
+    if pattern == 'ramp':
+        k = k * (0.2 + 3.0 * pos / L_)
+    elif pattern == 'spikes':
+        sel = (pos % 97 == 96) & (pos > 300)
+        k = torch.where(sel, q.roll(1, 0) * 4.0, k * 0.5)
+    else:
+        k = k * 0.1
+        q = q.abs() * 0.3
+        k = torch.where((pos >= 320) & (pos < 384), k + 2.0, k)     # one whole tile of uniformly higher scores
+    q, k = q.bfloat16(), k.bfloat16()
+    v = torch.randn(B * L_, H * D, device=DEV).bfloat16()
+    o = torch.empty(B * L_, H * D, dtype=torch.bfloat16, device=DEV)
+    lse = torch.empty(B * H * L_, device=DEV)
+    K().attention_fwd(q, k, v, o, lse, B=B, H=H, Lq=L_, Lk=L_, D=D, scale=scale)
+    do = torch.randn(B * L_, H * D, device=DEV).bfloat16()
+    dq, dk, dv = (torch.empty_like(q) for _ in range(3))
+    K().attention_bwd(q, k, v, o, do, lse, dq, dk, dv, B=B, H=H, Lq=L_, Lk=L_, D=D, scale=scale)
+    assert torch.isfinite(o.float()).all()
+    check_flash({'o': o, 'dq': dq, 'dk': dk, 'dv': dv}, q, k, v, do, B=B, H=H, Lq=L_, Lk=L_, D=D, scale=scale)
+
+
 @pytest.mark.parametrize('L_', [200, 1568])
 def test_flash_attention_prescaled_keys(L_):
     """The VideoMAE bf16 training form: the QKV GEMM's epilogue writes K pre-scaled by scale·log2(e) (colscale), the
