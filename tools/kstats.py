@@ -45,6 +45,20 @@ def main():
               f'({100 * busy / span:.1f} %)')
         gaps = [iv_b[0] - iv_a[1] for iv_a, iv_b in zip(sorted(iv), sorted(iv)[1:]) if iv_b[0] > iv_a[1]]
         print(f'inter-kernel gaps: {len(gaps) / n:.0f} per step, {sum(gaps) / n / 1e6:.3f} ms/step')
+        # where the idle time sits: gaps of the steady-state steps by (previous kernel -> next kernel), summed
+        st = sorted((a, b, nm) for a, b, nm in rows if ends[1] <= a < ends[-1])
+        by = collections.defaultdict(lambda: [0, 0])
+        ce, cn = None, None
+        for a, b, nm in st:
+            if ce is not None and a > ce:
+                key = (cn[:60], nm[:60])
+                by[key][0] += 1
+                by[key][1] += a - ce
+            if ce is None or b > ce:
+                ce, cn = b, nm
+        print('largest idle intervals by (kernel before -> kernel after), per step:')
+        for (x, y), (c, t) in sorted(by.items(), key=lambda kv: -kv[1][1])[:15]:
+            print(f'  {t / n / 1e3:8.1f} us  x{c / n:5.1f}  {x}  ->  {y}')
 
 
 if __name__ == '__main__':
