@@ -148,6 +148,289 @@ __device__ __forceinline__ void store_row64(E* __restrict__ row, const floatx16 
   }
 }
 
+__device__ __forceinline__ void stage128(const TileDma& t, int r0, char* lds, int wave) {
+  t.tile(r0, lds, wave);
+  t.tile(r0 + 64, lds + 8192, wave);
+}
+
+// ---------------------------------------------------------------------------------------------------------------
+// ragged tails: ≤ 32 rows (queries of the forward, keys of dK/dV) past the last full block, the OTHER sequence split
+// four ways — each wave takes 32 rows of every 128-row stage — and the four partials merged through the LDS.
+// NBUF = 2: double-buffered 128-row stages (64 KB, the stand-alone tail kernels).  NBUF = 1: one 32 KB stage buffer
+// (+1 KB), so a tail group fits the LDS of the bulk kernel's workgroup and runs INSIDE that launch — dispatched
+// first, its waves latency-bound beside the bulk waves on the same CUs instead of a launch of its own with the chip
+// mostly idle (attn_bwd_dkdv_bf16 `ntail`; attn_fwd_bf16 has the same hook, off by default: CMHAR_ATTN_FOLD_FWD).
+// Same arithmetic and merge order either way; the two compiled forms may still contract a multiply-add differently
+// (the folded forward's tail rows measured within 1 bf16 ulp of the stand-alone kernel's, dK/dV identical).
+// ---------------------------------------------------------------------------------------------------------------
+template <typename E, int NBUF>
+__device__ __forceinline__ void fwd_tail_group(char* smem, int H, int Lq, int Lk, int q_base, int hd, int b,
+                                               const bf16* __restrict__ Q, long ldq, const bf16* __restrict__ K,
+                                               long ldk, const bf16* __restrict__ V, long ldv, E* __restrict__ O,
+                                               long ldo, float* __restrict__ lse, float scale) {
+  // smem: NBUF × [K 128 rows 16 KB | V 16 KB]; the merge's O partials reuse the first 32 KB, its m / l the next 1 KB
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5;
+  const bf16* Kb = K + (long)b * Lk * ldk + hd * 64;
+  const bf16* Vb = V + (long)b * Lk * ldv + hd * 64;
+  const float c = scale * LOG2E;
+  const int myq = min(q_base + (lane & 31), Lq - 1);
+  bf16x8 qf[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) qf[t] = *(const bf16x8*)(Q + ((long)b * Lq + myq) * ldq + hd * 64 + 16 * t + 8 * h);
+  floatx16 o[2];
+#pragma unroll
+  for (int d = 0; d < 2; ++d)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) o[d][r] = 0.f;
+  float m = -INFINITY, l = 0.f;
+  const int nt = (Lk + 127) / 128;
+  TileDma tk, tv;
+  tk.init(Kb, ldk, Lk, wave, lane);
+  tv.init(Vb, ldv, Lk, wave, lane);
+  stage128(tk, 0, smem, wave);
+  stage128(tv, 0, smem + 16384, wave);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  const int sub = (wave >> 1) * 8192, r0 = 32 * (wave & 1);   // this wave's 32 keys of the 128-key stage
+  for (int st = 0; st < nt; ++st) {
+    char* Ks_ = smem + (NBUF == 2 ? (st & 1) * 32768 : 0);
+    char* Vs_ = Ks_ + 16384;
+    const bool more = st + 1 < nt;
+    if (NBUF == 2 && more) {
+      stage128(tk, (st + 1) * 128, smem + ((st + 1) & 1) * 32768, wave);
+      stage128(tv, (st + 1) * 128, smem + ((st + 1) & 1) * 32768 + 16384, wave);
+    }
+    const int kbase = st * 128 + 32 * wave;
+    if (kbase < Lk) {      // a wave with no valid key in this step skips it (its m, l, O stay untouched)
+      floatx16 s;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) s[r] = 0.f;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) s = mma32<E>(row_frag(Ks_ + sub, r0, t, lane), qf[t], s);
+      if (kbase + 32 > Lk) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          if (kbase + acc_row(r, h) >= Lk) s[r] = -INFINITY;
+      }
+      float mt = -INFINITY;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) mt = fmaxf(mt, s[r]);
+      mt = fmaxf(mt, xhalf(mt)) * c;
+      if (__builtin_amdgcn_ballot_w64(mt > m + 8.f) != 0) {      // lazy rescale, as attn_fwd_bf16
+        const float mn = fmaxf(m, mt);
+        const float alpha = fexp2(m - mn);
+        m = mn;
+        l *= alpha;
+#pragma unroll
+        for (int d = 0; d < 2; ++d)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) o[d][r] *= alpha;
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float p = fexp2(fmaf(s[r], c, -m));
+        s[r] = p;
+        l += p;
+      }
+      bf16x8 pb[2];
+#pragma unroll
+      for (int ss = 0; ss < 2; ++ss) pb[ss] = pack8<E>(s, ss);
+#pragma unroll
+      for (int ss = 0; ss < 2; ++ss)
+#pragma unroll
+        for (int d = 0; d < 2; ++d) o[d] = mma32<E>(tr_frag(Vs_ + sub, r0, ss, d * 32, lane), pb[ss], o[d]);
+    }
+    if (NBUF == 1 && more) {   // the one buffer is free once every wave is past this stage
+      __syncthreads();
+      stage128(tk, (st + 1) * 128, smem, wave);
+      stage128(tv, (st + 1) * 128, smem + 16384, wave);
+    }
+    if (more) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  // merge the four key quarters: m* = max m_w, L = Σ 2^(m_w − m*) l_w, O = Σ 2^(m_w − m*) O_w / L
+  float* Ow = (float*)smem;            // [4][32][64]
+  float* Mw = Ow + 4 * 32 * 64;        // [4][32]
+  float* Lw = Mw + 128;                // [4][32]
+  const float lt = l + xhalf(l);
+  const int ql = lane & 31;
+  if (h == 0) { Mw[wave * 32 + ql] = m; Lw[wave * 32 + ql] = lt; }
+#pragma unroll
+  for (int d = 0; d < 2; ++d)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) Ow[(wave * 32 + ql) * 64 + d * 32 + acc_row(r, h)] = o[d][r];
+  __syncthreads();
+  const int qi = tid >> 3, d0 = (tid & 7) * 8;
+  float mw[4], mx = -INFINITY;
+#pragma unroll
+  for (int w = 0; w < 4; ++w) { mw[w] = Mw[w * 32 + qi]; mx = fmaxf(mx, mw[w]); }
+  float wsum = 0.f, acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int w = 0; w < 4; ++w) {
+    const float f = fexp2(mw[w] - mx);       // a quarter that saw no key: m_w = −inf → weight 0
+    wsum += f * Lw[w * 32 + qi];
+    const float* src = Ow + (w * 32 + qi) * 64 + d0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] += f * src[j];
+  }
+  const int q = q_base + qi;
+  if (q < Lq) {
+    const float inv = 1.f / wsum;
+    typedef E __attribute__((ext_vector_type(8))) e8;
+    e8 v;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = (E)(acc[j] * inv);
+    *(e8*)(O + ((long)b * Lq + q) * ldo + hd * 64 + d0) = v;
+    if ((tid & 7) == 0) lse[((long)b * H + hd) * Lq + q] = mx + log2f(wsum);
+  }
+}
+
+template <bool PS, int NBUF>
+__device__ __forceinline__ void dkdv_tail_group(char* smem, int H, int Lq, int Lk, int k_base, int hd, int b,
+                                                const bf16* __restrict__ Q, long ldq, const bf16* __restrict__ K,
+                                                long ldk, const bf16* __restrict__ V, long ldv,
+                                                const bf16* __restrict__ dO, long lddo, const float* __restrict__ lse,
+                                                const float* __restrict__ delta, bf16* __restrict__ dK, long lddk,
+                                                bf16* __restrict__ dV, long lddv, float scale, float kscale) {
+  // smem: NBUF × [Q 128 rows 16 KB | dO 16 KB], then NBUF × 128 −lse/c and NBUF × 128 −δ; the merge reuses 32 KB
+  float* Ls = (float*)(smem + NBUF * 32768);
+  float* Ds = Ls + NBUF * 128;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5;
+  const bf16* Qb = Q + (long)b * Lq * ldq + hd * 64;
+  const bf16* Gb = dO + (long)b * Lq * lddo + hd * 64;
+  const float* lseb = lse + ((long)b * H + hd) * Lq;
+  const float* delb = delta + ((long)b * H + hd) * Lq;
+  const float c = scale * LOG2E;
+  const float inv_c = 1.f / c;
+  const int myk = min(k_base + (lane & 31), Lk - 1);
+  bf16x8 kf[4], vf[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    kf[t] = *(const bf16x8*)(K + ((long)b * Lk + myk) * ldk + hd * 64 + 16 * t + 8 * h);
+    vf[t] = *(const bf16x8*)(V + ((long)b * Lk + myk) * ldv + hd * 64 + 16 * t + 8 * h);
+  }
+  floatx16 dk[2], dv[2];
+#pragma unroll
+  for (int d = 0; d < 2; ++d)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) { dk[d][r] = 0.f; dv[d][r] = 0.f; }
+  const int nt = (Lq + 127) / 128;
+  TileDma tq, tg;
+  tq.init(Qb, ldq, Lq, wave, lane);
+  tg.init(Gb, lddo, Lq, wave, lane);
+  float lv = 0.f, dv_ = 0.f;
+  auto load = [&](int st) {
+    char* buf = smem + (st % NBUF) * 32768;
+    stage128(tq, st * 128, buf, wave);
+    stage128(tg, st * 128, buf + 16384, wave);
+    if (tid < 128) {
+      const int q = st * 128 + tid;
+      lv = q < Lq ? -lseb[q] * inv_c : -INFINITY;
+      dv_ = q < Lq ? -delb[q] : 0.f;
+    }
+  };
+  auto store_consts = [&](int st) {
+    if (tid < 128) { Ls[(st % NBUF) * 128 + tid] = lv; Ds[(st % NBUF) * 128 + tid] = dv_; }
+  };
+  load(0);
+  store_consts(0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  const int sub = (wave >> 1) * 8192, r0 = 32 * (wave & 1);   // this wave's 32 queries of the 128-query stage
+  for (int st = 0; st < nt; ++st) {
+    const char* Qs_ = smem + (st % NBUF) * 32768;
+    const char* Gs_ = Qs_ + 16384;
+    const float* L_ = Ls + (st % NBUF) * 128 + 32 * wave;
+    const float* D_ = Ds + (st % NBUF) * 128 + 32 * wave;
+    const bool more = st + 1 < nt;
+    if (NBUF == 2 && more) load(st + 1);
+    if (st * 128 + 32 * wave < Lq) {
+      floatx16 s, dp;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) { s[r] = L_[acc_row(r, h)]; dp[r] = D_[acc_row(r, h)]; }
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag(Qs_ + sub, r0, t, lane), kf[t], s, 0, 0, 0);
+        dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag(Gs_ + sub, r0, t, lane), vf[t], dp, 0, 0, 0);
+      }
+      bf16x8 pbv[2], dbv[2];
+#pragma unroll
+      for (int r = 0; r < 16; r += 2) {
+        const float2_t pv = PS ? float2_t{fexp2(s[r]), fexp2(s[r + 1])} : float2_t{fexp2(s[r] * c), fexp2(s[r + 1] * c)};
+        const float2_t dv2 = pv * float2_t{dp[r], dp[r + 1]};
+        const bf16x2_t pp = __builtin_convertvector(pv, bf16x2_t);
+        const bf16x2_t dd = __builtin_convertvector(dv2, bf16x2_t);
+        pbv[r >> 3][r & 7] = pp[0];
+        pbv[r >> 3][(r & 7) + 1] = pp[1];
+        dbv[r >> 3][r & 7] = dd[0];
+        dbv[r >> 3][(r & 7) + 1] = dd[1];
+      }
+#pragma unroll
+      for (int ss = 0; ss < 2; ++ss)
+#pragma unroll
+        for (int d = 0; d < 2; ++d) {
+          dv[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_frag(Gs_ + sub, r0, ss, d * 32, lane), pbv[ss], dv[d], 0, 0, 0);
+          dk[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_frag(Qs_ + sub, r0, ss, d * 32, lane), dbv[ss], dk[d], 0, 0, 0);
+        }
+    }
+    if (more) {
+      if (NBUF == 1) {   // the one buffer (and its row constants) is free once every wave is past this stage
+        __syncthreads();
+        load(st + 1);
+      }
+      store_consts(st + 1);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+  }
+  // sum the four query quarters' partials, dK then dV through one 32 KB [4][32][64] fp32 image
+  float* W = (float*)smem;
+  const int kl = lane & 31;
+  const int ki = tid >> 3, d0 = (tid & 7) * 8;
+  const int key = k_base + ki;
+#pragma unroll
+  for (int pass = 0; pass < 2; ++pass) {
+    const floatx16* part = pass == 0 ? dk : dv;
+    if (pass == 1) __syncthreads();   // the dK sums are read out
+#pragma unroll
+    for (int d = 0; d < 2; ++d)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) W[(wave * 32 + kl) * 64 + d * 32 + acc_row(r, h)] = part[d][r];
+    __syncthreads();
+    if (key < Lk) {
+      const float f = pass == 0 ? kscale : 1.f;
+      bf16x8 a;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float sum = 0.f;
+#pragma unroll
+        for (int w = 0; w < 4; ++w) sum += W[(w * 32 + ki) * 64 + d0 + j];
+        a[j] = (bf16)(sum * f);
+      }
+      bf16* dst = pass == 0 ? dK + ((long)b * Lk + key) * lddk : dV + ((long)b * Lk + key) * lddv;
+      *(bf16x8*)(dst + hd * 64 + d0) = a;
+    }
+  }
+}
+
+// (block, head, batch) of a bulk kernel's workgroup on a (nb + ntail, H, B) grid whose first ntail·H·B linear ids
+// (dispatched first) are tail groups: true for a tail group (bi.blk = its group within the head).  Both index spaces
+// are XCD-remapped as flash_block, so with ntail·H·B and nb·H·B multiples of 8 a head's tail group runs on the XCD
+// of its bulk blocks.  ntail = 0: flash_block.
+__device__ __forceinline__ bool tail_block(int ntail, int H, BlkIdx& bi) {
+  const int nx = gridDim.x, nyz = gridDim.y * gridDim.z;
+  const int lin = blockIdx.x + nx * (blockIdx.y + gridDim.y * blockIdx.z);
+  const int tails = ntail * nyz;
+  if (lin < tails) {
+    const int rt = xcd_remap(lin, tails), bh = rt / ntail;
+    bi = {rt % ntail, bh % H, bh / H};
+    return true;
+  }
+  const int nb = nx - ntail, r = xcd_remap(lin - tails, nb * nyz), bh = r / nb;
+  bi = {r % nb, bh % H, bh / H};
+  return false;
+}
+
 // CMHAR_ATTN_PRIO = 1: raise the wave's issue priority over each MFMA chain (as the GEMM's MFMA_Q) so the co-resident
 // waves' softmax / exp VALU work fills the matrix pipe's gaps instead of delaying the chain (A/B knob)
 #ifndef CMHAR_ATTN_PRIO
@@ -174,12 +457,18 @@ template <typename E, int QB>
 __global__ __launch_bounds__(256, 3) void attn_fwd_bf16(int H, int Lq, int Lk, int q_base, const bf16* __restrict__ Q,
                                                         long ldq, const bf16* __restrict__ K, long ldk,
                                                         const bf16* __restrict__ V, long ldv, E* __restrict__ O,
-                                                        long ldo, float* __restrict__ lse, float scale) {
-  __shared__ __attribute__((aligned(16))) char smem[4 * 8192];
+                                                        long ldo, float* __restrict__ lse, float scale,
+                                                        int ntail, int q_tail0) {
+  __shared__ __attribute__((aligned(16))) char smem[4 * 8192 + 1024];   // +1 KB: a folded tail group's merge
 #define Ks(buf) (smem + 8192 * (buf))
 #define Vs(buf) (smem + 16384 + 8192 * (buf))
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5;
-  const BlkIdx bi = flash_block(H);
+  BlkIdx bi;
+  if (tail_block(ntail, H, bi)) {   // ntail > 0: this workgroup is the 32-query tail group bi.blk of its head
+    fwd_tail_group<E, 1>(smem, H, Lq, Lk, q_tail0 + 32 * bi.blk, bi.hd, bi.b, Q, ldq, K, ldk, V, ldv, O, ldo, lse,
+                         scale);
+    return;
+  }
   const int hd = bi.hd, b = bi.b;
   const int q0 = q_base + bi.blk * (128 * QB) + wave * (32 * QB);
   const bf16* Qb = Q + (long)b * Lq * ldq + hd * 64;
@@ -330,14 +619,19 @@ __global__ __launch_bounds__(256, 3) void attn_bwd_dkdv_bf16(int H, int Lq, int 
                                                              const float* __restrict__ lse,
                                                              const float* __restrict__ delta, bf16* __restrict__ dK,
                                                              long lddk, bf16* __restrict__ dV, long lddv, float scale,
-                                                             float kscale) {
+                                                             float kscale, int ntail, int k_tail0) {
   __shared__ __attribute__((aligned(16))) char smem[4 * 8192 + 2 * 2 * 64 * 4];
 #define Qs(buf) (smem + 8192 * (buf))
 #define Gs(buf) (smem + 16384 + 8192 * (buf))
   float* Ls = (float*)(smem + 32768);          // [2][64] lse
   float* Ds = Ls + 128;                         // [2][64] delta
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5;
-  const BlkIdx bi = flash_block(H);
+  BlkIdx bi;
+  if (tail_block(ntail, H, bi)) {   // ntail > 0: the 32-key tail group bi.blk of its head (same 33 KB of LDS)
+    dkdv_tail_group<PS, 1>(smem, H, Lq, Lk, k_tail0 + 32 * bi.blk, bi.hd, bi.b, Q, ldq, K, ldk, V, ldv, dO, lddo, lse,
+                           delta, dK, lddk, dV, lddv, scale, kscale);
+    return;
+  }
   const int hd = bi.hd, b = bi.b;
   const int k0 = k_base + bi.blk * 128 + wave * 32;
   const bf16* Qb = Q + (long)b * Lq * ldq + hd * 64;
@@ -600,131 +894,16 @@ __global__ __launch_bounds__(256, QB == 1 ? 3 : 2) void attn_bwd_dq_bf16(int H, 
 #undef Ks
 #undef Vs
 
-__device__ __forceinline__ void stage128(const TileDma& t, int r0, char* lds, int wave) {
-  t.tile(r0, lds, wave);
-  t.tile(r0 + 64, lds + 8192, wave);
-}
-
 template <typename E>
 __global__ __launch_bounds__(256, 2) void attn_fwd_tail_bf16(int H, int Lq, int Lk, int q_base0,
                                                              const bf16* __restrict__ Q, long ldq,
                                                              const bf16* __restrict__ K, long ldk,
                                                              const bf16* __restrict__ V, long ldv, E* __restrict__ O,
                                                              long ldo, float* __restrict__ lse, float scale) {
-  __shared__ __attribute__((aligned(16))) char smem[65536];   // [2 buf][K 128 rows 16 KB | V 16 KB]
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5;
-  const int hd = blockIdx.y, b = blockIdx.z;
-  const int q_base = q_base0 + 32 * blockIdx.x;   // grid.x = ⌈tail / 32⌉ groups of 32 rows
-  const bf16* Kb = K + (long)b * Lk * ldk + hd * 64;
-  const bf16* Vb = V + (long)b * Lk * ldv + hd * 64;
-  const float c = scale * LOG2E;
-  const int myq = min(q_base + (lane & 31), Lq - 1);
-  bf16x8 qf[4];
-#pragma unroll
-  for (int t = 0; t < 4; ++t) qf[t] = *(const bf16x8*)(Q + ((long)b * Lq + myq) * ldq + hd * 64 + 16 * t + 8 * h);
-  floatx16 o[2];
-#pragma unroll
-  for (int d = 0; d < 2; ++d)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) o[d][r] = 0.f;
-  float m = -INFINITY, l = 0.f;
-  const int nt = (Lk + 127) / 128;
-  TileDma tk, tv;
-  tk.init(Kb, ldk, Lk, wave, lane);
-  tv.init(Vb, ldv, Lk, wave, lane);
-  stage128(tk, 0, smem, wave);
-  stage128(tv, 0, smem + 16384, wave);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  const int sub = (wave >> 1) * 8192, r0 = 32 * (wave & 1);   // this wave's 32 keys of the 128-key stage
-  for (int st = 0; st < nt; ++st) {
-    char* Ks_ = smem + (st & 1) * 32768;
-    char* Vs_ = Ks_ + 16384;
-    const bool more = st + 1 < nt;
-    if (more) {
-      stage128(tk, (st + 1) * 128, smem + ((st + 1) & 1) * 32768, wave);
-      stage128(tv, (st + 1) * 128, smem + ((st + 1) & 1) * 32768 + 16384, wave);
-    }
-    const int kbase = st * 128 + 32 * wave;
-    if (kbase < Lk) {      // a wave with no valid key in this step skips it (its m, l, O stay untouched)
-      floatx16 s;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) s[r] = 0.f;
-#pragma unroll
-      for (int t = 0; t < 4; ++t) s = mma32<E>(row_frag(Ks_ + sub, r0, t, lane), qf[t], s);
-      if (kbase + 32 > Lk) {
-#pragma unroll
-        for (int r = 0; r < 16; ++r)
-          if (kbase + acc_row(r, h) >= Lk) s[r] = -INFINITY;
-      }
-      float mt = -INFINITY;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) mt = fmaxf(mt, s[r]);
-      mt = fmaxf(mt, xhalf(mt)) * c;
-      if (__builtin_amdgcn_ballot_w64(mt > m + 8.f) != 0) {      // lazy rescale, as attn_fwd_bf16
-        const float mn = fmaxf(m, mt);
-        const float alpha = fexp2(m - mn);
-        m = mn;
-        l *= alpha;
-#pragma unroll
-        for (int d = 0; d < 2; ++d)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) o[d][r] *= alpha;
-      }
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const float p = fexp2(fmaf(s[r], c, -m));
-        s[r] = p;
-        l += p;
-      }
-      bf16x8 pb[2];
-#pragma unroll
-      for (int ss = 0; ss < 2; ++ss) pb[ss] = pack8<E>(s, ss);
-#pragma unroll
-      for (int ss = 0; ss < 2; ++ss)
-#pragma unroll
-        for (int d = 0; d < 2; ++d) o[d] = mma32<E>(tr_frag(Vs_ + sub, r0, ss, d * 32, lane), pb[ss], o[d]);
-    }
-    if (more) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-  }
-  // merge the four key quarters: m* = max m_w, L = Σ 2^(m_w − m*) l_w, O = Σ 2^(m_w − m*) O_w / L
-  float* Mw = (float*)smem;            // [4][32]
-  float* Lw = Mw + 128;                // [4][32]
-  float* Ow = Lw + 128;                // [4][32][64]
-  const float lt = l + xhalf(l);
-  const int ql = lane & 31;
-  if (h == 0) { Mw[wave * 32 + ql] = m; Lw[wave * 32 + ql] = lt; }
-#pragma unroll
-  for (int d = 0; d < 2; ++d)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) Ow[(wave * 32 + ql) * 64 + d * 32 + acc_row(r, h)] = o[d][r];
-  __syncthreads();
-  const int qi = tid >> 3, d0 = (tid & 7) * 8;
-  float mw[4], mx = -INFINITY;
-#pragma unroll
-  for (int w = 0; w < 4; ++w) { mw[w] = Mw[w * 32 + qi]; mx = fmaxf(mx, mw[w]); }
-  float wsum = 0.f, acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int w = 0; w < 4; ++w) {
-    const float f = fexp2(mw[w] - mx);       // a quarter that saw no key: m_w = −inf → weight 0
-    wsum += f * Lw[w * 32 + qi];
-    const float* src = Ow + (w * 32 + qi) * 64 + d0;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) acc[j] += f * src[j];
-  }
-  const int q = q_base + qi;
-  if (q < Lq) {
-    const float inv = 1.f / wsum;
-    typedef E __attribute__((ext_vector_type(8))) e8;
-    e8 v;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = (E)(acc[j] * inv);
-    *(e8*)(O + ((long)b * Lq + q) * ldo + hd * 64 + d0) = v;
-    if ((tid & 7) == 0) lse[((long)b * H + hd) * Lq + q] = mx + log2f(wsum);
-  }
+  __shared__ __attribute__((aligned(16))) char smem[65536];   // grid.x = ⌈tail / 32⌉ groups of 32 rows
+  fwd_tail_group<E, 2>(smem, H, Lq, Lk, q_base0 + 32 * blockIdx.x, blockIdx.y, blockIdx.z, Q, ldq, K, ldk, V, ldv, O,
+                       ldo, lse, scale);
 }
-
 template <bool PS>
 __global__ __launch_bounds__(256, 2) void attn_bwd_dq_tail_bf16(int H, int Lq, int Lk, int q_base0,
                                                                 const bf16* __restrict__ Q, long ldq,
@@ -847,124 +1026,9 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_tail_bf16(int H, int Lq,
                                                                   bf16* __restrict__ dK, long lddk,
                                                                   bf16* __restrict__ dV, long lddv, float scale,
                                                                   float kscale) {
-  __shared__ __attribute__((aligned(16))) char smem[65536 + 2 * 2 * 128 * 4];   // [2][Q 16 KB | dO 16 KB] + consts
-  float* Ls = (float*)(smem + 65536);          // [2][128] −lse/c
-  float* Ds = Ls + 256;                        // [2][128] −δ
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5;
-  const int hd = blockIdx.y, b = blockIdx.z;
-  const int k_base = k_base0 + 32 * blockIdx.x;   // grid.x = ⌈tail / 32⌉ groups of 32 keys
-  const bf16* Qb = Q + (long)b * Lq * ldq + hd * 64;
-  const bf16* Gb = dO + (long)b * Lq * lddo + hd * 64;
-  const float* lseb = lse + ((long)b * H + hd) * Lq;
-  const float* delb = delta + ((long)b * H + hd) * Lq;
-  const float c = scale * LOG2E;
-  const float inv_c = 1.f / c;
-  const int myk = min(k_base + (lane & 31), Lk - 1);
-  bf16x8 kf[4], vf[4];
-#pragma unroll
-  for (int t = 0; t < 4; ++t) {
-    kf[t] = *(const bf16x8*)(K + ((long)b * Lk + myk) * ldk + hd * 64 + 16 * t + 8 * h);
-    vf[t] = *(const bf16x8*)(V + ((long)b * Lk + myk) * ldv + hd * 64 + 16 * t + 8 * h);
-  }
-  floatx16 dk[2], dv[2];
-#pragma unroll
-  for (int d = 0; d < 2; ++d)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) { dk[d][r] = 0.f; dv[d][r] = 0.f; }
-  const int nt = (Lq + 127) / 128;
-  TileDma tq, tg;
-  tq.init(Qb, ldq, Lq, wave, lane);
-  tg.init(Gb, lddo, Lq, wave, lane);
-  float lv = 0.f, dv_ = 0.f;
-  auto load = [&](int st) {
-    char* buf = smem + (st & 1) * 32768;
-    stage128(tq, st * 128, buf, wave);
-    stage128(tg, st * 128, buf + 16384, wave);
-    if (tid < 128) {
-      const int q = st * 128 + tid;
-      lv = q < Lq ? -lseb[q] * inv_c : -INFINITY;
-      dv_ = q < Lq ? -delb[q] : 0.f;
-    }
-  };
-  auto store_consts = [&](int st) {
-    if (tid < 128) { Ls[(st & 1) * 128 + tid] = lv; Ds[(st & 1) * 128 + tid] = dv_; }
-  };
-  load(0);
-  store_consts(0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  const int sub = (wave >> 1) * 8192, r0 = 32 * (wave & 1);   // this wave's 32 queries of the 128-query stage
-  for (int st = 0; st < nt; ++st) {
-    const char* Qs_ = smem + (st & 1) * 32768;
-    const char* Gs_ = Qs_ + 16384;
-    const float* L_ = Ls + (st & 1) * 128 + 32 * wave;
-    const float* D_ = Ds + (st & 1) * 128 + 32 * wave;
-    const bool more = st + 1 < nt;
-    if (more) load(st + 1);
-    if (st * 128 + 32 * wave < Lq) {
-      floatx16 s, dp;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) { s[r] = L_[acc_row(r, h)]; dp[r] = D_[acc_row(r, h)]; }
-#pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag(Qs_ + sub, r0, t, lane), kf[t], s, 0, 0, 0);
-        dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag(Gs_ + sub, r0, t, lane), vf[t], dp, 0, 0, 0);
-      }
-      bf16x8 pbv[2], dbv[2];
-#pragma unroll
-      for (int r = 0; r < 16; r += 2) {
-        const float2_t pv = PS ? float2_t{fexp2(s[r]), fexp2(s[r + 1])} : float2_t{fexp2(s[r] * c), fexp2(s[r + 1] * c)};
-        const float2_t dv2 = pv * float2_t{dp[r], dp[r + 1]};
-        const bf16x2_t pp = __builtin_convertvector(pv, bf16x2_t);
-        const bf16x2_t dd = __builtin_convertvector(dv2, bf16x2_t);
-        pbv[r >> 3][r & 7] = pp[0];
-        pbv[r >> 3][(r & 7) + 1] = pp[1];
-        dbv[r >> 3][r & 7] = dd[0];
-        dbv[r >> 3][(r & 7) + 1] = dd[1];
-      }
-#pragma unroll
-      for (int ss = 0; ss < 2; ++ss)
-#pragma unroll
-        for (int d = 0; d < 2; ++d) {
-          dv[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_frag(Gs_ + sub, r0, ss, d * 32, lane), pbv[ss], dv[d], 0, 0, 0);
-          dk[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_frag(Qs_ + sub, r0, ss, d * 32, lane), dbv[ss], dk[d], 0, 0, 0);
-        }
-    }
-    if (more) {
-      store_consts(st + 1);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    __syncthreads();
-  }
-  float* Kw = (float*)smem;            // [4][32][64] dK partials
-  float* Vw = Kw + 4 * 32 * 64;        // [4][32][64] dV partials
-  const int kl = lane & 31;
-#pragma unroll
-  for (int d = 0; d < 2; ++d)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      Kw[(wave * 32 + kl) * 64 + d * 32 + acc_row(r, h)] = dk[d][r];
-      Vw[(wave * 32 + kl) * 64 + d * 32 + acc_row(r, h)] = dv[d][r];
-    }
-  __syncthreads();
-  const int ki = tid >> 3, d0 = (tid & 7) * 8;
-  const int key = k_base + ki;
-  if (key < Lk) {
-    bf16x8 a, v;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      float sk = 0.f, sv = 0.f;
-#pragma unroll
-      for (int w = 0; w < 4; ++w) {
-        sk += Kw[(w * 32 + ki) * 64 + d0 + j];
-        sv += Vw[(w * 32 + ki) * 64 + d0 + j];
-      }
-      a[j] = (bf16)(sk * kscale);
-      v[j] = (bf16)sv;
-    }
-    *(bf16x8*)(dK + ((long)b * Lk + key) * lddk + hd * 64 + d0) = a;
-    *(bf16x8*)(dV + ((long)b * Lk + key) * lddv + hd * 64 + d0) = v;
-  }
+  __shared__ __attribute__((aligned(16))) char smem[65536 + 2 * 2 * 128 * 4];   // grid.x = ⌈tail / 32⌉ key groups
+  dkdv_tail_group<PS, 2>(smem, H, Lq, Lk, k_base0 + 32 * blockIdx.x, blockIdx.y, blockIdx.z, Q, ldq, K, ldk, V, ldv, dO,
+                         lddo, lse, delta, dK, lddk, dV, lddv, scale, kscale);
 }
 
 // ---------------------------------------------------------------------------------------------------------------
@@ -1106,6 +1170,17 @@ __global__ __launch_bounds__(64) void attn_bwd_dkdv_f32(int H, int Lq, int Lk, c
 #ifndef CMHAR_ATTN_TAIL
 #define CMHAR_ATTN_TAIL 64
 #endif
+// 1: the tail groups run inside the bulk launch (first dispatched; see fwd_tail_group); 0: a tail launch of their own
+// after the bulk.  Measured in one process at B = 32, H = 12, L = 1568 (tools/debug/attn_ab.py, µs per layer, two
+// sessions): dK/dV folded 892.8 / 888.1 → 883.6 / 882.3 (backward), kept; the forward folded 317.9 / 315.9 → 339.6 /
+// 339.0 — its bulk grid is exactly three chip rounds of workgroups (2304 = 3 × 768), so the tail groups' slot time
+// adds a partial fourth round instead of filling idle slots — off (A/B knobs)
+#ifndef CMHAR_ATTN_FOLD
+#define CMHAR_ATTN_FOLD 1
+#endif
+#ifndef CMHAR_ATTN_FOLD_FWD
+#define CMHAR_ATTN_FOLD_FWD 0
+#endif
 
 // f32-MFMA flash kernels (csrc/attention_f32.hip) for fp32 storage, D = 64, no dropout
 void cmhar_attn_f32m_fwd(int B, int H, int Lq, int Lk, const float* Q, long ldq, const float* K, long ldk,
@@ -1137,19 +1212,22 @@ extern "C" int cmhar_attention_fwd(int dtype, int B, int H, int Lq, int Lk, int 
     // (CMHAR_ATTN_FWD_ONE_LAUNCH: 256-query workgroups everywhere, the last one per head partly idle)
     const int bulk = CMHAR_ATTN_FWD_ONE_LAUNCH ? cdiv(Lq, 256) * 256 : (Lq / 256) * 256;
     const bool tail = Lq > bulk && Lq - bulk <= CMHAR_ATTN_TAIL;
+    // the tail's 32-query groups folded into the bulk launch (tail_block), or a launch of their own
+    const int fold = tail && bulk > 0 && CMHAR_ATTN_FOLD_FWD ? cdiv(Lq - bulk, 32) : 0;
 #define FL(E)                                                                                                    \
   do {                                                                                                           \
     if (bulk > 0)                                                                                                \
-      attn_fwd_bf16<E, 2><<<dim3(bulk / 256, H, B), 256, 0, st>>>(H, Lq, Lk, 0, (const bf16*)Q, ldq, (const bf16*)K, \
-                                                                  ldk, (const bf16*)V, ldv, (E*)O, ldo, lse, scale); \
-    if (tail)                                                                                                    \
+      attn_fwd_bf16<E, 2><<<dim3(bulk / 256 + fold, H, B), 256, 0, st>>>(H, Lq, Lk, 0, (const bf16*)Q, ldq,         \
+                                                                         (const bf16*)K, ldk, (const bf16*)V, ldv, \
+                                                                         (E*)O, ldo, lse, scale, fold, bulk);    \
+    if (tail && !fold)                                                                                           \
       attn_fwd_tail_bf16<E><<<dim3(cdiv(Lq - bulk, 32), H, B), 256, 0, st>>>(H, Lq, Lk, bulk, (const bf16*)Q, ldq,   \
                                                                              (const bf16*)K, ldk,                \
                                                            (const bf16*)V, ldv, (E*)O, ldo, lse, scale);        \
     else if (Lq > bulk)                                                                                          \
       attn_fwd_bf16<E, 1><<<dim3(cdiv(Lq - bulk, 128), H, B), 256, 0, st>>>(H, Lq, Lk, bulk, (const bf16*)Q, ldq,   \
                                                                             (const bf16*)K, ldk, (const bf16*)V, ldv, \
-                                                                            (E*)O, ldo, lse, scale);             \
+                                                                            (E*)O, ldo, lse, scale, 0, 0);       \
   } while (0)
     if (dtype == CMHAR_F16) FL(f16); else FL(bf16);
 #undef FL
@@ -1207,11 +1285,13 @@ static void flash_bwd_bf16(int B, int H, int Lq, int Lk, const void* Q, long ldq
   const int kfull = (Lk / 128) * 128;
   const bool ktail = Lk > kfull && Lk - kfull <= CMHAR_ATTN_TAIL;
   const int kblocks = (ktail ? kfull : cdiv(Lk, 128) * 128) / 128;
+  const int fold = ktail && kblocks > 0 && CMHAR_ATTN_FOLD ? cdiv(Lk - kfull, 32) : 0;   // as the forward
   if (kblocks > 0)
-    attn_bwd_dkdv_bf16<PS><<<dim3(kblocks, H, B), 256, 0, st>>>(H, Lq, Lk, 0, (const bf16*)Q, ldq, (const bf16*)K,
-                                                                ldk, (const bf16*)V, ldv, (const bf16*)dO, lddo, lse,
-                                                                delta, (bf16*)dK, lddk, (bf16*)dV, lddv, s_in, scale);
-  if (ktail)
+    attn_bwd_dkdv_bf16<PS><<<dim3(kblocks + fold, H, B), 256, 0, st>>>(H, Lq, Lk, 0, (const bf16*)Q, ldq,
+                                                                       (const bf16*)K, ldk, (const bf16*)V, ldv,
+                                                                       (const bf16*)dO, lddo, lse, delta, (bf16*)dK,
+                                                                       lddk, (bf16*)dV, lddv, s_in, scale, fold, kfull);
+  if (ktail && !fold)
     attn_bwd_dkdv_tail_bf16<PS><<<dim3(cdiv(Lk - kfull, 32), H, B), 256, 0, st>>>(H, Lq, Lk, kfull, (const bf16*)Q,
                                                                                   ldq, (const bf16*)K,
                                                                ldk, (const bf16*)V, ldv, (const bf16*)dO, lddo, lse,
