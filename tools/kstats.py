@@ -1,6 +1,9 @@
 """Per-kernel summary of a rocprofv3 --kernel-trace CSV run: calls, total / average duration, share, plus the GPU-busy
 union and the per-step wall time of the last N steps (steps delimited by the AdamW kernel).
-python tools/kstats.py DIR [steps_in_run]"""
+python tools/kstats.py DIR [steps_in_run]
+With CMHAR_KSTATS_CONTEXT=pattern[,pattern...]: per steady-state step, which kernels launch right before / after the
+kernels whose names contain a pattern (small torch kernels: who issues them)."""
+import os
 import collections
 import csv
 import glob
@@ -59,6 +62,16 @@ def main():
         print('largest idle intervals by (kernel before -> kernel after), per step:')
         for (x, y), (c, t) in sorted(by.items(), key=lambda kv: -kv[1][1])[:15]:
             print(f'  {t / n / 1e3:8.1f} us  x{c / n:5.1f}  {x}  ->  {y}')
+        for pat in filter(None, os.environ.get('CMHAR_KSTATS_CONTEXT', '').split(',')):
+            ctx = collections.Counter()
+            for i, (a, b, nm) in enumerate(st):
+                if pat in nm:
+                    prev = st[i - 1][2][:70] if i else '-'
+                    nxt = st[i + 1][2][:70] if i + 1 < len(st) else '-'
+                    ctx[(prev, nxt)] += 1
+            print(f'context of "{pat}" per step ({sum(ctx.values()) / n:.1f} launches):')
+            for (x, y), c in ctx.most_common(25):
+                print(f'  x{c / n:5.1f}  {x}  ->  *  ->  {y}')
 
 
 if __name__ == '__main__':
