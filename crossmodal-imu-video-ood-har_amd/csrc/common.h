@@ -121,6 +121,29 @@ __device__ __forceinline__ void gelu_pair16(float x, float& g, float& gp) {
   g = x * cdf;
   gp = fmaf(x, 0.39894228040143268f * e1, cdf);
 }
+// gelu_pair16 on two values at once, written in packed-fp32 form (v_pk_fma_f32 / v_pk_mul_f32 / v_pk_add_f32 do two
+// lanes' worth per instruction; the reciprocal, exp2 and the sign select stay per value): the FC1 forward epilogue
+// evaluates it 154 M times per launch with the matrix pipes idle.  Same approximation as gelu_pair16 with its ½ folded
+// into P and exp(−x²/2) as exp2(x²·(−½·log2 e)) — results within its error bound (tests/test_kernels_gpu.py GELU
+// tests), not bit-identical to it.
+typedef __attribute__((ext_vector_type(2))) float f32x2;
+__device__ __forceinline__ void gelu_pair16x2(f32x2 x, f32x2& g, f32x2& gp) {
+  const f32x2 t = {__builtin_amdgcn_rcpf(fmaf(fabsf(x[0]), 0.70710678118654752f * 0.3275911f, 1.0f)),
+                   __builtin_amdgcn_rcpf(fmaf(fabsf(x[1]), 0.70710678118654752f * 0.3275911f, 1.0f))};
+  f32x2 p = {0.5f * 1.061405429f, 0.5f * 1.061405429f};
+  p = __builtin_elementwise_fma(p, t, f32x2{0.5f * -1.453152027f, 0.5f * -1.453152027f});
+  p = __builtin_elementwise_fma(p, t, f32x2{0.5f * 1.421413741f, 0.5f * 1.421413741f});
+  p = __builtin_elementwise_fma(p, t, f32x2{0.5f * -0.284496736f, 0.5f * -0.284496736f});
+  p = __builtin_elementwise_fma(p, t, f32x2{0.5f * 0.254829592f, 0.5f * 0.254829592f});
+  const f32x2 arg = x * x * f32x2{-0.5f * 1.4426950408889634f, -0.5f * 1.4426950408889634f};
+  const f32x2 e1 = {__builtin_amdgcn_exp2f(arg[0]), __builtin_amdgcn_exp2f(arg[1])};   // exp(−x²/2)
+  const f32x2 h = t * p * e1;                                                         // Φ(−|x|)
+  const f32x2 om = f32x2{1.0f, 1.0f} - h;
+  const f32x2 cdf = {x[0] < 0.f ? h[0] : om[0], x[1] < 0.f ? h[1] : om[1]};
+  g = x * cdf;
+  gp = __builtin_elementwise_fma(x, e1 * f32x2{0.39894228040143268f, 0.39894228040143268f}, cdf);
+}
+
 template <typename OutT>
 __device__ __forceinline__ void gelu_pair_for(float x, float& g, float& gp) {
   if constexpr (sizeof(OutT) == 2) gelu_pair16(x, g, gp);

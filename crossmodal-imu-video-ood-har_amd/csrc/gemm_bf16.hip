@@ -204,8 +204,18 @@ __device__ __forceinline__ void epilogue_store8(const Epilogue& e, OutT* __restr
   }
   if (e.act == ACT_GELU) {
     if (e.aux_out) store8<OutT>((OutT*)e.aux_out + (long)m * e.ldo + n0, x);
+    if constexpr (sizeof(OutT) == 2) {
 #pragma unroll
-    for (int j = 0; j < 8; ++j) x[j] = gelu_for<OutT>(x[j]);
+      for (int j = 0; j < 8; j += 2) {
+        f32x2 g, gp;
+        gelu_pair16x2(f32x2{x[j], x[j + 1]}, g, gp);
+        x[j] = g[0];
+        x[j + 1] = g[1];
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) x[j] = gelu_for<OutT>(x[j]);
+    }
   } else if (e.act == ACT_RELU) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) x[j] = fmaxf(x[j], 0.f);
@@ -215,8 +225,18 @@ __device__ __forceinline__ void epilogue_store8(const Epilogue& e, OutT* __restr
     } else {
       load8<OutT>((const OutT*)e.aux_in + (long)m * e.lda + n0, t, true);
     }
+    if constexpr (sizeof(OutT) == 2) {
 #pragma unroll
-    for (int j = 0; j < 8; ++j) x[j] *= gelu_grad_for<OutT>(t[j]);
+      for (int j = 0; j < 8; j += 2) {
+        f32x2 g, gp;
+        gelu_pair16x2(f32x2{t[j], t[j + 1]}, g, gp);
+        x[j] *= gp[0];
+        x[j + 1] *= gp[1];
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) x[j] *= gelu_grad_for<OutT>(t[j]);
+    }
   } else if (e.act == ACT_DRELU) {
     if constexpr (sizeof(OutT) == 2) {
       if (pre_aux) decode8<OutT>(pre, t); else load8<OutT>((const OutT*)e.aux_in + (long)m * e.lda + n0, t, true);
@@ -226,8 +246,20 @@ __device__ __forceinline__ void epilogue_store8(const Epilogue& e, OutT* __restr
 #pragma unroll
     for (int j = 0; j < 8; ++j) x[j] = t[j] > 0.f ? x[j] : 0.f;
   } else if (e.act == ACT_GELU_SAVEGRAD) {
+    if constexpr (sizeof(OutT) == 2) {   // the FC1 forward: packed-fp32 form (gelu_pair16x2)
 #pragma unroll
-    for (int j = 0; j < 8; ++j) gelu_pair_for<OutT>(x[j], x[j], t[j]);
+      for (int j = 0; j < 8; j += 2) {
+        f32x2 g, gp;
+        gelu_pair16x2(f32x2{x[j], x[j + 1]}, g, gp);
+        x[j] = g[0];
+        x[j + 1] = g[1];
+        t[j] = gp[0];
+        t[j + 1] = gp[1];
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) gelu_pair_for<OutT>(x[j], x[j], t[j]);
+    }
     if (e.aux_out) store8<OutT>((OutT*)e.aux_out + (long)m * e.ldo + n0, t);
   } else if (e.act == ACT_MULAUX) {
     if constexpr (sizeof(OutT) == 2) {
