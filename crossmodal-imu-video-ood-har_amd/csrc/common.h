@@ -128,20 +128,25 @@ __device__ __forceinline__ void gelu_pair16(float x, float& g, float& gp) {
 // tests), not bit-identical to it.
 typedef __attribute__((ext_vector_type(2))) float f32x2;
 __device__ __forceinline__ void gelu_pair16x2(f32x2 x, f32x2& g, f32x2& gp) {
+  // ed = φ(x) = exp(−x²/2)/√(2π) from one exp2 (the 1/√(2π) as a log2 offset), so Φ(−|x|) = t·P(t)·exp(−x²/2) =
+  // t·(P(t)·√(2π)/2)·ed — P's coefficients carry ½·√(2π) — and GELU′ = x·φ(x) + Φ(x) is one fma
+  constexpr float kS = 0.5f * 2.5066282746310002f;    // ½·√(2π)
   const f32x2 t = {__builtin_amdgcn_rcpf(fmaf(fabsf(x[0]), 0.70710678118654752f * 0.3275911f, 1.0f)),
                    __builtin_amdgcn_rcpf(fmaf(fabsf(x[1]), 0.70710678118654752f * 0.3275911f, 1.0f))};
-  f32x2 p = {0.5f * 1.061405429f, 0.5f * 1.061405429f};
-  p = __builtin_elementwise_fma(p, t, f32x2{0.5f * -1.453152027f, 0.5f * -1.453152027f});
-  p = __builtin_elementwise_fma(p, t, f32x2{0.5f * 1.421413741f, 0.5f * 1.421413741f});
-  p = __builtin_elementwise_fma(p, t, f32x2{0.5f * -0.284496736f, 0.5f * -0.284496736f});
-  p = __builtin_elementwise_fma(p, t, f32x2{0.5f * 0.254829592f, 0.5f * 0.254829592f});
-  const f32x2 arg = x * x * f32x2{-0.5f * 1.4426950408889634f, -0.5f * 1.4426950408889634f};
-  const f32x2 e1 = {__builtin_amdgcn_exp2f(arg[0]), __builtin_amdgcn_exp2f(arg[1])};   // exp(−x²/2)
-  const f32x2 h = t * p * e1;                                                         // Φ(−|x|)
+  f32x2 p = {kS * 1.061405429f, kS * 1.061405429f};
+  p = __builtin_elementwise_fma(p, t, f32x2{kS * -1.453152027f, kS * -1.453152027f});
+  p = __builtin_elementwise_fma(p, t, f32x2{kS * 1.421413741f, kS * 1.421413741f});
+  p = __builtin_elementwise_fma(p, t, f32x2{kS * -0.284496736f, kS * -0.284496736f});
+  p = __builtin_elementwise_fma(p, t, f32x2{kS * 0.254829592f, kS * 0.254829592f});
+  // log2(φ(x)) = x²·(−½·log2 e) + log2(1/√(2π))
+  const f32x2 arg = __builtin_elementwise_fma(x * x, f32x2{-0.5f * 1.4426950408889634f, -0.5f * 1.4426950408889634f},
+                                              f32x2{-1.3257480647361593f, -1.3257480647361593f});
+  const f32x2 ed = {__builtin_amdgcn_exp2f(arg[0]), __builtin_amdgcn_exp2f(arg[1])};   // φ(x)
+  const f32x2 h = t * p * ed;                                                         // Φ(−|x|)
   const f32x2 om = f32x2{1.0f, 1.0f} - h;
   const f32x2 cdf = {x[0] < 0.f ? h[0] : om[0], x[1] < 0.f ? h[1] : om[1]};
   g = x * cdf;
-  gp = __builtin_elementwise_fma(x, e1 * f32x2{0.39894228040143268f, 0.39894228040143268f}, cdf);
+  gp = __builtin_elementwise_fma(x, ed, cdf);
 }
 
 template <typename OutT>
