@@ -450,6 +450,13 @@ __device__ __forceinline__ bool tail_block(int ntail, int H, BlkIdx& bi) {
 // Forward per 32-key half at 3 waves per SIMD (168 VGPRs): 4 % faster than scoring whole 64-key tiles at 2 waves
 // per SIMD (tools/debug/attn_ab.py; the lazy-rescale points move, so not bit-identical to that form).  One launch
 // with the last 256-query workgroup of each head partly idle instead of the 128-query tail launch: 1 % slower.
+// CMHAR_ATTN_LSUM_MFMA = 1: the softmax row sum l of each 32-key half is taken on the matrix pipe as ones·Pᵀ over the
+// bf16 P the PV product consumes (two extra MFMAs per q-block and half, into the dead score accumulators) instead of
+// 16 VALU adds per lane: the forward is VALU-issue bound beside its MFMAs (exp, fma, add, max, cvt per score at head
+// dim 64), the matrix pipe is not.  l is then the sum of the rounded weights O's numerator uses.
+#ifndef CMHAR_ATTN_LSUM_MFMA
+#define CMHAR_ATTN_LSUM_MFMA 1
+#endif
 #ifndef CMHAR_ATTN_FWD_ONE_LAUNCH
 #define CMHAR_ATTN_FWD_ONE_LAUNCH 0
 #endif
@@ -505,6 +512,11 @@ __global__ __launch_bounds__(256, 3) void attn_fwd_bf16(int H, int Lq, int Lk, i
   // A wave whose queries all lie past Lq (the ragged last workgroup of a head) still helps stage K/V tiles and
   // joins every barrier, but issues no MFMA / softmax work: its SIMD's matrix pipe goes to the co-resident waves.
   const bool active = q0 < Lq;
+  // row-sum selector (CMHAR_ATTN_LSUM_MFMA): as a 16x16x32 A fragment, lane l is row l & 15, k-group l >> 4; ones
+  // where the row's query half ((row >> 2) & 1) matches the k-group's ((l >> 4) & 1), zeros elsewhere
+  const float sel = (((lane & 15) >> 2) & 1) == ((lane >> 4) & 1) ? 1.f : 0.f;
+  const float sel8[8] = {sel, sel, sel, sel, sel, sel, sel, sel};
+  const bf16x8 lsel = pack_frag8<E>(sel8);
   // One K/V tile; the LDS buffer index is a compile-time constant (the loop below runs the tiles in pairs), so
   // every LDS address folds into the ds_read immediate offsets instead of a v_add per read.
   auto tile = [&](auto CUR, int kt) __attribute__((always_inline)) {
@@ -567,10 +579,19 @@ __global__ __launch_bounds__(256, 3) void attn_fwd_bf16(int H, int Lq, int Lk, i
           for (int r = 0; r < 16; ++r) {
             const float p = fexp2(fmaf(s[j][r], c, -mn));
             s[j][r] = p;
-            l[j] += p;
+            if (!CMHAR_ATTN_LSUM_MFMA) l[j] += p;
           }
 #pragma unroll
           for (int ss = 0; ss < 2; ++ss) pb[j][ss] = pack8<E>(s[j], ss);
+          if (CMHAR_ATTN_LSUM_MFMA) {
+            // Σ_k P[q, k] over the half on a 16x16x32 MFMA: read as that shape's B operand, lane l's fragment is column
+            // n = l & 15 with k-group l >> 4, i.e. query n (k-groups 0, 2) or n + 16 (k-groups 1, 3) of the 16 keys of
+            // chunk ss; the A fragment `lsel` selects, for the rows a lane's accumulator holds (4·(l >> 4) .. +3),
+            // the k-groups of that lane's own query — so every lane receives its query's sum (4 equal values)
+            floatx4 ls = mma16<E>(lsel, pb[j][0], floatx4{0.f, 0.f, 0.f, 0.f});
+            ls = mma16<E>(lsel, pb[j][1], ls);
+            l[j] += ls[0];
+          }
         }
         PRIO_HI();
 #pragma unroll
@@ -593,7 +614,7 @@ __global__ __launch_bounds__(256, 3) void attn_fwd_bf16(int H, int Lq, int Lk, i
   }
 #pragma unroll
   for (int j = 0; j < QB; ++j) {
-    const float lj = pair_sum(l[j]);
+    const float lj = CMHAR_ATTN_LSUM_MFMA ? l[j] : pair_sum(l[j]);   // the MFMA row sum covers both lane halves' keys
     const float inv = 1.f / lj;
     const int q = q0 + 32 * j + (lane & 31);
     if (q < Lq) {
