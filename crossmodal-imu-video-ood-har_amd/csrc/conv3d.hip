@@ -1042,8 +1042,9 @@ __global__ __launch_bounds__(64 * NW, 2) void conv3d_wgrad_rows(Geom g, int Cout
     }
 }
 
-// Cout = 64, stride-1 H/W variant: a workgroup owns one it, one 64-channel slice and ALL nine (ih, iw) taps (576 dW
-// columns, 12 waves x 3 column blocks), and a chunk is up to R = ⌊256 / Wo⌋ consecutive output rows of one frame:
+// Stride-1 H/W variant: a workgroup owns one it, one 64-channel slice of the input, one 64-wide Cout slice and ALL
+// nine (ih, iw) taps (576 dW columns, 12 waves x 3 column blocks), and a chunk is up to R <= ⌊256 / Wo⌋ consecutive
+// output rows of one frame (R balanced over the frame's rows):
 // output row r and tap ih read input row r + ih, so the chunk's R + 2 input row segments serve all 3·R (row, ih)
 // pairs (the one-tap-row kernel stages 3·R) and each staged dz row feeds 576 columns instead of 192 — 2.3x the
 // MFMA work per staged byte for R3D-18 layer 1 (R = 4).
@@ -1403,11 +1404,13 @@ __global__ __launch_bounds__(256) void conv_split_reduce(int M, int Cout, int ns
   }
 }
 
-// Cout = 64, stride-1 H/W forward with all nine (ih, iw) taps per staged slab: a tile is up to R = ⌊256 / Wo⌋
-// consecutive output rows of one frame; per (it, 64-channel slice) it stages the R + 2 input row segments its
-// rows read under any ih once, then the three kh taps' weights one after another (slab kept), so each staged input
-// byte feeds 3·3 taps instead of 3 (the 256-row kernel restages per ih).  Same 4-wave 64-slot x 64-Cout layout,
-// LDS image and register prefetch as conv3d_fwd_rows<256>; BatchNorm statistics per tile (its row count written).
+// Stride-1 H/W forward with all nine (ih, iw) taps per staged slab: a tile is R consecutive output rows of one
+// frame (R·Wo <= 256, R balanced over the frame's rows) times one 64-wide Cout slice (the Cout slices of a frame
+// tile are consecutive workgroup ids, so they share the input rows in one XCD's L2); per (it, 64-channel slice) it
+// stages the R + 2 input row segments its rows read under any ih once, then the three kh taps' weights one after
+// another (slab kept), so each staged input byte feeds 3·3 taps instead of 3 (the 256-row kernel restages per ih).
+// Same 4-wave 64-slot x 64-Cout layout, LDS image and register prefetch as conv3d_fwd_rows<256>; BatchNorm
+// statistics per frame tile (its row count written by the first Cout slice).
 namespace fr3 {
 constexpr int SQ = 352, TN = 64, NT = 256, RS = 144;
 constexpr int SLAB = SQ * RS, WB = 3 * TN * RS, ELD = TN + 4;
@@ -1415,16 +1418,18 @@ constexpr int SL_PER = (SQ * 8 + NT - 1) / NT, W_PER = 3 * TN * 8 / NT;
 static_assert(256 * ELD * 4 + 2048 <= SLAB + WB, "epilogue staging + statistics scratch must fit the operand LDS");
 }  // namespace fr3
 
-__global__ __launch_bounds__(256, 2) void conv3d_fwd_rows3(Geom g, int R, int Ls, int cpf, const bf16* __restrict__ x,
-                                                           const bf16* __restrict__ Wt, const bf16* __restrict__ res,
-                                                           bf16* __restrict__ z, float* __restrict__ tstats) {
+__global__ __launch_bounds__(256, 2) void conv3d_fwd_rows3(Geom g, int Cout, int R, int Ls, int cpf,
+                                                           const bf16* __restrict__ x, const bf16* __restrict__ Wt,
+                                                           const bf16* __restrict__ res, bf16* __restrict__ z,
+                                                           float* __restrict__ tstats) {
   using namespace fr3;
   __shared__ __attribute__((aligned(16))) char smem[SLAB + WB];
   char* const slab = smem;
   char* const wl = smem + SLAB;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int ntile = gridDim.x;
-  const int t = xcd_remap(blockIdx.x, ntile);
+  const int ncot = Cout / TN, ntile = gridDim.x / ncot;          // frame tiles
+  const int tl = xcd_remap(blockIdx.x, gridDim.x);
+  const int t = tl / ncot, bn = (tl - t * ncot) * TN;
   const int f = t / cpf, ho0 = (t - f * cpf) * R, nr = min(R, g.Ho - ho0);
   const int to = f % g.To, n = f / g.To;
   const int used = nr * g.Wo;
@@ -1466,7 +1471,7 @@ __global__ __launch_bounds__(256, 2) void conv3d_fwd_rows3(Geom g, int R, int Ls
 #pragma unroll
     for (int i = 0; i < W_PER; ++i) {
       const int e = i * NT + tid, iw = e >> 9, co = (e >> 3) & 63, ch = e & 7;
-      rw[i] = *(const uint4_t*)(Wt + (long)co * g.Kp + ((it * g.kh + ih) * g.kw + iw) * g.C + cc * 64 + ch * 8);
+      rw[i] = *(const uint4_t*)(Wt + (long)(bn + co) * g.Kp + ((it * g.kh + ih) * g.kw + iw) * g.C + cc * 64 + ch * 8);
     }
   };
   auto store = [&](int st) {
@@ -1521,7 +1526,7 @@ __global__ __launch_bounds__(256, 2) void conv3d_fwd_rows3(Geom g, int R, int Ls
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
     const int rr = (tid >> 3) + 32 * k;
-    rq[k] = res && rr < used ? *(const uint4_t*)(res + (m0 + rr) * TN + cg) : uint4_t{0u, 0u, 0u, 0u};
+    rq[k] = res && rr < used ? *(const uint4_t*)(res + (m0 + rr) * Cout + bn + cg) : uint4_t{0u, 0u, 0u, 0u};
   }
 #pragma unroll
   for (int i = 0; i < 4; ++i)
@@ -1543,14 +1548,14 @@ __global__ __launch_bounds__(256, 2) void conv3d_fwd_rows3(Geom g, int R, int Ls
 #pragma unroll
       for (int j = 0; j < 8; ++j) v[j] += (float)q[j];
     }
-    zstore8(z + m * TN + cg, v);
+    zstore8(z + m * Cout + bn + cg, v);
   }
   if (tstats)
     tile_col_stats<NT>(TN, (float*)(smem + 256 * ELD * 4), tid, [&](int c, int r) { return T[r * ELD + c]; },
                        [&](int) { return used; }, [&](int c, float mu, float m2) {
-                         tstats[(long)t * TN + c] = mu;
-                         tstats[((long)ntile + t) * TN + c] = m2;
-                         if (c == 0) tile_counts(tstats, ntile, TN)[t] = (float)used;
+                         tstats[(long)t * Cout + bn + c] = mu;
+                         tstats[((long)ntile + t) * Cout + bn + c] = m2;
+                         if (c == 0 && bn == 0) tile_counts(tstats, ntile, Cout)[t] = (float)used;
                        });
 }
 
@@ -2016,21 +2021,25 @@ static bool igemm_ok(const Geom& g, int Cout) {
 
 // Statistics tiles the forward plan writes (see cmhar_conv3d_fwd; all its kernels use 128-row tiles) and the floats
 // the caller provides for them: tile and group partials plus their row counts.
-// Nine-tap forward (conv3d_fwd_rows3) plan: Cout = 64, 3x3 taps at unit H/W stride, R + 2 input rows of a tile in
-// the slab.  CMHAR_FWD_ROWS3=0 turns it off (A/B runs).
+// Nine-tap forward (conv3d_fwd_rows3) plan: Cout % 64 == 0, 3x3 taps at unit H/W stride, R + 2 input rows of a
+// tile in the slab, R = ⌈Ho / cpf⌉ with cpf = ⌈Ho / ⌊256 / Wo⌋⌉ tiles per frame (balanced: R3D-18 layer 2 takes
+// 4 x 7 rows, not 9 + 9 + 9 + 1), and at least 3/4 of the tile's 256 MFMA row slots used (layer 4's 7 x 7 frames
+// would use 49: it keeps the split-K row-slab kernel).  ntile counts frame tiles; the grid is ntile x Cout / 64.
+// CMHAR_FWD_ROWS3=0 turns it off, =1 keeps it to Cout = 64 (R3D-18 layer 1 only; A/B runs).
 struct Fwd3Plan { int R, Ls, cpf, ntile; };
 static bool fwd3_plan(const Geom& g, int Cout, Fwd3Plan& p) {
-  static const bool on = [] {
+  static const int mode = [] {
     const char* v = getenv("CMHAR_FWD_ROWS3");
-    return !(v && v[0] == '0');
+    return v && (v[0] == '0' || v[0] == '1') ? v[0] - '0' : 2;
   }();
-  if (!on || Cout != fr3::TN || g.kh != 3 || g.kw != 3 || g.sh != 1 || g.sw != 1 || g.C % 64 || g.Wo > 256 ||
-      (long)g.N * g.T * g.H * g.W >= (1L << 30))
+  if (!mode || (mode == 1 && Cout != fr3::TN) || Cout % fr3::TN || g.kh != 3 || g.kw != 3 || g.sh != 1 ||
+      g.sw != 1 || g.C % 64 || g.Wo > 256 || (long)g.N * g.T * g.H * g.W >= (1L << 30))
     return false;
-  p.R = min(256 / g.Wo, g.Ho);
+  const int r0 = min(256 / g.Wo, g.Ho);
+  p.cpf = (g.Ho + r0 - 1) / r0;
+  p.R = (g.Ho + p.cpf - 1) / p.cpf;
   p.Ls = g.Wo - 1 + g.kw;
-  if ((p.R + 2) * p.Ls > fr3::SQ) return false;
-  p.cpf = (g.Ho + p.R - 1) / p.R;
+  if ((p.R + 2) * p.Ls > fr3::SQ || 4 * p.R * g.Wo < 3 * 256 || (p.cpf - 1) * p.R >= g.Ho) return false;
   p.ntile = g.N * g.To * p.cpf;
   return true;
 }
@@ -2135,8 +2144,9 @@ extern "C" int cmhar_conv3d_fwd(const int* dims, int Cout, const void* x, const 
     case 1: {
       Fwd3Plan p3;
       fwd3_plan(g, Cout, p3);
-      conv3d_fwd_rows3<<<p3.ntile, 256, 0, stream>>>(g, p3.R, p3.Ls, p3.cpf, (const bf16*)x, (const bf16*)w,
-                                                     (const bf16*)res, (bf16*)z, tile_stats);
+      conv3d_fwd_rows3<<<p3.ntile * (Cout / fr3::TN), 256, 0, stream>>>(g, Cout, p3.R, p3.Ls, p3.cpf,
+                                                                         (const bf16*)x, (const bf16*)w,
+                                                                         (const bf16*)res, (bf16*)z, tile_stats);
       break;
     }
     case 2:
@@ -2252,21 +2262,27 @@ static bool rows_plan(const Geom& g, int Cout, RowsPlan& p) {
     return !(v && v[0] == '0');
   }();
   if (!on || g.kw != 3 || g.Wo > wr::SLOTS || Cout % 64 || g.C % 64) return false;
-  static const bool nine = [] {   // CMHAR_WGRAD_ROWS3=0: one-tap-row kernel for the Cout = 64 shapes too (A/B runs)
+  // CMHAR_WGRAD_ROWS3=0: one-tap-row kernel for every shape; 1 (default): nine-tap kernel for Cout = 64 only; 2: also
+  // on 64-wide Cout slices of wider convs — measured slower there (R3D-18 layer 2 295.1 -> 311.0 us, layer 3 154.4 ->
+  // 170.5, tools/debug/conv_bench.py; the one-tap-row kernel's 128-wide Cout tiles reuse each staged slab twice)
+  static const int nine = [] {
     const char* v = getenv("CMHAR_WGRAD_ROWS3");
-    return !(v && v[0] == '0');
+    return v && (v[0] == '0' || v[0] == '2') ? v[0] - '0' : 1;
   }();
-  if (nine && Cout == 64 && g.kh == 3 && g.sh == 1 && g.sw == 1) {
-    const int R3 = wr3::SLOTS / g.Wo;
+  if (nine && (nine == 2 || Cout == 64) && g.kh == 3 && g.sh == 1 && g.sw == 1) {
+    // chunks of R output rows of one frame, balanced over the frame (as the nine-tap forward's tiles)
+    const int r0 = min(wr3::SLOTS / g.Wo, g.Ho);
+    const int cpf = (g.Ho + r0 - 1) / r0, R = (g.Ho + cpf - 1) / cpf;
     const int Ls3 = g.Wo - 1 + g.kw;
-    if ((min(R3, g.Ho) + 2) * Ls3 <= wr3::SQ) {
+    // (and >= 3/4 of the 256 slots used: layer 4's 7 x 7 frames keep the one-tap-row kernel)
+    if ((R + 2) * Ls3 <= wr3::SQ && (cpf - 1) * R < g.Ho && 4 * R * g.Wo >= 3 * wr3::SLOTS) {
       p.grp = 9;
       p.cot = 64;
-      p.R = min(R3, g.Ho);
+      p.R = R;
       p.Ls = Ls3;
-      p.cpf = (g.Ho + p.R - 1) / p.R;
+      p.cpf = cpf;
       p.nchunk = g.N * g.To * p.cpf;
-      const int tiles = g.kt * (g.C / 64);
+      const int tiles = g.kt * (g.C / 64) * (Cout / 64);
       // one 12-wave workgroup per CU: ~2 rounds, >= 4 chunks each, <= ~80 MB of split partials
       int s = (512 + tiles - 1) / tiles;
       s = min(s, (int)((80L << 20) / ((long)Cout * g.K * 4)));
@@ -2329,7 +2345,7 @@ extern "C" int cmhar_conv3d_wgrad(const int* dims, int Cout, const void* x, cons
     if (rp.splits > 1 && !ws) return -2;
     float* dst = rp.splits > 1 ? ws : dw;
     if (rp.grp == 9) {
-      const dim3 grid3(g.kt * (g.C / 64), rp.splits);
+      const dim3 grid3(g.kt * (g.C / 64) * (Cout / 64), rp.splits);
       conv3d_wgrad_rows3<<<grid3, wr3::NT, 0, stream>>>(g, Cout, rp.R, rp.Ls, rp.cpf, rp.nchunk, rp.cps,
                                                         (const bf16*)x, (const bf16*)dz, dst);
       if (rp.splits > 1) {

@@ -315,13 +315,16 @@ def test_crossmodal_with_r3d_backbone_steps():
                                                   (64, 64, 3, 1, 1, (2, 12, 40, 38)),
                                                   (128, 256, 1, 2, 0, (2, 4, 7, 9)), (192, 72, 3, 1, 1, (1, 3, 6, 5)),
                                                   (128, 128, 3, 1, 1, (2, 4, 28, 28)), (64, 64, 3, 1, 1, (1, 4, 10, 56)),
-                                                  (256, 512, 3, 2, 1, (1, 4, 14, 14))])
+                                                  (256, 512, 3, 2, 1, (1, 4, 14, 14)), (256, 256, 3, 1, 1, (1, 3, 14, 14)),
+                                                  (128, 192, 3, 1, 1, (1, 2, 30, 30))])
 def test_conv3d_implicit_gemm_fwd_wgrad(cin, cout, k, s, p, shape):
     """Implicit-GEMM forward / weight gradient (bf16 operands, fp32 MFMA accumulation) vs F.conv3d in fp32 on the
     same bf16-rounded operands: forward ≤ 5e-3 rel (bf16 output rounding), wgrad ≤ 1e-4 rel (fp32 output).  The
     k = 3 cases with Cout % 64 == 0 take the row-slab weight gradient (conv3d_wgrad_rows: whole output rows per chunk
     — Wo = 7 / 38 / 56 / 28 give 9 / 1 / 1 / 2 rows per chunk, stride 2 slabs of 2·Wo + 1 positions, Cout tiles of
-    64 and 128, one and two 64-channel slices); 1x1x1 and Cout = 72 the generic gather kernel."""
+    64 and 128, one and two 64-channel slices); the stride-1 3x3x3 cases whose frames fill >= 3/4 of a 256-slot tile
+    take the nine-tap forward (conv3d_fwd_rows3) on 64-wide Cout slices — 28², 14² (one 14-row tile of 4 slices),
+    30² (Ho = 30 over 4 tiles of 8, 8, 8, 6 rows, 3 slices); 1x1x1 and Cout = 72 the generic gather kernel."""
     from cmhar import _lib as L
     from cmhar import kernels as K
     from cmhar import r3d
@@ -422,7 +425,8 @@ def test_conv3d_implicit_stem_fwd_wgrad(cin, k, s, p, shape):
                        torch.zeros(64, kt, kh, 8 - kw, 4))
 
 
-@pytest.mark.parametrize('cin,cout,shape,acc', [(64, 64, (2, 4, 9, 7), True), (128, 192, (1, 3, 5, 6), False)])
+@pytest.mark.parametrize('cin,cout,shape,acc', [(64, 64, (2, 4, 9, 7), True), (128, 192, (1, 3, 5, 6), False),
+                                                (128, 128, (2, 3, 14, 28), True), (192, 256, (1, 2, 14, 14), True)])
 def test_conv3d_implicit_gemm_dgrad(cin, cout, shape, acc):
     """Stride-1 input gradient as the flipped-weight implicit GEMM (+ the residual-branch gradient in its epilogue)
     vs torch autograd of F.conv3d on the same bf16-rounded operands: ≤ 5e-3 rel."""

@@ -2,8 +2,8 @@
 `bench.py --workload r3d` / tools/bench_r3d.py, B = 32 clips of 16 × 112², bf16) at its PRODUCTION geometry, through
 the entry points the step itself calls (`cmhar/r3d.py` `_conv_fwd` / `_conv_wgrad` / `_conv_dgrad`, which `_unit_fwd` /
 `_unit_bwd` run between the BatchNorms) — VERDICT r04 item 2.  Smaller-shape tests (tests/test_r3d_gpu.py) do not
-reach these plans: layer 1's nine-tap kernels at 1.6 M output rows, the stride-1 convs of layers 2–3 on the 256-row
-slab (forward and flipped-weight input gradient), layer 4's on the split-K slab, the stride-2 convs and the
+reach these plans: the nine-tap kernels of layers 1–3 (layer 1 at 1.6 M output rows, layers 2–3 on 64-wide Cout
+slices; forward and flipped-weight input gradient), layer 4's on the split-K slab, the stride-2 convs and the
 downsamples on the generic 128×128 gather kernel with their input gradients as dz·W on the GEMM + col2im (the
 residual-branch gradient accumulated), every weight gradient on the row-slab / nine-tap / gather kernels with its
 split reduce.
@@ -46,10 +46,10 @@ PLANS = {
     'layer1.conv': (1, 'flip:1', '1+r'),
     'layer2.0.conv1': (5, 'col2im', '2+r'),          # stride 2: the row slab does not fit, generic 128x128 gather
     'layer2.0.downsample': (5, 'col2im', '4+r'),
-    'layer2.conv2': (3, 'flip:3', '2+r'),
+    'layer2.conv2': (1, 'flip:1', '2+r'),            # nine-tap forward slab, 7-row tiles x 64-wide Cout slices
     'layer3.0.conv1': (5, 'col2im', '2+r'),
     'layer3.0.downsample': (5, 'col2im', '4+r'),
-    'layer3.conv2': (3, 'flip:3', '2+r'),
+    'layer3.conv2': (1, 'flip:1', '2+r'),            # nine-tap forward slab, one 14-row tile per frame
     'layer4.0.conv1': (5, 'col2im', '2+r'),
     'layer4.0.downsample': (5, 'col2im', '4+r'),
     'layer4.conv2': ('split', 'flip:split', '2'),    # one split of the weight gradient: no reduce
