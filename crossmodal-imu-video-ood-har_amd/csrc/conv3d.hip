@@ -12,6 +12,16 @@
 
 namespace {
 
+// Register-prefetched operand loads of padding / out-of-range slots read a valid address and are zeroed when they
+// are written to LDS, not when they are loaded: a select on a prefetched load's result right after the load makes
+// the compiler wait for that load there (s_waitcnt vmcnt(0) in the load phase, before the compute it was meant to
+// overlap).  CMHAR_LATE_ZERO=0 (build flag): the select at the load (A/B builds).
+#ifndef CMHAR_LATE_ZERO
+#define CMHAR_LATE_ZERO 1
+#endif
+constexpr bool kLateZero = CMHAR_LATE_ZERO != 0;
+__device__ __forceinline__ uint4_t zero_unless(bool ok, uint4_t v) { return ok ? v : uint4_t{0u, 0u, 0u, 0u}; }
+
 template <typename T, int V> __device__ __forceinline__ void vload(const T* p, float* v) {
   if constexpr (V == 8) Vec8<T>::load(p, v);
   else for (int j = 0; j < V; ++j) v[j] = to_f<T>(p[j]);
@@ -735,28 +745,33 @@ __global__ __launch_bounds__(256, JN == 2 ? 3 : 2) void conv3d_fwd_igemm(Geom g,
   }
   const int kk8 = (tid & 7) * 8;
   uint4_t ra[4], rb[4];
+  unsigned am = 0, bmk = 0;   // kLateZero: in-range bits of ra / rb
   auto load = [&](int k0) {
     const int tap = k0 / g.C, c0 = k0 - tap * g.C + kk8;
     const int iw = tap % g.kw, ih = (tap / g.kw) % g.kh, itp = tap / (g.kw * g.kh);
+    am = bmk = 0;
 #pragma unroll
     for (int it = 0; it < 4; ++it) {
       const long off = aok[it] ? tap_src(g, an[it], at[it], ah[it], aw[it], itp, ih, iw) : -1;
       const uint4_t v = *(const uint4_t*)(x + (off >= 0 ? off + c0 : 0));
-      ra[it] = off >= 0 ? v : uint4_t{0u, 0u, 0u, 0u};
+      ra[it] = kLateZero ? v : zero_unless(off >= 0, v);
+      am |= (unsigned)(off >= 0) << it;
     }
 #pragma unroll
     for (int it = 0; it < NB; ++it) {
       const int co = bn + it * 32 + (tid >> 3);
       const uint4_t w = *(const uint4_t*)(Wt + (long)(co < Cout ? co : 0) * g.Kp + k0 + kk8);
-      rb[it] = co < Cout ? w : uint4_t{0u, 0u, 0u, 0u};
+      rb[it] = kLateZero ? w : zero_unless(co < Cout, w);
+      bmk |= (unsigned)(co < Cout) << it;
     }
   };
   auto store = [&](int buf) {
 #pragma unroll
     for (int it = 0; it < 4; ++it) {
       const int off = kc_off(it * 32 + (tid >> 3), tid & 7);
-      *(uint4_t*)(smem + 16384 * buf + off) = ra[it];
-      if (it < NB) *(uint4_t*)(smem + Lds::B0 + Lds::BSTAGE * buf + off) = rb[it];
+      *(uint4_t*)(smem + 16384 * buf + off) = kLateZero ? zero_unless((am >> it) & 1, ra[it]) : ra[it];
+      if (it < NB)
+        *(uint4_t*)(smem + Lds::B0 + Lds::BSTAGE * buf + off) = kLateZero ? zero_unless((bmk >> it) & 1, rb[it]) : rb[it];
     }
   };
   floatx4 acc[4][JN];
@@ -948,7 +963,9 @@ __global__ __launch_bounds__(64 * NW, 2) void conv3d_wgrad_rows(Geom g, int Cout
     }
   const int dz_off = (8 * gq + q) * RS + lane_col;
   uint4_t rdz[DZ_PER], rsl[SL_PER];
+  unsigned dmk = 0, smk = 0;   // kLateZero: in-range bits of rdz / rsl
   auto load = [&](int c) {
+    dmk = smk = 0;
     const int rho0 = c * R;
     const long m0 = (long)rho0 * g.Wo;
     const int ho0 = rho0 % g.Ho, tn0 = rho0 / g.Ho, to0 = tn0 % g.To, n0 = tn0 / g.To;
@@ -957,7 +974,8 @@ __global__ __launch_bounds__(64 * NW, 2) void conv3d_wgrad_rows(Geom g, int Cout
       const int e = i * NT + tid, j = e / (COT / 8), ch = e % (COT / 8);
       const bool ok = e < DZ_N && j < used && m0 + j < M;
       const uint4_t v = *(const uint4_t*)(dz + (ok ? (m0 + j) * Cout : 0) + cot * COT + ch * 8);
-      rdz[i] = ok ? v : uint4_t{0u, 0u, 0u, 0u};
+      rdz[i] = kLateZero ? v : zero_unless(ok, v);
+      dmk |= (unsigned)ok << i;
     }
 #pragma unroll
     for (int i = 0; i < SL_PER; ++i) {
@@ -973,7 +991,8 @@ __global__ __launch_bounds__(64 * NW, 2) void conv3d_wgrad_rows(Geom g, int Cout
           off = ((((long)n * g.T + ti) * g.H + hi) * g.W + wi) * g.C + ct * 64 + ((i * NT + tid) & 7) * 8;
       }
       const uint4_t v = *(const uint4_t*)(x + (off >= 0 ? off : 0));
-      rsl[i] = off >= 0 ? v : uint4_t{0u, 0u, 0u, 0u};
+      rsl[i] = kLateZero ? v : zero_unless(off >= 0, v);
+      smk |= (unsigned)(off >= 0) << i;
     }
   };
   auto store = [&](int buf) {
@@ -981,12 +1000,13 @@ __global__ __launch_bounds__(64 * NW, 2) void conv3d_wgrad_rows(Geom g, int Cout
 #pragma unroll
     for (int i = 0; i < DZ_PER; ++i) {
       const int e = i * NT + tid, j = e / (COT / 8), ch = e % (COT / 8);
-      if (e < DZ_N) *(uint4_t*)(base + (ch >> 3) * DZ_SUB + j * RS + (ch & 7) * 16) = rdz[i];
+      if (e < DZ_N)
+        *(uint4_t*)(base + (ch >> 3) * DZ_SUB + j * RS + (ch & 7) * 16) = kLateZero ? zero_unless((dmk >> i) & 1, rdz[i]) : rdz[i];
     }
 #pragma unroll
     for (int i = 0; i < SL_PER; ++i) {
       const int e = i * NT + tid, qq = e >> 3, ch = e & 7;
-      if (e < SL_N) *(uint4_t*)(base + DZ_BYTES + qq * RS + ch * 16) = rsl[i];
+      if (e < SL_N) *(uint4_t*)(base + DZ_BYTES + qq * RS + ch * 16) = kLateZero ? zero_unless((smk >> i) & 1, rsl[i]) : rsl[i];
     }
   };
   floatx4 acc[NCB][NJ];
@@ -1093,7 +1113,9 @@ __global__ __launch_bounds__(768, 1) void conv3d_wgrad_rows3(Geom g, int Cout, i
     }
   const int dz_off = (8 * gq + q4) * RS + lane_col;
   uint4_t rdz[DZ_PER], rsl[SL_PER];
+  unsigned dmk = 0, smk = 0;   // kLateZero: in-range bits of rdz / rsl
   auto load = [&](int c) {
+    dmk = smk = 0;
     const int f = c / cpf, ho0 = (c - f * cpf) * R, nr = min(R, g.Ho - ho0);
     const int to = f % g.To, n = f / g.To;
     const long m0 = ((long)f * g.Ho + ho0) * g.Wo;
@@ -1103,7 +1125,8 @@ __global__ __launch_bounds__(768, 1) void conv3d_wgrad_rows3(Geom g, int Cout, i
       const int e = i * NT + tid, j = e >> 3, ch = e & 7;
       const bool ok = e < DZ_N && j < used;
       const uint4_t v = *(const uint4_t*)(dz + (ok ? (m0 + j) * Cout : 0) + cot * 64 + ch * 8);
-      rdz[i] = ok ? v : uint4_t{0u, 0u, 0u, 0u};
+      rdz[i] = kLateZero ? v : zero_unless(ok, v);
+      dmk |= (unsigned)ok << i;
     }
     const int ti = to * g.st - g.pt + it;
     const bool tok = ti >= 0 && ti < g.T;
@@ -1114,19 +1137,20 @@ __global__ __launch_bounds__(768, 1) void conv3d_wgrad_rows3(Geom g, int Cout, i
       if (tok && su[i] < nr + 2 && hi >= 0 && hi < g.H && wi >= 0 && wi < g.W)
         off = ((((long)n * g.T + ti) * g.H + hi) * g.W + wi) * g.C + ct * 64 + ((i * NT + tid) & 7) * 8;
       const uint4_t v = *(const uint4_t*)(x + (off >= 0 ? off : 0));
-      rsl[i] = off >= 0 ? v : uint4_t{0u, 0u, 0u, 0u};
+      rsl[i] = kLateZero ? v : zero_unless(off >= 0, v);
+      smk |= (unsigned)(off >= 0) << i;
     }
   };
   auto store = [&]() {
 #pragma unroll
     for (int i = 0; i < DZ_PER; ++i) {
       const int e = i * NT + tid;
-      if (e < DZ_N) *(uint4_t*)(dzs + (e >> 3) * RS + (e & 7) * 16) = rdz[i];
+      if (e < DZ_N) *(uint4_t*)(dzs + (e >> 3) * RS + (e & 7) * 16) = kLateZero ? zero_unless((dmk >> i) & 1, rdz[i]) : rdz[i];
     }
 #pragma unroll
     for (int i = 0; i < SL_PER; ++i) {
       const int e = i * NT + tid;
-      if (e < SL_N) *(uint4_t*)(sls + (e >> 3) * RS + (e & 7) * 16) = rsl[i];
+      if (e < SL_N) *(uint4_t*)(sls + (e >> 3) * RS + (e & 7) * 16) = kLateZero ? zero_unless((smk >> i) & 1, rsl[i]) : rsl[i];
     }
   };
   floatx4 acc[4][3];
@@ -1259,9 +1283,11 @@ __global__ __launch_bounds__(256, 2) void conv3d_fwd_rows(Geom g, int M, int Cou
   const int split = blockIdx.y, nsp = gridDim.y;
   const int ks0 = (int)((long)nks_all * split / nsp), nks = (int)((long)nks_all * (split + 1) / nsp);
   uint4_t rsl[SL_PER], rw[W_PER];
+  unsigned smk = 0;   // kLateZero: in-range bits of rsl
   __syncthreads();   // the row table
   auto load = [&](int ks) {
     const int cc = ks % ncc, tap = ks / ncc, ih = tap % g.kh, it = tap / g.kh;
+    smk = 0;
 #pragma unroll
     for (int i = 0; i < SL_PER; ++i) {
       long off = -1;
@@ -1273,7 +1299,8 @@ __global__ __launch_bounds__(256, 2) void conv3d_fwd_rows(Geom g, int M, int Cou
           off = ((long)tab[r] + ((long)it * g.H + ih) * g.W + pos) * g.C + cc * 64 + ((i * NT + tid) & 7) * 8;
       }
       const uint4_t v = *(const uint4_t*)(x + (off >= 0 ? off : 0));
-      rsl[i] = off >= 0 ? v : uint4_t{0u, 0u, 0u, 0u};
+      rsl[i] = kLateZero ? v : zero_unless(off >= 0, v);
+      smk |= (unsigned)(off >= 0) << i;
     }
 #pragma unroll
     for (int i = 0; i < W_PER; ++i) {
@@ -1285,7 +1312,7 @@ __global__ __launch_bounds__(256, 2) void conv3d_fwd_rows(Geom g, int M, int Cou
 #pragma unroll
     for (int i = 0; i < SL_PER; ++i) {
       const int e = i * NT + tid, q = e >> 3, ch = e & 7;
-      if (q < SQ) *(uint4_t*)(slab + q * RS + ch * 16) = rsl[i];
+      if (q < SQ) *(uint4_t*)(slab + q * RS + ch * 16) = kLateZero ? zero_unless((smk >> i) & 1, rsl[i]) : rsl[i];
     }
 #pragma unroll
     for (int i = 0; i < W_PER; ++i) {
@@ -1448,13 +1475,30 @@ __global__ __launch_bounds__(256, 2) void conv3d_fwd_rows3(Geom g, int Cout, int
   const int used = nr * g.Wo;
   const long m0 = ((long)f * g.Ho + ho0) * g.Wo;
   const int nq = (nr + 2) * Ls;
-  // block-invariant slab slots: input row u (0..nr+1) and position
-  int su[SL_PER], sp[SL_PER];
+  // Operands through buffer resources with 32-bit byte offsets (the plan keeps x within 1 GiB): an offset past the
+  // resource's range reads zeros, so the zero padding needs no select on the loaded value (a select right after a
+  // prefetched load makes the compiler wait for it there) and no 64-bit address arithmetic per load.
+  const unsigned xbytes = (unsigned)((long)g.N * g.T * g.H * g.W * g.C * 2);
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)x, (short)0, (int)xbytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc((void*)Wt, (short)0, 0x7fffffff, 0x00020000);
+  // block-invariant slab slots: byte offset of the slot's 16 B in frame ti = 0 of clip n (input row ho0 − ph + u,
+  // u = 0..nr+1, and position), or 2^31 in the H / W padding or past the slab.  A load adds the group's frame offset
+  // (< 2^30, or 2^30 for a frame in the T padding): every sum with a 2^30 / 2^31 term lies in [2^30, 2^32) — past the
+  // resource's <= 2^30 bytes, so it reads zeros — and no select or branch is needed per load.
+  unsigned pb[SL_PER];
 #pragma unroll
   for (int i = 0; i < SL_PER; ++i) {
     const int q = (i * NT + tid) >> 3;
-    su[i] = q < nq ? q / Ls : -1;
-    sp[i] = q < nq ? q - su[i] * Ls - g.pw : 0;
+    const int u = q / Ls, wi = q - u * Ls - g.pw, hi = ho0 - g.ph + u;
+    pb[i] = q < nq && hi >= 0 && hi < g.H && wi >= 0 && wi < g.W
+                ? (unsigned)(((((n * g.T) * g.H + hi) * g.W + wi) * g.C + ((i * NT + tid) & 7) * 8) * 2) : 0x80000000u;
+  }
+  // weight pieces of this thread: byte offset of row bn + co, tap iw, channel chunk (+ the stage's (it, ih, cc) part)
+  int wb[W_PER];
+#pragma unroll
+  for (int i = 0; i < W_PER; ++i) {
+    const int e = i * NT + tid, iw = e >> 9, co = (e >> 3) & 63, ch = e & 7;
+    wb[i] = ((bn + co) * g.Kp + iw * g.C + ch * 8) * 2;
   }
   // A fragment rows of this lane (slots 64·wave + 16i + lane&15 → slab row of tap ih = iw = 0); its 16-B chunk
   // within a 64-B K half is lane >> 4
@@ -1468,36 +1512,31 @@ __global__ __launch_bounds__(256, 2) void conv3d_fwd_rows3(Geom g, int Cout, int
   const int b_off = LY::at(lane & 15, cl);        // weight row 16j + lane&15 of tap iw: + (iw·TN + 16j) rows
   const int ncc = g.C / 64, nst = g.kt * ncc * 3;
   uint4_t rsl[SL_PER], rw[W_PER];
-  // stage s = (it, cc, ih), ih fastest; the slab changes with (it, cc), i.e. at ih = 0
-  auto load = [&](int st) {
+  // stage s = (it, cc, ih), ih fastest; the slab changes with the group (it, cc), i.e. at ih = 0
+  auto load_slab = [&](int grp) {
+    const int cc = grp % ncc, it = grp / ncc;
+    const int ti = to * g.st - g.pt + it;
+    const bool tok = ti >= 0 && ti < g.T;
+    const unsigned so = tok ? (unsigned)((ti * g.H * g.W * g.C + cc * 64) * 2) : 0x40000000u;
+#pragma unroll
+    for (int i = 0; i < SL_PER; ++i)
+      rsl[i] = __builtin_bit_cast(uint4_t, __builtin_amdgcn_raw_buffer_load_b128(xr, pb[i] + so, 0, 0));
+  };
+  auto load_w = [&](int st) {
     const int ih = st % 3, cc = (st / 3) % ncc, it = st / (3 * ncc);
-    if (ih == 0) {
-      const int ti = to * g.st - g.pt + it;
-      const bool tok = ti >= 0 && ti < g.T;
+    const int so = (((it * g.kh + ih) * g.kw) * g.C + cc * 64) * 2;    // wave-uniform: the scalar offset
 #pragma unroll
-      for (int i = 0; i < SL_PER; ++i) {
-        const int hi = ho0 - g.ph + su[i], wi = sp[i];
-        long off = -1;
-        if (tok && su[i] >= 0 && hi >= 0 && hi < g.H && wi >= 0 && wi < g.W)
-          off = ((((long)n * g.T + ti) * g.H + hi) * g.W + wi) * g.C + cc * 64 + ((i * NT + tid) & 7) * 8;
-        const uint4_t v = *(const uint4_t*)(x + (off >= 0 ? off : 0));
-        rsl[i] = off >= 0 ? v : uint4_t{0u, 0u, 0u, 0u};
-      }
-    }
+    for (int i = 0; i < W_PER; ++i)
+      rw[i] = __builtin_bit_cast(uint4_t, __builtin_amdgcn_raw_buffer_load_b128(wrs, wb[i], so, 0));
+  };
+  auto store_slab = [&]() {
 #pragma unroll
-    for (int i = 0; i < W_PER; ++i) {
-      const int e = i * NT + tid, iw = e >> 9, co = (e >> 3) & 63, ch = e & 7;
-      rw[i] = *(const uint4_t*)(Wt + (long)(bn + co) * g.Kp + ((it * g.kh + ih) * g.kw + iw) * g.C + cc * 64 + ch * 8);
+    for (int i = 0; i < SL_PER; ++i) {
+      const int e = i * NT + tid;
+      if ((e >> 3) < SQ) *(uint4_t*)(slab + LY::at(e >> 3, e & 7)) = rsl[i];
     }
   };
-  auto store = [&](int st) {
-    if (st % 3 == 0) {
-#pragma unroll
-      for (int i = 0; i < SL_PER; ++i) {
-        const int e = i * NT + tid;
-        if ((e >> 3) < SQ) *(uint4_t*)(slab + LY::at(e >> 3, e & 7)) = rsl[i];
-      }
-    }
+  auto store_w = [&]() {
 #pragma unroll
     for (int i = 0; i < W_PER; ++i) {
       const int e = i * NT + tid;
@@ -1509,13 +1548,8 @@ __global__ __launch_bounds__(256, 2) void conv3d_fwd_rows3(Geom g, int Cout, int
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
-  load(0);
-  store(0);
-  __syncthreads();
-  for (int st = 0; st < nst; ++st) {
-    const bool more = st + 1 < nst;
-    if (more) load(st + 1);
-    const int rsh = (st % 3) * Ls;                   // input row r + ih
+  auto compute = [&](int ih) {
+    const int rsh = ih * Ls;                         // input row r + ih
 #pragma unroll
     for (int iw = 0; iw < 3; ++iw)
 #pragma unroll
@@ -1535,8 +1569,27 @@ __global__ __launch_bounds__(256, 2) void conv3d_fwd_rows3(Geom g, int Cout, int
 #pragma unroll
           for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
       }
+  };
+  load_slab(0);
+  load_w(0);
+  store_slab();
+  store_w();
+  __syncthreads();
+  for (int st = 0; st < nst; ++st) {
+    // the next stage's operands in registers during this stage's MFMAs (the slab only when the group changes);
+    // loading the next group's slab at the group's first stage instead (three phases of prefetch) spilled
+    // (256 VGPRs + 140 B scratch) and ran layer 1 at 738 vs 491 us
+    const bool more = st + 1 < nst;
+    if (more) {
+      if ((st + 1) % 3 == 0) load_slab((st + 1) / 3);
+      load_w(st + 1);
+    }
+    compute(st % 3);
     __syncthreads();
-    if (more) store(st + 1);
+    if (more) {
+      if ((st + 1) % 3 == 0) store_slab();
+      store_w();
+    }
     __syncthreads();
   }
   float* T = (float*)smem;
@@ -2054,7 +2107,8 @@ static bool fwd3_plan(const Geom& g, int Cout, Fwd3Plan& p) {
     return v && (v[0] == '0' || v[0] == '1') ? v[0] - '0' : 2;
   }();
   if (!mode || (mode == 1 && Cout != fr3::TN) || Cout % fr3::TN || g.kh != 3 || g.kw != 3 || g.sh != 1 ||
-      g.sw != 1 || g.C % 64 || g.Wo > 256 || (long)g.N * g.T * g.H * g.W >= (1L << 30))
+      g.sw != 1 || g.C % 64 || g.Wo > 256 || (long)g.N * g.T * g.H * g.W * g.C * 2 > (1L << 30) ||
+      (long)Cout * g.Kp * 2 > 0x7fffffffL)   // 32-bit buffer offsets of x (<= 1 GiB) and of the weights
     return false;
   const int r0 = min(256 / g.Wo, g.Ho);
   p.cpf = (g.Ho + r0 - 1) / r0;
