@@ -722,7 +722,7 @@ template <int JN> struct FwdLds {
   static constexpr int BYTES = OPS > EPI + 2048 ? OPS : EPI + 2048;   // + tile_col_stats scratch past the image
 };
 
-template <int JN>
+template <int JN, bool BUF>
 __global__ __launch_bounds__(256, JN == 2 ? 3 : 2) void conv3d_fwd_igemm(Geom g, int M, int Cout, const bf16* __restrict__ x,
                                                            const bf16* __restrict__ Wt, const bf16* __restrict__ res,
                                                            bf16* __restrict__ z, float* __restrict__ tstats) {
@@ -745,7 +745,13 @@ __global__ __launch_bounds__(256, JN == 2 ? 3 : 2) void conv3d_fwd_igemm(Geom g,
   }
   const int kk8 = (tid & 7) * 8;
   uint4_t ra[4], rb[4];
-  unsigned am = 0, bmk = 0;   // kLateZero: in-range bits of ra / rb
+  // BUF: operands through buffer resources with 32-bit byte offsets (x and the weights under 2 GiB); padding and
+  // out-of-range rows / columns load from offset 2^31, past the resource, which reads zeros (as conv3d_fwd_rows3).
+  // Otherwise 64-bit addresses, the padding zeroed at the LDS store.
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)x, (short)0, (int)min((long)g.N * g.T * g.H * g.W * g.C * 2, 0x7fffffffL), 0x00020000);
+  const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc((void*)Wt, (short)0, 0x7fffffff, 0x00020000);
+  unsigned am = 0, bmk = 0;   // !BUF: in-range bits of ra / rb
   auto load = [&](int k0) {
     const int tap = k0 / g.C, c0 = k0 - tap * g.C + kk8;
     const int iw = tap % g.kw, ih = (tap / g.kw) % g.kh, itp = tap / (g.kw * g.kh);
@@ -753,25 +759,33 @@ __global__ __launch_bounds__(256, JN == 2 ? 3 : 2) void conv3d_fwd_igemm(Geom g,
 #pragma unroll
     for (int it = 0; it < 4; ++it) {
       const long off = aok[it] ? tap_src(g, an[it], at[it], ah[it], aw[it], itp, ih, iw) : -1;
-      const uint4_t v = *(const uint4_t*)(x + (off >= 0 ? off + c0 : 0));
-      ra[it] = kLateZero ? v : zero_unless(off >= 0, v);
-      am |= (unsigned)(off >= 0) << it;
+      if constexpr (BUF) {
+        const unsigned bo = off >= 0 ? (unsigned)((off + c0) * 2) : 0x80000000u;
+        ra[it] = __builtin_bit_cast(uint4_t, __builtin_amdgcn_raw_buffer_load_b128(xr, bo, 0, 0));
+      } else {
+        ra[it] = *(const uint4_t*)(x + (off >= 0 ? off + c0 : 0));
+        am |= (unsigned)(off >= 0) << it;
+      }
     }
 #pragma unroll
     for (int it = 0; it < NB; ++it) {
       const int co = bn + it * 32 + (tid >> 3);
-      const uint4_t w = *(const uint4_t*)(Wt + (long)(co < Cout ? co : 0) * g.Kp + k0 + kk8);
-      rb[it] = kLateZero ? w : zero_unless(co < Cout, w);
-      bmk |= (unsigned)(co < Cout) << it;
+      if constexpr (BUF) {
+        const unsigned bo = co < Cout ? (unsigned)((co * g.Kp + k0 + kk8) * 2) : 0x80000000u;
+        rb[it] = __builtin_bit_cast(uint4_t, __builtin_amdgcn_raw_buffer_load_b128(wrs, bo, 0, 0));
+      } else {
+        rb[it] = *(const uint4_t*)(Wt + (long)(co < Cout ? co : 0) * g.Kp + k0 + kk8);
+        bmk |= (unsigned)(co < Cout) << it;
+      }
     }
   };
   auto store = [&](int buf) {
 #pragma unroll
     for (int it = 0; it < 4; ++it) {
       const int off = kc_off(it * 32 + (tid >> 3), tid & 7);
-      *(uint4_t*)(smem + 16384 * buf + off) = kLateZero ? zero_unless((am >> it) & 1, ra[it]) : ra[it];
+      *(uint4_t*)(smem + 16384 * buf + off) = BUF ? ra[it] : zero_unless((am >> it) & 1, ra[it]);
       if (it < NB)
-        *(uint4_t*)(smem + Lds::B0 + Lds::BSTAGE * buf + off) = kLateZero ? zero_unless((bmk >> it) & 1, rb[it]) : rb[it];
+        *(uint4_t*)(smem + Lds::B0 + Lds::BSTAGE * buf + off) = BUF ? rb[it] : zero_unless((bmk >> it) & 1, rb[it]);
     }
   };
   floatx4 acc[4][JN];
@@ -962,24 +976,27 @@ __global__ __launch_bounds__(64 * NW, 2) void conv3d_wgrad_rows(Geom g, int Cout
       sl_off[kk][hh] = (k < used ? (k / g.Wo) * Ls + (k % g.Wo) * g.sw : 0) * RS + lane_col;
     }
   const int dz_off = (8 * gq + q) * RS + lane_col;
+  // operands through buffer resources with 32-bit byte offsets (the plan keeps x and dz within 1 GiB); padding and
+  // out-of-range slots load from offset 2^31, past the resource, which reads zeros (as conv3d_fwd_rows3)
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)x, (short)0, (int)((long)g.N * g.T * g.H * g.W * g.C * 2), 0x00020000);
+  const __amdgpu_buffer_rsrc_t dzr = __builtin_amdgcn_make_buffer_rsrc((void*)dz, (short)0, (int)((long)M * Cout * 2),
+                                                                        0x00020000);
   uint4_t rdz[DZ_PER], rsl[SL_PER];
-  unsigned dmk = 0, smk = 0;   // kLateZero: in-range bits of rdz / rsl
   auto load = [&](int c) {
-    dmk = smk = 0;
     const int rho0 = c * R;
-    const long m0 = (long)rho0 * g.Wo;
+    const int m0 = rho0 * g.Wo;
     const int ho0 = rho0 % g.Ho, tn0 = rho0 / g.Ho, to0 = tn0 % g.To, n0 = tn0 / g.To;
 #pragma unroll
     for (int i = 0; i < DZ_PER; ++i) {
       const int e = i * NT + tid, j = e / (COT / 8), ch = e % (COT / 8);
       const bool ok = e < DZ_N && j < used && m0 + j < M;
-      const uint4_t v = *(const uint4_t*)(dz + (ok ? (m0 + j) * Cout : 0) + cot * COT + ch * 8);
-      rdz[i] = kLateZero ? v : zero_unless(ok, v);
-      dmk |= (unsigned)ok << i;
+      const unsigned off = ok ? (unsigned)(((m0 + j) * Cout + cot * COT + ch * 8) * 2) : 0x80000000u;
+      rdz[i] = __builtin_bit_cast(uint4_t, __builtin_amdgcn_raw_buffer_load_b128(dzr, off, 0, 0));
     }
 #pragma unroll
     for (int i = 0; i < SL_PER; ++i) {
-      long off = -1;
+      unsigned off = 0x80000000u;
       if (sr[i] >= 0 && rho0 + sr[i] < rows_total) {
         int ho = ho0 + sr[i], to = to0, n = n0;
         while (ho >= g.Ho) {          // at most R / Ho + 1 wraps
@@ -988,11 +1005,9 @@ __global__ __launch_bounds__(64 * NW, 2) void conv3d_wgrad_rows(Geom g, int Cout
         }
         const int ti = to * g.st - g.pt + it, hi = ho * g.sh + sdh[i], wi = swi[i];
         if (ti >= 0 && ti < g.T && hi >= 0 && hi < g.H && wi >= 0 && wi < g.W)
-          off = ((((long)n * g.T + ti) * g.H + hi) * g.W + wi) * g.C + ct * 64 + ((i * NT + tid) & 7) * 8;
+          off = (unsigned)(((((n * g.T + ti) * g.H + hi) * g.W + wi) * g.C + ct * 64 + ((i * NT + tid) & 7) * 8) * 2);
       }
-      const uint4_t v = *(const uint4_t*)(x + (off >= 0 ? off : 0));
-      rsl[i] = kLateZero ? v : zero_unless(off >= 0, v);
-      smk |= (unsigned)(off >= 0) << i;
+      rsl[i] = __builtin_bit_cast(uint4_t, __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 0));
     }
   };
   auto store = [&](int buf) {
@@ -1000,13 +1015,12 @@ __global__ __launch_bounds__(64 * NW, 2) void conv3d_wgrad_rows(Geom g, int Cout
 #pragma unroll
     for (int i = 0; i < DZ_PER; ++i) {
       const int e = i * NT + tid, j = e / (COT / 8), ch = e % (COT / 8);
-      if (e < DZ_N)
-        *(uint4_t*)(base + (ch >> 3) * DZ_SUB + j * RS + (ch & 7) * 16) = kLateZero ? zero_unless((dmk >> i) & 1, rdz[i]) : rdz[i];
+      if (e < DZ_N) *(uint4_t*)(base + (ch >> 3) * DZ_SUB + j * RS + (ch & 7) * 16) = rdz[i];
     }
 #pragma unroll
     for (int i = 0; i < SL_PER; ++i) {
       const int e = i * NT + tid, qq = e >> 3, ch = e & 7;
-      if (e < SL_N) *(uint4_t*)(base + DZ_BYTES + qq * RS + ch * 16) = kLateZero ? zero_unless((smk >> i) & 1, rsl[i]) : rsl[i];
+      if (e < SL_N) *(uint4_t*)(base + DZ_BYTES + qq * RS + ch * 16) = rsl[i];
     }
   };
   floatx4 acc[NCB][NJ];
@@ -1090,13 +1104,21 @@ __global__ __launch_bounds__(768, 1) void conv3d_wgrad_rows3(Geom g, int Cout, i
   const int ct = tl % nct;
   const int it = tl / nct;
   const int c_beg = split * chunks_per_split, c_end = min(nchunk, c_beg + chunks_per_split);
-  // chunk-invariant slab slots: (input row u, position)
-  int su[SL_PER], sp[SL_PER];
+  // operands through buffer resources with 32-bit byte offsets (the plan keeps x and dz within 1 GiB); padding and
+  // out-of-range slots load from offset 2^31, past the resource, which reads zeros (as conv3d_fwd_rows3)
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)x, (short)0, (int)((long)g.N * g.T * g.H * g.W * g.C * 2), 0x00020000);
+  const __amdgpu_buffer_rsrc_t dzr = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)dz, (short)0, (int)((long)g.N * g.To * g.Ho * g.Wo * Cout * 2), 0x00020000);
+  // chunk-invariant slab slots: input row u of the chunk's slab and the byte offset of the slot's 16 B relative to
+  // the slab's first input row (-1 in the W padding)
+  int su[SL_PER], sb[SL_PER];
 #pragma unroll
   for (int i = 0; i < SL_PER; ++i) {
     const int q = (i * NT + tid) >> 3;
     su[i] = q / Ls;
-    sp[i] = q - su[i] * Ls - g.pw;
+    const int wi = q - su[i] * Ls - g.pw;
+    sb[i] = wi >= 0 && wi < g.W ? ((su[i] * g.W + wi) * g.C + ct * 64 + ((i * NT + tid) & 7) * 8) * 2 : -1;
   }
   // fragment rows of this lane: slot k → (r, wo) → slab row r·Ls + wo (+ ih·Ls + iw per column block); slots past
   // the chunk's rows read row 0 (their dz is zero)
@@ -1113,44 +1135,38 @@ __global__ __launch_bounds__(768, 1) void conv3d_wgrad_rows3(Geom g, int Cout, i
     }
   const int dz_off = (8 * gq + q4) * RS + lane_col;
   uint4_t rdz[DZ_PER], rsl[SL_PER];
-  unsigned dmk = 0, smk = 0;   // kLateZero: in-range bits of rdz / rsl
   auto load = [&](int c) {
-    dmk = smk = 0;
     const int f = c / cpf, ho0 = (c - f * cpf) * R, nr = min(R, g.Ho - ho0);
     const int to = f % g.To, n = f / g.To;
-    const long m0 = ((long)f * g.Ho + ho0) * g.Wo;
+    const int m0 = (f * g.Ho + ho0) * g.Wo;
     const int used = nr * g.Wo;
 #pragma unroll
     for (int i = 0; i < DZ_PER; ++i) {
       const int e = i * NT + tid, j = e >> 3, ch = e & 7;
-      const bool ok = e < DZ_N && j < used;
-      const uint4_t v = *(const uint4_t*)(dz + (ok ? (m0 + j) * Cout : 0) + cot * 64 + ch * 8);
-      rdz[i] = kLateZero ? v : zero_unless(ok, v);
-      dmk |= (unsigned)ok << i;
+      const unsigned off = e < DZ_N && j < used ? (unsigned)(((m0 + j) * Cout + cot * 64 + ch * 8) * 2) : 0x80000000u;
+      rdz[i] = __builtin_bit_cast(uint4_t, __builtin_amdgcn_raw_buffer_load_b128(dzr, off, 0, 0));
     }
+    // slab row u is input row ho0 − ph + u of frame ti: in range for u in [u_lo, u_hi) (none when ti is padding)
     const int ti = to * g.st - g.pt + it;
     const bool tok = ti >= 0 && ti < g.T;
+    const int u_lo = tok ? g.ph - ho0 : 0x7fffffff, u_hi = min(g.H + g.ph - ho0, nr + 2);
+    const int base = (((n * g.T + ti) * g.H + ho0 - g.ph) * g.W) * g.C * 2;
 #pragma unroll
     for (int i = 0; i < SL_PER; ++i) {
-      const int hi = ho0 - g.ph + su[i], wi = sp[i];
-      long off = -1;
-      if (tok && su[i] < nr + 2 && hi >= 0 && hi < g.H && wi >= 0 && wi < g.W)
-        off = ((((long)n * g.T + ti) * g.H + hi) * g.W + wi) * g.C + ct * 64 + ((i * NT + tid) & 7) * 8;
-      const uint4_t v = *(const uint4_t*)(x + (off >= 0 ? off : 0));
-      rsl[i] = kLateZero ? v : zero_unless(off >= 0, v);
-      smk |= (unsigned)(off >= 0) << i;
+      const unsigned off = su[i] >= u_lo && su[i] < u_hi && sb[i] >= 0 ? (unsigned)(base + sb[i]) : 0x80000000u;
+      rsl[i] = __builtin_bit_cast(uint4_t, __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 0));
     }
   };
   auto store = [&]() {
 #pragma unroll
     for (int i = 0; i < DZ_PER; ++i) {
       const int e = i * NT + tid;
-      if (e < DZ_N) *(uint4_t*)(dzs + (e >> 3) * RS + (e & 7) * 16) = kLateZero ? zero_unless((dmk >> i) & 1, rdz[i]) : rdz[i];
+      if (e < DZ_N) *(uint4_t*)(dzs + (e >> 3) * RS + (e & 7) * 16) = rdz[i];
     }
 #pragma unroll
     for (int i = 0; i < SL_PER; ++i) {
       const int e = i * NT + tid;
-      if (e < SL_N) *(uint4_t*)(sls + (e >> 3) * RS + (e & 7) * 16) = kLateZero ? zero_unless((smk >> i) & 1, rsl[i]) : rsl[i];
+      if (e < SL_N) *(uint4_t*)(sls + (e >> 3) * RS + (e & 7) * 16) = rsl[i];
     }
   };
   floatx4 acc[4][3];
@@ -1283,36 +1299,42 @@ __global__ __launch_bounds__(256, 2) void conv3d_fwd_rows(Geom g, int M, int Cou
   const int split = blockIdx.y, nsp = gridDim.y;
   const int ks0 = (int)((long)nks_all * split / nsp), nks = (int)((long)nks_all * (split + 1) / nsp);
   uint4_t rsl[SL_PER], rw[W_PER];
-  unsigned smk = 0;   // kLateZero: in-range bits of rsl
+  // operands through buffer resources with 32-bit byte offsets (the plan keeps x within 1 GiB); padding slots load
+  // from offset 2^31, past the resource, which reads zeros (as conv3d_fwd_rows3)
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)x, (short)0, (int)((long)g.N * g.T * g.H * g.W * g.C * 2), 0x00020000);
+  const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc((void*)Wt, (short)0, 0x7fffffff, 0x00020000);
+  int wb[W_PER];   // this thread's weight pieces: byte offset of row bn + co, tap iw, channel chunk
+#pragma unroll
+  for (int i = 0; i < W_PER; ++i) {
+    const int e = i * NT + tid, iw = e >> 9, co = (e >> 3) & 63, ch = e & 7;
+    wb[i] = ((bn + co) * g.Kp + iw * g.C + ch * 8) * 2;
+  }
   __syncthreads();   // the row table
   auto load = [&](int ks) {
     const int cc = ks % ncc, tap = ks / ncc, ih = tap % g.kh, it = tap / g.kh;
-    smk = 0;
 #pragma unroll
     for (int i = 0; i < SL_PER; ++i) {
-      long off = -1;
+      unsigned off = 0x80000000u;
       if (spos[i] >= 0) {
         const int r = spos[i] >> 8, pos = spos[i] & 255;
         const unsigned th = (unsigned)tab[64 + r];
         const int ti = (int)(th & 0xffffu) - 0x8000 + it, hi = (int)(th >> 16) - 0x8000 + ih, wi = pos - g.pw;
         if (ti >= 0 && ti < g.T && hi >= 0 && hi < g.H && wi >= 0 && wi < g.W)
-          off = ((long)tab[r] + ((long)it * g.H + ih) * g.W + pos) * g.C + cc * 64 + ((i * NT + tid) & 7) * 8;
+          off = (unsigned)(((tab[r] + (it * g.H + ih) * g.W + pos) * g.C + cc * 64 + ((i * NT + tid) & 7) * 8) * 2);
       }
-      const uint4_t v = *(const uint4_t*)(x + (off >= 0 ? off : 0));
-      rsl[i] = kLateZero ? v : zero_unless(off >= 0, v);
-      smk |= (unsigned)(off >= 0) << i;
+      rsl[i] = __builtin_bit_cast(uint4_t, __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 0));
     }
+    const int so = (((it * g.kh + ih) * g.kw) * g.C + cc * 64) * 2;    // wave-uniform: the scalar offset
 #pragma unroll
-    for (int i = 0; i < W_PER; ++i) {
-      const int e = i * NT + tid, iw = e >> 9, co = (e >> 3) & 63, ch = e & 7;
-      rw[i] = *(const uint4_t*)(Wt + (long)(bn + co) * g.Kp + ((it * g.kh + ih) * g.kw + iw) * g.C + cc * 64 + ch * 8);
-    }
+    for (int i = 0; i < W_PER; ++i)
+      rw[i] = __builtin_bit_cast(uint4_t, __builtin_amdgcn_raw_buffer_load_b128(wrs, wb[i], so, 0));
   };
   auto store = [&]() {
 #pragma unroll
     for (int i = 0; i < SL_PER; ++i) {
       const int e = i * NT + tid, q = e >> 3, ch = e & 7;
-      if (q < SQ) *(uint4_t*)(slab + q * RS + ch * 16) = kLateZero ? zero_unless((smk >> i) & 1, rsl[i]) : rsl[i];
+      if (q < SQ) *(uint4_t*)(slab + q * RS + ch * 16) = rsl[i];
     }
 #pragma unroll
     for (int i = 0; i < W_PER; ++i) {
@@ -2150,7 +2172,9 @@ static int fwd_split_count(const Geom& g, int Cout) {
   if (fwd3_plan(g, Cout, p3)) return 0;
   const int M = g.N * g.To * g.Ho * g.Wo;
   const int Ls = (g.Wo - 1) * g.sw + g.kw;
-  if (g.kw != 3 || Cout % fr::TN || g.Wo > 255 || Ls > 255 || (long)g.N * g.T * g.H * g.W >= (1L << 30)) return 0;
+  if (g.kw != 3 || Cout % fr::TN || g.Wo > 255 || Ls > 255 || (long)g.N * g.T * g.H * g.W * g.C * 2 > (1L << 30) ||
+      (long)Cout * g.Kp * 2 > 0x7fffffffL)
+    return 0;
   if ((long)((128 + g.Wo - 2) / g.Wo + 1) * Ls > fr::Cfg<128>::SQ) return 0;
   const long t128 = (long)((M + 127) / 128) * (Cout / fr::TN);
   if (t128 >= 256) return 0;
@@ -2195,7 +2219,7 @@ static int fwd_plan(const Geom& g, int Cout) {
   const int Ls = (g.Wo - 1) * g.sw + g.kw;
   auto fits = [&](int tm, int sq) { return (long)((tm + g.Wo - 2) / g.Wo + 1) * Ls <= sq; };   // rows a tile touches
   if (rows_on && g.kw == 3 && Cout % fr::TN == 0 && g.Wo <= 255 && Ls <= 255 &&
-      (long)g.N * g.T * g.H * g.W < (1L << 30)) {
+      (long)g.N * g.T * g.H * g.W * g.C * 2 <= (1L << 30) && (long)Cout * g.Kp * 2 <= 0x7fffffffL) {   // 32-bit offsets
     // 256-row tiles while they give every CU a workgroup, else 128-row tiles (R3D-18 layer 4: 268 -> 164 us; layer 3
     // at 392 256-row tiles measured 167 vs 199 us, so it keeps them)
     const long t256 = (long)((M + 255) / 256) * (Cout / fr::TN);
@@ -2239,13 +2263,21 @@ extern "C" int cmhar_conv3d_fwd(const int* dims, int Cout, const void* x, const 
       conv3d_fwd_rows<256><<<((M + 255) / 256) * (Cout / fr::TN), 256, 0, stream>>>(
           g, M, Cout, Ls, (const bf16*)x, (const bf16*)w, (const bf16*)res, (bf16*)z, tile_stats);
       break;
-    case 4:
-      conv3d_fwd_igemm<2><<<(M + 127) / 128, 256, 0, stream>>>(g, M, Cout, (const bf16*)x, (const bf16*)w,
-                                                                (const bf16*)res, (bf16*)z, tile_stats);
-      break;
-    default:
-      conv3d_fwd_igemm<4><<<((M + 127) / 128) * ((Cout + 127) / 128), 256, 0, stream>>>(
-          g, M, Cout, (const bf16*)x, (const bf16*)w, (const bf16*)res, (bf16*)z, tile_stats);
+    default: {
+      // 32-bit buffer offsets when x and the weights are under 2 GiB
+      const bool buf = (long)g.N * g.T * g.H * g.W * g.C * 2 <= 0x7fffffffL && (long)Cout * g.Kp * 2 <= 0x7fffffffL;
+#define IG(JN, BUF, GRID)                                                                                        \
+  conv3d_fwd_igemm<JN, BUF><<<GRID, 256, 0, stream>>>(g, M, Cout, (const bf16*)x, (const bf16*)w, (const bf16*)res, \
+                                                      (bf16*)z, tile_stats)
+      if (plan == 4) {
+        if (buf) IG(2, true, (M + 127) / 128);
+        else IG(2, false, (M + 127) / 128);
+      } else {
+        if (buf) IG(4, true, ((M + 127) / 128) * ((Cout + 127) / 128));
+        else IG(4, false, ((M + 127) / 128) * ((Cout + 127) / 128));
+      }
+#undef IG
+    }
   }
   CMHAR_CHECK_LAUNCH();
   return 0;
@@ -2356,8 +2388,10 @@ static bool rows_plan(const Geom& g, int Cout, RowsPlan& p) {
     const int r0 = min(wr3::SLOTS / g.Wo, g.Ho);
     const int cpf = (g.Ho + r0 - 1) / r0, R = (g.Ho + cpf - 1) / cpf;
     const int Ls3 = g.Wo - 1 + g.kw;
-    // (and >= 3/4 of the 256 slots used: layer 4's 7 x 7 frames keep the one-tap-row kernel)
-    if ((R + 2) * Ls3 <= wr3::SQ && (cpf - 1) * R < g.Ho && 4 * R * g.Wo >= 3 * wr3::SLOTS) {
+    // (and >= 3/4 of the 256 slots used: layer 4's 7 x 7 frames keep the one-tap-row kernel); x and dz within 1 GiB
+    // (32-bit buffer offsets)
+    if ((R + 2) * Ls3 <= wr3::SQ && (cpf - 1) * R < g.Ho && 4 * R * g.Wo >= 3 * wr3::SLOTS &&
+        (long)g.N * g.T * g.H * g.W * g.C * 2 <= (1L << 30) && (long)g.N * g.To * g.Ho * g.Wo * Cout * 2 <= (1L << 30)) {
       p.grp = 9;
       p.cot = 64;
       p.R = R;
@@ -2378,6 +2412,9 @@ static bool rows_plan(const Geom& g, int Cout, RowsPlan& p) {
   p.R = wr::SLOTS / g.Wo;
   p.Ls = (g.Wo - 1) * g.sw + g.kw;
   if (p.R * p.Ls > wr::MAXQ) return false;
+  // 32-bit buffer offsets of x and dz
+  if ((long)g.N * g.T * g.H * g.W * g.C * 2 > (1L << 30) || (long)g.N * g.To * g.Ho * g.Wo * Cout * 2 > (1L << 30))
+    return false;
   p.rows = g.N * g.To * g.Ho;
   p.cot = Cout % 128 == 0 ? 128 : 64;
   // Cout = 64: three kh taps per workgroup when their slabs fit 64 rows each

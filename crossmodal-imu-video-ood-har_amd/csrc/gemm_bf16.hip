@@ -29,11 +29,15 @@ __device__ __forceinline__ int mc_off(int k, int chunk) { return k * 256 + ((chu
 template <bool KC>
 struct Stage {
   uint4_t r[4];
+  unsigned ok = 0xfu;   // in-range bits of r (BOUNDS loads)
   // Load this operand's tile (rows r0.., k0..) into registers; rows = M or N index.  BOUNDS: rows / k past the
-  // matrix edge read a clamped (valid) address and are zeroed by a value select — never a branch around a load.
+  // matrix edge read a clamped (valid) address — never a branch around a load — and are zeroed when the tile is
+  // written to LDS: a select on the value right after the load makes the compiler wait for that load there, before
+  // the compute the register prefetch is meant to overlap (conv3d.hip, kLateZero).
   template <bool BOUNDS>
   __device__ __forceinline__ void load(const bf16* __restrict__ P, long ld, int rows_total, int r0, int k0,
                                        int kend, int tid) {
+    if (BOUNDS) ok = 0;
 #pragma unroll
     for (int it = 0; it < 4; ++it) {
       const int c = it * NT + tid;
@@ -41,10 +45,10 @@ struct Stage {
       if (KC) { row = c >> 3; kk = (c & 7) * 8; } else { kk = c >> 4; row = (c & 15) * 8; }
       const int gr = r0 + row, gk = k0 + kk;
       if (BOUNDS) {
-        const bool ok = gr < rows_total && gk < kend;
-        const bf16* src = ok ? (KC ? (P + (long)gr * ld + gk) : (P + (long)gk * ld + gr)) : P;
-        const uint4_t v = *(const uint4_t*)src;
-        r[it] = ok ? v : uint4_t{0u, 0u, 0u, 0u};
+        const bool in = gr < rows_total && gk < kend;
+        const bf16* src = in ? (KC ? (P + (long)gr * ld + gk) : (P + (long)gk * ld + gr)) : P;
+        r[it] = *(const uint4_t*)src;
+        ok |= (unsigned)in << it;
       } else {
         r[it] = *(const uint4_t*)(KC ? (P + (long)gr * ld + gk) : (P + (long)gk * ld + gr));
       }
@@ -56,7 +60,7 @@ struct Stage {
       const int c = it * NT + tid;
       int off;
       if (KC) off = kc_off(c >> 3, c & 7); else off = mc_off(c >> 4, c & 15);
-      *(uint4_t*)(lds + off) = r[it];
+      *(uint4_t*)(lds + off) = (ok >> it) & 1 ? r[it] : uint4_t{0u, 0u, 0u, 0u};
     }
   }
 };
