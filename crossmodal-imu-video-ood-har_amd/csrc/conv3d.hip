@@ -1829,61 +1829,20 @@ __global__ __launch_bounds__(512, 1) void conv3d_stem_wgrad(Geom g, int R, int c
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
-  // Tile t + 1 (its dz rows and input rows of plane it) is loaded into registers while tile t is multiplied,
-  // through buffer resources: out-of-range rows / positions / channels read from an offset with bit 31 set, past
-  // the resource, which returns zero (branch-free; no select on the loaded values, as conv3d_stem_fwd).
-  constexpr int NTW = 512, DPT = 256 * 8 / NTW, RPT = (UMAX * ((RB - 16) / 8) + NTW - 1) / NTW;
-  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)x, (short)0, (int)min((long)g.N * g.T * g.H * g.W * g.C * 2, 0x7fffffffL), 0x00020000);
-  const __amdgpu_buffer_rsrc_t dzr = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)dz, (short)0, (int)min((long)g.N * g.To * g.Ho * g.Wo * 64 * 2, 0x7fffffffL), 0x00020000);
-  uint4_t rdz[DPT];
-  unsigned short rx[RPT][4];
-  int lo[RPT];                    // LDS byte offset of this thread's staged positions (tile-invariant; -1: none)
-  auto load_tile = [&](int t) {
-    const int f = t / cpf, ho0 = (t - f * cpf) * R, nr = min(R, g.Ho - ho0);
-    const int to = f % g.To, n = f / g.To;
-    const int used = nr * g.Wo, U = (nr - 1) * g.sh + g.kh, nel = U * Lrow;
-    const int m0 = (f * g.Ho + ho0) * g.Wo;
-#pragma unroll
-    for (int k = 0; k < DPT; ++k) {
-      const int e = k * NTW + tid, j = e >> 3, ch = e & 7;
-      rdz[k] = __builtin_bit_cast(uint4_t, __builtin_amdgcn_raw_buffer_load_b128(
-          dzr, (unsigned)(((m0 + j) * 64 + ch * 8) * 2) | ((unsigned)(j >= used) << 31), 0, 0));
-    }
-    const int ti = to * g.st - g.pt + it;
-    const bool tok = ti >= 0 && ti < g.T;
-#pragma unroll
-    for (int k = 0; k < RPT; ++k) {
-      const int e = k * NTW + tid, u = e / Lrow, pp = e - u * Lrow, hi = ho0 * g.sh - g.ph + u, wi = pp - g.pw;
-      lo[k] = e < nel ? u * RB + pp * 8 : -1;
-      const bool pok = tok && e < nel && hi >= 0 && hi < g.H && wi >= 0 && wi < g.W;
-      const int go = (((n * g.T + ti) * g.H + hi) * g.W + wi) * g.C * 2;
-#pragma unroll
-      for (int c = 0; c < 4; ++c)
-        rx[k][c] = __builtin_amdgcn_raw_buffer_load_b16(xr, (unsigned)(go + 2 * c) | ((unsigned)!(pok && c < g.C) << 31),
-                                                        0, 0);
-    }
-  };
-  auto store_tile = [&]() {
-#pragma unroll
-    for (int k = 0; k < DPT; ++k) {
-      const int e = k * NTW + tid, j = e >> 3, ch = e & 7;
-      *(uint4_t*)(dzs + j * 144 + ch * 16) = rdz[k];
-    }
-#pragma unroll
-    for (int k = 0; k < RPT; ++k)
-      if (lo[k] >= 0)
-        *(short4_t*)(rows + lo[k]) = short4_t{(short)rx[k][0], (short)rx[k][1], (short)rx[k][2], (short)rx[k][3]};
-  };
-  if (t_beg < t_end) load_tile(t_beg);
   for (int t = t_beg; t < t_end; ++t) {
     const int f = t / cpf, ho0 = (t - f * cpf) * R, nr = min(R, g.Ho - ho0);
-    const int used = nr * g.Wo;
+    const int to = f % g.To, n = f / g.To;
+    const int used = nr * g.Wo, U = (nr - 1) * g.sh + g.kh;
+    const long m0 = ((long)f * g.Ho + ho0) * g.Wo;
     if (t > t_beg) __syncthreads();
-    store_tile();
+    for (int e = tid; e < 256 * 8; e += nt) {
+      const int j = e >> 3, ch = e & 7;
+      const bool okr = j < used;
+      const uint4_t v = *(const uint4_t*)(dz + (okr ? (m0 + j) * 64 : 0) + ch * 8);
+      *(uint4_t*)(dzs + j * 144 + ch * 16) = okr ? v : uint4_t{0u, 0u, 0u, 0u};
+    }
+    stem_rows(g, x, n, to * g.st - g.pt + it, ho0, U, Lrow, rows, tid, nt);
     __syncthreads();
-    if (t + 1 < t_end) load_tile(t + 1);
     if (active) {
       const int kmax = (used + 31) / 32;
       for (int kk = 0; kk < kmax; ++kk) {
