@@ -86,6 +86,45 @@ def test_r3d_production_plans():
     assert got == PLANS, {k: (got[k], PLANS[k]) for k in got if got[k] != PLANS[k]}
 
 
+def test_r3d_plans_past_buffer_range():
+    """The row-slab / nine-tap kernels address x and dz through buffer resources with 32-bit offsets (padding = an
+    out-of-range offset that reads zero), so their plans require x (and dz) within 1 GiB; past that, a geometry falls
+    back to the generic implicit GEMM (its 64-bit instantiation beyond 2 GiB).  Host-side plan queries, no GPU."""
+    from cmhar import _lib as L
+    from cmhar import r3d
+    lib = L.lib()
+    conv = _conv(64, 64, 3, 1, 1)
+    for n, fwd, wg in [(32, 1, 1), (160, 1, 1), (168, 4, 4)]:    # x = N·16·56²·64·2 B: 205 MB, 1.028 GB, 1.079 GB
+        shp = (n, 16, 56, 56, 64)
+        dims = r3d._dims(shp, conv, r3d._r8(conv.weight[0].numel()))
+        assert lib.cmhar_conv3d_fwd_plan(dims, 64) == fwd, n
+        assert lib.cmhar_conv3d_fwd_split_ws(dims, 64) == 0
+        assert lib.cmhar_conv3d_wgrad_plan(dims, 64) == wg, n
+
+
+@pytest.mark.gpu
+def test_conv3d_generic_forward_past_2gib():
+    """The generic implicit-GEMM forward keeps a 64-bit-address instantiation for inputs over 2 GiB (R3D-18's
+    layer2.0.conv1 geometry at N = 336: x = 2.16 GB): its output on the first clips equals, bit for bit, the
+    buffer-resource instantiation's on those clips alone (each clip's convolution is independent), and the last
+    clip's too."""
+    from cmhar import r3d
+    torch.manual_seed(11)
+    conv = _conv(64, 128, 3, 2, 1).to(DEV)
+    n_big = 336
+    x = torch.randn(n_big, 16, 56, 56, 64, device=DEV, dtype=torch.bfloat16)
+    assert x.numel() * 2 > (1 << 31)
+    wp = r3d._pack(conv, torch.bfloat16)
+    with torch.no_grad():
+        z_big = r3d._conv_fwd(x, tuple(x.shape), conv, wp, stats=False)[0]
+        for sl in (slice(0, 2), slice(n_big - 1, n_big)):
+            xs = x[sl].contiguous()
+            z_s = r3d._conv_fwd(xs, tuple(xs.shape), conv, wp, stats=False)[0]
+            per = z_s.shape[0] // xs.shape[0]
+            assert torch.equal(z_big[sl.start * per:sl.stop * per], z_s)
+    torch.cuda.synchronize()
+
+
 def _operands(kind, cin, cout, k, s, p, shape, seed):
     g = torch.Generator(device=DEV).manual_seed(seed)
     N, T_, H, W = shape
