@@ -2371,7 +2371,8 @@ extern "C" int cmhar_conv3d_stem_fwd(const int* dims, int Cout, const void* x, c
   return 0;
 }
 static int stem_splits(const Geom& g, const StemPlan& p, int& tps) {
-  int s = max(1, min((512 + g.kt - 1) / g.kt, p.ntile / 8));
+  // at most 512 workgroups (rounded up, R3D-18's kt = 3 stem gave 513)
+  int s = max(1, min(512 / g.kt, p.ntile / 8));
   tps = (p.ntile + s - 1) / s;
   return (p.ntile + tps - 1) / tps;
 }
@@ -2404,7 +2405,7 @@ extern "C" int cmhar_conv3d_stem_wgrad(const int* dims, int Cout, const void* x,
 static int wgrad_splits(const Geom& g, int Cout, int& mlen) {
   const int M = g.N * g.To * g.Ho * g.Wo;
   const int tiles = ((Cout + 127) / 128) * ((g.K + 127) / 128);
-  int s = (2048 + tiles - 1) / tiles;
+  int s = max(1, 2048 / tiles);   // whole rounds: rounding up can leave a last round of a few workgroups
   const int smax = (M + 511) / 512;
   if (s > smax) s = smax;
   if (s < 1) s = 1;
@@ -2445,8 +2446,9 @@ static bool rows_plan(const Geom& g, int Cout, RowsPlan& p) {
       p.cpf = cpf;
       p.nchunk = g.N * g.To * p.cpf;
       const int tiles = g.kt * (g.C / 64) * (Cout / 64);
-      // one 12-wave workgroup per CU: ~2 rounds, >= 4 chunks each, <= ~80 MB of split partials
-      int s = (512 + tiles - 1) / tiles;
+      // one 12-wave workgroup per CU: at most 2 full rounds (rounding the split count up gave R3D-18 layer 1 513
+      // workgroups: a third round of one), >= 4 chunks each, <= ~80 MB of split partials
+      int s = max(1, 512 / tiles);
       s = min(s, (int)((80L << 20) / ((long)Cout * g.K * 4)));
       s = max(1, min(s, p.nchunk / 4));
       p.cps = (p.nchunk + s - 1) / s;
@@ -2471,7 +2473,7 @@ static bool rows_plan(const Geom& g, int Cout, RowsPlan& p) {
   const int tiles = g.kt * (g.kh / p.grp) * (g.C / 64) * (Cout / p.cot);
   // ~2048 workgroups, >= 8 chunks each, and at most ~48 MB of fp32 partials (every split adds a Cout x K slab that
   // is written here and read back by the reduce: at 2048 workgroups that was ~200 MB per conv, 1.7 ms per step)
-  int s = (2048 + tiles - 1) / tiles;
+  int s = 2048 / tiles;             // whole rounds (rounded up, a last round of a few workgroups)
   s = min(s, (int)((48L << 20) / ((long)Cout * g.K * 4)));
   s = max(1, min(s, nchunk / 8));
   p.cps = (nchunk + s - 1) / s;
