@@ -2471,13 +2471,17 @@ static bool rows_plan(const Geom& g, int Cout, RowsPlan& p) {
   p.grp = 1;
   const int nchunk = (p.rows + p.R - 1) / p.R;
   const int tiles = g.kt * (g.kh / p.grp) * (g.C / 64) * (Cout / p.cot);
-  // ~2048 workgroups, >= 8 chunks each, and at most ~48 MB of fp32 partials (every split adds a Cout x K slab that
-  // is written here and read back by the reduce: at 2048 workgroups that was ~200 MB per conv, 1.7 ms per step)
-  int s = 2048 / tiles;             // whole rounds (rounded up, a last round of a few workgroups)
-  s = min(s, (int)((48L << 20) / ((long)Cout * g.K * 4)));
-  s = max(1, min(s, nchunk / 8));
-  p.cps = (nchunk + s - 1) / s;
-  p.splits = (nchunk + p.cps - 1) / p.cps;
+  // at most ~2048 workgroups, >= 8 chunks each, and at most ~56 MB of fp32 partials (every split adds a Cout x K
+  // slab that is written here and read back by the reduce: at 2048 workgroups that was ~200 MB per conv, 1.7 ms per
+  // step); within that, the split count with the least time ∝ rounds of the 512 workgroup slots x chunks per split
+  // (whole rounds: R3D-18 layer 3 takes 7 splits = 504 workgroups, not 6 = 432)
+  const int smax = max(1, min(min(2048 / tiles, (int)((56L << 20) / ((long)Cout * g.K * 4))), nchunk / 8));
+  long best = -1;
+  for (int c = 1; c <= smax; ++c) {
+    const int cps = (nchunk + c - 1) / c, sp = (nchunk + cps - 1) / cps;
+    const long t = (long)((tiles * sp + 511) / 512) * cps;
+    if (best < 0 || t < best) { best = t; p.cps = cps; p.splits = sp; }
+  }
   return true;
 }
 
