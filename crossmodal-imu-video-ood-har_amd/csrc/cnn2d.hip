@@ -121,33 +121,93 @@ __device__ __forceinline__ void load_dw_weights(const float* __restrict__ wt, in
   }
 }
 
-template <typename T, int K>
+// 8 elements of T through a buffer resource, issued (ld) apart from their use (get): the K² taps of an output are
+// all in flight together.  An offset with bit 31 set lies past the resource (whose range the launch keeps within
+// 2^31 bytes) and reads zero: the padding taps need no branch around their load — a branch per tap made every
+// tap's load wait for the previous one — and contribute fmaf(0, w, acc) = acc, the same sum as skipping them.
+template <typename T> struct Raw8;
+template <> struct Raw8<bf16> {
+  uint4_t r;
+  __device__ __forceinline__ void ld(__amdgpu_buffer_rsrc_t rs, unsigned off) {
+    r = __builtin_bit_cast(uint4_t, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
+  }
+  __device__ __forceinline__ void get(float* v) const {
+    const bf16x8 b = __builtin_bit_cast(bf16x8, r);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = (float)b[j];
+  }
+};
+template <> struct Raw8<float> {
+  uint4_t a, b;
+  __device__ __forceinline__ void ld(__amdgpu_buffer_rsrc_t rs, unsigned off) {
+    a = __builtin_bit_cast(uint4_t, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
+    b = __builtin_bit_cast(uint4_t, __builtin_amdgcn_raw_buffer_load_b128(rs, off + 16, 0, 0));
+  }
+  __device__ __forceinline__ void get(float* v) const {
+    const floatx4 x0 = __builtin_bit_cast(floatx4, a), x1 = __builtin_bit_cast(floatx4, b);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { v[j] = x0[j]; v[4 + j] = x1[j]; }
+  }
+};
+template <typename T>
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const T* p, long elems) {
+  return __builtin_amdgcn_make_buffer_rsrc((void*)p, (short)0, (int)min(elems * (long)sizeof(T), 0x7fffffffL),
+                                           0x00020000);
+}
+// byte offset of element e, or past the range when !ok
+template <typename T>
+__device__ __forceinline__ unsigned buf_off(int e, bool ok) {
+  return (unsigned)(e * (int)sizeof(T)) | ((unsigned)!ok << 31);
+}
+// the buffer form applies when every tensor the kernel reads stays below 2^31 bytes
+inline bool dw_buf_ok(long elems, int dtype_bytes) { return elems * dtype_bytes < (1L << 31); }
+
+template <typename T, int K, bool BUF>
 __global__ __launch_bounds__(256) void dwconv_cl_fwd(Pool g, const T* __restrict__ x, const float* __restrict__ wt,
                                                      T* __restrict__ z) {
   const int cv = g.C / 8;
   // 32-bit index decomposition (host-checked: N·Ho·Wo·C/8 < 2^31): 64-bit division is a long software sequence
   const unsigned total = (unsigned)g.N * g.Ho * g.Wo * cv;
+  const __amdgpu_buffer_rsrc_t xr = buf_rsrc(x, (long)g.N * g.H * g.W * g.C);
   for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
     const int c0 = (int)(i % (unsigned)cv) * 8;
     unsigned r = i / (unsigned)cv;
     const int wo = (int)(r % (unsigned)g.Wo); r /= (unsigned)g.Wo;
     const int ho = (int)(r % (unsigned)g.Ho);
     const int n = (int)(r / (unsigned)g.Ho);
-    float wv[8 * K * K];
-    load_dw_weights<K>(wt, c0, wv);
     float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    const T* xn = x + (size_t)n * g.H * g.W * g.C + c0;
+    if constexpr (BUF) {
+      Raw8<T> rv[K * K];
 #pragma unroll
-    for (int ih = 0; ih < K; ++ih) {
-      const int h = ho * g.s - g.p + ih;
+      for (int t = 0; t < K * K; ++t) {
+        const int h = ho * g.s - g.p + t / K, w = wo * g.s - g.p + t % K;
+        rv[t].ld(xr, buf_off<T>(((n * g.H + h) * g.W + w) * g.C + c0, h >= 0 && h < g.H && w >= 0 && w < g.W));
+      }
+      float wv[8 * K * K];
+      load_dw_weights<K>(wt, c0, wv);
 #pragma unroll
-      for (int iw = 0; iw < K; ++iw) {
-        const int w = wo * g.s - g.p + iw;
-        if (h >= 0 && h < g.H && w >= 0 && w < g.W) {
-          float v[8];
-          Vec8<T>::load(xn + ((size_t)h * g.W + w) * g.C, v);
+      for (int t = 0; t < K * K; ++t) {
+        float v[8];
+        rv[t].get(v);
 #pragma unroll
-          for (int j = 0; j < 8; ++j) acc[j] = fmaf(v[j], wv[j * K * K + ih * K + iw], acc[j]);
+        for (int j = 0; j < 8; ++j) acc[j] = fmaf(v[j], wv[j * K * K + t], acc[j]);
+      }
+    } else {
+      float wv[8 * K * K];
+      load_dw_weights<K>(wt, c0, wv);
+      const T* xn = x + (size_t)n * g.H * g.W * g.C + c0;
+#pragma unroll
+      for (int ih = 0; ih < K; ++ih) {
+        const int h = ho * g.s - g.p + ih;
+#pragma unroll
+        for (int iw = 0; iw < K; ++iw) {
+          const int w = wo * g.s - g.p + iw;
+          if (h >= 0 && h < g.H && w >= 0 && w < g.W) {
+            float v[8];
+            Vec8<T>::load(xn + ((size_t)h * g.W + w) * g.C, v);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) acc[j] = fmaf(v[j], wv[j * K * K + ih * K + iw], acc[j]);
+          }
         }
       }
     }
@@ -156,20 +216,41 @@ __global__ __launch_bounds__(256) void dwconv_cl_fwd(Pool g, const T* __restrict
 }
 
 // dx[n, h, w, c] = Σ_taps dz[n, ho, wo, c] · w[c, tap] over the outputs whose window holds (h, w) at that tap
-template <typename T, int K>
+template <typename T, int K, bool BUF>
 __global__ __launch_bounds__(256) void dwconv_cl_dgrad(Pool g, const T* __restrict__ dz, const float* __restrict__ wt,
                                                        T* __restrict__ dx) {
   const int cv = g.C / 8;
   const unsigned total = (unsigned)g.N * g.H * g.W * cv;     // < 2^31 (host-checked)
+  const __amdgpu_buffer_rsrc_t dzr = buf_rsrc(dz, (long)g.N * g.Ho * g.Wo * g.C);
   for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
     const int c0 = (int)(i % (unsigned)cv) * 8;
     unsigned r = i / (unsigned)cv;
     const int w = (int)(r % (unsigned)g.W); r /= (unsigned)g.W;
     const int h = (int)(r % (unsigned)g.H);
     const int n = (int)(r / (unsigned)g.H);
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if constexpr (BUF) {
+      Raw8<T> rv[K * K];
+#pragma unroll
+      for (int t = 0; t < K * K; ++t) {
+        const int hh = h + g.p - t / K, ww = w + g.p - t % K, ho = hh / g.s, wo = ww / g.s;
+        const bool ok = hh >= 0 && hh % g.s == 0 && ho < g.Ho && ww >= 0 && ww % g.s == 0 && wo < g.Wo;
+        rv[t].ld(dzr, buf_off<T>(((n * g.Ho + ho) * g.Wo + wo) * g.C + c0, ok));
+      }
+      float wv[8 * K * K];
+      load_dw_weights<K>(wt, c0, wv);
+#pragma unroll
+      for (int t = 0; t < K * K; ++t) {
+        float v[8];
+        rv[t].get(v);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[j] = fmaf(v[j], wv[j * K * K + t], acc[j]);
+      }
+      Vec8<T>::store(dx + (size_t)i * 8, acc);
+      continue;
+    }
     float wv[8 * K * K];
     load_dw_weights<K>(wt, c0, wv);
-    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     const T* dzn = dz + (size_t)n * g.Ho * g.Wo * g.C + c0;
 #pragma unroll
     for (int ih = 0; ih < K; ++ih) {
@@ -195,7 +276,7 @@ __global__ __launch_bounds__(256) void dwconv_cl_dgrad(Pool g, const T* __restri
 // accumulators in registers; two rows per iteration so the next row's 1 + K² loads are in flight under the current
 // row's FMAs; the block's row slots are combined in a fixed order through LDS one tap at a time.
 // part: [nchunk][K²][C].
-template <typename T, int K>
+template <typename T, int K, bool BUF>
 __global__ __launch_bounds__(256) void dwconv_cl_wgrad_partial(Pool g, int rows_per_chunk, const T* __restrict__ x,
                                                                const T* __restrict__ dz, float* __restrict__ part) {
   constexpr int KK = K * K;
@@ -206,6 +287,7 @@ __global__ __launch_bounds__(256) void dwconv_cl_wgrad_partial(Pool g, int rows_
   const long M = (long)g.N * g.Ho * g.Wo;
   const long r0 = (long)blockIdx.x * rows_per_chunk;
   const long r1 = min(r0 + rows_per_chunk, M);
+  const __amdgpu_buffer_rsrc_t xr = buf_rsrc(x, (long)g.N * g.H * g.W * g.C);
   float acc[KK][8];
 #pragma unroll
   for (int t = 0; t < KK; ++t)
@@ -218,6 +300,22 @@ __global__ __launch_bounds__(256) void dwconv_cl_wgrad_partial(Pool g, int rows_
     const int n = (int)(r / (unsigned)g.Ho);
     float gz[8];
     Vec8<T>::load(dz + (size_t)row * g.C + c0, gz);
+    if constexpr (BUF) {
+      Raw8<T> rv[KK];
+#pragma unroll
+      for (int t = 0; t < KK; ++t) {
+        const int h = ho * g.s - g.p + t / K, w = wo * g.s - g.p + t % K;
+        rv[t].ld(xr, buf_off<T>(((n * g.H + h) * g.W + w) * g.C + c0, h >= 0 && h < g.H && w >= 0 && w < g.W));
+      }
+#pragma unroll
+      for (int t = 0; t < KK; ++t) {
+        float v[8];
+        rv[t].get(v);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[t][j] = fmaf(gz[j], v[j], acc[t][j]);
+      }
+      return;
+    }
     const T* xn = x + (size_t)n * g.H * g.W * g.C + c0;
 #pragma unroll
     for (int t = 0; t < KK; ++t) {
@@ -459,7 +557,12 @@ extern "C" int cmhar_dwconv2d_cl_fwd(int dtype, int N, int H, int W, int C, int 
   const Pool g = make_pool(N, H, W, C, k, s, p);
   if (!pool_ok(g) || !w) return -1;
   const long work = (long)N * g.Ho * g.Wo * (C / 8);
-#define FK(T, KK) dwconv_cl_fwd<T, KK><<<grid_for(work), 256, 0, stream>>>(g, (const T*)x, w, (T*)z)
+  const bool buf = dw_buf_ok((long)N * H * W * C, dtype == CMHAR_F32 ? 4 : 2);
+#define FK(T, KK)                                                                                               \
+  do {                                                                                                          \
+    if (buf) dwconv_cl_fwd<T, KK, true><<<grid_for(work), 256, 0, stream>>>(g, (const T*)x, w, (T*)z);          \
+    else dwconv_cl_fwd<T, KK, false><<<grid_for(work), 256, 0, stream>>>(g, (const T*)x, w, (T*)z);             \
+  } while (0)
 #define F(T) do { if (k == 3) FK(T, 3); else if (k == 2) FK(T, 2); else FK(T, 1); } while (0)
   DT_SWITCH(dtype, F);
 #undef F
@@ -473,7 +576,12 @@ extern "C" int cmhar_dwconv2d_cl_dgrad(int dtype, int N, int H, int W, int C, in
   const Pool g = make_pool(N, H, W, C, k, s, p);
   if (!pool_ok(g) || !w) return -1;
   const long work = (long)N * H * W * (C / 8);
-#define FK(T, KK) dwconv_cl_dgrad<T, KK><<<grid_for(work), 256, 0, stream>>>(g, (const T*)dz, w, (T*)dx)
+  const bool buf = dw_buf_ok((long)N * g.Ho * g.Wo * C, dtype == CMHAR_F32 ? 4 : 2);
+#define FK(T, KK)                                                                                               \
+  do {                                                                                                          \
+    if (buf) dwconv_cl_dgrad<T, KK, true><<<grid_for(work), 256, 0, stream>>>(g, (const T*)dz, w, (T*)dx);      \
+    else dwconv_cl_dgrad<T, KK, false><<<grid_for(work), 256, 0, stream>>>(g, (const T*)dz, w, (T*)dx);         \
+  } while (0)
 #define F(T) do { if (k == 3) FK(T, 3); else if (k == 2) FK(T, 2); else FK(T, 1); } while (0)
   DT_SWITCH(dtype, F);
 #undef F
@@ -495,7 +603,12 @@ extern "C" int cmhar_dwconv2d_cl_wgrad(int dtype, int N, int H, int W, int C, in
   const long M = (long)N * g.Ho * g.Wo;
   const int nch = dw_chunks(M);
   const int rpc = (int)((M + nch - 1) / nch);
-#define FK(T, KK) dwconv_cl_wgrad_partial<T, KK><<<nch, 256, 0, stream>>>(g, rpc, (const T*)x, (const T*)dz, ws)
+  const bool buf = dw_buf_ok((long)N * H * W * C, dtype == CMHAR_F32 ? 4 : 2);
+#define FK(T, KK)                                                                                               \
+  do {                                                                                                          \
+    if (buf) dwconv_cl_wgrad_partial<T, KK, true><<<nch, 256, 0, stream>>>(g, rpc, (const T*)x, (const T*)dz, ws); \
+    else dwconv_cl_wgrad_partial<T, KK, false><<<nch, 256, 0, stream>>>(g, rpc, (const T*)x, (const T*)dz, ws);    \
+  } while (0)
 #define F(T) do { if (k == 3) FK(T, 3); else if (k == 2) FK(T, 2); else FK(T, 1); } while (0)
   DT_SWITCH(dtype, F);
 #undef F
