@@ -177,6 +177,63 @@ __global__ __launch_bounds__(256) void col2im3d_kernel(Geom g, const T* __restri
   }
 }
 
+// The same gather for bf16 with 8 channels per thread, its loads issued together: per dimension the taps that can
+// reach an input position are i0, i0 + s, … (i0 = (x + p) mod s, at most MT = ⌈k / s⌉ of them), so a fixed MT³
+// nest enumerates the candidates in the tap order of col2im3d_kernel; each candidate's load goes through a buffer
+// resource, an invalid one at an offset past the range (bit 31) that reads zero (+0 leaves the sum's bits unchanged),
+// and all MT³ loads are in flight before the first add — the branches of col2im3d_kernel made each wait for the one
+// before.  dcol stays within 2^31 bytes (host-checked).
+template <int MT>
+__global__ __launch_bounds__(256) void col2im3d_gather(Geom g, const bf16* __restrict__ dcol, bf16* __restrict__ dx,
+                                                       int accumulate) {
+  const int cv = g.C / 8;
+  const unsigned total = (unsigned)g.N * g.T * g.H * g.W * cv;
+  const __amdgpu_buffer_rsrc_t dr = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)dcol, (short)0, (int)min((long)g.N * g.To * g.Ho * g.Wo * g.Kp * 2, 0x7fffffffL), 0x00020000);
+  for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    const unsigned pos = i / cv;
+    const int c = (int)(i - pos * cv) * 8;
+    unsigned r = pos;
+    const int w = r % g.W; r /= g.W;
+    const int h = r % g.H; r /= g.H;
+    const int t = r % g.T;
+    const int n = r / g.T;
+    const int it0 = (t + g.pt) % g.st, ih0 = (h + g.ph) % g.sh, iw0 = (w + g.pw) % g.sw;
+    uint4_t v[MT * MT * MT];
+#pragma unroll
+    for (int a = 0; a < MT; ++a)
+#pragma unroll
+      for (int b = 0; b < MT; ++b)
+#pragma unroll
+        for (int d = 0; d < MT; ++d) {
+          const int it = it0 + a * g.st, ih = ih0 + b * g.sh, iw = iw0 + d * g.sw;
+          const int to = (t + g.pt - it) / g.st, ho = (h + g.ph - ih) / g.sh, wo = (w + g.pw - iw) / g.sw;
+          const bool ok = it < g.kt && ih < g.kh && iw < g.kw && t + g.pt - it >= 0 && h + g.ph - ih >= 0 &&
+                          w + g.pw - iw >= 0 && to < g.To && ho < g.Ho && wo < g.Wo;
+          const int e = (((n * g.To + to) * g.Ho + ho) * g.Wo + wo) * g.Kp + ((it * g.kh + ih) * g.kw + iw) * g.C + c;
+          v[(a * MT + b) * MT + d] = __builtin_bit_cast(uint4_t, __builtin_amdgcn_raw_buffer_load_b128(
+              dr, (unsigned)(e * 2) | ((unsigned)!ok << 31), 0, 0));
+        }
+    float acc[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] = 0.f;
+#pragma unroll
+    for (int q = 0; q < MT * MT * MT; ++q) {
+      const bf16x8 b8 = __builtin_bit_cast(bf16x8, v[q]);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] += (float)b8[j];
+    }
+    bf16* dst = dx + (long)pos * g.C + c;
+    if (accumulate) {
+      float o[8];
+      Vec8<bf16>::load(dst, o);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] += o[j];
+    }
+    Vec8<bf16>::store(dst, acc);
+  }
+}
+
 // ---- BatchNorm over the [M, C] channels-last view ----------------------------------------------------------------
 // Column partial sums over a chunk of rows: each thread reads 8 consecutive channels of a row (one 16-B bf16
 // vector), TPR = C/8 threads cover a row and the block's RPI = 256/TPR row slots are combined in a fixed order.
@@ -1979,7 +2036,13 @@ extern "C" int cmhar_conv3d_col2im(int dtype, const int* dims, const void* dcol,
   const bool vec = g.C % 8 == 0;
   const long work = (long)g.N * g.T * g.H * g.W * (vec ? g.C / 8 : g.C);
   const int grid = grid_for(work);
-  if (dtype == CMHAR_BF16) {
+  const int mt = max(max(cdiv(g.kt, g.st), cdiv(g.kh, g.sh)), cdiv(g.kw, g.sw));
+  const bool gather = dtype == CMHAR_BF16 && vec && mt <= 3 && (long)g.N * g.To * g.Ho * g.Wo * g.Kp * 2 < (1L << 31);
+  if (gather) {
+    if (mt == 1) col2im3d_gather<1><<<grid, 256, 0, stream>>>(g, (const bf16*)dcol, (bf16*)dx, accumulate);
+    else if (mt == 2) col2im3d_gather<2><<<grid, 256, 0, stream>>>(g, (const bf16*)dcol, (bf16*)dx, accumulate);
+    else col2im3d_gather<3><<<grid, 256, 0, stream>>>(g, (const bf16*)dcol, (bf16*)dx, accumulate);
+  } else if (dtype == CMHAR_BF16) {
     if (vec) col2im3d_kernel<bf16, 8><<<grid, 256, 0, stream>>>(g, (const bf16*)dcol, (bf16*)dx, accumulate);
     else col2im3d_kernel<bf16, 1><<<grid, 256, 0, stream>>>(g, (const bf16*)dcol, (bf16*)dx, accumulate);
   } else if (dtype == CMHAR_F32) {
