@@ -1729,22 +1729,6 @@ constexpr int FWD_LDS = (ROWS_B + W_B) > 256 * ELD * 4 + 2048 ? (ROWS_B + W_B) :
 __device__ __forceinline__ bool ok(const Geom& g) { return g.C <= 4 && g.kw <= 8 && g.sw == 2 && g.kh <= KHMAX; }
 }  // namespace stm
 
-// Stage the tile's input rows for tap plane it: row u = input row ho0·sh − ph + u, positions p = 0..Lrow−1 ↔ input
-// column p − pw, 4 channels (zero past C and outside the image).  One position (8 B) per thread per step.
-__device__ __forceinline__ void stem_rows(const Geom& g, const bf16* __restrict__ x, int n, int ti, int ho0, int U,
-                                          int Lrow, char* lds, int tid, int nt) {
-  const bool tok = ti >= 0 && ti < g.T;
-  for (int e = tid; e < U * Lrow; e += nt) {
-    const int u = e / Lrow, pp = e - u * Lrow, hi = ho0 * g.sh - g.ph + u, wi = pp - g.pw;
-    short v[4] = {0, 0, 0, 0};
-    if (tok && hi >= 0 && hi < g.H && wi >= 0 && wi < g.W) {
-      const short* src = (const short*)(x + ((((long)n * g.T + ti) * g.H + hi) * g.W + wi) * g.C);
-      for (int c = 0; c < g.C; ++c) v[c] = src[c];
-    }
-    *(short4_t*)(lds + u * stm::RB + pp * 8) = short4_t{v[0], v[1], v[2], v[3]};
-  }
-}
-
 __global__ __launch_bounds__(256, 2) void conv3d_stem_fwd(Geom g, int R, int cpf, const bf16* __restrict__ x,
                                                           const bf16* __restrict__ W4, bf16* __restrict__ z,
                                                           float* __restrict__ tstats) {
@@ -1886,19 +1870,52 @@ __global__ __launch_bounds__(512, 1) void conv3d_stem_wgrad(Geom g, int R, int c
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+  // The tile's loads (dz rows, input rows of plane it) are all issued before its LDS stores, through buffer resources
+  // with out-of-range offsets (bit 31) for the padding, which read zero: the select after each dz load and the branch
+  // around each input load made every load wait for the one before.  (A register pipeline one tile ahead measured
+  // 355 -> 459 us per launch in the step trace; this keeps the synchronous staging.)
+  constexpr int NTW = 64 * KHMAX, DPT = 256 * 8 / NTW, RPT = (UMAX * ((RB - 16) / 8) + NTW - 1) / NTW;
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)x, (short)0, (int)min((long)g.N * g.T * g.H * g.W * g.C * 2, 0x7fffffffL), 0x00020000);
+  const __amdgpu_buffer_rsrc_t dzr = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)dz, (short)0, (int)min((long)g.N * g.To * g.Ho * g.Wo * 64 * 2, 0x7fffffffL), 0x00020000);
   for (int t = t_beg; t < t_end; ++t) {
     const int f = t / cpf, ho0 = (t - f * cpf) * R, nr = min(R, g.Ho - ho0);
     const int to = f % g.To, n = f / g.To;
-    const int used = nr * g.Wo, U = (nr - 1) * g.sh + g.kh;
-    const long m0 = ((long)f * g.Ho + ho0) * g.Wo;
-    if (t > t_beg) __syncthreads();
-    for (int e = tid; e < 256 * 8; e += nt) {
-      const int j = e >> 3, ch = e & 7;
-      const bool okr = j < used;
-      const uint4_t v = *(const uint4_t*)(dz + (okr ? (m0 + j) * 64 : 0) + ch * 8);
-      *(uint4_t*)(dzs + j * 144 + ch * 16) = okr ? v : uint4_t{0u, 0u, 0u, 0u};
+    const int used = nr * g.Wo, U = (nr - 1) * g.sh + g.kh, nel = U * Lrow;
+    const int m0 = (f * g.Ho + ho0) * g.Wo;
+    uint4_t rdz[DPT];
+#pragma unroll
+    for (int k = 0; k < DPT; ++k) {
+      const int e = k * NTW + tid, j = e >> 3, ch = e & 7;
+      rdz[k] = __builtin_bit_cast(uint4_t, __builtin_amdgcn_raw_buffer_load_b128(
+          dzr, (unsigned)(((m0 + j) * 64 + ch * 8) * 2) | ((unsigned)(j >= used) << 31), 0, 0));
     }
-    stem_rows(g, x, n, to * g.st - g.pt + it, ho0, U, Lrow, rows, tid, nt);
+    const int ti = to * g.st - g.pt + it;
+    const bool tok = ti >= 0 && ti < g.T;
+    unsigned short rx[RPT][4];
+#pragma unroll
+    for (int k = 0; k < RPT; ++k) {
+      const int e = k * NTW + tid, u = e / Lrow, pp = e - u * Lrow, hi = ho0 * g.sh - g.ph + u, wi = pp - g.pw;
+      const bool pok = tok && e < nel && hi >= 0 && hi < g.H && wi >= 0 && wi < g.W;
+      const int go = (((n * g.T + ti) * g.H + hi) * g.W + wi) * g.C * 2;
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+        rx[k][c] = __builtin_amdgcn_raw_buffer_load_b16(xr, (unsigned)(go + 2 * c) | ((unsigned)!(pok && c < g.C) << 31),
+                                                        0, 0);
+    }
+    if (t > t_beg) __syncthreads();
+#pragma unroll
+    for (int k = 0; k < DPT; ++k) {
+      const int e = k * NTW + tid, j = e >> 3, ch = e & 7;
+      *(uint4_t*)(dzs + j * 144 + ch * 16) = rdz[k];
+    }
+#pragma unroll
+    for (int k = 0; k < RPT; ++k) {
+      const int e = k * NTW + tid, u = e / Lrow, pp = e - u * Lrow;
+      if (e < nel)
+        *(short4_t*)(rows + u * RB + pp * 8) = short4_t{(short)rx[k][0], (short)rx[k][1], (short)rx[k][2], (short)rx[k][3]};
+    }
     __syncthreads();
     if (active) {
       const int kmax = (used + 31) / 32;

@@ -41,6 +41,26 @@ def main():
     dev = torch.device('cuda')
     st = L.stream(dev)
     keep = set(a.layers.split(',')) if a.layers else None
+    if keep is None or 'stem' in keep:
+        # the implicit stem: 3 -> 64, 3x7x7, stride (1, 2, 2), pad (1, 3, 3) on the 16x112^2 clips
+        from cmhar import r3d
+        N = a.batch
+        conv = torch.nn.Conv3d(3, 64, (3, 7, 7), (1, 2, 2), (1, 3, 3), bias=False).to(dev)
+        x = torch.randn(N, 16, 112, 112, 3, device=dev).bfloat16()
+        shp = tuple(x.shape)
+        dims = r3d._dims(shp, conv, r3d._stem_kp(conv))
+        w4 = r3d._pack_stem(conv)
+        M = N * 16 * 56 * 56
+        z = torch.empty(M, 64, device=dev, dtype=torch.bfloat16)
+        dz = torch.randn(M, 64, device=dev).bfloat16()
+        dw4 = torch.empty(64, r3d._stem_kp(conv), device=dev)
+        ws = K.workspace(L.lib().cmhar_conv3d_stem_wgrad_ws(dims, 64), dev)
+        fl = 2 * M * 64 * 3 * 7 * 7 * 3
+        tf = timed(lambda: L.call('cmhar_conv3d_stem_fwd', dims, 64, K.ptr(x), K.ptr(w4), K.ptr(z), None, st), a.reps)
+        tw = timed(lambda: L.call('cmhar_conv3d_stem_wgrad', dims, 64, K.ptr(x), K.ptr(dz), K.ptr(dw4), K.ptr(ws), st),
+                   a.reps)
+        print(f'{"stem":15s} M={M:8d} K={441:6d} Cout={64:4d}  fwd {tf * 1e3:7.1f} us {fl / tf / 1e9:6.0f} TF   '
+              f'wgrad {tw * 1e3:7.1f} us {fl / tw / 1e9:6.0f} TF', flush=True)
     for name, T, H, C, Co, s in LAYERS:
         if keep is not None and name not in keep:
             continue
