@@ -87,6 +87,61 @@ def test_depthwise_conv_fwd_dgrad_wgrad_fp32(C, s, HW):
     assert rel(dw, w.grad) < 1e-5
 
 
+@pytest.mark.parametrize('C,s,HW', [(32, 1, (17, 19)), (144, 2, (28, 28)), (96, 2, (15, 9))])
+def test_depthwise_conv_bf16_matches_fp32(C, s, HW):
+    """bf16 depthwise conv (the MobileNetV2 path: all K² tap loads through a buffer resource, the padding taps at an
+    out-of-range offset that reads zero) vs the fp32 conv on the same bf16-rounded operands: forward and input
+    gradient within bf16 output rounding (5e-3 rel), weight gradient (fp32 accumulation) within 1e-4."""
+    from cmhar import _lib as L
+    from cmhar import kernels as K
+    torch.manual_seed(3)
+    N = 3
+    H, W = HW
+    x = torch.randn(N, C, H, W).bfloat16().float().requires_grad_(True)
+    w = (torch.randn(C, 1, 3, 3) * 0.3).requires_grad_(True)
+    ref = F.conv2d(x, w, stride=s, padding=1, groups=C)
+    dz = torch.randn_like(ref).bfloat16().float()
+    ref.backward(dz)
+    Ho, Wo = ref.shape[2:]
+    xc = x.detach().permute(0, 2, 3, 1).contiguous().to(DEV).bfloat16()
+    wc = w.detach().to(DEV)
+    st = L.stream(xc.device)
+    z = torch.empty(N * Ho * Wo, C, device=DEV, dtype=torch.bfloat16)
+    L.call('cmhar_dwconv2d_cl_fwd', L.BF16, N, H, W, C, 3, s, 1, xc.data_ptr(), wc.data_ptr(), z.data_ptr(), st)
+    assert rel(z.float().cpu().view(N, Ho, Wo, C).permute(0, 3, 1, 2), ref) < 5e-3
+    dzc = dz.permute(0, 2, 3, 1).contiguous().to(DEV).bfloat16()
+    dx = torch.empty_like(xc)
+    L.call('cmhar_dwconv2d_cl_dgrad', L.BF16, N, H, W, C, 3, s, 1, dzc.data_ptr(), wc.data_ptr(), dx.data_ptr(), st)
+    assert rel(dx.float().cpu().permute(0, 3, 1, 2), x.grad) < 5e-3
+    dw = torch.empty(C, 1, 3, 3, device=DEV)
+    ws = K.workspace(L.lib().cmhar_dwconv2d_cl_wgrad_ws(N, H, W, C, 3, s, 1), xc.device)
+    L.call('cmhar_dwconv2d_cl_wgrad', L.BF16, N, H, W, C, 3, s, 1, xc.data_ptr(), dzc.data_ptr(), dw.data_ptr(),
+           ws.data_ptr(), st)
+    assert rel(dw, w.grad) < 1e-4
+
+
+def test_depthwise_conv_past_2gib_matches_buffer_form():
+    """Past 2^31 bytes of input the depthwise forward keeps its 64-bit-address form; on the first and last frames it
+    equals, bit for bit, the buffer-resource form run on those frames alone (each frame is independent)."""
+    from cmhar import _lib as L
+    torch.manual_seed(5)
+    N, H, W, C = 900, 112, 112, 96                      # 2.17 GB of bf16 input
+    x = torch.randn(N, H, W, C, device=DEV, dtype=torch.bfloat16)
+    assert x.numel() * 2 > (1 << 31)
+    wc = torch.randn(C, 1, 3, 3, device=DEV) * 0.3
+    st = L.stream(x.device)
+    z = torch.empty(N * H * W, C, device=DEV, dtype=torch.bfloat16)
+    L.call('cmhar_dwconv2d_cl_fwd', L.BF16, N, H, W, C, 3, 1, 1, x.data_ptr(), wc.data_ptr(), z.data_ptr(), st)
+    per = H * W
+    for f0, f1 in ((0, 2), (N - 1, N)):
+        xs = x[f0:f1].contiguous()
+        zs = torch.empty((f1 - f0) * per, C, device=DEV, dtype=torch.bfloat16)
+        L.call('cmhar_dwconv2d_cl_fwd', L.BF16, f1 - f0, H, W, C, 3, 1, 1, xs.data_ptr(), wc.data_ptr(), zs.data_ptr(),
+               st)
+        assert torch.equal(z[f0 * per:f1 * per], zs)
+    torch.cuda.synchronize()
+
+
 @pytest.mark.parametrize('C,act,res', [(96, 2, True), (144, 2, False), (1280, 2, False), (24, 0, True), (320, 1, False)])
 def test_bn_channels_last_any_width_relu6(C, act, res):
     from cmhar import _lib as L
