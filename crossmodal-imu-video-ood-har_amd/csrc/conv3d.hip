@@ -2503,12 +2503,13 @@ static bool rows_plan(const Geom& g, int Cout, RowsPlan& p) {
     return !(v && v[0] == '0');
   }();
   if (!on || g.kw != 3 || g.Wo > wr::SLOTS || Cout % 64 || g.C % 64) return false;
-  // CMHAR_WGRAD_ROWS3=0: one-tap-row kernel for every shape; 1 (default): nine-tap kernel for Cout = 64 only; 2: also
-  // on 64-wide Cout slices of wider convs — measured slower there (R3D-18 layer 2 295.1 -> 311.0 us, layer 3 154.4 ->
-  // 170.5, tools/debug/conv_bench.py; the one-tap-row kernel's 128-wide Cout tiles reuse each staged slab twice)
+  // CMHAR_WGRAD_ROWS3=0: one-tap-row kernel for every shape; 1: nine-tap kernel for Cout = 64 only; 2 (default): also
+  // on 64-wide Cout slices of wider convs.  Measured slower there before the buffer-resource loads (R3D-18 layer 2
+  // 295.1 -> 311.0 us); with them faster (layer 2 278.7 -> 232.6 us, layer 3 143.3 -> 127.6, step 2198 -> 2221 clips/s,
+  // tools/gpu_r05_envab.sh): the nine-tap kernel's longer K per staged chunk beats the 128-wide tiles' slab reuse
   static const int nine = [] {
     const char* v = getenv("CMHAR_WGRAD_ROWS3");
-    return v && (v[0] == '0' || v[0] == '2') ? v[0] - '0' : 1;
+    return v && (v[0] == '0' || v[0] == '1') ? v[0] - '0' : 2;
   }();
   if (nine && (nine == 2 || Cout == 64) && g.kh == 3 && g.sh == 1 && g.sw == 1) {
     // chunks of R output rows of one frame, balanced over the frame (as the nine-tap forward's tiles)

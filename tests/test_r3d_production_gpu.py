@@ -46,10 +46,10 @@ PLANS = {
     'layer1.conv': (1, 'flip:1', '1+r'),
     'layer2.0.conv1': (5, 'col2im', '2+r'),          # stride 2: the row slab does not fit, generic 128x128 gather
     'layer2.0.downsample': (5, 'col2im', '4+r'),
-    'layer2.conv2': (1, 'flip:1', '2+r'),            # nine-tap forward slab, 7-row tiles x 64-wide Cout slices
+    'layer2.conv2': (1, 'flip:1', '1+r'),            # nine-tap slab fwd / wgrad, 7-row tiles x 64-wide Cout slices
     'layer3.0.conv1': (5, 'col2im', '2+r'),
     'layer3.0.downsample': (5, 'col2im', '4+r'),
-    'layer3.conv2': (1, 'flip:1', '2+r'),            # nine-tap forward slab, one 14-row tile per frame
+    'layer3.conv2': (1, 'flip:1', '1+r'),            # nine-tap slab fwd / wgrad, one 14-row tile per frame
     'layer4.0.conv1': (5, 'col2im', '2+r'),
     'layer4.0.downsample': (5, 'col2im', '4+r'),
     'layer4.conv2': ('split', 'flip:split', '2'),    # one split of the weight gradient: no reduce
