@@ -16,6 +16,17 @@ namespace {
 // are written to LDS, not when they are loaded: a select on a prefetched load's result right after the load makes
 // the compiler wait for that load there (s_waitcnt vmcnt(0) in the load phase, before the compute it was meant to
 // overlap).  CMHAR_LATE_ZERO=0 (build flag): the select at the load (A/B builds).
+// s_setprio(1) over a conv kernel's MFMA phase, so a CU's co-resident workgroup in its LDS-store phase does not
+// take issue slots from it (nine-tap forward: R3D-18 layer 2 203.0 -> 196.9 us, layer 3 95.8 -> 92.2, A/B builds)
+#ifndef CMHAR_ROWS3_PRIO
+#define CMHAR_ROWS3_PRIO 1   // conv3d_fwd_rows3
+#endif
+#ifndef CMHAR_ROWS_PRIO
+#define CMHAR_ROWS_PRIO 0    // conv3d_fwd_rows
+#endif
+#ifndef CMHAR_IGEMM_PRIO
+#define CMHAR_IGEMM_PRIO 0   // conv3d_fwd_igemm
+#endif
 #ifndef CMHAR_LATE_ZERO
 #define CMHAR_LATE_ZERO 1
 #endif
@@ -782,7 +793,8 @@ template <int JN> struct FwdLds {
 template <int JN, bool BUF>
 __global__ __launch_bounds__(256, JN == 2 ? 3 : 2) void conv3d_fwd_igemm(Geom g, int M, int Cout, const bf16* __restrict__ x,
                                                            const bf16* __restrict__ Wt, const bf16* __restrict__ res,
-                                                           bf16* __restrict__ z, float* __restrict__ tstats) {
+                                                           bf16* __restrict__ z, float* __restrict__ tstats, int kps,
+                                                           float* __restrict__ part) {
   using namespace ig;
   using Lds = FwdLds<JN>;
   __shared__ __attribute__((aligned(16))) char smem[Lds::BYTES];
@@ -850,17 +862,24 @@ __global__ __launch_bounds__(256, JN == 2 ? 3 : 2) void conv3d_fwd_igemm(Geom g,
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 0; j < JN; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
-  const int nk = g.K / BK;
-  load(0);
+  // K-steps [kb, ke): all of them, or split blockIdx.y's share (part: its fp32 partial tile, no statistics)
+  const int nk = g.K / BK, kb = blockIdx.y * kps, ke = min(nk, kb + kps);
+  load(kb * BK);
   store(0);
   __syncthreads();
-  for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
-    const bool more = kt + 1 < nk;
+  for (int kt = kb; kt < ke; ++kt) {
+    const int cur = (kt - kb) & 1;
+    const bool more = kt + 1 < ke;
     if (more) load((kt + 1) * BK);
+    if (CMHAR_IGEMM_PRIO) __builtin_amdgcn_s_setprio(1);
     mma_tile<true, true, JN>(smem + 16384 * cur, smem + Lds::B0 + Lds::BSTAGE * cur, wr, wc, lane, acc);
+    if (CMHAR_IGEMM_PRIO) __builtin_amdgcn_s_setprio(0);
     if (more) store(cur ^ 1);
     __syncthreads();
+  }
+  if (part) {
+    store_tile<float, JN>(smem, acc, wr, wc, lane, tid, bm, bn, M, Cout, part + (long)blockIdx.y * M * Cout, Cout);
+    return;
   }
   store_tile<bf16, JN>(smem, acc, wr, wc, lane, tid, bm, bn, M, Cout, z, Cout, res);
   if (tstats) {
@@ -1410,6 +1429,7 @@ __global__ __launch_bounds__(256, 2) void conv3d_fwd_rows(Geom g, int M, int Cou
   for (int ks = ks0; ks < nks; ++ks) {
     const bool more = ks + 1 < nks;
     if (more) load(ks + 1);
+    if (CMHAR_ROWS_PRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int iw = 0; iw < 3; ++iw)
 #pragma unroll
@@ -1425,6 +1445,7 @@ __global__ __launch_bounds__(256, 2) void conv3d_fwd_rows(Geom g, int M, int Cou
 #pragma unroll
           for (int j = 0; j < JB; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
       }
+    if (CMHAR_ROWS_PRIO) __builtin_amdgcn_s_setprio(0);
     __syncthreads();
     if (more) store();
     __syncthreads();
@@ -1663,7 +1684,9 @@ __global__ __launch_bounds__(256, 2) void conv3d_fwd_rows3(Geom g, int Cout, int
       if ((st + 1) % 3 == 0) load_slab((st + 1) / 3);
       load_w(st + 1);
     }
+    if (CMHAR_ROWS3_PRIO) __builtin_amdgcn_s_setprio(1);
     compute(st % 3);
+    if (CMHAR_ROWS3_PRIO) __builtin_amdgcn_s_setprio(0);
     __syncthreads();
     if (more) {
       if ((st + 1) % 3 == 0) store_slab();
@@ -2288,12 +2311,36 @@ extern "C" long cmhar_conv3d_fwd_stats_floats(const int* dims, int Cout) {
 // per tile, fp32 partials in the caller's workspace, conv_split_reduce sums them in order (+ residual) and rounds
 // once.  No BatchNorm tile statistics (the caller takes the statistics passes over z: small at these sizes).
 // 0 = not this plan.  CMHAR_FWD_SPLIT=0 turns it off (A/B runs).
-static int fwd_split_count(const Geom& g, int Cout) {
+// The generic implicit GEMM (strided convs: R3D-18 layer 4's stride-2 3x3 conv, 3136 x 512 = 100 128x128 tiles, and
+// its 1x1 downsample) splits the same way over its BK-wide K-steps: split y takes kps of them (ig_split_kps).
+static int fwd_plan(const Geom& g, int Cout);
+static bool fwd_split_on() {
   static const bool on = [] {
     const char* v = getenv("CMHAR_FWD_SPLIT");
     return !(v && v[0] == '0');
   }();
-  if (!on || !igemm_ok(g, Cout)) return 0;
+  return on;
+}
+static int ig_split_count(const Geom& g, int Cout, int& kps) {
+  kps = 0;
+  if (!fwd_split_on() || !igemm_ok(g, Cout)) return 0;
+  const int plan = fwd_plan(g, Cout);
+  if ((plan != 4 && plan != 5) || (long)g.N * g.T * g.H * g.W * g.C * 2 > 0x7fffffffL ||
+      (long)Cout * g.Kp * 2 > 0x7fffffffL)   // the buffer-resource instantiation only
+    return 0;
+  const int M = g.N * g.To * g.Ho * g.Wo;
+  const long tiles = (long)((M + 127) / 128) * (plan == 4 ? 1 : (Cout + 127) / 128);
+  if (tiles >= 256) return 0;
+  const int nk = g.K / ig::BK;
+  const int s0 = (int)std::min<long>(4, (512 + tiles - 1) / tiles);
+  if (s0 < 2 || nk < 2 * s0) return 0;
+  kps = (nk + s0 - 1) / s0;
+  return (nk + kps - 1) / kps;   // every split non-empty
+}
+static int fwd_split_count(const Geom& g, int Cout) {
+  if (!fwd_split_on() || !igemm_ok(g, Cout)) return 0;
+  int kps;
+  if (const int s = ig_split_count(g, Cout, kps)) return s;
   Fwd3Plan p3;
   if (fwd3_plan(g, Cout, p3)) return 0;
   const int M = g.N * g.To * g.Ho * g.Wo;
@@ -2319,6 +2366,18 @@ extern "C" int cmhar_conv3d_fwd_split(const int* dims, int Cout, const void* x, 
   const int s = fwd_split_count(g, Cout);
   if (!s || !ws) return -1;
   const int M = g.N * g.To * g.Ho * g.Wo;
+  int kps;
+  if (ig_split_count(g, Cout, kps)) {
+    if (fwd_plan(g, Cout) == 4)
+      conv3d_fwd_igemm<2, true><<<dim3((M + 127) / 128, s), 256, 0, stream>>>(
+          g, M, Cout, (const bf16*)x, (const bf16*)w, nullptr, nullptr, nullptr, kps, ws);
+    else
+      conv3d_fwd_igemm<4, true><<<dim3(((M + 127) / 128) * ((Cout + 127) / 128), s), 256, 0, stream>>>(
+          g, M, Cout, (const bf16*)x, (const bf16*)w, nullptr, nullptr, nullptr, kps, ws);
+    conv_split_reduce<<<grid_for((long)M * Cout / 8), 256, 0, stream>>>(M, Cout, s, ws, (const bf16*)res, (bf16*)z);
+    CMHAR_CHECK_LAUNCH();
+    return 0;
+  }
   const int Ls = (g.Wo - 1) * g.sw + g.kw;
   const int t128 = ((M + 127) / 128) * (Cout / fr::TN);
   conv3d_fwd_rows<128><<<dim3(t128, s), 256, 0, stream>>>(g, M, Cout, Ls, (const bf16*)x, (const bf16*)w, nullptr,
@@ -2394,7 +2453,7 @@ extern "C" int cmhar_conv3d_fwd(const int* dims, int Cout, const void* x, const 
       const bool buf = (long)g.N * g.T * g.H * g.W * g.C * 2 <= 0x7fffffffL && (long)Cout * g.Kp * 2 <= 0x7fffffffL;
 #define IG(JN, BUF, GRID)                                                                                        \
   conv3d_fwd_igemm<JN, BUF><<<GRID, 256, 0, stream>>>(g, M, Cout, (const bf16*)x, (const bf16*)w, (const bf16*)res, \
-                                                      (bf16*)z, tile_stats)
+                                                      (bf16*)z, tile_stats, g.K / ig::BK, nullptr)
       if (plan == 4) {
         if (buf) IG(2, true, (M + 127) / 128);
         else IG(2, false, (M + 127) / 128);

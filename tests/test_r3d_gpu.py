@@ -503,38 +503,38 @@ def test_bn_bwd_nores_rounding_boundaries(relu):
 
 
 @pytest.mark.parametrize('res', [False, True])
-@pytest.mark.parametrize('geom', ['r3d_layer4', 'resnet18_layer4_kt1'])
+@pytest.mark.parametrize('geom', ['r3d_layer4', 'resnet18_layer4_kt1', 'r3d_layer4_stride2'])
 def test_conv3d_fwd_split_layer4(res, geom):
     """The split-K implicit-GEMM forward at R3D-18 layer 4's geometry (batch 32: 32×2×7×7 = 3136 output rows, 512 → 512,
-    3×3×3 'same') and at a 2-D (kt = 1) ResNet-18 layer-4 conv run through the conv3d machinery (32 frames of 7×7,
-    (1,3,3) taps — ADVICE r04): planned (`cmhar_conv3d_fwd_split_ws` > 0), against the fp32 conv of the same bf16
-    operands (+ the residual, as the dgrad call adds dx_acc) within the bf16 output rounding, and within one bf16 ulp (of
-    the value or of the output's rms near zero) of the unsplit kernel (`cmhar_conv3d_fwd`, the same products summed in a
-    different order).  A stride-2 conv never takes the split plan (its slab does not fit the 128-row tile: asserted)."""
+    3×3×3 'same'; the row-slab kernel split over its K-steps), at a 2-D (kt = 1) ResNet-18 layer-4 conv run through the
+    conv3d machinery (32 frames of 7×7, (1,3,3) taps — ADVICE r04), and at layer 4's stride-2 conv (256 → 512 from
+    32×4×14×14: the generic gather kernel, 100 128×128 tiles, split over its 64-wide K-steps): planned
+    (`cmhar_conv3d_fwd_split_ws` > 0), against the fp32 conv of the same bf16 operands (+ the residual, as the dgrad
+    call adds dx_acc) within the bf16 output rounding, and within one bf16 ulp (of the value or of the output's rms near
+    zero) of the unsplit kernel (`cmhar_conv3d_fwd`, the same products summed in a different order)."""
     from cmhar import _lib as L
     from cmhar import kernels as K
     from cmhar import r3d
     torch.manual_seed(9)
     if geom == 'r3d_layer4':
-        N, C, T, S, k, pd = 32, 512, 2, 7, (3, 3, 3), (1, 1, 1)
+        N, Ci, C, T, S, k, st, pd = 32, 512, 512, 2, 7, (3, 3, 3), 1, (1, 1, 1)
+    elif geom == 'resnet18_layer4_kt1':
+        N, Ci, C, T, S, k, st, pd = 32, 512, 512, 1, 7, (1, 3, 3), 1, (0, 1, 1)
     else:
-        N, C, T, S, k, pd = 32, 512, 1, 7, (1, 3, 3), (0, 1, 1)
-    conv = torch.nn.Conv3d(C, C, k, 1, pd, bias=False)
-    x = torch.randn(N, C, T, S, S).bfloat16().float()
+        N, Ci, C, T, S, k, st, pd = 32, 256, 512, 4, 14, (3, 3, 3), 2, (1, 1, 1)
+    conv = torch.nn.Conv3d(Ci, C, k, st, pd, bias=False)
+    x = torch.randn(N, Ci, T, S, S).bfloat16().float()
     wq = conv.weight.detach().bfloat16().float()
-    ref = F.conv3d(x.to(DEV), wq.to(DEV), padding=pd)
+    ref = F.conv3d(x.to(DEV), wq.to(DEV), stride=st, padding=pd)
     conv = conv.to(DEV)
     xc = x.permute(0, 2, 3, 4, 1).contiguous().to(DEV).bfloat16()
     shp = tuple(xc.shape)
     Kp = r3d._r8(conv.weight[0].numel())
     wp = r3d._pack(conv, torch.bfloat16)
-    M = N * T * S * S
+    M = ref.shape[0] * ref.shape[2] * ref.shape[3] * ref.shape[4]
     dims = r3d._dims(shp, conv, Kp)
     n = L.lib().cmhar_conv3d_fwd_split_ws(dims, C)
     assert n > 0 and n % (M * C) == 0
-    s2 = torch.nn.Conv3d(C // 2, C, k, 2, pd, bias=False)
-    assert L.lib().cmhar_conv3d_fwd_split_ws(r3d._dims((N, T * 2 if k[0] == 3 else 1, 2 * S, 2 * S, C // 2), s2,
-                                                       r3d._r8(s2.weight[0].numel())), C) == 0
     rr = torch.randn(M, C, device=DEV).bfloat16() if res else None
     z = torch.empty(M, C, dtype=torch.bfloat16, device=DEV)
     ws = K.workspace(n, xc.device)

@@ -4,7 +4,7 @@ the entry points the step itself calls (`cmhar/r3d.py` `_conv_fwd` / `_conv_wgra
 `_unit_bwd` run between the BatchNorms) — VERDICT r04 item 2.  Smaller-shape tests (tests/test_r3d_gpu.py) do not
 reach these plans: the nine-tap kernels of layers 1–3 (layer 1 at 1.6 M output rows, layers 2–3 on 64-wide Cout
 slices; forward and flipped-weight input gradient), layer 4's on the split-K slab, the stride-2 convs and the
-downsamples on the generic 128×128 gather kernel with their input gradients as dz·W on the GEMM + col2im (the
+downsamples on the generic 128×128 gather kernel (layer 4's stride-2 conv split over K) with their input gradients as dz·W on the GEMM + col2im (the
 residual-branch gradient accumulated), every weight gradient on the row-slab / nine-tap / gather kernels with its
 split reduce.
 
@@ -50,7 +50,7 @@ PLANS = {
     'layer3.0.conv1': (5, 'col2im', '2+r'),
     'layer3.0.downsample': (5, 'col2im', '4+r'),
     'layer3.conv2': (1, 'flip:1', '1+r'),            # nine-tap slab fwd / wgrad, one 14-row tile per frame
-    'layer4.0.conv1': (5, 'col2im', '2+r'),
+    'layer4.0.conv1': ('split', 'col2im', '2+r'),    # stride 2, 100 128x128 tiles: generic gather split over K
     'layer4.0.downsample': (5, 'col2im', '4+r'),
     'layer4.conv2': ('split', 'flip:split', '2'),    # one split of the weight gradient: no reduce
 }
@@ -107,7 +107,9 @@ def test_conv3d_generic_forward_past_2gib():
     """The generic implicit-GEMM forward keeps a 64-bit-address instantiation for inputs over 2 GiB (R3D-18's
     layer2.0.conv1 geometry at N = 336: x = 2.16 GB): its output on the first clips equals, bit for bit, the
     buffer-resource instantiation's on those clips alone (each clip's convolution is independent), and the last
-    clip's too."""
+    clips' too.  Slices of 8 clips (392 tiles): fewer would take the split-K plan, whose fp32 partial sums associate
+    differently."""
+    from cmhar import _lib as L
     from cmhar import r3d
     torch.manual_seed(11)
     conv = _conv(64, 128, 3, 2, 1).to(DEV)
@@ -117,8 +119,9 @@ def test_conv3d_generic_forward_past_2gib():
     wp = r3d._pack(conv, torch.bfloat16)
     with torch.no_grad():
         z_big = r3d._conv_fwd(x, tuple(x.shape), conv, wp, stats=False)[0]
-        for sl in (slice(0, 2), slice(n_big - 1, n_big)):
+        for sl in (slice(0, 8), slice(n_big - 8, n_big)):
             xs = x[sl].contiguous()
+            assert L.lib().cmhar_conv3d_fwd_split_ws(r3d._dims(tuple(xs.shape), conv, wp.shape[1]), 128) == 0
             z_s = r3d._conv_fwd(xs, tuple(xs.shape), conv, wp, stats=False)[0]
             per = z_s.shape[0] // xs.shape[0]
             assert torch.equal(z_big[sl.start * per:sl.stop * per], z_s)
