@@ -2586,9 +2586,15 @@ static bool rows_plan(const Geom& g, int Cout, RowsPlan& p) {
       p.cpf = cpf;
       p.nchunk = g.N * g.To * p.cpf;
       const int tiles = g.kt * (g.C / 64) * (Cout / 64);
-      // one 12-wave workgroup per CU: at most 2 full rounds (rounding the split count up gave R3D-18 layer 1 513
-      // workgroups: a third round of one), >= 4 chunks each, <= ~80 MB of split partials
-      int s = max(1, 512 / tiles);
+      // one 12-wave workgroup per CU: one full round (rounding the split count up gave R3D-18 layer 1 513
+      // workgroups: a third round of one; 512 = two rounds wrote twice the split partials — layer 1 382.1 -> 358.6 us,
+      // layer 2 209.0 -> 199.5, layer 3 120.2 -> 110.4 at 256, step 2263 -> 2294 clips/s; 768 / 1024: 2189 / 2188),
+      // >= 4 chunks each, <= ~80 MB of split partials
+      static const int wgs = [] {   // CMHAR_WGRAD3_WGS: target workgroups (A/B runs)
+        const char* v = getenv("CMHAR_WGRAD3_WGS");
+        return v ? max(1, atoi(v)) : 256;
+      }();
+      int s = max(1, wgs / tiles);
       s = min(s, (int)((80L << 20) / ((long)Cout * g.K * 4)));
       s = max(1, min(s, p.nchunk / 4));
       p.cps = (p.nchunk + s - 1) / s;
