@@ -2511,7 +2511,11 @@ extern "C" int cmhar_conv3d_stem_fwd(const int* dims, int Cout, const void* x, c
 }
 static int stem_splits(const Geom& g, const StemPlan& p, int& tps) {
   // at most 512 workgroups (rounded up, R3D-18's kt = 3 stem gave 513)
-  int s = max(1, min(512 / g.kt, p.ntile / 8));
+  static const int wgs = [] {   // CMHAR_STEM_WGS: target workgroups (A/B runs)
+    const char* v = getenv("CMHAR_STEM_WGS");
+    return v ? max(1, atoi(v)) : 512;
+  }();
+  int s = max(1, min(wgs / g.kt, p.ntile / 8));
   tps = (p.ntile + s - 1) / s;
   return (p.ntile + tps - 1) / tps;
 }
@@ -2544,7 +2548,11 @@ extern "C" int cmhar_conv3d_stem_wgrad(const int* dims, int Cout, const void* x,
 static int wgrad_splits(const Geom& g, int Cout, int& mlen) {
   const int M = g.N * g.To * g.Ho * g.Wo;
   const int tiles = ((Cout + 127) / 128) * ((g.K + 127) / 128);
-  int s = max(1, 2048 / tiles);   // whole rounds: rounding up can leave a last round of a few workgroups
+  static const int wgs = [] {   // CMHAR_WGRAD_IG_WGS: target workgroups (A/B runs)
+    const char* v = getenv("CMHAR_WGRAD_IG_WGS");
+    return v ? max(1, atoi(v)) : 2048;
+  }();
+  int s = max(1, wgs / tiles);   // whole rounds: rounding up can leave a last round of a few workgroups
   const int smax = (M + 511) / 512;
   if (s > smax) s = smax;
   if (s < 1) s = 1;
@@ -2621,7 +2629,11 @@ static bool rows_plan(const Geom& g, int Cout, RowsPlan& p) {
   // slab that is written here and read back by the reduce: at 2048 workgroups that was ~200 MB per conv, 1.7 ms per
   // step); within that, the split count with the least time ∝ rounds of the 512 workgroup slots x chunks per split
   // (whole rounds: R3D-18 layer 3 takes 7 splits = 504 workgroups, not 6 = 432)
-  const int smax = max(1, min(min(2048 / tiles, (int)((56L << 20) / ((long)Cout * g.K * 4))), nchunk / 8));
+  static const int wgs = [] {   // CMHAR_WGRAD_ROWS_WGS: target workgroups (A/B runs)
+    const char* v = getenv("CMHAR_WGRAD_ROWS_WGS");
+    return v ? max(1, atoi(v)) : 2048;
+  }();
+  const int smax = max(1, min(min(wgs / tiles, (int)((56L << 20) / ((long)Cout * g.K * 4))), nchunk / 8));
   long best = -1;
   for (int c = 1; c <= smax; ++c) {
     const int cps = (nchunk + c - 1) / c, sp = (nchunk + cps - 1) / cps;
