@@ -50,6 +50,7 @@ _SIGS = {
     'cmhar_gemm_f16': (i32, [i32, i32, i32, i32, i32, vp, i64, vp, i64, vp, i64, C.POINTER(Epilogue), i32, vp, vp]),
     'cmhar_gemm_bf16_ws': (i64, [i32, i32, i32]),
     'cmhar_gemm_bf16_plan': (i32, [i32, i32, i32, i32, i32, i32, i32]),
+    'cmhar_gemm_bf16_plan2': (i32, [i32, i32, i32, i32, i32, i32, i32, i32]),
     'cmhar_gemm_generic': (i32, [i32, i32, i32, i32, i32, i32, vp, i64, i64, i64, vp, i64, i64, i64, vp, i64, i64,
                                  C.POINTER(Epilogue), vp]),
     'cmhar_gemm_generic_splitk': (i32, [i32, i32, i32, i32, i32, i32, vp, i64, i64, vp, i64, i64, vp, i64,

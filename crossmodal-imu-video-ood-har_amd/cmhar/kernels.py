@@ -55,15 +55,17 @@ _GEMM_SYMBOL = {0: 'gemm_bf16_kernel<true,true,{o}>', 1: 'gemm_bf16_kernel<true,
 _PLAN = {}
 
 
-def _gemm_trace_name(layout, M, N, K, s, has_ws, rowsum, out_dtype):
+def _gemm_trace_name(layout, M, N, K, s, has_ws, rowsum, out_dtype, reads=False):
     """Trace label of a bf16 GEMM call: the GEMM kernel (template name as rocprofv3 lists it, without the trailing
-    integer parameters) that the library's own plan (cmhar_gemm_bf16_plan) launches; a split-K / tail reduce that
-    follows it is launched outside the traced interval."""
+    integer parameters) that the library's own plan (cmhar_gemm_bf16_plan2; reads: the epilogue reads a residual /
+    aux_in / rowadd operand or accumulates into C) launches; a split-K / tail reduce that follows it is launched
+    outside the traced interval."""
     key = (layout, M, N, K, s, has_ws, rowsum)
-    plan = _PLAN.get(key)
-    if plan is None:
-        plan = _PLAN[key] = int(L.lib().cmhar_gemm_bf16_plan(layout, M, N, K, s, int(has_ws), int(rowsum)))
+    plan = L.lib().cmhar_gemm_bf16_plan2(layout, M, N, K, s, int(has_ws), int(rowsum), int(reads))
+    _PLAN[key] = plan
     o = 'float' if (plan in (3, 5, 6) or out_dtype == torch.float32) else 'bf16'
+    if plan == 7:
+        return f'gemm8p_persist_kernel<{o}>'
     if plan in (4, 6):
         ak, bk = layout != 2, layout == 0
         return f'gemm8p_kernel<{str(ak).lower()},{str(bk).lower()},{o}>'
@@ -250,7 +252,8 @@ def gemm(layout: int, a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, *, bi
                 ws = workspace(n, out.device)
         ev = name = None
         if TRACE.active:
-            name = _gemm_trace_name(layout, M, N, K, s, ws is not None, rowsum is not None, out.dtype)
+            reads = residual is not None or aux_in is not None or rowadd is not None or beta != 0.0
+            name = _gemm_trace_name(layout, M, N, K, s, ws is not None, rowsum is not None, out.dtype, reads)
             ev = TRACE.begin(name)
         if ev is None and reduce_stream is not None and s > 1:
             args = (layout, L.dtype_code(out.dtype), M, N, K, ptr(a), a.stride(0), ptr(b), b.stride(0), ptr(out),

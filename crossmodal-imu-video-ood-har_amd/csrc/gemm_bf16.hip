@@ -171,6 +171,8 @@ __device__ __forceinline__ const OutT* epi_stream(const Epilogue& e, long& ld) {
 static inline bool epi_has_stream(const Epilogue& e) {
   return e.residual != nullptr || e.act == ACT_DGELU || e.act == ACT_DRELU || e.act == ACT_MULAUX;
 }
+// an epilogue that reads any per-element or per-row operand (the persistent kernel's exclusion, persist_ok)
+static inline bool epi_reads(const Epilogue& e) { return epi_has_stream(e) || e.rowadd != nullptr || e.beta != 0.f; }
 template <typename OutT>
 __device__ __forceinline__ void decode8(const uint4_t& r, float (&x)[8]) {
   typedef OutT __attribute__((ext_vector_type(8))) v8;
@@ -295,6 +297,217 @@ __device__ __forceinline__ void epilogue_store8(const Epilogue& e, OutT* __restr
     for (int j = 0; j < 8; ++j) x[j] += e.beta * t[j];
   }
   store8<OutT>(dst, x);
+}
+
+// ---------------------------------------------------------------------------------------------------------------
+// Register-direct epilogue of the 256² kernels (CMHAR_EPI_DIRECT = 1; instantiations without a streamed epilogue
+// operand).  The K loop runs with the MFMA operands swapped — acc = (B fragment) x (A fragment), i.e. Cᵀ per 16x16
+// block, the same products in the same order (bit-identical) — so lane l holds in acc[i][j][r] ONE row
+// (i*16 + (l&15)) and FOUR consecutive columns (j*16 + 4*(l>>4) + r) of the wave's 128x64 block.  A v_permlane16_swap
+// per accumulator register pairs blocks (2p, 2p+1) and a row_ror:8 DPP exchange pairs the lane halves (pair_rows), so
+// every store instruction covers 8 rows x 128 contiguous bytes straight from registers — no LDS staging round trip
+// (64 4-B ds_writes per lane per pass, a wait, the read-back).  fp32 partial slabs (raw) need no pairing: a block's 4
+// columns are one 16-B store.  Measured in the bench step (rocprofv3 per launch, tools/debug/trace_ab.sh): FC2 forward
+// (tail split) -3 %, weight gradients -1 to -2.5 %, the plain forward epilogues within +-1.5 %; the epilogues that
+// stream a 16-bit operand (residual, GELU') were 11-20 % SLOWER with every prefetch depth tried (4, 8, all 16 segments
+// before the first store) — the legacy loop's LDS staging is what hides those loads — so the PFS instantiations keep
+// the staged epilogue.
+// ablation builds of the persistent kernel (tools/debug): 1 = K-tile 2's DMA wait leaves the previous tile's stores in
+// flight (racy: timing only), 2 = no epilogue
+#ifndef CMHAR_PERSIST_ABL
+#define CMHAR_PERSIST_ABL 0
+#endif
+// CMHAR_PERSIST_PROBE (debug builds, tools/debug/persist_probe.py): in-kernel s_memtime stamps of wave 0 / wave 4 of
+// every workgroup around each tile boundary, read back by cmhar_debug_persist_probe
+#ifndef CMHAR_PERSIST_PROBE
+#define CMHAR_PERSIST_PROBE 0
+#endif
+#if CMHAR_PERSIST_PROBE
+__device__ unsigned long long g_persist_probe[256 * 12 * 2 * 6];
+#endif
+// start-time stagger of the persistent kernel's workgroups, in units of s_sleep(127) (~8 k cycles) per quarter
+#ifndef CMHAR_PERSIST_STAGGER
+#define CMHAR_PERSIST_STAGGER 0
+#endif
+#ifndef CMHAR_EPI_DIRECT
+#define CMHAR_EPI_DIRECT 1
+#endif
+// segments of the streamed operand in flight (even, 2..8): all 128 accumulators stay live across the rolled epilogue
+// loop
+#ifndef CMHAR_EPI_DIRECT_PD
+#define CMHAR_EPI_DIRECT_PD 8
+#endif
+// acc += (x-fragment) · (w-fragment) in the accumulator layout the epilogue expects
+template <typename E, bool DIRECT>
+__device__ __forceinline__ floatx4 mma_ab(bf16x8 a, bf16x8 b, floatx4 c) {
+  return DIRECT ? mma16<E>(b, a, c) : mma16<E>(a, b, c);
+}
+// Row block i of the accumulators (16 rows x the wave's 64 columns) as two store segments of 8 whole rows each.
+// After the permlane16 pairing a lane holds row li = l&15, 8 columns at 32p + cofs(g) for p = 0 (v0) and 1 (v1); a
+// row_ror:8 DPP exchange between the lane halves li < 8 / li >= 8 then gives segment X = rows 0-7 (lanes li < 8 keep
+// their p = 0 columns, lanes li >= 8 take the p = 1 columns of row li - 8) and segment Y = rows 8-15 (the mirror), so
+// that every store instruction covers 8 rows x 128 contiguous bytes, the legacy staging loop's pattern (16 rows x 64 B
+// per instruction measured 3-4 % slower in the step: 730 -> 710 clips/s).  Lane l of a segment: row (l & 7) (+8 for Y),
+// columns 32*((l >> 3) & 1) + cofs(l >> 4) .. +7.  A switch on the (wave-uniform) block index with a static accumulator
+// access in every case keeps the epilogue loop rolled — fully unrolled, the inlined epilogue_store8 bodies took the
+// kernels from ~4.5 k to 14-18 k instructions (past the instruction cache), and a dynamic acc index put acc in scratch.
+__device__ __forceinline__ float dpp_ror8(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x128, 0xf, 0xf, false));   // row_ror:8
+}
+__device__ __forceinline__ void pair_rows(const floatx4 (&acc)[8][4], int i, bool lo, float (&x)[8], float (&y)[8]) {
+  float v0[8], v1[8];
+  auto take = [&](const floatx4(&a)[4]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const auto s0 = __builtin_amdgcn_permlane16_swap(__float_as_uint(a[0][r]), __float_as_uint(a[1][r]), false, false);
+      const auto s1 = __builtin_amdgcn_permlane16_swap(__float_as_uint(a[2][r]), __float_as_uint(a[3][r]), false, false);
+      v0[r] = __uint_as_float(s0[0]);
+      v0[4 + r] = __uint_as_float(s0[1]);
+      v1[r] = __uint_as_float(s1[0]);
+      v1[4 + r] = __uint_as_float(s1[1]);
+    }
+  };
+  switch (i) {
+    case 0: take(acc[0]); break;
+    case 1: take(acc[1]); break;
+    case 2: take(acc[2]); break;
+    case 3: take(acc[3]); break;
+    case 4: take(acc[4]); break;
+    case 5: take(acc[5]); break;
+    case 6: take(acc[6]); break;
+    default: take(acc[7]); break;
+  }
+#pragma unroll
+  for (int r = 0; r < 8; ++r) {
+    const float got = dpp_ror8(lo ? v1[r] : v0[r]);   // lanes li < 8 send v1 and receive v0 of row li + 8
+    x[r] = lo ? v0[r] : got;
+    y[r] = lo ? got : v1[r];
+  }
+}
+// m0 / n0: the wave block's first row / column; raw (fp32 partials of the wave block's first row, row stride raw_ld)
+// or null for the product epilogue.  PFS: the epilogue's streamed 16-bit operand (epi_stream) is loaded PD segments
+// ahead of its use (the first PD before the first store).
+// The epilogues epi_direct's fast path takes: alpha 1, no dropout, nothing read (residual, aux_in, rowadd, beta),
+// no activation or the GELU pair with its GELU' output (16-bit outputs only)
+__host__ __device__ inline bool epi_fast_ok(const Epilogue& e) {
+  return e.alpha == 1.f && e.pdrop <= 0.f && !e.residual && !e.aux_in && !e.rowadd && e.beta == 0.f &&
+         (e.act == ACT_NONE || (e.act == ACT_GELU_SAVEGRAD && e.aux_out));
+}
+// This lane's 8 bias columns (zeros without a bias): an unconditional load (a dummy valid address without one), so
+// that no load is left pending on a path the compiler cannot rule out — a loop-carried pending load of a persistent
+// kernel's epilogue made hipcc wait vmcnt before the next tile's first MFMAs (WAW on the load's registers).
+__device__ __forceinline__ void epi_bias(const Epilogue& e, const void* dummy, int n0, int lane, floatx4 (&bh)[2]) {
+  const int g = lane >> 4, li = lane & 15;
+  const int cn = n0 + 32 * (li >> 3) + (((g & 1) << 4) | ((g >> 1) << 3));
+  const float* p = e.bias ? e.bias + cn : (const float*)dummy;
+  bh[0] = *(const floatx4*)p;
+  bh[1] = *(const floatx4*)(p + 4);
+}
+// FAST_ONLY: the caller guarantees the fast path's epilogue (epi_fast_ok) — the generic per-element path is not
+// compiled in (the persistent kernel: its registers are at the limit)
+template <typename OutT, bool PFS, bool BIAS_IN = false, bool FAST_ONLY = false>
+__device__ __forceinline__ void epi_direct(const Epilogue& e, OutT* __restrict__ C, long ldc, float* __restrict__ raw,
+                                           long raw_ld, int m0, int n0, int lane, const floatx4 (&acc)[8][4],
+                                           const floatx4* bias_in = nullptr) {
+  const int g = lane >> 4, li = lane & 15;
+  if (raw) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) *(floatx4*)(raw + (long)(i * 16 + li) * raw_ld + j * 16 + 4 * g) = acc[i][j];
+    return;
+  }
+  const bool lo = li < 8;
+  const int cn = n0 + 32 * (li >> 3) + (((g & 1) << 4) | ((g >> 1) << 3));   // this lane's 8 columns, both segments
+  const int rl = m0 + (li & 7);                                              // this lane's row in segment X of block 0
+  floatx4 bh[2] = {floatx4{0.f, 0.f, 0.f, 0.f}, floatx4{0.f, 0.f, 0.f, 0.f}};
+  if constexpr (BIAS_IN) {   // loaded by epi_bias and already zeroed without a bias by the caller
+    bh[0] = bias_in[0];
+    bh[1] = bias_in[1];
+  } else if (e.bias) {
+    bh[0] = *(const floatx4*)(e.bias + cn);
+    bh[1] = *(const floatx4*)(e.bias + cn + 4);
+  }
+  // Fast path (16-bit output; bias, key-column scale, GELU pair — the persistent kernel's launches): packed-fp32
+  // math on the two segments and nothing else per element.  The in-kernel timeline (tools/debug/persist_probe.py)
+  // showed the generic epilogue VALU-bound: 12.6-15.7 k cycles per QKV tile (~26 % of the tile) for 16 stores per
+  // wave — a wave64 VALU instruction holds its SIMD 4 cycles, and epilogue_store8's per-element alpha multiply,
+  // bias add, colscale select and row / column address arithmetic ran ~150 instructions per 16 values.
+  if constexpr (sizeof(OutT) == 2 && !PFS) {
+    const bool gp = e.act == ACT_GELU_SAVEGRAD && e.aux_out;
+    if (FAST_ONLY || epi_fast_ok(e)) {
+      typedef __attribute__((ext_vector_type(2))) float f2;
+      f2 b2[4], s2 = {1.f, 1.f};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) b2[k] = f2{bh[k >> 1][2 * (k & 1)], bh[k >> 1][2 * (k & 1) + 1]};
+      const bool cs = cn >= e.colscale_lo && cn < e.colscale_hi;   // a multiple-of-8 range: whole segments
+      if (cs) s2 = f2{e.colscale, e.colscale};
+      const bool any_cs = e.colscale_hi > e.colscale_lo;
+      OutT* const c0 = C + (long)rl * ldc + cn;
+      OutT* const a0 = gp ? (OutT*)e.aux_out + (long)rl * e.ldo + cn : nullptr;
+      auto seg = [&](const float (&v)[8], OutT* dst, OutT* adst) __attribute__((always_inline)) {
+        f2 x[4], t[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          x[k] = f2{v[2 * k], v[2 * k + 1]} + b2[k];
+          if (any_cs) x[k] = x[k] * s2;
+          if (gp) gelu_pair16x2(x[k], x[k], t[k]);
+        }
+        typedef OutT __attribute__((ext_vector_type(2))) o2;
+        typedef int __attribute__((ext_vector_type(4))) i4;
+        i4 o, a;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          o[k] = __builtin_bit_cast(int, __builtin_convertvector(x[k], o2));
+          if (gp) a[k] = __builtin_bit_cast(int, __builtin_convertvector(t[k], o2));
+        }
+        if (gp) __builtin_nontemporal_store(a, (i4*)adst);
+        __builtin_nontemporal_store(o, (i4*)dst);
+      };
+#pragma unroll 1
+      for (int i = 0; i < 8; ++i) {
+        float x[8], y[8];
+        pair_rows(acc, i, lo, x, y);
+        const long ro = (long)i * 16 * ldc, ra = gp ? (long)i * 16 * e.ldo : 0;
+        seg(x, c0 + ro, a0 + ra);
+        seg(y, c0 + ro + 8 * ldc, a0 + ra + 8 * e.ldo);
+      }
+      return;
+    }
+  }
+  if constexpr (FAST_ONLY) return;
+  long pld = 0;
+  const OutT* const ps = PFS && sizeof(OutT) == 2 ? epi_stream<OutT>(e, pld) : nullptr;
+  // segment c = 2i + h: row rl + 16i + 8h
+  auto pf = [&](int c) -> uint4_t {
+    return ps ? *(const uint4_t*)(ps + (long)(rl + c * 8) * pld + cn) : uint4_t{0u, 0u, 0u, 0u};
+  };
+  constexpr int PD = CMHAR_EPI_DIRECT_PD;
+  uint4_t pw[PD];
+#pragma unroll
+  for (int j = 0; j < PD; ++j) pw[j] = PFS ? pf(j) : uint4_t{0u, 0u, 0u, 0u};
+#pragma unroll 1
+  for (int i = 0; i < 8; ++i) {
+    const uint4_t q0 = pw[0], q1 = pw[1];
+    if constexpr (PFS) {
+#pragma unroll
+      for (int j = 0; j + 2 < PD; ++j) pw[j] = pw[j + 2];
+      if (2 * i + PD < 16) {
+        pw[PD - 2] = pf(2 * i + PD);
+        pw[PD - 1] = pf(2 * i + PD + 1);
+      }
+    }
+    float x[8], y[8];
+    pair_rows(acc, i, lo, x, y);
+    // the column index made opaque per iteration: hoisted out of the loop, the column-dependent parts of the
+    // epilogue (the dropout hash's per-column terms, 64-bit column offsets) sat in 32+ VGPRs next to the 128 live
+    // accumulators and spilled
+    int nc = cn;
+    asm volatile("" : "+v"(nc));
+    const int m = rl + i * 16;
+    epilogue_store8<OutT>(e, C, ldc, m, nc, x, ps != nullptr, q0, bh);
+    epilogue_store8<OutT>(e, C, ldc, m + 8, nc, y, ps != nullptr, q1, bh);
+  }
 }
 
 constexpr int EPI_LD = BN + 4;                       // padded fp32 staging row: conflict-free acc writes
@@ -608,6 +821,7 @@ __global__ __launch_bounds__(NT2, 2) void gemm256_kernel(int M, int N, int K, co
                                                          int raw_out, float* __restrict__ sk_ws, int n_dp,
                                                          int sk_klen) {
   constexpr bool kAD = CMHAR_GEMM8P_ASM_DMA && (!A_KC || !B_KC);   // see dma_asm
+  constexpr bool kDirect = CMHAR_EPI_DIRECT && MODE == 0 && !PFS;   // register-direct epilogue (epi_direct)
   // the L2 prefetch is a builtin LDS-DMA (compiler-managed M0): never in a K loop whose DMA the asm issues
   constexpr bool PF = CMHAR_GEMM_L2PF && NA == 2 && MODE == 0 && !kAD;
   static_assert(!(PF && kAD), "builtin LDS-DMA (L2 prefetch) beside asm-issued DMA: M0 is not tracked across dma_asm");
@@ -732,7 +946,7 @@ __global__ __launch_bounds__(NT2, 2) void gemm256_kernel(int M, int N, int K, co
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = mma16<E>(af[i], bf0[j], acc[i][j]);
+      for (int j = 0; j < 4; ++j) acc[i][j] = mma_ab<E, kDirect>(af[i], bf0[j], acc[i][j]);
       if (!A_KC && rs && wc == (i >> 1))
         accb[i & 1] = mma16<E>(af[i], ones, accb[i & 1]);
       af[i] = frag256<A_KC>(a_s, wr * 128 + i * 16, 1, lane);
@@ -741,7 +955,7 @@ __global__ __launch_bounds__(NT2, 2) void gemm256_kernel(int M, int N, int K, co
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = mma16<E>(af[i], bf1[j], acc[i][j]);
+      for (int j = 0; j < 4; ++j) acc[i][j] = mma_ab<E, kDirect>(af[i], bf1[j], acc[i][j]);
       if (!A_KC && rs && wc == (i >> 1))
         accb[i & 1] = mma16<E>(af[i], ones, accb[i & 1]);
     }
@@ -757,7 +971,7 @@ __global__ __launch_bounds__(NT2, 2) void gemm256_kernel(int M, int N, int K, co
 #pragma unroll
     for (int i = 4; i < 8; ++i) {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = mma16<E>(af[i], bf1[j], acc[i][j]);
+      for (int j = 0; j < 4; ++j) acc[i][j] = mma_ab<E, kDirect>(af[i], bf1[j], acc[i][j]);
       if (!A_KC && rs && wc == (i >> 1))
         accb[i & 1] = mma16<E>(af[i], ones, accb[i & 1]);
       if (more) af[i] = frag256<A_KC>(nxt, wr * 128 + i * 16, 0, lane);
@@ -777,6 +991,12 @@ __global__ __launch_bounds__(NT2, 2) void gemm256_kernel(int M, int N, int K, co
         if (rs_slab) rs_slab[m] = accb[ii][r];
         else e.rowsum[m] = e.rowsum_beta != 0.f ? accb[ii][r] + e.rowsum_beta * e.rowsum[m] : accb[ii][r];
       }
+  }
+  if constexpr (kDirect) {
+    float* raw = raw_out ? (float*)C + (long)(bm + wr * 128) * ldc + bn + wc * 64
+                 : sk ? sk_ws + split * sk_stride + (long)(bm + wr * 128 - tail_m0) * N + bn + wc * 64 : nullptr;
+    epi_direct<OutT, PFS>(e, C, ldc, raw, raw_out ? ldc : N, bm + wr * 128, bn + wc * 64, lane, acc);
+    return;
   }
   __syncthreads();
   if (MODE == 4 || MODE == 7 || MODE == 8) {   // keep every accumulator live, store nothing
@@ -909,6 +1129,15 @@ struct DmaHalf {
     base = (const char*)(KC ? P + (long)r0 * ld : P + r0);
     kstride = KC ? 2 : ld * 2;
   }
+  // the same pieces from another tile's origin (the persistent kernel walks several tiles with one set of offsets)
+  __device__ __forceinline__ void half_from(const char* org, int k0, char* lds, int h, int wave) const {
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void*)(org + (long)k0 * kstride), (short)0,
+                                                                       0x7fffffff, 0x00020000);
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void_ptr)(lds + (16 * h + 2 * wave + t) * 1024), 16,
+                                               voff[h][t], 0, 0, 0);
+  }
   template <bool ASM = false>
   __device__ __forceinline__ void half(int k0, char* lds, int h, int wave) const {
     if constexpr (ASM) {
@@ -927,6 +1156,11 @@ struct DmaHalf {
 
 #ifndef CMHAR_GEMM8P_ABLATE
 #define CMHAR_GEMM8P_ABLATE 0
+#endif
+// CMHAR_GEMM8P_BEARLY (A/B knob, two A buffers): the weight operand B of K-tile t+1 staged in phase 1 and A's lower
+// half in phase 2 (the default order is the reverse: B then gets two barrier intervals of lead, A's lower half three)
+#ifndef CMHAR_GEMM8P_BEARLY
+#define CMHAR_GEMM8P_BEARLY 0
 #endif
 
 
@@ -1003,6 +1237,11 @@ __global__ __launch_bounds__(NT2, 2) void gemm8p_kernel(int M, int N, int K, con
   static_assert(NA == 2 || NA == 3, "two or three A buffers");
   // transposed-read instantiations issue their DMA by inline asm (see dma_asm)
   constexpr bool kAD = CMHAR_GEMM8P_ASM_DMA && (!A_KC || !B_KC);
+  constexpr bool kDirect = CMHAR_EPI_DIRECT && CMHAR_GEMM8P_ABLATE == 0 && !PFS;   // register-direct epilogue
+  // ablation builds 3 / 4 / 5 (tools/debug): K loop only, without the B / A / both operand DMA inside the loop (the
+  // prologue still stages the first K-tiles; later K-tiles read stale LDS)
+  constexpr bool kAblNoB = CMHAR_GEMM8P_ABLATE == 3 || CMHAR_GEMM8P_ABLATE == 5;
+  constexpr bool kAblNoA = CMHAR_GEMM8P_ABLATE == 4 || CMHAR_GEMM8P_ABLATE == 5;
   __shared__ __attribute__((aligned(16))) char smem[NA == 3 ? 163840 : SMEM2];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1069,7 +1308,7 @@ __global__ __launch_bounds__(NT2, 2) void gemm8p_kernel(int M, int N, int K, con
     _Pragma("unroll") for (int kk = 0; kk < 2; ++kk)                                                          \
     _Pragma("unroll") for (int i = 0; i < 4; ++i)                                                             \
     _Pragma("unroll") for (int j = 0; j < 2; ++j)                                                             \
-      acc[(QM) * 4 + i][qn_ * 2 + j] = mma16<E>(af[kk][i], BF[kk][j],           \
+      acc[(QM) * 4 + i][qn_ * 2 + j] = mma_ab<E, kDirect>(af[kk][i], BF[kk][j],         \
                                                                              acc[(QM) * 4 + i][qn_ * 2 + j]); \
     if (!A_KC && rs && qn_ == (QM)) /* bias gradient: each A fragment once, at its first quadrant */         \
       _Pragma("unroll") for (int kk = 0; kk < 2; ++kk)                                                        \
@@ -1102,11 +1341,16 @@ __global__ __launch_bounds__(NT2, 2) void gemm8p_kernel(int M, int N, int K, con
     }
     if constexpr (NA == 3) {
       if (n1) {
-        db.template half<kAD>(k1, bbuf(t + 1), 0, wave);
-        db.template half<kAD>(k1, bbuf(t + 1), 1, wave);
+        if (!kAblNoB) db.template half<kAD>(k1, bbuf(t + 1), 0, wave);
+        if (!kAblNoB) db.template half<kAD>(k1, bbuf(t + 1), 1, wave);
+      }
+    } else if (CMHAR_GEMM8P_BEARLY) {
+      if (n1) {
+        if (!kAblNoB) db.template half<kAD>(k1, bbuf(t + 1), 0, wave);
+        if (!kAblNoB) db.template half<kAD>(k1, bbuf(t + 1), 1, wave);
       }
     } else {
-      if (n1) da.template half<kAD>(k1, abuf(t + 1), 1, wave);
+      if (n1) if (!kAblNoA) da.template half<kAD>(k1, abuf(t + 1), 1, wave);
     }
     END_LOADS();
     {
@@ -1119,11 +1363,13 @@ __global__ __launch_bounds__(NT2, 2) void gemm8p_kernel(int M, int N, int K, con
 #pragma unroll
       for (int j = 0; j < 2; ++j) b1[kk][j] = frag256<B_KC>(bs, wc * 64 + 32 + j * 16, kk, lane);
     if constexpr (NA == 3) {
-      if (n2) da.template half<kAD>(k2, abuf(t + 2), 1, wave);
+      if (n2) if (!kAblNoA) da.template half<kAD>(k2, abuf(t + 2), 1, wave);
+    } else if (CMHAR_GEMM8P_BEARLY) {
+      if (n1) if (!kAblNoA) da.template half<kAD>(k1, abuf(t + 1), 1, wave);
     } else {
       if (n1) {
-        db.template half<kAD>(k1, bbuf(t + 1), 0, wave);
-        db.template half<kAD>(k1, bbuf(t + 1), 1, wave);
+        if (!kAblNoB) db.template half<kAD>(k1, bbuf(t + 1), 0, wave);
+        if (!kAblNoB) db.template half<kAD>(k1, bbuf(t + 1), 1, wave);
       }
     }
     END_LOADS();
@@ -1145,14 +1391,14 @@ __global__ __launch_bounds__(NT2, 2) void gemm8p_kernel(int M, int N, int K, con
     // of t+2 first, then a wait that leaves t+2's four A pieces in flight
     if constexpr (NA == 3) {
       if (n2) {
-        da.template half<kAD>(k2, abuf(t + 2), 0, wave);
+        if (!kAblNoA) da.template half<kAD>(k2, abuf(t + 2), 0, wave);
         asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
       } else {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
     } else {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      if (n2) da.template half<kAD>(k2, abuf(t + 2), 0, wave);
+      if (n2) if (!kAblNoA) da.template half<kAD>(k2, abuf(t + 2), 0, wave);
     }
     END_LOADS();
     {
@@ -1173,8 +1419,13 @@ __global__ __launch_bounds__(NT2, 2) void gemm8p_kernel(int M, int N, int K, con
         else e.rowsum[m] = e.rowsum_beta != 0.f ? accb[ii][r] + e.rowsum_beta * e.rowsum[m] : accb[ii][r];
       }
   }
+  if constexpr (kDirect) {
+    epi_direct<OutT, PFS>(e, C, ldc, raw_out ? (float*)C + (long)(bm + wr * 128) * ldc + bn + wc * 64 : nullptr, ldc,
+                          bm + wr * 128, bn + wc * 64, lane, acc);
+    return;
+  }
   __syncthreads();
-#if CMHAR_GEMM8P_ABLATE == 1   // ablation build (tools/debug): K loop only, every accumulator kept live
+#if CMHAR_GEMM8P_ABLATE == 1 || CMHAR_GEMM8P_ABLATE >= 3   // ablation builds: K loop only, accumulators kept live
   {
     float t = 0.f;
 #pragma unroll
@@ -1260,6 +1511,252 @@ __global__ __launch_bounds__(NT2, 2) void gemm8p_kernel(int M, int N, int K, con
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   }
+}
+
+// ---------------------------------------------------------------------------------------------------------------
+// Persistent 8-phase forward-layout kernel (CMHAR_GEMM8P_PERSIST; whole K, no streamed epilogue operand): one
+// workgroup per CU walks tiles v = blockIdx.x + G·s (G = the CU count, a multiple of 8, so that iteration s of every
+// workgroup is exactly round s of the one-tile-per-workgroup launch: the same tile set per XCD at the same time).  The
+// 8-phase K loop runs over the CONCATENATED K-tiles of the workgroup's tiles — the next tile's K-tile 0 (and the lower
+// A half of its K-tile 1) is staged under the current tile's last K-tile exactly like any other K-tile.  At a tile
+// boundary each wave, right after its last MFMA quadrant (group 0 one interval before group 1, while the other group's
+// MFMAs run): (1) issues the rest of the next tile's K-tile 1 (A upper half + B) into the buffer the finished K-tile
+// just released — BEFORE (2) the register-direct epilogue (epi_direct: no LDS) issues its stores.  vmcnt counts loads,
+// stores and LDS-DMA in issue order (gfx9 has no separate store counter), so the K-tile-1 wait in the next tile's
+// K-tile 0 is a counted `vmcnt(S)` that leaves the S epilogue memory operations of this wave in flight: the stores drain
+// under the next tile's K loop instead of holding the workgroup (and its CU) until they are acknowledged, and the next
+// workgroup's launch and first-K-tile latency disappear.  No inter-workgroup communication: a workgroup that is not
+// resident yet just starts later.
+template <typename E, typename OutT>
+__global__ __launch_bounds__(NT2, 2) void gemm8p_persist_kernel(int M, int N, int K, const bf16* __restrict__ A,
+                                                                long lda, const bf16* __restrict__ B, long ldb,
+                                                                OutT* __restrict__ C, long ldc, Epilogue e,
+                                                                int ngroup) {
+  __shared__ __attribute__((aligned(16))) char smem[131072];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave >> 2, wc = wave & 3;
+  const int tiles_n = N / TN2, tiles_m = M / TM2, ntile = tiles_m * tiles_n;
+  const int nk = K / TK2;   // even, >= 2 (host-checked)
+  const int G = gridDim.x;
+  // tile origin (rows bm, columns bn) of iteration s, as gemm8p_kernel maps block id v
+  auto tile_of = [&](int s, int& bm, int& bn) -> bool {
+    const int v = blockIdx.x + G * s;
+    if (v >= ntile) return false;
+    const int bid = xcd_remap(v, ntile);
+    int tm = bid / tiles_n, tn = bid % tiles_n;
+    if (ngroup > 1) {
+      const int cw = (tiles_n + ngroup - 1) / ngroup;
+      const int gi = min(bid / (tiles_m * cw), ngroup - 1);
+      const int wg = min(cw, tiles_n - gi * cw);
+      const int loc = bid - gi * tiles_m * cw;
+      tm = loc / wg;
+      tn = gi * cw + loc % wg;
+    }
+    bm = tm * TM2;
+    bn = tn * TN2;
+    return true;
+  };
+  int bm, bn, bm2 = 0, bn2 = 0;
+  if (!tile_of(0, bm, bn)) return;
+  bool nxt = tile_of(1, bm2, bn2);
+  DmaHalf<true> da, db;
+  da.init(A, lda, bm, wave, lane);
+  db.init(B, ldb, bn, wave, lane);
+  const char* a_cur = (const char*)(A + (long)bm * lda);
+  const char* b_cur = (const char*)(B + (long)bn * ldb);
+  const char* a_nxt = (const char*)(A + (long)bm2 * lda);
+  const char* b_nxt = (const char*)(B + (long)bn2 * ldb);
+  auto abuf = [&](int t) -> char* { return smem + (t & 1) * 65536; };
+  auto bbuf = [&](int t) -> char* { return smem + (t & 1) * 65536 + 32768; };
+  // K-tile t of the concatenated stream, t >= nk meaning the next tile's K-tile t - nk
+  auto stage_a = [&](int t, int h) {
+    if (t < nk) da.half_from(a_cur, t * TK2, abuf(t), h, wave);
+    else if (nxt) da.half_from(a_nxt, (t - nk) * TK2, abuf(t), h, wave);
+  };
+  auto stage_b = [&](int t) {
+    if (t < nk) {
+      db.half_from(b_cur, t * TK2, bbuf(t), 0, wave);
+      db.half_from(b_cur, t * TK2, bbuf(t), 1, wave);
+    } else if (nxt) {
+      db.half_from(b_nxt, (t - nk) * TK2, bbuf(t), 0, wave);
+      db.half_from(b_nxt, (t - nk) * TK2, bbuf(t), 1, wave);
+    }
+  };
+
+  floatx4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+  bf16x8 af[2][4], b0[2][2], b1[2][2];
+
+  if (CMHAR_PERSIST_STAGGER > 0) {   // A/B knob: start-time stagger (quarters of the CUs of each XCD)
+    const int q = (blockIdx.x >> 3) & 3;
+    for (int r = 0; r < q * CMHAR_PERSIST_STAGGER; ++r) __builtin_amdgcn_s_sleep(127);
+  }
+  // prologue (first tile only): K-tile 0 whole + K-tile 1's A half 0, wait for K-tile 0
+  stage_a(0, 0);
+  stage_a(0, 1);
+  stage_b(0);
+  stage_a(1, 0);
+  asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  if (wr == 1) __builtin_amdgcn_s_barrier();   // group 1 runs one interval behind
+  __builtin_amdgcn_sched_barrier(0);
+
+#define MFMA_QP(QM, BF)                                                                                       \
+  do {                                                                                                        \
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                                                        \
+    __builtin_amdgcn_sched_barrier(0);                                                                        \
+    __builtin_amdgcn_s_setprio(1);                                                                            \
+    _Pragma("unroll") for (int kk = 0; kk < 2; ++kk)                                                          \
+    _Pragma("unroll") for (int i = 0; i < 4; ++i)                                                             \
+    _Pragma("unroll") for (int j = 0; j < 2; ++j)                                                             \
+      acc[(QM) * 4 + i][qn_ * 2 + j] = mma_ab<E, true>(af[kk][i], BF[kk][j], acc[(QM) * 4 + i][qn_ * 2 + j]);  \
+    __builtin_amdgcn_s_setprio(0);                                                                            \
+    __builtin_amdgcn_sched_barrier(0);                                                                        \
+    __builtin_amdgcn_s_barrier();                                                                             \
+    __builtin_amdgcn_sched_barrier(0);                                                                        \
+  } while (0)
+#define END_LOADS_P()                                                                                         \
+  do {                                                                                                        \
+    __builtin_amdgcn_sched_barrier(0);                                                                        \
+    __builtin_amdgcn_s_barrier();                                                                             \
+    __builtin_amdgcn_sched_barrier(0);                                                                        \
+  } while (0)
+
+  // memory operations a boundary epilogue of this wave surely issues after the pre-issued K-tile-1 DMA (a lower
+  // bound: vmcnt(S) must leave only operations younger than that DMA in flight) — its 16 C stores (one 16-B store per
+  // row segment), plus 16 GELU' / pre-activation stores when the epilogue writes them
+  const bool aux_st = e.aux_out && (e.act == ACT_GELU || e.act == ACT_GELU_SAVEGRAD);
+  const int s_ops = 16 + (aux_st ? 16 : 0);
+  bool pre = false;   // this tile's K-tile 1 (A upper half + B) was issued at the previous boundary
+  floatx4 bh[2];      // the tile's bias columns, fetched at the start of its last K-tile
+  // one K-tile of the 8-phase loop; skip: K-tile 0 of a tile whose K-tile 1 was issued at the boundary; last: the
+  // tile's last K-tile (peeled, so that the bias loads it issues have a straight-line path to their first use in the
+  // epilogue — the compiler then waits for them with a count that leaves the later DMA in flight; loaded before the
+  // K loop, or in a rolled iteration, it had no count and waited vmcnt(0), draining the boundary DMA)
+  auto ktile = [&](int t, bool skip, bool last) __attribute__((always_inline)) {
+    const char* as = abuf(t);
+    const char* bs = bbuf(t);
+    if (last) epi_bias(e, B, bn + wc * 64, lane, bh);
+    // phase 1: A0 + B0, stage A upper half of t+1; MFMA quadrant (0,0)
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j) b0[kk][j] = frag256<true>(bs, wc * 64 + j * 16, kk, lane);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) af[kk][i] = frag8p_a<true>(as, wr * 128 + i * 16, kk, lane);
+    }
+    if (!skip) stage_a(t + 1, 1);
+    END_LOADS_P();
+    {
+      constexpr int qn_ = 0;
+      MFMA_QP(0, b0);
+    }
+    // phase 2: B1, stage both B halves of t+1; quadrant (0,1)
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) b1[kk][j] = frag256<true>(bs, wc * 64 + 32 + j * 16, kk, lane);
+    if (!skip) stage_b(t + 1);
+    END_LOADS_P();
+    {
+      constexpr int qn_ = 1;
+      MFMA_QP(0, b1);
+    }
+    // phase 3: A1; quadrant (1,1)
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) af[kk][i] = frag8p_a<true>(as, wr * 128 + 64 + i * 16, kk, lane);
+    END_LOADS_P();
+    {
+      constexpr int qn_ = 1;
+      MFMA_QP(1, b1);
+    }
+    // phase 4: all of t+1 landed (own pieces; after a boundary: everything but the epilogue's memory operations),
+    // then A lower half of t+2; quadrant (1,0)
+    if (skip) {
+      if (s_ops >= 32) asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    } else if (CMHAR_PERSIST_ABL == 1 && t == 1) {   // ablation build: K-tile 2's wait leaves the stores in flight
+      asm volatile("s_waitcnt vmcnt(16)" ::: "memory");   // (wrong data when the stores are not done: timing only)
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (last) {   // the bias loads are older than t+1's DMA: consumed here, the compiler's wait for them is free
+        const floatx4 z = {0.f, 0.f, 0.f, 0.f};
+        bh[0] = e.bias ? bh[0] : z;
+        bh[1] = e.bias ? bh[1] : z;
+        asm volatile("" : "+v"(bh[0]), "+v"(bh[1]));   // pinned here (a pure select would sink into the epilogue)
+      }
+    }
+    stage_a(t + 2, 0);
+    END_LOADS_P();
+    {
+      constexpr int qn_ = 0;
+      MFMA_QP(1, b0);
+    }
+  };
+  auto stamp = [&](int s, int k) {
+#if CMHAR_PERSIST_PROBE
+    const unsigned long long tm = __builtin_amdgcn_s_memtime();
+    if ((wave & 3) == 0 && lane == 0 && blockIdx.x < 256 && s < 12)
+      g_persist_probe[((blockIdx.x * 12 + s) * 2 + wr) * 6 + k] = tm;
+#endif
+  };
+  for (int s = 0;; ++s) {
+    stamp(s, 0);
+    ktile(0, pre, false);
+    stamp(s, 1);
+#pragma unroll 1
+    for (int t = 1; t < nk - 1; ++t) ktile(t, false, false);
+    ktile(nk - 1, false, true);
+    stamp(s, 2);
+    // tile boundary (this wave's MFMAs of the tile are done; every read of the last K-tile's buffers has returned).
+    // The groups re-align first (group 0 waits out group 1's last quadrant), so that both run their epilogues at
+    // once, as the one-tile kernel does: with the ping-pong offset kept, group 1's epilogue interval followed group 0's
+    // and the store phases of the two groups serialised (QKV 190 -> 224 us)
+    __builtin_amdgcn_sched_barrier(0);
+    if (wr == 0) __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    if (nxt) {
+      stage_a(nk + 1, 1);
+      stage_b(nk + 1);
+    }
+    asm volatile("" ::: "memory");   // the epilogue's memory operations stay younger than that DMA (vmcnt(S) below)
+    stamp(s, 3);
+    if (CMHAR_PERSIST_ABL != 2)      // ablation build 2: no epilogue at all
+      epi_direct<OutT, false, true, true>(e, C, ldc, nullptr, 0, bm + wr * 128, bn + wc * 64, lane, acc, bh);
+    else {
+      float sum = 0.f;
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) sum += acc[i][j][0] + acc[i][j][1] + acc[i][j][2] + acc[i][j][3];
+      if (sum == 1234.5f) C[tid] = (OutT)sum;
+    }
+    stamp(s, 4);
+    if (!nxt) break;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+    bm = bm2;
+    bn = bn2;
+    a_cur = a_nxt;
+    b_cur = b_nxt;
+    nxt = tile_of(s + 2, bm2, bn2);
+    a_nxt = (const char*)(A + (long)bm2 * lda);
+    b_nxt = (const char*)(B + (long)bn2 * ldb);
+    pre = true;
+    __builtin_amdgcn_sched_barrier(0);
+    if (wr == 1) __builtin_amdgcn_s_barrier();   // group 1 falls one interval behind again (as in the prologue)
+    __builtin_amdgcn_sched_barrier(0);
+  }
+#undef MFMA_QP
+#undef END_LOADS_P
 }
 
 // Tail split for a whole-K 256² GEMM whose tile count leaves the last round of the chip mostly empty: keep full
@@ -1351,11 +1848,44 @@ static int gemm8p_na(bool ak) {
   return ak ? fwd : wg;
 }
 
+// The persistent 8-phase forward kernel (gemm8p_persist_kernel) for whole-K forward-layout launches whose epilogue
+// streams no 16-bit operand; CMHAR_GEMM8P_PERSIST=0/1 overrides the build default (A/B measurements; identical bits).
+#ifndef CMHAR_GEMM8P_PERSIST_DEFAULT
+#define CMHAR_GEMM8P_PERSIST_DEFAULT 1
+#endif
+static bool use_8p_persist() {
+  static const bool v = [] {
+    const char* s = getenv("CMHAR_GEMM8P_PERSIST");
+    return s ? atoi(s) != 0 : CMHAR_GEMM8P_PERSIST_DEFAULT != 0;
+  }();
+  return v;
+}
+// CUs of the current device (the persistent grid); 0 when it is not a multiple of 8 (the XCD round-robin the tile
+// order relies on), which disables the persistent kernel
+static int persist_grid() {
+  int dev = 0, n = 0;
+  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    return 0;
+  return n % 8 == 0 ? n : 0;
+}
+static bool persist_ok(bool ak, bool bkc, int M, int N, int K, bool stream_epi, bool fast_epi) {
+  // stream_epi: the epilogue reads a [M, N] operand or C itself (residual / aux_in / rowadd / beta) — its loads' waits
+  // would drain the stores in flight; those launches keep gemm8p_kernel
+  if (!(ak && bkc) || stream_epi || !fast_epi || !use_8p_persist() || !CMHAR_EPI_DIRECT) return false;
+  if (K % (2 * TK2) != 0) return false;                       // an even K-tile count
+  // ≥ 3 chip rounds of tiles: at 2.3 rounds (the K = 768 out-projection input gradient, 588 tiles) the persistent
+  // form measured 4 % slower; from QKV's 6.9 rounds (1764 tiles) up it is faster (no relaunch, next K-tiles in flight)
+  static const int g = persist_grid();
+  return g > 0 && (M / TM2) * (N / TN2) >= 3 * g;
+}
+
 // Which kernel(s) a cmhar_gemm_bf16 call launches (also exported for trace labels: cmhar_gemm_bf16_plan).
 enum GemmPlan {
-  PLAN_128 = 0, PLAN_256 = 1, PLAN_256_TAIL = 2, PLAN_256_SPLITK = 3, PLAN_8P = 4, PLAN_128_SPLITK = 5, PLAN_8P_SPLITK = 6
+  PLAN_128 = 0, PLAN_256 = 1, PLAN_256_TAIL = 2, PLAN_256_SPLITK = 3, PLAN_8P = 4, PLAN_128_SPLITK = 5, PLAN_8P_SPLITK = 6,
+  PLAN_8P_PERSIST = 7
 };
-static int gemm_plan(bool ak, bool bkc, int M, int N, int K, int splits, bool has_ws, bool rowsum) {
+static int gemm_plan(bool ak, bool bkc, int M, int N, int K, int splits, bool has_ws, bool rowsum,
+                     bool stream_epi = false, bool fast_epi = true) {
   const bool big = M % TM2 == 0 && N % TN2 == 0 && K % TK2 == 0;
   if (!big) {
     const int klen = splits > 1 ? cdiv(cdiv(K, splits), BK) * BK : K;
@@ -1368,7 +1898,8 @@ static int gemm_plan(bool ak, bool bkc, int M, int N, int K, int splits, bool ha
   if (nsplit > 1) return wgrad8p ? PLAN_8P_SPLITK : PLAN_256_SPLITK;
   if (wgrad8p) return PLAN_8P;
   if (has_ws && !rowsum && tail_split(M, N, K).n_dp > 0) return PLAN_256_TAIL;   // (8-phase instead: FC2 fwd 5 % slower)
-  if (ak && K >= 2 * TK2 && use_8p() && (bkc || use_8p_dgrad())) return PLAN_8P;
+  if (ak && K >= 2 * TK2 && use_8p() && (bkc || use_8p_dgrad()))
+    return persist_ok(ak, bkc, M, N, K, stream_epi, fast_epi) ? PLAN_8P_PERSIST : PLAN_8P;
   return PLAN_256;
 }
 
@@ -1407,10 +1938,11 @@ int launch(int M, int N, int K, const bf16* A, long lda, const bf16* B, long ldb
     if (splits > 1) klen = cdiv(cdiv(K, splits), TK2) * TK2;
     const int nsplit = cdiv(K, klen);
     dim3 grid((M / TM2) * (N / TN2), 1, nsplit);
-    const int plan = gemm_plan(AK, BKc, M, N, K, splits, ws != nullptr, e.rowsum != nullptr);
   // epilogues with a streamed 16-bit operand run the PFS instantiation (the operand loaded two row groups ahead);
   // the others keep the plain store loop (CMHAR_EPI_PF2=0: never)
   const bool pfs = CMHAR_EPI_PF2 && sizeof(OutT) == 2 && epi_has_stream(e);
+    const int plan = gemm_plan(AK, BKc, M, N, K, splits, ws != nullptr, e.rowsum != nullptr, epi_reads(e),
+                               sizeof(OutT) == 2 && epi_fast_ok(e));
     if (plan == PLAN_256_TAIL) {
       const TailSplit ts = tail_split(M, N, K);
       if (ph_gemm && pfs)
@@ -1435,6 +1967,13 @@ int launch(int M, int N, int K, const bf16* A, long lda, const bf16* B, long ldb
         gemm8p_kernel<E, AK, BKc, OutT, false, 3><<<grid, NT2, 0, st>>>(M, N, K, A, lda, B, ldb, C, ldc, e, K, 0, 0, ng);
       else if (ph_gemm)
         gemm8p_kernel<E, AK, BKc, OutT><<<grid, NT2, 0, st>>>(M, N, K, A, lda, B, ldb, C, ldc, e, K, 0, 0, ng);
+    } else if (plan == PLAN_8P_PERSIST) {
+      if constexpr (AK && BKc) {
+        static const int g = persist_grid();
+        if (ph_gemm)
+          gemm8p_persist_kernel<E, OutT><<<g, NT2, 0, st>>>(M, N, K, A, lda, B, ldb, C, ldc, e,
+                                                            gemm8p_groups(AK, BKc, N, K));
+      }
     } else if (plan == PLAN_8P_SPLITK) {
       if (ph_gemm && gemm8p_na(AK) == 3)
         gemm8p_kernel<E, AK, BKc, float, false, 3><<<grid, NT2, 0, st>>>(M, N, K, A, lda, B, ldb, ws, N, e, klen, ss, 1,
@@ -1494,6 +2033,18 @@ extern "C" long cmhar_gemm_bf16_ws(int M, int N, int K) {
 extern "C" int cmhar_gemm_bf16_plan(int layout, int M, int N, int K, int splits, int has_ws, int rowsum) {
   if (layout < 0 || layout > 2) return -1;
   return gemm_plan(layout != 2, layout == 0, M, N, K, splits, has_ws != 0, rowsum != 0);
+}
+#if CMHAR_PERSIST_PROBE
+extern "C" int cmhar_debug_persist_probe(unsigned long long* host, long n) {
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_persist_probe), n * sizeof(unsigned long long), 0,
+                                  hipMemcpyDeviceToHost);
+}
+#endif
+// As cmhar_gemm_bf16_plan for an epilogue that reads an operand (residual, aux_in, rowadd, beta) or not.
+extern "C" int cmhar_gemm_bf16_plan2(int layout, int M, int N, int K, int splits, int has_ws, int rowsum,
+                                     int stream_epi) {
+  if (layout < 0 || layout > 2) return -1;
+  return gemm_plan(layout != 2, layout == 0, M, N, K, splits, has_ws != 0, rowsum != 0, stream_epi != 0);
 }
 
 // cmhar_gemm_bf16 with a phase mask (bit 0 = GEMM kernel, bit 1 = split-K / tail reduce): phases 1 then 2 is the

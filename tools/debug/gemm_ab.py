@@ -22,6 +22,8 @@ from cmhar import kernels as K  # noqa: E402
 def load(path):
     L = C.CDLL(os.path.abspath(path))
     for name, (res, args) in _lib._SIGS.items():
+        if not hasattr(L, name):   # an older build without this entry point
+            continue
         fn = getattr(L, name)
         fn.restype = res
         fn.argtypes = args
