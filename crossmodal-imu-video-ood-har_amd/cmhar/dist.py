@@ -119,12 +119,13 @@ def sink_param_order(backbone) -> List[torch.nn.Parameter]:
 
 
 class _Bucket:
-    __slots__ = ('params', 'kind', 'start', 'end', 'ready', 'launched', 'flat', 'live', 'streams', 'fill')
+    __slots__ = ('params', 'kind', 'start', 'end', 'ready', 'launched', 'flat', 'live', 'streams', 'fill', 'ones')
 
     def __init__(self, params, kind, start=0, end=0, fill=False):
         self.params, self.kind, self.start, self.end = params, kind, start, end
         self.ready, self.launched, self.flat, self.live, self.streams = set(), False, None, None, {}
-        self.fill = fill      # hook bucket: a parameter with no local gradient gets the reduced sum as its .grad
+        self.ones = None      # presence flags of a fully-live hook bucket (see GradReducer._flatten_and_reduce)
+        self.fill = fill      # hook bucket filled in the learning step (the trailing one holds never-used parameters)
 
 
 def _cut(params, limit):
@@ -283,12 +284,17 @@ class GradReducer:
         b.launched = True
 
     def _flatten_and_reduce(self, b):
+        # [gradients | one presence flag per parameter]: the reduced flags count the ranks that produced each
+        # gradient, so that finish() can give a parameter the sum when ANY rank has one and leave it None when none
+        # does — the same decision on every rank (a trailing-bucket parameter used by some ranks only)
         n = sum(p.numel() for p in b.params)
+        k = len(b.params)
         dev = b.params[0].device
-        if b.flat is None or b.flat.numel() != n or b.flat.device != dev:
-            b.flat = torch.empty(n, dtype=torch.float32, device=dev)
-        if len(b.live) == len(b.params):
-            torch.cat([p.grad.reshape(-1).float() for p in b.params], out=b.flat)
+        if b.flat is None or b.flat.numel() != n + k or b.flat.device != dev:
+            b.flat = torch.empty(n + k, dtype=torch.float32, device=dev)
+            b.ones = torch.ones(k, dtype=torch.float32, device=dev)
+        if len(b.live) == k:
+            torch.cat([p.grad.reshape(-1).float() for p in b.params] + [b.ones], out=b.flat)
         else:
             b.flat.zero_()
             off = 0
@@ -296,6 +302,7 @@ class GradReducer:
                 if p.grad is not None:
                     b.flat[off:off + p.numel()].copy_(p.grad.reshape(-1))
                 off += p.numel()
+            b.flat[n:].copy_(torch.tensor([float(p.grad is not None) for p in b.params], dtype=torch.float32))
         self.pending.append(dist.all_reduce(b.flat, group=self.group, async_op=True))
         self.n_collectives += 1
 
@@ -326,15 +333,21 @@ class GradReducer:
         dst, src = [], []
         for b in self.buckets:
             if b.kind == 'hook' and b.launched and b.flat is not None:
+                # a parameter without a local gradient takes the sum when some rank produced one, else stays None;
+                # the ranks' counts are read only for such buckets (one small device -> host read, none in a step
+                # where every hook parameter has its gradient)
+                counts = None
+                if any(p.grad is None for p in b.params):
+                    counts = b.flat[b.flat.numel() - len(b.params):].tolist()
                 off = 0
-                for p in b.params:
+                for i, p in enumerate(b.params):
                     n = p.numel()
                     red = b.flat[off:off + n].view_as(p)
                     if p.grad is not None:
                         dst.append(p.grad)
                         src.append(red)
-                    elif b.fill:           # used in the first step on every rank, no gradient here this step
-                        p.grad = red.clone()
+                    elif counts[i] > 0:    # produced on another rank this step
+                        p.grad = red.to(p.dtype, copy=True)
                     off += n
         if dst:
             torch._foreach_copy_(dst, src)     # the reduced values back into .grad: one multi-tensor launch

@@ -131,7 +131,10 @@ class FusedAdamW(torch.optim.Optimizer):
                 norm_out = _grad_norm(allp, float(self.max_grad_norm), apply_clip=False)
                 self.last_grad_norm = norm_out[0]
                 gscale = norm_out
-                if extra and self.write_clipped_grad:   # as clip_grad_norm_ leaves them (owned: in the AdamW pass)
+                # gradients this optimizer does not own are scaled in place whatever write_clipped_grad says: another
+                # optimizer may step them, and must see them clipped as clip_grad_norm_ leaves them; the
+                # owned ones are clipped inside the AdamW pass (written back only with write_clipped_grad)
+                if extra:
                     torch._foreach_mul_(extra, norm_out[1])
         for gi, group in enumerate(self.param_groups):
             b1, b2 = group['betas']

@@ -1245,7 +1245,7 @@ extern "C" int cmhar_attention_fwd(int dtype, int B, int H, int Lq, int Lk, int 
       attn_fwd_tail_bf16<E><<<dim3(cdiv(Lq - bulk, 32), H, B), 256, 0, st>>>(H, Lq, Lk, bulk, (const bf16*)Q, ldq,   \
                                                                              (const bf16*)K, ldk,                \
                                                            (const bf16*)V, ldv, (E*)O, ldo, lse, scale);        \
-    else if (Lq > bulk)                                                                                          \
+    else if (Lq > bulk && !tail)   /* (folded tail groups: nothing left to launch) */                        \
       attn_fwd_bf16<E, 1><<<dim3(cdiv(Lq - bulk, 128), H, B), 256, 0, st>>>(H, Lq, Lk, bulk, (const bf16*)Q, ldq,   \
                                                                             (const bf16*)K, ldk, (const bf16*)V, ldv, \
                                                                             (E*)O, ldo, lse, scale, 0, 0);       \

@@ -1055,8 +1055,8 @@ __global__ __launch_bounds__(64 * NW, 2) void conv3d_wgrad_rows(Geom g, int Cout
   // operands through buffer resources with 32-bit byte offsets (the plan keeps x and dz within 1 GiB); padding and
   // out-of-range slots load from offset 2^31, past the resource, which reads zeros (as conv3d_fwd_rows3)
   const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)x, (short)0, (int)((long)g.N * g.T * g.H * g.W * g.C * 2), 0x00020000);
-  const __amdgpu_buffer_rsrc_t dzr = __builtin_amdgcn_make_buffer_rsrc((void*)dz, (short)0, (int)((long)M * Cout * 2),
+      (void*)x, (short)0, (int)min((long)g.N * g.T * g.H * g.W * g.C * 2, 0x7fffffffL), 0x00020000);
+  const __amdgpu_buffer_rsrc_t dzr = __builtin_amdgcn_make_buffer_rsrc((void*)dz, (short)0, (int)min((long)M * Cout * 2, 0x7fffffffL),
                                                                         0x00020000);
   uint4_t rdz[DZ_PER], rsl[SL_PER];
   auto load = [&](int c) {
@@ -1183,9 +1183,9 @@ __global__ __launch_bounds__(768, 1) void conv3d_wgrad_rows3(Geom g, int Cout, i
   // operands through buffer resources with 32-bit byte offsets (the plan keeps x and dz within 1 GiB); padding and
   // out-of-range slots load from offset 2^31, past the resource, which reads zeros (as conv3d_fwd_rows3)
   const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)x, (short)0, (int)((long)g.N * g.T * g.H * g.W * g.C * 2), 0x00020000);
+      (void*)x, (short)0, (int)min((long)g.N * g.T * g.H * g.W * g.C * 2, 0x7fffffffL), 0x00020000);
   const __amdgpu_buffer_rsrc_t dzr = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)dz, (short)0, (int)((long)g.N * g.To * g.Ho * g.Wo * Cout * 2), 0x00020000);
+      (void*)dz, (short)0, (int)min((long)g.N * g.To * g.Ho * g.Wo * Cout * 2, 0x7fffffffL), 0x00020000);
   // chunk-invariant slab slots: input row u of the chunk's slab and the byte offset of the slot's 16 B relative to
   // the slab's first input row (-1 in the W padding)
   int su[SL_PER], sb[SL_PER];
@@ -1378,7 +1378,7 @@ __global__ __launch_bounds__(256, 2) void conv3d_fwd_rows(Geom g, int M, int Cou
   // operands through buffer resources with 32-bit byte offsets (the plan keeps x within 1 GiB); padding slots load
   // from offset 2^31, past the resource, which reads zeros (as conv3d_fwd_rows3)
   const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)x, (short)0, (int)((long)g.N * g.T * g.H * g.W * g.C * 2), 0x00020000);
+      (void*)x, (short)0, (int)min((long)g.N * g.T * g.H * g.W * g.C * 2, 0x7fffffffL), 0x00020000);
   const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc((void*)Wt, (short)0, 0x7fffffff, 0x00020000);
   int wb[W_PER];   // this thread's weight pieces: byte offset of row bn + co, tap iw, channel chunk
 #pragma unroll
@@ -1578,7 +1578,7 @@ __global__ __launch_bounds__(256, 2) void conv3d_fwd_rows3(Geom g, int Cout, int
   // Operands through buffer resources with 32-bit byte offsets (the plan keeps x within 1 GiB): an offset past the
   // resource's range reads zeros, so the zero padding needs no select on the loaded value (a select right after a
   // prefetched load makes the compiler wait for it there) and no 64-bit address arithmetic per load.
-  const unsigned xbytes = (unsigned)((long)g.N * g.T * g.H * g.W * g.C * 2);
+  const unsigned xbytes = (unsigned)min((long)g.N * g.T * g.H * g.W * g.C * 2, 0x7fffffffL);
   const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)x, (short)0, (int)xbytes, 0x00020000);
   const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc((void*)Wt, (short)0, 0x7fffffff, 0x00020000);
   // block-invariant slab slots: byte offset of the slot's 16 B in frame ti = 0 of clip n (input row ho0 − ph + u,

@@ -345,6 +345,62 @@ def test_grad_reducer_partial_use_after_learning():
     _spawn(_partial_use_worker)
 
 
+def _presence_worker(rank, world, port):
+    """None gradients decided the same on every rank from the reduced presence counts.  Step 1 (after
+    the learning step): NO rank uses the video tower — its parameters (a filled hook bucket) keep .grad None instead
+    of an all-zero gradient that AdamW would decay.  Step 2: only rank 1 uses `unused.temperature` (a parameter of the
+    trailing bucket, never used in the learning step) — every rank ends with rank 1's gradient, so all replicas step
+    it; `unused.bias` stays None everywhere."""
+    _init(rank, world, port)
+    from cmhar.dist import GradReducer, broadcast_parameters
+    torch.manual_seed(101)
+    model = _TwoTowerUnused().train()
+    broadcast_parameters(model)
+    reducer = GradReducer(model, backbone=None, bucket_mb=60 * 4 / (1 << 20))
+    X, Y = _data(world)
+    bl = X.shape[0] // world
+
+    def local_loss(m, r, step):
+        a, b = m(X[r * bl:(r + 1) * bl], Y[r * bl:(r + 1) * bl])
+        loss = (a * (r + 1)).sum()
+        if step != 1:
+            loss = loss + (b * b).sum()
+        if step == 2 and r == 1:
+            loss = loss + 3.0 * m.unused.temperature
+        return loss
+
+    for step in range(3):
+        model.zero_grad(set_to_none=True)
+        start = {k: v.clone() for k, v in model.state_dict().items()}
+        reducer.start_step()
+        local_loss(model, rank, step).backward()
+        reducer.finish()
+        want = {}
+        for r in range(world):
+            ref = _TwoTowerUnused().train()
+            ref.load_state_dict(start)
+            local_loss(ref, r, step).backward()
+            for n, q in ref.named_parameters():
+                if q.grad is not None:
+                    want[n] = want[n] + q.grad if n in want else q.grad.clone()
+        for n, p in model.named_parameters():
+            if n not in want:
+                assert p.grad is None, (step, n)
+            else:
+                assert p.grad is not None, (step, n)
+                assert p.grad.dtype == p.dtype
+                torch.testing.assert_close(p.grad, want[n], rtol=1e-5, atol=1e-6, msg=f'{step} {n}')
+        if step == 1:
+            assert all(p.grad is None for p in model.video.parameters())
+        if step == 2:
+            assert model.unused.temperature.grad is not None and model.unused.bias.grad is None
+    dist.destroy_process_group()
+
+
+def test_grad_reducer_presence_counts():
+    _spawn(_presence_worker)
+
+
 # ---------------------------------------------------------------------------------------------------------------
 # 8 ranks (the reference's DataParallel over every GPU of an 8-GPU node, main.py:89-93; BASELINE config 3): the
 # protocol rehearsed at the rank count the scaling bench uses, gloo on CPU (VERDICT r04 item 6)
@@ -423,3 +479,69 @@ def _real_layout_worker(rank, world, port):
 
 def test_grad_reducer_real_layout_8_ranks():
     _spawn(_real_layout_worker, world=8)
+
+
+# ---------------------------------------------------------------------------------------------------------------
+# BASELINE config 4 (cross-attention fusion classifier, global batch 64 = 8 ranks x 8 clips, CE loss) at its rank count
+class _FusionHead(nn.Module):
+    """CrossAttentionFusion + classifier parameters under cmhar/fusion.py's state_dict names, computed by the CPU
+    restatement (oracle/fusion_cpu.fusion_forward) — the HIP module cannot run in a CPU process."""
+
+    def __init__(self, imu_dim=128, video_dim=768, d=256, classes=32):
+        super().__init__()
+        self.q_proj = nn.Linear(imu_dim, d)
+        self.kv_proj = nn.Linear(video_dim, 2 * d)
+        self.res_proj = nn.Linear(imu_dim, d)
+        self.out_proj = nn.Linear(d, d)
+        self.norm = nn.LayerNorm(d)
+        self.classifier = nn.Linear(d, classes)
+
+    def forward(self, imu_tokens, video_tokens):
+        from oracle.fusion_cpu import fusion_forward
+        return fusion_forward(dict(self.named_parameters()), imu_tokens, video_tokens, num_heads=4)[0]
+
+
+def _fusion_dp_worker(rank, world, port):
+    """Config 4's data parallelism (reference main.py:89-93, DataParallel over every GPU): each rank runs the fusion
+    classifier on its 8 clips (26 IMU tokens x 784 video tokens each), scales its local mean CE by B_local / B_global
+    (ClassificationTrainer._global_share: one SUM all-reduce of the local counts) and the GradReducer SUMs the
+    gradients.  Checked against ONE process on the 64-clip concatenation (oracle/fusion_cpu as the model): the ranks'
+    loss shares sum to the global-batch mean CE and every reduced gradient equals its gradient; two steps (the second
+    on the learned hook order)."""
+    _init(rank, world, port)
+    from cmhar.dist import GradReducer, all_reduce_sum_, broadcast_parameters
+    torch.manual_seed(200 + rank)               # different init per rank: broadcast must fix it
+    model = _FusionHead()
+    broadcast_parameters(model)
+    reducer = GradReducer(model, backbone=None)
+    bl, Lq, Lk = 8, 26, 784
+    g = torch.Generator().manual_seed(5)
+    imu = torch.randn(world * bl, Lq, 128, generator=g)
+    video = 0.5 * torch.randn(world * bl, Lk, 768, generator=g)
+    labels = torch.randint(0, 32, (world * bl,), generator=g)
+    sl = slice(rank * bl, (rank + 1) * bl)
+    for step in range(2):
+        model.zero_grad(set_to_none=True)
+        loss = F.cross_entropy(model(imu[sl], video[sl]), labels[sl])
+        n = all_reduce_sum_(torch.full((1,), float(bl)))
+        loss = loss * (bl / n)
+        reducer.start_step()
+        loss.backward()
+        reducer.finish()
+        total = all_reduce_sum_(loss.detach().clone())
+        ref = _FusionHead()
+        ref.load_state_dict(model.state_dict())
+        rloss = F.cross_entropy(ref(imu, video), labels)
+        rloss.backward()
+        assert abs(total.item() - rloss.item()) <= 1e-5 * abs(rloss.item()), (step, total.item(), rloss.item())
+        for (name, p), (_, q) in zip(model.named_parameters(), ref.named_parameters()):
+            torch.testing.assert_close(p.grad, q.grad, rtol=1e-4, atol=1e-6, msg=f'{step} {name}')
+    if step == 1:
+        assert reducer.learned
+    dist.destroy_process_group()
+
+
+def test_fusion_classifier_dataparallel_8_ranks():
+    """config 4's global-mean CE over 8 shards = the single-process loss on the 64-clip
+    concatenation, summed gradients = its gradient."""
+    _spawn(_fusion_dp_worker, world=8)
