@@ -461,8 +461,13 @@ __device__ __forceinline__ void epi_direct(const Epilogue& e, OutT* __restrict__
           o[k] = __builtin_bit_cast(int, __builtin_convertvector(x[k], o2));
           if (gp) a[k] = __builtin_bit_cast(int, __builtin_convertvector(t[k], o2));
         }
-        if (gp) __builtin_nontemporal_store(a, (i4*)adst);
-        __builtin_nontemporal_store(o, (i4*)dst);
+        if (CMHAR_NT_STORE) {
+          if (gp) __builtin_nontemporal_store(a, (i4*)adst);
+          __builtin_nontemporal_store(o, (i4*)dst);
+        } else {
+          if (gp) *(i4*)adst = a;
+          *(i4*)dst = o;
+        }
       };
 #pragma unroll 1
       for (int i = 0; i < 8; ++i) {
@@ -1513,6 +1518,103 @@ __global__ __launch_bounds__(NT2, 2) void gemm8p_kernel(int M, int N, int K, con
   }
 }
 
+// Epilogue of the persistent kernel (its launches: 16-bit output, bias already in the accumulators — the tile's
+// MFMAs start from it —, key-column scale, GELU pair).  Lane l holds row (i*16 + (l&15)) and columns j*16 + 4(l>>4) + r
+// (swapped MFMA operands); one v_permlane16_swap per register pairs blocks (2p, 2p+1) so that a lane holds 8
+// consecutive columns 32p + {0,16,8,24}[l>>4] of its row, stored as one 16-B store (16 rows x 64 B per instruction).
+// The s_memtime timeline (tools/debug/persist_probe.py) had the generic direct epilogue at 9.3 k / 12.2 k cycles per
+// QKV tile for the two wave groups with ~84 VALU per 16 values (a wave64 VALU instruction holds its SIMD 4 cycles);
+// here: 8 swaps, the scale, 8 converts and the address per 16 values, unrolled (the plain form), or one rolled
+// iteration per row block with the accumulators picked by a switch (the GELU pair, whose math dominates).
+__device__ __forceinline__ void swap_rows(const floatx4 (&a)[4], int p, float (&v)[8]) {
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const auto s = __builtin_amdgcn_permlane16_swap(__float_as_uint(a[2 * p][r]), __float_as_uint(a[2 * p + 1][r]),
+                                                    false, false);
+    v[r] = __uint_as_float(s[0]);
+    v[4 + r] = __uint_as_float(s[1]);
+  }
+}
+template <typename OutT>
+__device__ __forceinline__ void epi_persist(const Epilogue& e, OutT* __restrict__ C, long ldc, int m0, int n0,
+                                            int lane, const floatx4 (&acc)[8][4]) {
+  typedef __attribute__((ext_vector_type(2))) float f2;
+  typedef OutT __attribute__((ext_vector_type(2))) o2;
+  typedef int __attribute__((ext_vector_type(4))) i4;
+  const int g = lane >> 4, li = lane & 15;
+  const int cofs = ((g & 1) << 4) | ((g >> 1) << 3);
+  const bool gp = e.act == ACT_GELU_SAVEGRAD && e.aux_out;
+  const bool any_cs = e.colscale_hi > e.colscale_lo;
+  f2 s2[2];
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {
+    const int col = n0 + 32 * p + cofs;   // a multiple-of-8 scale range: whole 8-column groups
+    const float sc = col >= e.colscale_lo && col < e.colscale_hi ? e.colscale : 1.f;
+    s2[p] = f2{sc, sc};
+  }
+  OutT* const c0 = C + (long)(m0 + li) * ldc + n0 + cofs;
+  auto put = [&](const i4& v, OutT* dst) __attribute__((always_inline)) {
+    if (CMHAR_NT_STORE) __builtin_nontemporal_store(v, (i4*)dst);
+    else *(i4*)dst = v;
+  };
+  if (!gp) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int p = 0; p < 2; ++p) {
+        float v[8];
+        swap_rows(acc[i], p, v);
+        i4 o;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          f2 x = {v[2 * k], v[2 * k + 1]};
+          if (any_cs) x = x * s2[p];
+          o[k] = __builtin_bit_cast(int, __builtin_convertvector(x, o2));
+        }
+        put(o, c0 + (long)i * 16 * ldc + 32 * p);
+      }
+    return;
+  }
+  OutT* const a0 = (OutT*)e.aux_out + (long)(m0 + li) * e.ldo + n0 + cofs;
+#pragma unroll 1
+  for (int i = 0; i < 8; ++i) {
+    float v[2][8];
+    switch (i) {
+#define CMHAR_PICK(I) case I: swap_rows(acc[I], 0, v[0]); swap_rows(acc[I], 1, v[1]); break;
+      CMHAR_PICK(0) CMHAR_PICK(1) CMHAR_PICK(2) CMHAR_PICK(3) CMHAR_PICK(4) CMHAR_PICK(5) CMHAR_PICK(6)
+      default: swap_rows(acc[7], 0, v[0]); swap_rows(acc[7], 1, v[1]); break;
+#undef CMHAR_PICK
+    }
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      i4 o, a;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        f2 x = {v[p][2 * k], v[p][2 * k + 1]}, t;
+        if (any_cs) x = x * s2[p];
+        gelu_pair16x2(x, x, t);
+        o[k] = __builtin_bit_cast(int, __builtin_convertvector(x, o2));
+        a[k] = __builtin_bit_cast(int, __builtin_convertvector(t, o2));
+      }
+      put(a, a0 + (long)i * 16 * e.ldo + 32 * p);
+      put(o, c0 + (long)i * 16 * ldc + 32 * p);
+    }
+  }
+}
+// The bias columns of a lane in the swapped accumulator layout (block j: columns n0 + j*16 + 4(l>>4) .. +3) — the
+// persistent kernel starts each tile's accumulators from them (zeros without a bias) — read from the workgroup's LDS
+// copy of the bias vector: a global load there left a pending load across the epilogue, whose wait the compiler could
+// not count past the stores (it waited vmcnt(0..3) at the next tile's first MFMAs, draining the epilogue's stores)
+constexpr int kPersistBiasMax = 4096;   // bias floats an LDS copy holds (N of a persistent launch, host-checked)
+__device__ __forceinline__ void bias_init(const Epilogue& e, const float* lds_bias, int n0, int lane, floatx4 (&b)[4]) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) b[j] = floatx4{0.f, 0.f, 0.f, 0.f};
+  if (e.bias) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) b[j] = *(const floatx4*)(lds_bias + n0 + j * 16 + 4 * (lane >> 4));
+  }
+}
+
 // ---------------------------------------------------------------------------------------------------------------
 // Persistent 8-phase forward-layout kernel (CMHAR_GEMM8P_PERSIST; whole K, no streamed epilogue operand): one
 // workgroup per CU walks tiles v = blockIdx.x + G·s (G = the CU count, a multiple of 8, so that iteration s of every
@@ -1532,12 +1634,15 @@ __global__ __launch_bounds__(NT2, 2) void gemm8p_persist_kernel(int M, int N, in
                                                                 long lda, const bf16* __restrict__ B, long ldb,
                                                                 OutT* __restrict__ C, long ldc, Epilogue e,
                                                                 int ngroup) {
-  __shared__ __attribute__((aligned(16))) char smem[131072];
+  __shared__ __attribute__((aligned(16))) char smem[131072 + kPersistBiasMax * 4];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = wave >> 2, wc = wave & 3;
   const int tiles_n = N / TN2, tiles_m = M / TM2, ntile = tiles_m * tiles_n;
   const int nk = K / TK2;   // even, >= 2 (host-checked)
+  float* const lds_bias = (float*)(smem + 131072);   // N <= kPersistBiasMax (host-checked)
+  if (e.bias)
+    for (int c = tid * 4; c < N; c += NT2 * 4) *(floatx4*)(lds_bias + c) = *(const floatx4*)(e.bias + c);
   const int G = gridDim.x;
   // tile origin (rows bm, columns bn) of iteration s, as gemm8p_kernel maps block id v
   auto tile_of = [&](int s, int& bm, int& bn) -> bool {
@@ -1584,11 +1689,15 @@ __global__ __launch_bounds__(NT2, 2) void gemm8p_persist_kernel(int M, int N, in
     }
   };
 
-  floatx4 acc[8][4];
+  // accumulators start from the bias (the epilogue then adds none): out = bias + Σ_k a·b, summed in that order —
+  // exact on integer data, within fp32 rounding of (Σ_k a·b) + bias otherwise
+  floatx4 acc[8][4], binit[4];
+  __syncthreads();   // the LDS bias copy
+  bias_init(e, lds_bias, bn + wc * 64, lane, binit);
 #pragma unroll
   for (int i = 0; i < 8; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < 4; ++j) acc[i][j] = binit[j];
   bf16x8 af[2][4], b0[2][2], b1[2][2];
 
   if (CMHAR_PERSIST_STAGGER > 0) {   // A/B knob: start-time stagger (quarters of the CUs of each XCD)
@@ -1632,15 +1741,10 @@ __global__ __launch_bounds__(NT2, 2) void gemm8p_persist_kernel(int M, int N, in
   const bool aux_st = e.aux_out && (e.act == ACT_GELU || e.act == ACT_GELU_SAVEGRAD);
   const int s_ops = 16 + (aux_st ? 16 : 0);
   bool pre = false;   // this tile's K-tile 1 (A upper half + B) was issued at the previous boundary
-  floatx4 bh[2];      // the tile's bias columns, fetched at the start of its last K-tile
-  // one K-tile of the 8-phase loop; skip: K-tile 0 of a tile whose K-tile 1 was issued at the boundary; last: the
-  // tile's last K-tile (peeled, so that the bias loads it issues have a straight-line path to their first use in the
-  // epilogue — the compiler then waits for them with a count that leaves the later DMA in flight; loaded before the
-  // K loop, or in a rolled iteration, it had no count and waited vmcnt(0), draining the boundary DMA)
-  auto ktile = [&](int t, bool skip, bool last) __attribute__((always_inline)) {
+  // one K-tile of the 8-phase loop; skip: K-tile 0 of a tile whose K-tile 1 was issued at the boundary
+  auto ktile = [&](int t, bool skip) __attribute__((always_inline)) {
     const char* as = abuf(t);
     const char* bs = bbuf(t);
-    if (last) epi_bias(e, B, bn + wc * 64, lane, bh);
     // phase 1: A0 + B0, stage A upper half of t+1; MFMA quadrant (0,0)
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
@@ -1685,12 +1789,6 @@ __global__ __launch_bounds__(NT2, 2) void gemm8p_persist_kernel(int M, int N, in
       asm volatile("s_waitcnt vmcnt(16)" ::: "memory");   // (wrong data when the stores are not done: timing only)
     } else {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      if (last) {   // the bias loads are older than t+1's DMA: consumed here, the compiler's wait for them is free
-        const floatx4 z = {0.f, 0.f, 0.f, 0.f};
-        bh[0] = e.bias ? bh[0] : z;
-        bh[1] = e.bias ? bh[1] : z;
-        asm volatile("" : "+v"(bh[0]), "+v"(bh[1]));   // pinned here (a pure select would sink into the epilogue)
-      }
     }
     stage_a(t + 2, 0);
     END_LOADS_P();
@@ -1708,11 +1806,10 @@ __global__ __launch_bounds__(NT2, 2) void gemm8p_persist_kernel(int M, int N, in
   };
   for (int s = 0;; ++s) {
     stamp(s, 0);
-    ktile(0, pre, false);
+    ktile(0, pre);
     stamp(s, 1);
 #pragma unroll 1
-    for (int t = 1; t < nk - 1; ++t) ktile(t, false, false);
-    ktile(nk - 1, false, true);
+    for (int t = 1; t < nk; ++t) ktile(t, false);
     stamp(s, 2);
     // tile boundary (this wave's MFMAs of the tile are done; every read of the last K-tile's buffers has returned).
     // The groups re-align first (group 0 waits out group 1's last quadrant), so that both run their epilogues at
@@ -1721,6 +1818,8 @@ __global__ __launch_bounds__(NT2, 2) void gemm8p_persist_kernel(int M, int N, in
     __builtin_amdgcn_sched_barrier(0);
     if (wr == 0) __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
+    // the next tile's bias columns (LDS)
+    if (nxt) bias_init(e, lds_bias, bn2 + wc * 64, lane, binit);
     if (nxt) {
       stage_a(nk + 1, 1);
       stage_b(nk + 1);
@@ -1728,7 +1827,7 @@ __global__ __launch_bounds__(NT2, 2) void gemm8p_persist_kernel(int M, int N, in
     asm volatile("" ::: "memory");   // the epilogue's memory operations stay younger than that DMA (vmcnt(S) below)
     stamp(s, 3);
     if (CMHAR_PERSIST_ABL != 2)      // ablation build 2: no epilogue at all
-      epi_direct<OutT, false, true, true>(e, C, ldc, nullptr, 0, bm + wr * 128, bn + wc * 64, lane, acc, bh);
+      epi_persist<OutT>(e, C, ldc, bm + wr * 128, bn + wc * 64, lane, acc);
     else {
       float sum = 0.f;
 #pragma unroll
@@ -1742,7 +1841,7 @@ __global__ __launch_bounds__(NT2, 2) void gemm8p_persist_kernel(int M, int N, in
 #pragma unroll
     for (int i = 0; i < 8; ++i)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+      for (int j = 0; j < 4; ++j) acc[i][j] = binit[j];
     bm = bm2;
     bn = bn2;
     a_cur = a_nxt;
@@ -1848,6 +1947,10 @@ static int gemm8p_na(bool ak) {
   return ak ? fwd : wg;
 }
 
+// chip rounds of 256² tiles from which a launch takes the persistent kernel (debug builds lower it)
+#ifndef CMHAR_PERSIST_MIN_ROUNDS
+#define CMHAR_PERSIST_MIN_ROUNDS 3
+#endif
 // The persistent 8-phase forward kernel (gemm8p_persist_kernel) for whole-K forward-layout launches whose epilogue
 // streams no 16-bit operand; CMHAR_GEMM8P_PERSIST=0/1 overrides the build default (A/B measurements; identical bits).
 #ifndef CMHAR_GEMM8P_PERSIST_DEFAULT
@@ -1872,11 +1975,12 @@ static bool persist_ok(bool ak, bool bkc, int M, int N, int K, bool stream_epi, 
   // stream_epi: the epilogue reads a [M, N] operand or C itself (residual / aux_in / rowadd / beta) — its loads' waits
   // would drain the stores in flight; those launches keep gemm8p_kernel
   if (!(ak && bkc) || stream_epi || !fast_epi || !use_8p_persist() || !CMHAR_EPI_DIRECT) return false;
+  if (N > kPersistBiasMax || N % 4) return false;             // the LDS copy of the bias
   if (K % (2 * TK2) != 0) return false;                       // an even K-tile count
   // ≥ 3 chip rounds of tiles: at 2.3 rounds (the K = 768 out-projection input gradient, 588 tiles) the persistent
   // form measured 4 % slower; from QKV's 6.9 rounds (1764 tiles) up it is faster (no relaunch, next K-tiles in flight)
   static const int g = persist_grid();
-  return g > 0 && (M / TM2) * (N / TN2) >= 3 * g;
+  return g > 0 && (M / TM2) * (N / TN2) >= CMHAR_PERSIST_MIN_ROUNDS * g;
 }
 
 // Which kernel(s) a cmhar_gemm_bf16 call launches (also exported for trace labels: cmhar_gemm_bf16_plan).
@@ -1968,7 +2072,7 @@ int launch(int M, int N, int K, const bf16* A, long lda, const bf16* B, long ldb
       else if (ph_gemm)
         gemm8p_kernel<E, AK, BKc, OutT><<<grid, NT2, 0, st>>>(M, N, K, A, lda, B, ldb, C, ldc, e, K, 0, 0, ng);
     } else if (plan == PLAN_8P_PERSIST) {
-      if constexpr (AK && BKc) {
+      if constexpr (AK && BKc && sizeof(OutT) == 2) {   // (the plan requires a 16-bit output)
         static const int g = persist_grid();
         if (ph_gemm)
           gemm8p_persist_kernel<E, OutT><<<g, NT2, 0, st>>>(M, N, K, A, lda, B, ldb, C, ldc, e,
