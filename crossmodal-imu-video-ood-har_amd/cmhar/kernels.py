@@ -57,9 +57,8 @@ _PLAN = {}
 
 def _gemm_trace_name(layout, M, N, K, s, has_ws, rowsum, out_dtype, reads=False):
     """Trace label of a bf16 GEMM call: the GEMM kernel (template name as rocprofv3 lists it, without the trailing
-    integer parameters) that the library's own plan (cmhar_gemm_bf16_plan2; reads: the epilogue reads a residual /
-    aux_in / rowadd operand or accumulates into C) launches; a split-K / tail reduce that follows it is launched
-    outside the traced interval."""
+    integer parameters) that the library's own plan (cmhar_gemm_bf16_plan2; reads: an epilogue the persistent forward
+    kernel does not take) launches; a split-K / tail reduce that follows it is launched outside the traced interval."""
     key = (layout, M, N, K, s, has_ws, rowsum)
     plan = L.lib().cmhar_gemm_bf16_plan2(layout, M, N, K, s, int(has_ws), int(rowsum), int(reads))
     _PLAN[key] = plan
@@ -252,8 +251,12 @@ def gemm(layout: int, a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, *, bi
                 ws = workspace(n, out.device)
         ev = name = None
         if TRACE.active:
-            reads = residual is not None or aux_in is not None or rowadd is not None or beta != 0.0
-            name = _gemm_trace_name(layout, M, N, K, s, ws is not None, rowsum is not None, out.dtype, reads)
+            # an epilogue the persistent forward kernel does not take (the library's epi_persist_ok)
+            pok = (alpha == 1.0 and pdrop <= 0.0 and rowadd is None and beta == 0.0 and
+                   ((act == L.ACT_NONE and aux_in is None) or
+                    (act == L.ACT_GELU_SAVEGRAD and aux_out is not None and residual is None and aux_in is None) or
+                    (act == L.ACT_MULAUX and aux_in is not None and residual is None)))
+            name = _gemm_trace_name(layout, M, N, K, s, ws is not None, rowsum is not None, out.dtype, not pok)
             ev = TRACE.begin(name)
         if ev is None and reduce_stream is not None and s > 1:
             args = (layout, L.dtype_code(out.dtype), M, N, K, ptr(a), a.stride(0), ptr(b), b.stride(0), ptr(out),

@@ -159,7 +159,7 @@ __device__ __forceinline__ void stage128(const TileDma& t, int r0, char* lds, in
 // NBUF = 2: double-buffered 128-row stages (64 KB, the stand-alone tail kernels).  NBUF = 1: one 32 KB stage buffer
 // (+1 KB), so a tail group fits the LDS of the bulk kernel's workgroup and runs INSIDE that launch — dispatched
 // first, its waves latency-bound beside the bulk waves on the same CUs instead of a launch of its own with the chip
-// mostly idle (attn_bwd_dkdv_bf16 `ntail`; attn_fwd_bf16 has the same hook, off by default: CMHAR_ATTN_FOLD_FWD).
+// mostly idle (attn_bwd_dkdv_bf16 `ntail`; attn_fwd_bf16 the same: CMHAR_ATTN_FOLD_FWD).
 // Same arithmetic and merge order either way; the two compiled forms may still contract a multiply-add differently
 // (the folded forward's tail rows measured within 1 bf16 ulp of the stand-alone kernel's, dK/dV identical).
 // ---------------------------------------------------------------------------------------------------------------
@@ -1193,14 +1193,14 @@ __global__ __launch_bounds__(64) void attn_bwd_dkdv_f32(int H, int Lq, int Lk, c
 #endif
 // 1: the tail groups run inside the bulk launch (first dispatched; see fwd_tail_group); 0: a tail launch of their own
 // after the bulk.  Measured in one process at B = 32, H = 12, L = 1568 (tools/debug/attn_ab.py, µs per layer, two
-// sessions): dK/dV folded 892.8 / 888.1 → 883.6 / 882.3 (backward), kept; the forward folded 317.9 / 315.9 → 339.6 /
-// 339.0 — its bulk grid is exactly three chip rounds of workgroups (2304 = 3 × 768), so the tail groups' slot time
-// adds a partial fourth round instead of filling idle slots — off (A/B knobs)
+// sessions): dK/dV folded 892.8 / 888.1 → 883.6 / 882.3 (backward), kept; the forward folded 339.8 → 323.5
+// (round 6, after the round-5 A/B was found to launch the QB=1 kernel over the folded rows a second time), output
+// bit-identical to the stand-alone tail kernel (tools/debug/attn_rowdiff.py) — kept (A/B knobs)
 #ifndef CMHAR_ATTN_FOLD
 #define CMHAR_ATTN_FOLD 1
 #endif
 #ifndef CMHAR_ATTN_FOLD_FWD
-#define CMHAR_ATTN_FOLD_FWD 0
+#define CMHAR_ATTN_FOLD_FWD 1
 #endif
 
 // f32-MFMA flash kernels (csrc/attention_f32.hip) for fp32 storage, D = 64, no dropout

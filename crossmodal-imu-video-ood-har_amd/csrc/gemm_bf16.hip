@@ -393,6 +393,16 @@ __host__ __device__ inline bool epi_fast_ok(const Epilogue& e) {
   return e.alpha == 1.f && e.pdrop <= 0.f && !e.residual && !e.aux_in && !e.rowadd && e.beta == 0.f &&
          (e.act == ACT_NONE || (e.act == ACT_GELU_SAVEGRAD && e.aux_out));
 }
+// The epilogues the persistent kernel takes (epi_persist): alpha 1, no dropout / rowadd / beta; either nothing else,
+// the GELU pair with its GELU' output, the product with a 16-bit aux_in (ACT_MULAUX: FC2's input gradient × GELU'), or
+// a 16-bit residual
+__host__ __device__ inline bool epi_persist_ok(const Epilogue& e) {
+  if (e.alpha != 1.f || e.pdrop > 0.f || e.rowadd || e.beta != 0.f) return false;
+  if (e.act == ACT_NONE) return !e.aux_in;
+  if (e.act == ACT_GELU_SAVEGRAD) return e.aux_out && !e.residual && !e.aux_in;
+  if (e.act == ACT_MULAUX) return e.aux_in && !e.residual;
+  return false;
+}
 // This lane's 8 bias columns (zeros without a bias): an unconditional load (a dummy valid address without one), so
 // that no load is left pending on a path the compiler cannot rule out — a loop-carried pending load of a persistent
 // kernel's epilogue made hipcc wait vmcnt before the next tile's first MFMAs (WAW on the load's registers).
@@ -1541,7 +1551,11 @@ __device__ __forceinline__ void epi_persist(const Epilogue& e, OutT* __restrict_
   typedef __attribute__((ext_vector_type(2))) float f2;
   typedef OutT __attribute__((ext_vector_type(2))) o2;
   typedef int __attribute__((ext_vector_type(4))) i4;
-  const int g = lane >> 4, li = lane & 15;
+  // (the lane made opaque per tile: hoisted out of the tile loop, its 64-bit row/column bases were spilled — and the
+  // scratch reload's vmcnt(0) drained the next tile's pre-issued DMA)
+  int lz = lane;
+  asm volatile("" : "+v"(lz));
+  const int g = lz >> 4, li = lz & 15;
   const int cofs = ((g & 1) << 4) | ((g >> 1) << 3);
   const bool gp = e.act == ACT_GELU_SAVEGRAD && e.aux_out;
   const bool any_cs = e.colscale_hi > e.colscale_lo;
@@ -1558,6 +1572,21 @@ __device__ __forceinline__ void epi_persist(const Epilogue& e, OutT* __restrict_
     else *(i4*)dst = v;
   };
   if (!gp) {
+    // streamed operand (16-bit, this lane's 8 columns per segment): every segment's 16 B loaded up front — issued
+    // after the boundary DMA, so each one's wait (counted by the compiler) leaves the stores of the earlier
+    // segments in flight
+    const bool mul = e.act == ACT_MULAUX;
+    const OutT* const sp = mul ? (const OutT*)e.aux_in : (const OutT*)e.residual;
+    const long sld = mul ? e.lda : e.ldr;
+    i4 sv[16];
+    if (sp) {
+      const OutT* const s0 = sp + (long)(m0 + li) * sld + n0 + cofs;
+#pragma unroll
+      for (int c = 0; c < 16; ++c) {   // (16-B aligned: the host checks 8-element leading dimensions)
+        const i4* q = (const i4*)__builtin_assume_aligned(s0 + (long)(c >> 1) * 16 * sld + 32 * (c & 1), 16);
+        sv[c] = __builtin_nontemporal_load(q);
+      }
+    }
 #pragma unroll
     for (int i = 0; i < 8; ++i)
 #pragma unroll
@@ -1569,6 +1598,12 @@ __device__ __forceinline__ void epi_persist(const Epilogue& e, OutT* __restrict_
         for (int k = 0; k < 4; ++k) {
           f2 x = {v[2 * k], v[2 * k + 1]};
           if (any_cs) x = x * s2[p];
+          if (sp) {
+            // (element copied out first: a bit_cast straight off an ext-vector subscript reads element 0)
+            const int w = sv[2 * i + p][k];
+            const f2 t = __builtin_convertvector(__builtin_bit_cast(o2, w), f2);
+            x = mul ? x * t : x + t;
+          }
           o[k] = __builtin_bit_cast(int, __builtin_convertvector(x, o2));
         }
         put(o, c0 + (long)i * 16 * ldc + 32 * p);
@@ -1971,10 +2006,9 @@ static int persist_grid() {
     return 0;
   return n % 8 == 0 ? n : 0;
 }
-static bool persist_ok(bool ak, bool bkc, int M, int N, int K, bool stream_epi, bool fast_epi) {
-  // stream_epi: the epilogue reads a [M, N] operand or C itself (residual / aux_in / rowadd / beta) — its loads' waits
-  // would drain the stores in flight; those launches keep gemm8p_kernel
-  if (!(ak && bkc) || stream_epi || !fast_epi || !use_8p_persist() || !CMHAR_EPI_DIRECT) return false;
+static bool persist_ok(bool ak, bool bkc, int M, int N, int K, bool pepi) {
+  // pepi: a 16-bit output and an epilogue epi_persist handles (epi_persist_ok)
+  if (!(ak && bkc) || !pepi || !use_8p_persist() || !CMHAR_EPI_DIRECT) return false;
   if (N > kPersistBiasMax || N % 4) return false;             // the LDS copy of the bias
   if (K % (2 * TK2) != 0) return false;                       // an even K-tile count
   // ≥ 3 chip rounds of tiles: at 2.3 rounds (the K = 768 out-projection input gradient, 588 tiles) the persistent
@@ -1989,7 +2023,7 @@ enum GemmPlan {
   PLAN_8P_PERSIST = 7
 };
 static int gemm_plan(bool ak, bool bkc, int M, int N, int K, int splits, bool has_ws, bool rowsum,
-                     bool stream_epi = false, bool fast_epi = true) {
+                     bool pepi = true) {
   const bool big = M % TM2 == 0 && N % TN2 == 0 && K % TK2 == 0;
   if (!big) {
     const int klen = splits > 1 ? cdiv(cdiv(K, splits), BK) * BK : K;
@@ -2003,7 +2037,7 @@ static int gemm_plan(bool ak, bool bkc, int M, int N, int K, int splits, bool ha
   if (wgrad8p) return PLAN_8P;
   if (has_ws && !rowsum && tail_split(M, N, K).n_dp > 0) return PLAN_256_TAIL;   // (8-phase instead: FC2 fwd 5 % slower)
   if (ak && K >= 2 * TK2 && use_8p() && (bkc || use_8p_dgrad()))
-    return persist_ok(ak, bkc, M, N, K, stream_epi, fast_epi) ? PLAN_8P_PERSIST : PLAN_8P;
+    return persist_ok(ak, bkc, M, N, K, pepi) ? PLAN_8P_PERSIST : PLAN_8P;
   return PLAN_256;
 }
 
@@ -2045,8 +2079,8 @@ int launch(int M, int N, int K, const bf16* A, long lda, const bf16* B, long ldb
   // epilogues with a streamed 16-bit operand run the PFS instantiation (the operand loaded two row groups ahead);
   // the others keep the plain store loop (CMHAR_EPI_PF2=0: never)
   const bool pfs = CMHAR_EPI_PF2 && sizeof(OutT) == 2 && epi_has_stream(e);
-    const int plan = gemm_plan(AK, BKc, M, N, K, splits, ws != nullptr, e.rowsum != nullptr, epi_reads(e),
-                               sizeof(OutT) == 2 && epi_fast_ok(e));
+    const int plan = gemm_plan(AK, BKc, M, N, K, splits, ws != nullptr, e.rowsum != nullptr,
+                               sizeof(OutT) == 2 && epi_persist_ok(e));
     if (plan == PLAN_256_TAIL) {
       const TailSplit ts = tail_split(M, N, K);
       if (ph_gemm && pfs)
@@ -2144,11 +2178,12 @@ extern "C" int cmhar_debug_persist_probe(unsigned long long* host, long n) {
                                   hipMemcpyDeviceToHost);
 }
 #endif
-// As cmhar_gemm_bf16_plan for an epilogue that reads an operand (residual, aux_in, rowadd, beta) or not.
+// As cmhar_gemm_bf16_plan for a 16-bit output whose epilogue is (reads = 0) or is not (reads != 0) one the persistent
+// kernel takes (epi_persist_ok: plain, GELU pair, × aux_in, + residual; not rowadd / beta / dropout / alpha != 1).
 extern "C" int cmhar_gemm_bf16_plan2(int layout, int M, int N, int K, int splits, int has_ws, int rowsum,
-                                     int stream_epi) {
+                                     int reads) {
   if (layout < 0 || layout > 2) return -1;
-  return gemm_plan(layout != 2, layout == 0, M, N, K, splits, has_ws != 0, rowsum != 0, stream_epi != 0);
+  return gemm_plan(layout != 2, layout == 0, M, N, K, splits, has_ws != 0, rowsum != 0, reads == 0);
 }
 
 // cmhar_gemm_bf16 with a phase mask (bit 0 = GEMM kernel, bit 1 = split-K / tail reduce): phases 1 then 2 is the

@@ -67,10 +67,10 @@ long cmhar_gemm_bf16_ws(int M, int N, int K);
  * (forward / weight-gradient layouts), 5 = 128² split-K + reduce, 6 = 8-phase 256² split-K + reduce (weight
  * gradients); -1 = bad layout.  Used for trace labels (bench.py kernel breakdown). */
 int cmhar_gemm_bf16_plan(int layout, int M, int N, int K, int splits, int has_ws, int rowsum);
-/* As cmhar_gemm_bf16_plan for an epilogue that reads an operand (reads != 0: residual, aux_in, rowadd, or beta
- * accumulation into C) or not; 7 = the persistent 8-phase forward kernel (whole-K forward-layout launches whose
- * epilogue reads nothing, more 256² tiles than CUs, an even K-tile count).  cmhar_gemm_bf16_plan answers for
- * reads == 0. */
+/* As cmhar_gemm_bf16_plan for a 16-bit output whose epilogue the persistent forward kernel takes (reads == 0: alpha
+ * 1, no dropout / rowadd / beta; plain, the GELU pair, x aux_in or + residual) or not (reads != 0); 7 = the persistent
+ * 8-phase forward kernel (whole-K forward-layout launches of at least three chip rounds of 256² tiles, an even K-tile
+ * count, N <= 4096).  cmhar_gemm_bf16_plan answers for reads == 0. */
 int cmhar_gemm_bf16_plan2(int layout, int M, int N, int K, int splits, int has_ws, int rowsum, int reads);
 /* cmhar_gemm_bf16 restricted to a phase mask: bit 0 = the GEMM kernel, bit 1 = the split-K / tail reduce (3 = the
  * whole call).  Calling phases 1 then 2 on one stream equals one cmhar_gemm_bf16 call; bench.py uses the split to

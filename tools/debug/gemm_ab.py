@@ -93,6 +93,9 @@ def main():
                  ('dgrad', lambda: K.gemm(1, dy, w, dx, **dkw), lambda: torch.matmul(dy, w, out=dx)),
                  ('wgrad', lambda: K.gemm(2, dy, x, dw), lambda: torch.matmul(dy.t(), x, out=dw) if dt == torch.float32
                   else dw.copy_(dy.t() @ x))]
+        if epi and name == 'fc2':   # the step's FC2 input gradient: layout 0 over the transposed weight copy
+            wt = w.t().contiguous()
+            cases.append(('dgradT', lambda: K.gemm(0, dy, wt, dx, **dkw), lambda: torch.matmul(dy, w, out=dx)))
         for tag, fn0, tfn in cases:
             if name == 'embed' and tag == 'dgrad':
                 continue
@@ -106,7 +109,7 @@ def main():
                 for _ in range(3):
                     fn()
                 torch.cuda.synchronize()
-                outs.append(y.clone() if tag == 'fwd' else dx.clone() if tag == 'dgrad' else dw.clone())
+                outs.append(y.clone() if tag == 'fwd' else dx.clone() if tag.startswith('dgrad') else dw.clone())
             same = all(torch.equal(outs[0], o) for o, lb in zip(outs[1:], libs[1:]) if lb is not None)
             ts = [[] for _ in range(nv)]
             for _ in range(rounds):
@@ -114,7 +117,7 @@ def main():
                     _lib._lib = libs[v]
                     ts[v].append(timed(fn_of(v)))
             med = [statistics.median(t) for t in ts]
-            mult = 1 if name == 'embed' else 12
+            mult = 1 if name == 'embed' else 0 if tag == 'dgradT' else 12
             for v in range(nv):
                 tot[v] += med[v] * mult
             cols = ' | '.join(f'{"T" if libs[v] is None else chr(65 + v)} {med[v] * 1e3:7.1f} us {fl / med[v] / 1e9:5.0f} TF' for v in range(nv))

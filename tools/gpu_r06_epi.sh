@@ -7,7 +7,7 @@ set -o pipefail
 export TMPDIR=/tmp
 mkdir -p gpurun_out
 timeout -k 10 400 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu \
-  tests/test_kernels_gpu.py -k "gemm or wgrad or tubelet or dgrad" tests/test_production_shapes_gpu.py \
+  tests/test_kernels_gpu.py -k "gemm or wgrad or tubelet or dgrad or attn or attention" tests/test_production_shapes_gpu.py \
   > gpurun_out/${TAG}_tests.log 2>&1 || { tail -30 gpurun_out/${TAG}_tests.log; exit 1; }
 tail -3 gpurun_out/${TAG}_tests.log
 LIBS="crossmodal-imu-video-ood-har_amd/cmhar/libcmhar.so $*"
