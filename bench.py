@@ -46,8 +46,8 @@ PEAK_F32_TFLOPS = 157.3        # f32-input MFMA (= the f32 vector rate; no xf32 
 PEAK_HBM_GBS = 8000.0
 
 
-TRAFFIC_JSON = os.path.join(REPO, 'profiles', 'r05_pmc_traffic.json')
-MFMA_JSON = os.path.join(REPO, 'profiles', 'r05_pmc_mfma.json')
+TRAFFIC_JSON = os.path.join(REPO, 'profiles', 'r06_pmc_traffic.json')
+MFMA_JSON = os.path.join(REPO, 'profiles', 'r06_pmc_mfma.json')
 
 # per-workload defaults of --batch / --frames / --image / --imu-len / --dtype (BASELINE.json configs)
 WORKLOADS = {

@@ -433,6 +433,18 @@ __device__ __forceinline__ bool tail_block(int ntail, int H, BlkIdx& bi) {
 
 // CMHAR_ATTN_PRIO = 1: raise the wave's issue priority over each MFMA chain (as the GEMM's MFMA_Q) so the co-resident
 // waves' softmax / exp VALU work fills the matrix pipe's gaps instead of delaying the chain (A/B knob)
+// CMHAR_ATTN_ABL_NODMA: see attn_bwd_dq_bf16
+#ifndef CMHAR_ATTN_ABL_NODMA
+#define CMHAR_ATTN_ABL_NODMA 0
+#endif
+// CMHAR_ATTN_DMA_POS (backward kernels, A/B knob): where a tile's DMA for the next tile is issued — 0 at the tile's
+// start, 1 after the first block's score / dP MFMA chain (the pieces then issue while those MFMAs drain), 2 split:
+// the first operand's pieces at the start, the second's after that chain.  Round 6, one process
+// (tools/debug/attn_ab.py, backward µs per layer): 878.2 / 944.2 / 908.9 — the tile start stays.  For scale, the
+// in-loop DMA removed altogether (CMHAR_ATTN_ABL_NODMA, stale tiles): dK/dV −52 µs, dQ −45 µs of ~870.
+#ifndef CMHAR_ATTN_DMA_POS
+#define CMHAR_ATTN_DMA_POS 0
+#endif
 #ifndef CMHAR_ATTN_PRIO
 #define CMHAR_ATTN_PRIO 0
 #endif
@@ -683,12 +695,16 @@ __global__ __launch_bounds__(256, 3) void attn_bwd_dkdv_bf16(int H, int Lq, int 
   int lq = 0;
   // row constants, staged pre-negated (and -lse pre-divided by c) as accumulator seeds.  Every lane loads (no branch
   // around the loads: hipcc waited vmcnt(0) right after a branch-guarded load, draining the tile DMA just issued)
-  auto load_rows = [&](int qt, char* qs, char* gs) {
-    tq.tile(qt * 64, qs, wave);
+  auto load_q = [&](int qt, char* qs) { tq.tile(qt * 64, qs, wave); };
+  auto load_g = [&](int qt, char* gs) {
     tg.tile(qt * 64, gs, wave);
     lq = qt * 64 + lane;
     lv = lseb[min(lq, Lq - 1)];
     dv_ = delb[min(lq, Lq - 1)];
+  };
+  auto load_rows = [&](int qt, char* qs, char* gs) {
+    load_q(qt, qs);
+    load_g(qt, gs);
   };
   auto store_rows = [&](int buf) {
     if (tid < 64) {
@@ -705,8 +721,10 @@ __global__ __launch_bounds__(256, 3) void attn_bwd_dkdv_bf16(int H, int Lq, int 
   // the ds_read immediate offsets
   auto tile = [&](auto CUR, int qt) __attribute__((always_inline)) {
     constexpr int cur = decltype(CUR)::value;
-    const bool more = qt + 1 < nt;
-    if (more) load_rows(qt + 1, Qs(cur ^ 1), Gs(cur ^ 1));
+    const bool more = qt + 1 < nt && !(CMHAR_ATTN_ABL_NODMA & 1);
+    constexpr int pos = CMHAR_ATTN_DMA_POS;
+    if (more && (pos == 0 || !active)) load_rows(qt + 1, Qs(cur ^ 1), Gs(cur ^ 1));
+    else if (more && pos == 2) load_q(qt + 1, Qs(cur ^ 1));
     const float* L_ = Ls + cur * 64;
     const float* D_ = Ds + cur * 64;
 #pragma unroll
@@ -727,6 +745,12 @@ __global__ __launch_bounds__(256, 3) void attn_bwd_dkdv_bf16(int H, int Lq, int 
         dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag(Gs(cur), qb * 32, t, lane), vf[t], dp, 0, 0, 0);
       }
       PRIO_LO();
+      if (pos != 0 && qb == 0 && more) {
+        __builtin_amdgcn_sched_barrier(0);
+        if (pos == 1) load_rows(qt + 1, Qs(cur ^ 1), Gs(cur ^ 1));
+        else load_g(qt + 1, Gs(cur ^ 1));
+        __builtin_amdgcn_sched_barrier(0);
+      }
       // p = exp2(c·s), dS = P ∘ (dP − δ), then both packed to bf16 — written in aligned register pairs (one
       // v_pk_mul_f32 + one v_cvt_pk_bf16_f32 per pair; element-wise, the compiler paired (1,2),(3,4),... and spent
       // v_mov / v_alignbit / v_perm re-pairing them for the packs; the backward got 3 % faster, bit-identical.  The
@@ -780,6 +804,14 @@ __global__ __launch_bounds__(256, 3) void attn_bwd_dkdv_bf16(int H, int Lq, int 
 // and written for the dK/dV kernel, which runs after this one on the same stream.
 // Three waves per SIMD for dQ: with the fragments read just before their MFMAs (not hoisted per key block) the
 // kernel fits 168 VGPRs without spilling; measured 7 % faster than two waves per SIMD
+// CMHAR_ATTN_DQ_NBUF = 3: K/V tiles triple-buffered (48 KiB per workgroup, three per CU): tile kt+2's DMA is issued at
+// the start of tile kt and the end-of-tile wait leaves it in flight (vmcnt(4)), two tiles of lead instead of one.
+// Measured (round 6, attn_ab.py): backward 866.5 → 881.4 µs per layer — the staging is not latency-bound; off.
+// CMHAR_ATTN_ABL_NODMA (ablation builds, tools/debug; bit 0 dK/dV, bit 1 dQ): the in-loop tile DMA skipped —
+// later tiles read stale LDS — to price the staging stream.
+#ifndef CMHAR_ATTN_DQ_NBUF
+#define CMHAR_ATTN_DQ_NBUF 2
+#endif
 template <int QB, bool PS = false>
 __global__ __launch_bounds__(256, QB == 1 ? 3 : 2) void attn_bwd_dq_bf16(int H, int Lq, int Lk, int q_base,
                                                            const bf16* __restrict__ Q, long ldq,
@@ -790,9 +822,13 @@ __global__ __launch_bounds__(256, QB == 1 ? 3 : 2) void attn_bwd_dq_bf16(int H, 
                                                            const float* __restrict__ lse,
                                                            float* __restrict__ delta, bf16* __restrict__ dQ,
                                                            long lddq, float scale) {
-  __shared__ __attribute__((aligned(16))) char smem[4 * 8192];
+  constexpr int NB = CMHAR_ATTN_DQ_NBUF;
+  static_assert(NB == 2 || NB == 3, "two or three K/V buffers");
+  __shared__ __attribute__((aligned(16))) char smem[NB * 16384];
+#undef Ks
+#undef Vs
 #define Ks(buf) (smem + 8192 * (buf))
-#define Vs(buf) (smem + 16384 + 8192 * (buf))
+#define Vs(buf) (smem + 8192 * NB + 8192 * (buf))
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5;
   const BlkIdx bi = flash_block(H);
   const int hd = bi.hd, b = bi.b;
@@ -835,18 +871,28 @@ __global__ __launch_bounds__(256, QB == 1 ? 3 : 2) void attn_bwd_dq_bf16(int H, 
   tv.init(Vb, ldv, Lk, wave, lane);
   tk.tile(0, Ks(0), wave);
   tv.tile(0, Vs(0), wave);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (NB == 3 && nt > 1) {
+    tk.tile(64, Ks(1), wave);
+    tv.tile(64, Vs(1), wave);
+    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
   __syncthreads();
   const bool active = q0 < Lq;      // waves past the last query only stage tiles and join barriers (see forward)
-  // one tile per call, LDS buffer index a compile-time constant (tiles run in pairs): LDS addresses fold into
-  // the ds_read immediate offsets
+  // one tile per call, LDS buffer index a compile-time constant (tiles run in pairs / triples): LDS addresses fold
+  // into the ds_read immediate offsets
   auto tile = [&](auto CUR, int kt) __attribute__((always_inline)) {
     constexpr int cur = decltype(CUR)::value;
     const bool more = kt + 1 < nt;
-    if (more) {   // next tile DMA'd into the other buffer (its last reader passed the previous tile's barrier)
-      tk.tile((kt + 1) * 64, Ks(cur ^ 1), wave);
-      tv.tile((kt + 1) * 64, Vs(cur ^ 1), wave);
-    }
+    // NB = 2: the next tile into the other buffer; NB = 3: the tile after next into the buffer the previous tile
+    // used (its last reader passed the previous tile's barrier)
+    const int ahead = NB - 1;
+    const bool issue = kt + ahead < nt && !(CMHAR_ATTN_ABL_NODMA & 2);
+    constexpr int nb = (cur + NB - 1) % NB;
+    constexpr int pos = CMHAR_ATTN_DMA_POS;
+    if (issue && (pos != 1 || !active)) tk.tile((kt + ahead) * 64, Ks(nb), wave);
+    if (issue && (pos == 0 || !active)) tv.tile((kt + ahead) * 64, Vs(nb), wave);
     const int kbase = kt * 64;
 #pragma unroll
     for (int kb = 0; kb < 2; ++kb) {
@@ -868,6 +914,12 @@ __global__ __launch_bounds__(256, QB == 1 ? 3 : 2) void attn_bwd_dq_bf16(int H, 
         }
       }
       PRIO_LO();
+      if (pos != 0 && kb == 0 && issue) {
+        __builtin_amdgcn_sched_barrier(0);
+        if (pos == 1) tk.tile((kt + ahead) * 64, Ks(nb), wave);
+        tv.tile((kt + ahead) * 64, Vs(nb), wave);
+        __builtin_amdgcn_sched_barrier(0);
+      }
       if (kbase + 64 > Lk) {   // ragged last tile only (wave-uniform branch)
 #pragma unroll
         for (int j = 0; j < QB; ++j)
@@ -899,12 +951,23 @@ __global__ __launch_bounds__(256, QB == 1 ? 3 : 2) void attn_bwd_dq_bf16(int H, 
         }
       PRIO_LO();
     }
-    if (more) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // own pieces of the next tile landed
+    if (more) {   // own pieces of the next tile landed (NB = 3: the tile after it still in flight)
+      if (issue && NB == 3) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
     __syncthreads();
   };
-  for (int kt = 0; kt < nt; kt += 2) {
-    tile(std::integral_constant<int, 0>{}, kt);
-    if (kt + 1 < nt) tile(std::integral_constant<int, 1>{}, kt + 1);
+  if constexpr (NB == 3) {
+    for (int kt = 0; kt < nt; kt += 3) {
+      tile(std::integral_constant<int, 0>{}, kt);
+      if (kt + 1 < nt) tile(std::integral_constant<int, 1>{}, kt + 1);
+      if (kt + 2 < nt) tile(std::integral_constant<int, 2>{}, kt + 2);
+    }
+  } else {
+    for (int kt = 0; kt < nt; kt += 2) {
+      tile(std::integral_constant<int, 0>{}, kt);
+      if (kt + 1 < nt) tile(std::integral_constant<int, 1>{}, kt + 1);
+    }
   }
 #pragma unroll
   for (int j = 0; j < QB; ++j) {

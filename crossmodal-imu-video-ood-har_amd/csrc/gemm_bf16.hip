@@ -2006,6 +2006,29 @@ static int persist_grid() {
     return 0;
   return n % 8 == 0 ? n : 0;
 }
+// CMHAR_PERSIST_BALANCE = 1 (CMHAR_PERSIST_BALANCE env overrides): the persistent grid sized so that every workgroup
+// runs the same number of tiles, ⌈tiles / ⌈tiles / CUs⌉⌉ rounded up to a multiple of 8 (the N = 768 launches: 588
+// tiles = 2.3 chip rounds → 200 workgroups of 3 tiles instead of 256 with a 30 %-full last round), and launches from
+// 2 chip rounds up take the persistent kernel — ahead of the tail split.  Round 6 (tools/debug/gemm_ab.py --epi, one
+// process): out-proj forward 86.8 → 94.7 µs, FC2 forward 245.4 → 250.9, embed 115.9 → 108.5, bench step 726.1 / 727.8
+// → 726.8 / 724.2 clips/s — off.  (hipBLASLt's stream-K kernel runs the out-proj shape on 196 workgroups of 3 tiles
+// at 63 µs; ours does not speed up per tile with fewer CUs busy.)
+#ifndef CMHAR_PERSIST_BALANCE_DEFAULT
+#define CMHAR_PERSIST_BALANCE_DEFAULT 0
+#endif
+static bool persist_balance() {
+  static const bool v = [] {
+    const char* s = getenv("CMHAR_PERSIST_BALANCE");
+    return s ? atoi(s) != 0 : CMHAR_PERSIST_BALANCE_DEFAULT != 0;
+  }();
+  return v;
+}
+static int persist_grid_for(int tiles) {
+  static const int g = persist_grid();
+  if (!persist_balance() || g == 0) return g;
+  const int rounds = cdiv(tiles, g);
+  return min(g, cdiv(cdiv(tiles, rounds), 8) * 8);
+}
 static bool persist_ok(bool ak, bool bkc, int M, int N, int K, bool pepi) {
   // pepi: a 16-bit output and an epilogue epi_persist handles (epi_persist_ok)
   if (!(ak && bkc) || !pepi || !use_8p_persist() || !CMHAR_EPI_DIRECT) return false;
@@ -2014,7 +2037,7 @@ static bool persist_ok(bool ak, bool bkc, int M, int N, int K, bool pepi) {
   // ≥ 3 chip rounds of tiles: at 2.3 rounds (the K = 768 out-projection input gradient, 588 tiles) the persistent
   // form measured 4 % slower; from QKV's 6.9 rounds (1764 tiles) up it is faster (no relaunch, next K-tiles in flight)
   static const int g = persist_grid();
-  return g > 0 && (M / TM2) * (N / TN2) >= CMHAR_PERSIST_MIN_ROUNDS * g;
+  return g > 0 && (M / TM2) * (N / TN2) >= (persist_balance() ? 2 : CMHAR_PERSIST_MIN_ROUNDS) * g;
 }
 
 // Which kernel(s) a cmhar_gemm_bf16 call launches (also exported for trace labels: cmhar_gemm_bf16_plan).
@@ -2035,6 +2058,7 @@ static int gemm_plan(bool ak, bool bkc, int M, int N, int K, int splits, bool ha
   const bool wgrad8p = !ak && use_8p_wgrad() && klen >= 2 * TK2 && K - (nsplit - 1) * klen >= 2 * TK2;
   if (nsplit > 1) return wgrad8p ? PLAN_8P_SPLITK : PLAN_256_SPLITK;
   if (wgrad8p) return PLAN_8P;
+  if (persist_balance() && ak && use_8p() && bkc && persist_ok(ak, bkc, M, N, K, pepi)) return PLAN_8P_PERSIST;
   if (has_ws && !rowsum && tail_split(M, N, K).n_dp > 0) return PLAN_256_TAIL;   // (8-phase instead: FC2 fwd 5 % slower)
   if (ak && K >= 2 * TK2 && use_8p() && (bkc || use_8p_dgrad()))
     return persist_ok(ak, bkc, M, N, K, pepi) ? PLAN_8P_PERSIST : PLAN_8P;
@@ -2107,7 +2131,7 @@ int launch(int M, int N, int K, const bf16* A, long lda, const bf16* B, long ldb
         gemm8p_kernel<E, AK, BKc, OutT><<<grid, NT2, 0, st>>>(M, N, K, A, lda, B, ldb, C, ldc, e, K, 0, 0, ng);
     } else if (plan == PLAN_8P_PERSIST) {
       if constexpr (AK && BKc && sizeof(OutT) == 2) {   // (the plan requires a 16-bit output)
-        static const int g = persist_grid();
+        const int g = persist_grid_for((M / TM2) * (N / TN2));
         if (ph_gemm)
           gemm8p_persist_kernel<E, OutT><<<g, NT2, 0, st>>>(M, N, K, A, lda, B, ldb, C, ldc, e,
                                                             gemm8p_groups(AK, BKc, N, K));
