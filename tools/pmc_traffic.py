@@ -43,7 +43,8 @@ def main():
                    'cmd': sys.argv[5] if len(sys.argv) > 5 else None, 'kernels': out}, f,
                   indent=1, sort_keys=True)
     for k, v in sorted(out.items(), key=lambda kv: -kv[1]['hbm_bytes_per_launch'] * kv[1]['dispatches'])[:12]:
-        print(f"{v['hbm_bytes_per_launch'] / 1e6:10.1f} MB/launch  x{v['dispatches']:4d}  {k[:100]}")
+        print(f"{v['hbm_bytes_per_launch'] / 1e6:10.1f} MB/launch (fetch {v['fetch_bytes_per_launch'] / 1e6:8.1f}, "
+              f"write {v['write_bytes_per_launch'] / 1e6:8.1f})  x{v['dispatches']:4d}  {k[:100]}")
 
 
 if __name__ == '__main__':
