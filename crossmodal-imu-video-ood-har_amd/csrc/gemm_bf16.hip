@@ -14,6 +14,8 @@
 // cmhar_splitk_reduce combines with the epilogue.
 #include "common.h"
 
+#include <map>
+#include <mutex>
 #include <type_traits>
 
 namespace {
@@ -1645,8 +1647,10 @@ __device__ __forceinline__ void bias_init(const Epilogue& e, const float* lds_bi
 #pragma unroll
   for (int j = 0; j < 4; ++j) b[j] = floatx4{0.f, 0.f, 0.f, 0.f};
   if (e.bias) {
+    int lz = lane;                        // (opaque per call: a hoisted lane-dependent address was spilled)
+    asm volatile("" : "+v"(lz));
 #pragma unroll
-    for (int j = 0; j < 4; ++j) b[j] = *(const floatx4*)(lds_bias + n0 + j * 16 + 4 * (lane >> 4));
+    for (int j = 0; j < 4; ++j) b[j] = *(const floatx4*)(lds_bias + n0 + j * 16 + 4 * (lz >> 4));
   }
 }
 
@@ -1664,26 +1668,61 @@ __device__ __forceinline__ void bias_init(const Epilogue& e, const float* lds_bi
 // under the next tile's K loop instead of holding the workgroup (and its CU) until they are acknowledged, and the next
 // workgroup's launch and first-K-tile latency disappear.  No inter-workgroup communication: a workgroup that is not
 // resident yet just starts later.
+//
+// Tile claiming (sched != nullptr, CMHAR_PERSIST_DYNAMIC): instead of the fixed walk v = blockIdx + G·s, a workgroup
+// claims its tiles from its XCD's counter (sched[blockIdx % 8], the XCD's contiguous chunk of the xcd_remap order) —
+// one returning vector atomic of thread 0 per tile, issued one tile ahead inside K-tile 1, before that K-tile's
+// vmcnt(0), and handed to the other waves through LDS.  A workgroup that starts late (its CU held by a kernel of
+// another stream: the IMU branch's 32 long workgroups) then claims fewer tiles instead of finishing its fixed share
+// that much later.  Every tile is computed exactly as before, so the output is the same whoever claims it.  The last
+// workgroup to finish (sched[8] counts them) puts the counters back to zero for the next launch on the stream.
 template <typename E, typename OutT>
 __global__ __launch_bounds__(NT2, 2) void gemm8p_persist_kernel(int M, int N, int K, const bf16* __restrict__ A,
                                                                 long lda, const bf16* __restrict__ B, long ldb,
                                                                 OutT* __restrict__ C, long ldc, Epilogue e,
-                                                                int ngroup) {
-  __shared__ __attribute__((aligned(16))) char smem[131072 + kPersistBiasMax * 4];
-  const int tid = threadIdx.x, lane = tid & 63;
+                                                                int ngroup, unsigned* sched) {
+  __shared__ __attribute__((aligned(16))) char smem[131072 + kPersistBiasMax * 4 + 16];
+  const int tid = threadIdx.x, lane = tid & 63, lane_ = lane;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = wave >> 2, wc = wave & 3;
   const int tiles_n = N / TN2, tiles_m = M / TM2, ntile = tiles_m * tiles_n;
-  const int nk = K / TK2;   // even, >= 2 (host-checked)
+  const int nk = K / TK2;   // even, >= 2 (host-checked; >= 4 with sched)
   float* const lds_bias = (float*)(smem + 131072);   // N <= kPersistBiasMax (host-checked)
+  int* const slot = (int*)(smem + 131072 + kPersistBiasMax * 4);   // claimed tiles handed to the other waves
   if (e.bias)
     for (int c = tid * 4; c < N; c += NT2 * 4) *(floatx4*)(lds_bias + c) = *(const floatx4*)(e.bias + c);
   const int G = gridDim.x;
-  // tile origin (rows bm, columns bn) of iteration s, as gemm8p_kernel maps block id v
+  // this workgroup's XCD chunk of the xcd_remap order (the tiles its XCD's counter hands out)
+  const int xcd = blockIdx.x & 7, q8 = ntile >> 3, r8 = ntile & 7;
+  const int xstart = xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8;
+  const int xcnt = q8 + (xcd < r8 ? 1 : 0);
+  auto valid = [&](unsigned v) -> int { return v < (unsigned)xcnt ? (int)v : -1; };
+  auto finish = [&]() {        // thread 0 only, after its last claim
+    if (atomicAdd(sched + 8, 1u) == (unsigned)(G - 1)) {
+#pragma unroll
+      for (int x = 0; x < 9; ++x) atomicExch(sched + x, 0u);
+    }
+  };
+  if (sched) {
+    if (tid == 0) {   // the first two tiles in one claim (counter values only grow: if the first is past the chunk, so
+      const unsigned v = atomicAdd(sched + xcd, 2u);   // is the second)
+      slot[0] = valid(v);
+      slot[1] = valid(v + 1);
+    }
+    __syncthreads();
+  }
+  // tile origin (rows bm, columns bn) of iteration s (static walk) or of claimed chunk index s (sched), as
+  // gemm8p_kernel maps block id v
   auto tile_of = [&](int s, int& bm, int& bn) -> bool {
-    const int v = blockIdx.x + G * s;
-    if (v >= ntile) return false;
-    const int bid = xcd_remap(v, ntile);
+    int bid;
+    if (sched) {
+      if (s < 0) return false;
+      bid = xstart + s;
+    } else {
+      const int v = blockIdx.x + G * s;
+      if (v >= ntile) return false;
+      bid = xcd_remap(v, ntile);
+    }
     int tm = bid / tiles_n, tn = bid % tiles_n;
     if (ngroup > 1) {
       const int cw = (tiles_n + ngroup - 1) / ngroup;
@@ -1698,8 +1737,11 @@ __global__ __launch_bounds__(NT2, 2) void gemm8p_persist_kernel(int M, int N, in
     return true;
   };
   int bm, bn, bm2 = 0, bn2 = 0;
-  if (!tile_of(0, bm, bn)) return;
-  bool nxt = tile_of(1, bm2, bn2);
+  if (!tile_of(sched ? slot[0] : 0, bm, bn)) {
+    if (sched && tid == 0) finish();
+    return;
+  }
+  bool nxt = tile_of(sched ? slot[1] : 1, bm2, bn2);
   DmaHalf<true> da, db;
   da.init(A, lda, bm, wave, lane);
   db.init(B, ldb, bn, wave, lane);
@@ -1727,7 +1769,7 @@ __global__ __launch_bounds__(NT2, 2) void gemm8p_persist_kernel(int M, int N, in
   // accumulators start from the bias (the epilogue then adds none): out = bias + Σ_k a·b, summed in that order —
   // exact on integer data, within fp32 rounding of (Σ_k a·b) + bias otherwise
   floatx4 acc[8][4], binit[4];
-  __syncthreads();   // the LDS bias copy
+  if (!sched) __syncthreads();   // the LDS bias copy (with sched: the barrier above)
   bias_init(e, lds_bias, bn + wc * 64, lane, binit);
 #pragma unroll
   for (int i = 0; i < 8; ++i)
@@ -1780,6 +1822,10 @@ __global__ __launch_bounds__(NT2, 2) void gemm8p_persist_kernel(int M, int N, in
   auto ktile = [&](int t, bool skip) __attribute__((always_inline)) {
     const char* as = abuf(t);
     const char* bs = bbuf(t);
+    // the fragment addresses recomputed per K-tile from an opaque lane (hoisted out of the tile loop they held ~a dozen
+    // VGPRs for the whole kernel and pushed it into scratch once tile claiming was added)
+    int lane = lane_;
+    asm volatile("" : "+v"(lane));
     // phase 1: A0 + B0, stage A upper half of t+1; MFMA quadrant (0,0)
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
@@ -1816,7 +1862,15 @@ __global__ __launch_bounds__(NT2, 2) void gemm8p_persist_kernel(int M, int N, in
       MFMA_QP(1, b1);
     }
     // phase 4: all of t+1 landed (own pieces; after a boundary: everything but the epilogue's memory operations),
-    // then A lower half of t+2; quadrant (1,0)
+    // then A lower half of t+2; quadrant (1,0).  sched: thread 0 claims the tile after next in K-tile 1, just before
+    // that K-tile's vmcnt(0), and hands it over through LDS after it (no wait of its own on the atomic's return)
+    // (the atomic as inline asm: the compiler then neither waits on its return right away nor moves it to a scalar
+    // register; the vmcnt(0) below retires it, and the compiler's own counted waits only over-count with it)
+    unsigned claimed = ~0u;
+    if (sched && t == 1 && nxt && tid == 0) {
+      asm volatile("global_atomic_add %0, %1, %2, %3 sc0" : "=v"(claimed) : "v"(xcd * 4), "v"(1u), "s"(sched)
+                   : "memory");
+    }
     if (skip) {
       if (s_ops >= 32) asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
       else asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
@@ -1824,6 +1878,10 @@ __global__ __launch_bounds__(NT2, 2) void gemm8p_persist_kernel(int M, int N, in
       asm volatile("s_waitcnt vmcnt(16)" ::: "memory");   // (wrong data when the stores are not done: timing only)
     } else {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    if (sched && t == 1 && tid == 0) {
+      asm volatile("" : "+v"(claimed));   // first use of the atomic's return: after the vmcnt(0) above, not before it
+      slot[2] = valid(claimed);           // (-1 when there is no next tile: nothing was claimed)
     }
     stage_a(t + 2, 0);
     END_LOADS_P();
@@ -1872,7 +1930,10 @@ __global__ __launch_bounds__(NT2, 2) void gemm8p_persist_kernel(int M, int N, in
       if (sum == 1234.5f) C[tid] = (OutT)sum;
     }
     stamp(s, 4);
-    if (!nxt) break;
+    if (!nxt) {
+      if (sched && tid == 0) finish();
+      break;
+    }
 #pragma unroll
     for (int i = 0; i < 8; ++i)
 #pragma unroll
@@ -1881,7 +1942,14 @@ __global__ __launch_bounds__(NT2, 2) void gemm8p_persist_kernel(int M, int N, in
     bn = bn2;
     a_cur = a_nxt;
     b_cur = b_nxt;
-    nxt = tile_of(s + 2, bm2, bn2);
+    int claimed_next = -1;
+    if (sched) {   // the tile after next (claimed in K-tile 1), read by inline asm: a compiler LDS read here, behind the
+                   // LDS-DMA in flight, got a vmcnt(0) that drained the epilogue's stores
+      asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(claimed_next)
+                   : "v"((unsigned)(uintptr_t)(slot + 2)) : "memory");
+      claimed_next = __builtin_amdgcn_readfirstlane(claimed_next);
+    }
+    nxt = tile_of(sched ? claimed_next : s + 2, bm2, bn2);
     a_nxt = (const char*)(A + (long)bm2 * lda);
     b_nxt = (const char*)(B + (long)bn2 * ldb);
     pre = true;
@@ -2029,6 +2097,31 @@ static int persist_grid_for(int tiles) {
   const int rounds = cdiv(tiles, g);
   return min(g, cdiv(cdiv(tiles, rounds), 8) * 8);
 }
+// Tile claiming for the persistent kernel (see gemm8p_persist_kernel): one counter block per (device, stream) — 8
+// per-XCD counters + a finished-workgroup count, zeroed once here and by each launch's last workgroup after that.
+// CMHAR_PERSIST_DYNAMIC=0: the fixed tile walk (A/B runs; identical output).
+#ifndef CMHAR_PERSIST_DYNAMIC_DEFAULT
+#define CMHAR_PERSIST_DYNAMIC_DEFAULT 1
+#endif
+static unsigned* persist_sched(hipStream_t st) {
+  static const bool on = [] {
+    const char* v = getenv("CMHAR_PERSIST_DYNAMIC");
+    return v ? atoi(v) != 0 : CMHAR_PERSIST_DYNAMIC_DEFAULT != 0;
+  }();
+  if (!on) return nullptr;
+  static std::mutex mu;
+  static std::map<std::pair<int, hipStream_t>, unsigned*> blocks;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+  std::lock_guard<std::mutex> lk(mu);
+  auto it = blocks.find({dev, st});
+  if (it != blocks.end()) return it->second;
+  void* p = nullptr;
+  if (hipMalloc(&p, 16 * sizeof(unsigned)) != hipSuccess) return nullptr;
+  if (hipMemsetAsync(p, 0, 16 * sizeof(unsigned), st) != hipSuccess) { (void)hipFree(p); return nullptr; }
+  blocks[{dev, st}] = (unsigned*)p;
+  return (unsigned*)p;
+}
 static bool persist_ok(bool ak, bool bkc, int M, int N, int K, bool pepi) {
   // pepi: a 16-bit output and an epilogue epi_persist handles (epi_persist_ok)
   if (!(ak && bkc) || !pepi || !use_8p_persist() || !CMHAR_EPI_DIRECT) return false;
@@ -2132,9 +2225,11 @@ int launch(int M, int N, int K, const bf16* A, long lda, const bf16* B, long ldb
     } else if (plan == PLAN_8P_PERSIST) {
       if constexpr (AK && BKc && sizeof(OutT) == 2) {   // (the plan requires a 16-bit output)
         const int g = persist_grid_for((M / TM2) * (N / TN2));
+        // (claiming hands the tile after next over in K-tile 1: at least 4 K-tiles per tile)
+        unsigned* sched = K / TK2 >= 4 ? persist_sched(st) : nullptr;
         if (ph_gemm)
           gemm8p_persist_kernel<E, OutT><<<g, NT2, 0, st>>>(M, N, K, A, lda, B, ldb, C, ldc, e,
-                                                            gemm8p_groups(AK, BKc, N, K));
+                                                            gemm8p_groups(AK, BKc, N, K), sched);
       }
     } else if (plan == PLAN_8P_SPLITK) {
       if (ph_gemm && gemm8p_na(AK) == 3)
