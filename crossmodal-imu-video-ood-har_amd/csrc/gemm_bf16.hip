@@ -2036,6 +2036,8 @@ static bool use_8p_wgrad() {
 #ifndef CMHAR_GEMM8P_NA_DEFAULT
 #define CMHAR_GEMM8P_NA_DEFAULT 2
 #endif
+// (weight gradients with three A buffers, round 6: 252 VGPRs, no scratch, identical bits, but QKV / FC1 / out-proj
+// wgrad 177 / 222 / 76 -> 188 / 243 / 84 us and FC2 240 -> 232 in one process, bench step -1.8 %: two)
 #ifndef CMHAR_GEMM8P_WGRAD_NA_DEFAULT
 #define CMHAR_GEMM8P_WGRAD_NA_DEFAULT 2
 #endif

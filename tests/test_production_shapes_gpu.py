@@ -260,6 +260,46 @@ def test_bench_gemm_plans_are_the_bench_plans():
         assert plan(2, n, k, M, rowsum=True) == 6, (n, k)     # weight gradients: 8-phase split-K, bias row sum
 
 
+def test_persistent_gemm_tile_claiming_across_streams():
+    """The persistent kernel's tile claiming (per-XCD counters, one counter block per stream, reset by each launch's
+    last workgroup): the QKV forward launch run alone, then on two streams at once while a third keeps the chip busy
+    with fp32 matmuls (workgroups of the persistent launches start late and claim fewer tiles), then alone again —
+    every output bit-identical to the solo run (each tile is computed the same whoever claims it; a tile claimed twice
+    or not at all would show)."""
+    lib = L().lib()
+    if lib.cmhar_gemm_bf16_plan2(0, M, 3 * HD, HD, 1, 0, 0, 0) != 7:
+        pytest.skip('persistent kernel disabled (CMHAR_GEMM8P_PERSIST=0)')
+    g = _Gen('rand', seed=11)
+    with torch.no_grad():
+        xs = [g.op((M, HD)) for _ in range(2)]
+        ws = [g.op((3 * HD, HD), sigma=0.05) for _ in range(2)]
+        bs = [g.vec(3 * HD) for _ in range(2)]
+        solo = []
+        for x, w, b in zip(xs, ws, bs):
+            y = torch.empty(M, 3 * HD, device=DEV, dtype=torch.bfloat16)
+            K().gemm(0, x, w, y, bias=b)
+            solo.append(y)
+        torch.cuda.synchronize()
+        busy = torch.randn(4096, 4096, device=DEV)
+        streams = [torch.cuda.Stream() for _ in range(3)]
+        outs = [[torch.empty_like(solo[i]) for _ in range(3)] for i in range(2)]
+        for rep in range(3):
+            with torch.cuda.stream(streams[2]):
+                for _ in range(4):
+                    busy = (busy @ busy).clamp_(-1, 1)
+            for i in range(2):
+                with torch.cuda.stream(streams[i]):
+                    K().gemm(0, xs[i], ws[i], outs[i][rep], bias=bs[i])
+        torch.cuda.synchronize()
+        again = torch.empty_like(solo[0])
+        K().gemm(0, xs[0], ws[0], again, bias=bs[0])
+        torch.cuda.synchronize()
+        for i in range(2):
+            for rep in range(3):
+                assert torch.equal(outs[i][rep], solo[i]), (i, rep)
+        assert torch.equal(again, solo[0])
+
+
 def test_flash_attention_production_shape():
     """The bench step's attention launch (VideoMAE-B, B = 32, H = 12, L = 1568: a 384-head grid) in its training form:
     keys pre-scaled by c = scale·log2(e) in the packed QKV buffer (as the QKV GEMM's colscale epilogue writes them,
