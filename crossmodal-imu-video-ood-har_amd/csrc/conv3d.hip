@@ -1159,20 +1159,34 @@ __global__ __launch_bounds__(64 * NW, 2) void conv3d_wgrad_rows(Geom g, int Cout
 // pairs (the one-tap-row kernel stages 3·R) and each staged dz row feeds 576 columns instead of 192 — 2.3x the
 // MFMA work per staged byte for R3D-18 layer 1 (R = 4).
 namespace wr3 {
-constexpr int SLOTS = 256, SQ = 352, NW = 12, NT = 64 * NW, RS = 144;
-constexpr int DZB = SLOTS * RS, SLB = SQ * RS;
-constexpr int DZ_N = SLOTS * 8, SL_N = SQ * 8, DZ_PER = (DZ_N + NT - 1) / NT, SL_PER = (SL_N + NT - 1) / NT;
+constexpr int SLOTS = 256, SQ = 352, RS = 144;
+constexpr int DZB = SLOTS * RS, DZ_N = SLOTS * 8;
+// CS = input channels per workgroup: 64 (one 12-wave workgroup per CU, 36 column blocks) or 32 (CMHAR_WGRAD3_CS=32:
+// two 6-wave workgroups per CU, 18 column blocks each, 80-B slab rows — each stages the dz chunk itself, and the two
+// run out of phase, one's LDS stores and barriers beside the other's MFMAs).  Round 6 (168 VGPRs,
+// 65 KB LDS, R3D tests green): layer 1 / 2 / 3 weight gradients 405.7 / 207.5 / 114.3 -> 524.9 / 288.7 / 154.5 us,
+// the R3D-18 step 2218 / 2253 -> 2192 / 2167 clips/s — the duplicated dz staging costs more than the overlap wins; 64)
+template <int CS> struct C3 {
+  static constexpr int NW = CS == 64 ? 12 : 6, NT = 64 * NW, CPT = CS / 16, NCB = 9 * CPT;
+  static constexpr int SLC = CS / 8, RSL = CS * 2 + 16;               // 16-B chunks per slab slot, slab row bytes
+  static constexpr int SLB = SQ * RSL, SL_N = SQ * SLC;
+  static constexpr int DZ_PER = (DZ_N + NT - 1) / NT, SL_PER = (SL_N + NT - 1) / NT;
+  static_assert(NCB == 3 * NW, "three column blocks per wave");
+};
 }  // namespace wr3
 
-__global__ __launch_bounds__(768, 1) void conv3d_wgrad_rows3(Geom g, int Cout, int R, int Ls, int cpf, int nchunk,
-                                                             int chunks_per_split, const bf16* __restrict__ x,
-                                                             const bf16* __restrict__ dz, float* __restrict__ out) {
+template <int CS>
+__global__ __launch_bounds__(wr3::C3<CS>::NT, CS == 64 ? 1 : 2) void conv3d_wgrad_rows3(
+    Geom g, int Cout, int R, int Ls, int cpf, int nchunk, int chunks_per_split, const bf16* __restrict__ x,
+    const bf16* __restrict__ dz, float* __restrict__ out) {
   using namespace wr3;
-  __shared__ __attribute__((aligned(16))) char smem[DZB + SLB];
+  typedef C3<CS> Q;
+  constexpr int NT = Q::NT, RSL = Q::RSL, SLC = Q::SLC, CPT = Q::CPT, DZ_PER = Q::DZ_PER, SL_PER = Q::SL_PER;
+  __shared__ __attribute__((aligned(16))) char smem[DZB + Q::SLB];
   char* const dzs = smem;
   char* const sls = smem + DZB;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int nct = g.C / 64, ncot = Cout / 64, ntile = g.kt * nct * ncot;
+  const int nct = g.C / CS, ncot = Cout / 64, ntile = g.kt * nct * ncot;
   const int lin = xcd_remap(blockIdx.x + ntile * blockIdx.y, ntile * gridDim.y);
   const int split = lin / ntile;
   int tl = lin % ntile;
@@ -1191,10 +1205,10 @@ __global__ __launch_bounds__(768, 1) void conv3d_wgrad_rows3(Geom g, int Cout, i
   int su[SL_PER], sb[SL_PER];
 #pragma unroll
   for (int i = 0; i < SL_PER; ++i) {
-    const int q = (i * NT + tid) >> 3;
+    const int q = (i * NT + tid) / SLC;
     su[i] = q / Ls;
     const int wi = q - su[i] * Ls - g.pw;
-    sb[i] = wi >= 0 && wi < g.W ? ((su[i] * g.W + wi) * g.C + ct * 64 + ((i * NT + tid) & 7) * 8) * 2 : -1;
+    sb[i] = wi >= 0 && wi < g.W ? ((su[i] * g.W + wi) * g.C + ct * CS + ((i * NT + tid) % SLC) * 8) * 2 : -1;
   }
   // fragment rows of this lane: slot k → (r, wo) → slab row r·Ls + wo (+ ih·Ls + iw per column block); slots past
   // the chunk's rows read row 0 (their dz is zero)
@@ -1207,7 +1221,7 @@ __global__ __launch_bounds__(768, 1) void conv3d_wgrad_rows3(Geom g, int Cout, i
 #pragma unroll
     for (int hh = 0; hh < 2; ++hh) {
       const int k = 32 * kk + 8 * gq + 4 * hh + q4;
-      sl_off[kk][hh] = (k < used_max ? (k / g.Wo) * Ls + (k % g.Wo) : 0) * RS + lane_col;
+      sl_off[kk][hh] = (k < used_max ? (k / g.Wo) * Ls + (k % g.Wo) : 0) * RSL + lane_col;
     }
   const int dz_off = (8 * gq + q4) * RS + lane_col;
   uint4_t rdz[DZ_PER], rsl[SL_PER];
@@ -1242,7 +1256,7 @@ __global__ __launch_bounds__(768, 1) void conv3d_wgrad_rows3(Geom g, int Cout, i
 #pragma unroll
     for (int i = 0; i < SL_PER; ++i) {
       const int e = i * NT + tid;
-      if (e < SL_N) *(uint4_t*)(sls + (e >> 3) * RS + (e & 7) * 16) = rsl[i];
+      if (e < Q::SL_N) *(uint4_t*)(sls + (e / SLC) * RSL + (e % SLC) * 16) = rsl[i];
     }
   };
   floatx4 acc[4][3];
@@ -1250,11 +1264,12 @@ __global__ __launch_bounds__(768, 1) void conv3d_wgrad_rows3(Geom g, int Cout, i
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 0; j < 3; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+  // column block cb = (ih, iw, 16-channel chunk cc) of this wave's three
   int cofs[3];
 #pragma unroll
   for (int j = 0; j < 3; ++j) {
-    const int cb = 3 * wave + j, ih = cb / 12, iw = (cb % 12) >> 2;
-    cofs[j] = (ih * Ls + iw) * RS + (cb & 3) * 32;
+    const int cb = 3 * wave + j, ih = cb / (3 * CPT), iw = (cb % (3 * CPT)) / CPT, cc = cb % CPT;
+    cofs[j] = (ih * Ls + iw) * RSL + cc * 32;
   }
   if (c_beg < c_end) {
     load(c_beg);
@@ -1292,8 +1307,8 @@ __global__ __launch_bounds__(768, 1) void conv3d_wgrad_rows3(Geom g, int Cout, i
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 0; j < 3; ++j) {
-      const int cb = 3 * wave + j, ih = cb / 12, iw = (cb % 12) >> 2;
-      const long col = ((long)(it * g.kh + ih) * g.kw + iw) * g.C + ct * 64 + (cb & 3) * 16 + (lane & 15);
+      const int cb = 3 * wave + j, ih = cb / (3 * CPT), iw = (cb % (3 * CPT)) / CPT, cc = cb % CPT;
+      const long col = ((long)(it * g.kh + ih) * g.kw + iw) * g.C + ct * CS + cc * 16 + (lane & 15);
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int co = cot * 64 + 16 * i + 4 * (lane >> 4) + r;
@@ -2563,7 +2578,19 @@ static int wgrad_splits(const Geom& g, int Cout, int& mlen) {
 // Row-slab weight-gradient plan (conv3d_wgrad_rows): kw = 3, whole output rows of <= 64 positions per chunk, the
 // chunk's input slab within MAXQ rows, Cout a multiple of 64.  Splits of the output-row chunks give ~2048 workgroups
 // (>= 4 chunks each); every split writes a full [Cout][K] partial (the kernel covers all K columns of its tiles).
-struct RowsPlan { int R, Ls, rows, cps, splits, cot, grp, cpf, nchunk; };
+struct RowsPlan { int R, Ls, rows, cps, splits, cot, grp, cpf, nchunk, cs; };
+// channels per workgroup of the nine-tap weight gradient (wr3::C3): CMHAR_WGRAD3_CS=32 / 64 overrides the default
+#ifndef CMHAR_WGRAD3_CS_DEFAULT
+#define CMHAR_WGRAD3_CS_DEFAULT 64
+#endif
+static int wgrad3_cs() {
+  static const int v = [] {
+    const char* e = getenv("CMHAR_WGRAD3_CS");
+    const int c = e ? atoi(e) : CMHAR_WGRAD3_CS_DEFAULT;
+    return c == 32 ? 32 : 64;
+  }();
+  return v;
+}
 static bool rows_plan(const Geom& g, int Cout, RowsPlan& p) {
   static const bool on = [] {
     const char* v = getenv("CMHAR_WGRAD_ROWS");
@@ -2589,12 +2616,13 @@ static bool rows_plan(const Geom& g, int Cout, RowsPlan& p) {
         (long)g.N * g.T * g.H * g.W * g.C * 2 <= (1L << 30) && (long)g.N * g.To * g.Ho * g.Wo * Cout * 2 <= (1L << 30)) {
       p.grp = 9;
       p.cot = 64;
+      p.cs = wgrad3_cs();
       p.R = R;
       p.Ls = Ls3;
       p.cpf = cpf;
       p.nchunk = g.N * g.To * p.cpf;
-      const int tiles = g.kt * (g.C / 64) * (Cout / 64);
-      // one 12-wave workgroup per CU: one full round (rounding the split count up gave R3D-18 layer 1 513
+      const int tiles = g.kt * (g.C / p.cs) * (Cout / 64);
+      // one 12-wave workgroup per CU (CS = 32: two 6-wave ones): one full round (rounding the split count up gave R3D-18 layer 1 513
       // workgroups: a third round of one; 512 = two rounds wrote twice the split partials — layer 1 382.1 -> 358.6 us,
       // layer 2 209.0 -> 199.5, layer 3 120.2 -> 110.4 at 256, step 2263 -> 2294 clips/s; 768 / 1024: 2189 / 2188),
       // >= 4 chunks each, <= ~80 MB of split partials
@@ -2602,7 +2630,7 @@ static bool rows_plan(const Geom& g, int Cout, RowsPlan& p) {
         const char* v = getenv("CMHAR_WGRAD3_WGS");
         return v ? max(1, atoi(v)) : 256;
       }();
-      int s = max(1, wgs / tiles);
+      int s = max(1, (p.cs == 64 ? wgs : 2 * wgs) / tiles);
       s = min(s, (int)((80L << 20) / ((long)Cout * g.K * 4)));
       s = max(1, min(s, p.nchunk / 4));
       p.cps = (p.nchunk + s - 1) / s;
@@ -2611,6 +2639,7 @@ static bool rows_plan(const Geom& g, int Cout, RowsPlan& p) {
       return true;
     }
   }
+  p.cs = 64;
   p.R = wr::SLOTS / g.Wo;
   p.Ls = (g.Wo - 1) * g.sw + g.kw;
   if (p.R * p.Ls > wr::MAXQ) return false;
@@ -2674,9 +2703,13 @@ extern "C" int cmhar_conv3d_wgrad(const int* dims, int Cout, const void* x, cons
     if (rp.splits > 1 && !ws) return -2;
     float* dst = rp.splits > 1 ? ws : dw;
     if (rp.grp == 9) {
-      const dim3 grid3(g.kt * (g.C / 64) * (Cout / 64), rp.splits);
-      conv3d_wgrad_rows3<<<grid3, wr3::NT, 0, stream>>>(g, Cout, rp.R, rp.Ls, rp.cpf, rp.nchunk, rp.cps,
-                                                        (const bf16*)x, (const bf16*)dz, dst);
+      const dim3 grid3(g.kt * (g.C / rp.cs) * (Cout / 64), rp.splits);
+      if (rp.cs == 32)
+        conv3d_wgrad_rows3<32><<<grid3, wr3::C3<32>::NT, 0, stream>>>(g, Cout, rp.R, rp.Ls, rp.cpf, rp.nchunk, rp.cps,
+                                                                      (const bf16*)x, (const bf16*)dz, dst);
+      else
+        conv3d_wgrad_rows3<64><<<grid3, wr3::C3<64>::NT, 0, stream>>>(g, Cout, rp.R, rp.Ls, rp.cpf, rp.nchunk, rp.cps,
+                                                                      (const bf16*)x, (const bf16*)dz, dst);
       if (rp.splits > 1) {
         const long slab = (long)Cout * g.K, n4 = slab / 4;
         conv3d_wgrad_reduce<<<grid_for(n4), 256, 0, stream>>>(n4, rp.splits, slab, ws, dw);
