@@ -2198,8 +2198,12 @@ int launch(int M, int N, int K, const bf16* A, long lda, const bf16* B, long ldb
   // epilogues with a streamed 16-bit operand run the PFS instantiation (the operand loaded two row groups ahead);
   // the others keep the plain store loop (CMHAR_EPI_PF2=0: never)
   const bool pfs = CMHAR_EPI_PF2 && sizeof(OutT) == 2 && epi_has_stream(e);
-    const int plan = gemm_plan(AK, BKc, M, N, K, splits, ws != nullptr, e.rowsum != nullptr,
-                               sizeof(OutT) == 2 && epi_persist_ok(e));
+    // (the persistent epilogue moves its streamed operands with 16-B vector accesses declared aligned: operands
+    // that are not 16-B aligned with 8-element leading dimensions keep the other kernels)
+    const auto al16 = [](const void* p, long ld) { return !p || (((uintptr_t)p & 15) == 0 && ld % 8 == 0); };
+    const bool pepi = sizeof(OutT) == 2 && epi_persist_ok(e) && al16(e.residual, e.ldr) && al16(e.aux_in, e.lda) &&
+                      al16(e.aux_out, e.ldo) && al16(C, ldc);
+    const int plan = gemm_plan(AK, BKc, M, N, K, splits, ws != nullptr, e.rowsum != nullptr, pepi);
     if (plan == PLAN_256_TAIL) {
       const TailSplit ts = tail_split(M, N, K);
       if (ph_gemm && pfs)
