@@ -70,7 +70,10 @@ int cmhar_gemm_bf16_plan(int layout, int M, int N, int K, int splits, int has_ws
 /* As cmhar_gemm_bf16_plan for a 16-bit output whose epilogue the persistent forward kernel takes (reads == 0: alpha
  * 1, no dropout / rowadd / beta; plain, the GELU pair, x aux_in or + residual) or not (reads != 0); 7 = the persistent
  * 8-phase forward kernel (whole-K forward-layout launches of at least three chip rounds of 256² tiles, an even K-tile
- * count, N <= 4096).  cmhar_gemm_bf16_plan answers for reads == 0. */
+ * count, N <= 4096; at run time also 16-B aligned C / epilogue operands with leading dimensions % 8 == 0).
+ * cmhar_gemm_bf16_plan answers for reads == 0.  A plan-7 launch with at least four K-tiles claims its tiles from a
+ * 64-B counter block the library allocates (hipMalloc) on the first such launch per (device, stream) and keeps for
+ * the process; each launch leaves it zeroed (CMHAR_PERSIST_DYNAMIC=0: the fixed tile walk, no allocation). */
 int cmhar_gemm_bf16_plan2(int layout, int M, int N, int K, int splits, int has_ws, int rowsum, int reads);
 /* cmhar_gemm_bf16 restricted to a phase mask: bit 0 = the GEMM kernel, bit 1 = the split-K / tail reduce (3 = the
  * whole call).  Calling phases 1 then 2 on one stream equals one cmhar_gemm_bf16 call; bench.py uses the split to
