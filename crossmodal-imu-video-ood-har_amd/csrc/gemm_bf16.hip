@@ -640,6 +640,11 @@ __global__ __launch_bounds__(NT, 2) void gemm_bf16_kernel(int M, int N, int K, c
 #ifndef CMHAR_NT_REDUCE_LOAD
 #define CMHAR_NT_REDUCE_LOAD 1
 #endif
+// slabs whose loads the reduce keeps in flight together (A/B knob; 8 measured the same as 4 on the weight-gradient
+// reduces in round 6: QKV / FC1 / FC2 wgrad + reduce 176.4 / 226.4 / 239.2 vs 177.0 / 227.0 / 237.5 us)
+#ifndef CMHAR_REDUCE_DEPTH
+#define CMHAR_REDUCE_DEPTH 4
+#endif
 // Sum split-K fp32 partial slabs and apply the epilogue; 8 consecutive columns per thread when N % 8 == 0.
 // m_base: the slabs hold rows m_base .. m_base+M-1 of C (tail-split hybrid); 0 for a plain split-K GEMM.
 template <typename OutT>
@@ -664,15 +669,16 @@ __global__ void splitk_reduce_kernel(int M, int N, int splits, const float* __re
 #pragma unroll
       for (int j = 0; j < 4; ++j) { s[j] += a[j]; s[4 + j] += b[j]; }
     };
-    // four slabs' loads in flight before they are added in slab order (one pair per iteration left the reduce
+    // RD slabs' loads in flight before they are added in slab order (one pair per iteration left the reduce
     // latency-bound); same order of additions, same bits
+    constexpr int RD = CMHAR_REDUCE_DEPTH;
     int z = 0;
-    for (; z + 3 < splits; z += 4) {
-      floatx4 a[4], b[4];
+    for (; z + RD - 1 < splits; z += RD) {
+      floatx4 a[RD], b[RD];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) ld(z + u, a[u], b[u]);
+      for (int u = 0; u < RD; ++u) ld(z + u, a[u], b[u]);
 #pragma unroll
-      for (int u = 0; u < 4; ++u) add(a[u], b[u]);
+      for (int u = 0; u < RD; ++u) add(a[u], b[u]);
     }
     for (; z < splits; ++z) {
       floatx4 a, b;
