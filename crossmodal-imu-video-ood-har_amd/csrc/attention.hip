@@ -643,8 +643,17 @@ __global__ __launch_bounds__(256, 3) void attn_fwd_bf16(int H, int Lq, int Lk, i
 // the launch passes scale = 1/log2e, so c = 1 and p = exp2(acc) needs no multiply per score (−6 % backward time:
 // the kernels are VALU-issue bound beside their MFMAs); kscale is the dK output factor (the true softmax scale, so
 // dK is the gradient of the unscaled key and the QKV backward is unchanged).
+// CMHAR_ATTN_DKDV_PIPE = 1 (A/B knob): the tile's two 32-query blocks software-pipelined — block 1's S / dP MFMA
+// chains issued right after block 0's, ahead of block 0's exp / dS VALU, which then runs while the matrix pipe works
+// through block 1's chains (and block 1's VALU beside block 0's dV / dK MFMAs); both blocks' S / dP live at once, so
+// two waves per SIMD (210 VGPRs).  Same operations per element in the same order: identical bits.  Round 6
+// (tools/debug/attn_ab.py): backward 858.2 -> 897.9 us per layer — three waves per SIMD interleave better than the
+// explicit pipeline at two; off.
+#ifndef CMHAR_ATTN_DKDV_PIPE
+#define CMHAR_ATTN_DKDV_PIPE 0
+#endif
 template <bool PS = false>
-__global__ __launch_bounds__(256, 3) void attn_bwd_dkdv_bf16(int H, int Lq, int Lk, int k_base,
+__global__ __launch_bounds__(256, CMHAR_ATTN_DKDV_PIPE ? 2 : 3) void attn_bwd_dkdv_bf16(int H, int Lq, int Lk, int k_base,
                                                              const bf16* __restrict__ Q,
                                                              long ldq, const bf16* __restrict__ K, long ldk,
                                                              const bf16* __restrict__ V, long ldv,
@@ -727,9 +736,56 @@ __global__ __launch_bounds__(256, 3) void attn_bwd_dkdv_bf16(int H, int Lq, int 
     else if (more && pos == 2) load_q(qt + 1, Qs(cur ^ 1));
     const float* L_ = Ls + cur * 64;
     const float* D_ = Ds + cur * 64;
+    if (CMHAR_ATTN_DKDV_PIPE && active) {
+      floatx16 s[2], dp[2];
+      auto chain = [&](int qb) __attribute__((always_inline)) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int q = qb * 32 + acc_row(r, h);
+          s[qb][r] = L_[q];
+          dp[qb][r] = D_[q];
+        }
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          s[qb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag(Qs(cur), qb * 32, t, lane), kf[t], s[qb], 0, 0, 0);
+          dp[qb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag(Gs(cur), qb * 32, t, lane), vf[t], dp[qb], 0, 0, 0);
+        }
+      };
+      auto finish_block = [&](int qb) __attribute__((always_inline)) {
+        bf16x8 pbv[2], dbv[2];
+#pragma unroll
+        for (int r = 0; r < 16; r += 2) {
+          const float2_t pv = PS ? float2_t{fexp2(s[qb][r]), fexp2(s[qb][r + 1])}
+                                 : float2_t{fexp2(s[qb][r] * c), fexp2(s[qb][r + 1] * c)};
+          const float2_t dv2 = pv * float2_t{dp[qb][r], dp[qb][r + 1]};
+          const bf16x2_t pp = __builtin_convertvector(pv, bf16x2_t);
+          const bf16x2_t dd = __builtin_convertvector(dv2, bf16x2_t);
+          pbv[r >> 3][r & 7] = pp[0];
+          pbv[r >> 3][(r & 7) + 1] = pp[1];
+          dbv[r >> 3][r & 7] = dd[0];
+          dbv[r >> 3][(r & 7) + 1] = dd[1];
+        }
+#pragma unroll
+        for (int ss = 0; ss < 2; ++ss) {
+          const bf16x8 pb = pbv[ss], db = dbv[ss];
+#pragma unroll
+          for (int d = 0; d < 2; ++d) {
+            dv[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_frag(Gs(cur), qb * 32, ss, d * 32, lane), pb, dv[d], 0, 0, 0);
+            dk[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_frag(Qs(cur), qb * 32, ss, d * 32, lane), db, dk[d], 0, 0, 0);
+          }
+        }
+      };
+      chain(0);
+      __builtin_amdgcn_sched_barrier(0);
+      chain(1);
+      __builtin_amdgcn_sched_barrier(0);
+      finish_block(0);
+      __builtin_amdgcn_sched_barrier(0);
+      finish_block(1);
+    }
 #pragma unroll
     for (int qb = 0; qb < 2; ++qb) {
-      if (!active) break;
+      if (!active || CMHAR_ATTN_DKDV_PIPE) break;
       // S = Q·Kᵀ (key on lane), pre-loaded with -lse/c so that p = exp2(c*acc)
       floatx16 s, dp;
 #pragma unroll
