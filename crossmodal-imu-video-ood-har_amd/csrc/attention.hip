@@ -41,6 +41,15 @@ typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2_t;
 // trip, no ds_write): each wave issues 2 of the tile's 8 pieces of 1 KiB (8 rows × 128 B); the DMA's LDS destination
 // is lane-linear, so the att_off XOR swizzle is applied to each lane's SOURCE chunk (an involution).  Rows at or past
 // `rows_total` fall outside the buffer resource's num_records and read as zero.  Per-lane offsets are computed once; a tile costs two scalar resource updates and 2 DMA instructions.
+// CMHAR_ATTN_ASM_DMA = 1: the pieces issued by inline asm (as the GEMM's dma_asm, gemm_bf16.hip): with the builtin,
+// hipcc sees an LDS write in flight and puts `s_waitcnt vmcnt(0)` in front of the first transposed LDS read
+// (ds_read_b64_tr_b16) that follows — in the backward kernels that drained the NEXT tile's DMA near the start of every
+// tile's MFMAs.  The kernels order every DMA themselves (vmcnt waits + barriers), as with the builtin.  M0 is written
+// without the compiler knowing: every LDS-DMA of this file goes through TileDma, so no compiler-generated M0 use shares
+// a kernel with it.
+#ifndef CMHAR_ATTN_ASM_DMA
+#define CMHAR_ATTN_ASM_DMA 1
+#endif
 struct TileDma {
   const char* base;   // row 0 of the head slice
   long row_bytes;     // ld * 2
@@ -61,10 +70,26 @@ struct TileDma {
     const long off = (long)r0 * row_bytes;
     const long left = valid - off;
     const int nrec = (int)(left > 0 ? (left < 0x7fffffff ? left : 0x7fffffff) : 0);
-    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)(base + off), (short)0, nrec, 0x00020000);
+    if constexpr (CMHAR_ATTN_ASM_DMA) {
+      const unsigned long long a = (unsigned long long)(base + off);
+      uint4_t rs;
+      rs[0] = __builtin_amdgcn_readfirstlane((unsigned)a);
+      rs[1] = __builtin_amdgcn_readfirstlane((unsigned)(a >> 32)) & 0xffffu;
+      rs[2] = __builtin_amdgcn_readfirstlane((unsigned)nrec);
+      rs[3] = 0x00020000u;
 #pragma unroll
-    for (int t = 0; t < 2; ++t)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (att_lds_ptr)(lds + (2 * wave + t) * 1024), 16, voff[t], 0, 0, 0);
+      for (int t = 0; t < 2; ++t) {
+        const unsigned la = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(att_lds_ptr)(lds + (2 * wave + t) * 1024));
+        // (s_nop: the SALU write of M0 needs one wait state before the LDS-DMA reads it)
+        asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds" :: "s"(la), "v"(voff[t]),
+                     "s"(rs) : "memory");
+      }
+    } else {
+      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)(base + off), (short)0, nrec, 0x00020000);
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (att_lds_ptr)(lds + (2 * wave + t) * 1024), 16, voff[t], 0, 0, 0);
+    }
   }
 };
 
@@ -169,7 +194,7 @@ __device__ __forceinline__ void fwd_tail_group(char* smem, int H, int Lq, int Lk
                                                long ldk, const bf16* __restrict__ V, long ldv, E* __restrict__ O,
                                                long ldo, float* __restrict__ lse, float scale) {
   // smem: NBUF × [K 128 rows 16 KB | V 16 KB]; the merge's O partials reuse the first 32 KB, its m / l the next 1 KB
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6), h = lane >> 5;
   const bf16* Kb = K + (long)b * Lk * ldk + hd * 64;
   const bf16* Vb = V + (long)b * Lk * ldv + hd * 64;
   const float c = scale * LOG2E;
@@ -295,7 +320,7 @@ __device__ __forceinline__ void dkdv_tail_group(char* smem, int H, int Lq, int L
   // smem: NBUF × [Q 128 rows 16 KB | dO 16 KB], then NBUF × 128 −lse/c and NBUF × 128 −δ; the merge reuses 32 KB
   float* Ls = (float*)(smem + NBUF * 32768);
   float* Ds = Ls + NBUF * 128;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6), h = lane >> 5;
   const bf16* Qb = Q + (long)b * Lq * ldq + hd * 64;
   const bf16* Gb = dO + (long)b * Lq * lddo + hd * 64;
   const float* lseb = lse + ((long)b * H + hd) * Lq;
@@ -309,6 +334,11 @@ __device__ __forceinline__ void dkdv_tail_group(char* smem, int H, int Lq, int L
     kf[t] = *(const bf16x8*)(K + ((long)b * Lk + myk) * ldk + hd * 64 + 16 * t + 8 * h);
     vf[t] = *(const bf16x8*)(V + ((long)b * Lk + myk) * ldv + hd * 64 + 16 * t + 8 * h);
   }
+  // (register operands retired here, before the tile loop: otherwise the compiler's wait for these loads sits inside
+  // the loop, counted as if its own loads were the only memory operations in flight — with the DMA issued by inline
+  // asm (CMHAR_ATTN_ASM_DMA) that stalled every tile on the next tile's DMA)
+#pragma unroll
+  for (int t = 0; t < 4; ++t) asm volatile("" :: "v"(kf[t]), "v"(vf[t]));
   floatx16 dk[2], dv[2];
 #pragma unroll
   for (int d = 0; d < 2; ++d)
@@ -323,11 +353,12 @@ __device__ __forceinline__ void dkdv_tail_group(char* smem, int H, int Lq, int L
     char* buf = smem + (st % NBUF) * 32768;
     stage128(tq, st * 128, buf, wave);
     stage128(tg, st * 128, buf + 16384, wave);
-    if (tid < 128) {
-      const int q = st * 128 + tid;
-      lv = q < Lq ? -lseb[q] * inv_c : -INFINITY;
-      dv_ = q < Lq ? -delb[q] : 0.f;
-    }
+    // every lane loads (clamped row; only threads < 128 store): a branch-guarded load got a vmcnt(0) right after
+    // it, draining the tile DMA just issued (as the bulk kernel's load_rows)
+    const int q = st * 128 + (tid & 127);
+    const float lr = lseb[min(q, Lq - 1)], dr = delb[min(q, Lq - 1)];
+    lv = q < Lq ? -lr * inv_c : -INFINITY;
+    dv_ = q < Lq ? -dr : 0.f;
   };
   auto store_consts = [&](int st) {
     if (tid < 128) { Ls[(st % NBUF) * 128 + tid] = lv; Ds[(st % NBUF) * 128 + tid] = dv_; }
@@ -481,7 +512,7 @@ __global__ __launch_bounds__(256, 3) void attn_fwd_bf16(int H, int Lq, int Lk, i
   __shared__ __attribute__((aligned(16))) char smem[4 * 8192 + 1024];   // +1 KB: a folded tail group's merge
 #define Ks(buf) (smem + 8192 * (buf))
 #define Vs(buf) (smem + 16384 + 8192 * (buf))
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6), h = lane >> 5;
   BlkIdx bi;
   if (tail_block(ntail, H, bi)) {   // ntail > 0: this workgroup is the 32-query tail group bi.blk of its head
     fwd_tail_group<E, 1>(smem, H, Lq, Lk, q_tail0 + 32 * bi.blk, bi.hd, bi.b, Q, ldq, K, ldk, V, ldv, O, ldo, lse,
@@ -502,6 +533,13 @@ __global__ __launch_bounds__(256, 3) void attn_fwd_bf16(int H, int Lq, int Lk, i
 #pragma unroll
     for (int t = 0; t < 4; ++t) qf[j][t] = *(const bf16x8*)(Qb + (long)myq * ldq + 16 * t + 8 * h);
   }
+  // (register operands retired here, before the tile loop: otherwise the compiler's wait for these loads sits inside
+  // the loop, counted as if its own loads were the only memory operations in flight — with the DMA issued by inline
+  // asm (CMHAR_ATTN_ASM_DMA) that stalled every tile on the next tile's DMA)
+#pragma unroll
+  for (int j = 0; j < QB; ++j)
+#pragma unroll
+    for (int t = 0; t < 4; ++t) asm volatile("" :: "v"(qf[j][t]));
   floatx16 o[QB][2];
 #pragma unroll
   for (int j = 0; j < QB; ++j)
@@ -667,7 +705,7 @@ __global__ __launch_bounds__(256, CMHAR_ATTN_DKDV_PIPE ? 2 : 3) void attn_bwd_dk
 #define Gs(buf) (smem + 16384 + 8192 * (buf))
   float* Ls = (float*)(smem + 32768);          // [2][64] lse
   float* Ds = Ls + 128;                         // [2][64] delta
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6), h = lane >> 5;
   BlkIdx bi;
   if (tail_block(ntail, H, bi)) {   // ntail > 0: the 32-key tail group bi.blk of its head (same 33 KB of LDS)
     dkdv_tail_group<PS, 1>(smem, H, Lq, Lk, k_tail0 + 32 * bi.blk, bi.hd, bi.b, Q, ldq, K, ldk, V, ldv, dO, lddo, lse,
@@ -690,6 +728,11 @@ __global__ __launch_bounds__(256, CMHAR_ATTN_DKDV_PIPE ? 2 : 3) void attn_bwd_dk
     kf[t] = *(const bf16x8*)(K + ((long)b * Lk + myk) * ldk + hd * 64 + 16 * t + 8 * h);
     vf[t] = *(const bf16x8*)(V + ((long)b * Lk + myk) * ldv + hd * 64 + 16 * t + 8 * h);
   }
+  // (register operands retired here, before the tile loop: otherwise the compiler's wait for these loads sits inside
+  // the loop, counted as if its own loads were the only memory operations in flight — with the DMA issued by inline
+  // asm (CMHAR_ATTN_ASM_DMA) that stalled every tile on the next tile's DMA)
+#pragma unroll
+  for (int t = 0; t < 4; ++t) asm volatile("" :: "v"(kf[t]), "v"(vf[t]));
   floatx16 dk[2], dv[2];
 #pragma unroll
   for (int d = 0; d < 2; ++d)
@@ -885,7 +928,7 @@ __global__ __launch_bounds__(256, QB == 1 ? 3 : 2) void attn_bwd_dq_bf16(int H, 
 #undef Vs
 #define Ks(buf) (smem + 8192 * (buf))
 #define Vs(buf) (smem + 8192 * NB + 8192 * (buf))
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6), h = lane >> 5;
   const BlkIdx bi = flash_block(H);
   const int hd = bi.hd, b = bi.b;
   const int q0 = q_base + bi.blk * (128 * QB) + wave * (32 * QB);
@@ -913,6 +956,15 @@ __global__ __launch_bounds__(256, QB == 1 ? 3 : 2) void attn_bwd_dq_bf16(int H, 
     d_ = pair_sum(d_);
     Dl[j] = d_;
     if (h == 0 && q0 + 32 * j + (lane & 31) < Lq) delta[((long)b * H + hd) * Lq + myq] = d_;
+  }
+  // (register operands retired here, before the tile loop: otherwise the compiler's wait for these loads sits inside
+  // the loop, counted as if its own loads were the only memory operations in flight — with the DMA issued by inline
+  // asm (CMHAR_ATTN_ASM_DMA) that stalled every tile on the next tile's DMA)
+#pragma unroll
+  for (int j = 0; j < QB; ++j) {
+    asm volatile("" :: "v"(sL[j]), "v"(Dl[j]));
+#pragma unroll
+    for (int t = 0; t < 4; ++t) asm volatile("" :: "v"(qf[j][t]), "v"(gf[j][t]));
   }
   floatx16 dq[QB][2];
 #pragma unroll
@@ -1055,7 +1107,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_tail_bf16(int H, int Lq, i
                                                                 float* __restrict__ delta, bf16* __restrict__ dQ,
                                                                 long lddq, float scale) {
   __shared__ __attribute__((aligned(16))) char smem[65536];   // [2 buf][K 16 KB | V 16 KB]
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6), h = lane >> 5;
   const int hd = blockIdx.y, b = blockIdx.z;
   const int q_base = q_base0 + 32 * blockIdx.x;   // grid.x = ⌈tail / 32⌉ groups of 32 rows
   const bf16* Kb = K + (long)b * Lk * ldk + hd * 64;
