@@ -57,6 +57,7 @@ _SIGS = {
                                         C.POINTER(Epilogue), vp, vp]),
     'cmhar_attention_fwd': (i32, [i32, i32, i32, i32, i32, i32, vp, i64, vp, i64, vp, i64, vp, i64, vp, f32, f32, u64,
                                   vp]),
+    'cmhar_attention_fwd_opt': (i32, [i32]),
     'cmhar_attention_bwd': (i32, [i32, i32, i32, i32, i32, i32, vp, i64, vp, i64, vp, i64, vp, i64, vp, i64, vp, vp,
                                   vp, i64, vp, i64, vp, i64, f32, f32, u64, vp]),
     'cmhar_attention_bwd_prescaled': (i32, [i32, i32, i32, i32, vp, i64, vp, i64, vp, i64, vp, i64, vp, i64, vp, vp,

@@ -371,6 +371,13 @@ def attention_fwd(q, k, v, out, lse, *, B, H, Lq, Lk, D, scale, pdrop=0.0, seed=
     return out
 
 
+def attention_fwd_opt(mode=-1):
+    """The bf16 / fp16 flash forward's bulk launch mode: 1 = optimistic running max + exact rerun of the workgroups
+    whose rows left its range (default), 0 = one exact lazy-rescale launch; mode < 0 only queries.  Returns the
+    previous mode (`cmhar_attention_fwd_opt`)."""
+    return L.lib().cmhar_attention_fwd_opt(int(mode))
+
+
 def attention_bwd(q, k, v, o, do, lse, dq, dk, dv, *, B, H, Lq, Lk, D, scale, pdrop=0.0, seed=0):
     for t, n, Lx in ((q, 'q', Lq), (k, 'k', Lk), (v, 'v', Lk), (o, 'o', Lq), (do, 'do', Lq), (dq, 'dq', Lq),
                      (dk, 'dk', Lk), (dv, 'dv', Lk)):

@@ -14,7 +14,11 @@
 #include "common.h"
 #include "rowops.h"
 
+#include <atomic>
+#include <cstdlib>
 #include <initializer_list>
+#include <map>
+#include <mutex>
 #include <type_traits>
 #include <utility>
 
@@ -503,15 +507,31 @@ __device__ __forceinline__ bool tail_block(int ntail, int H, BlkIdx& bi) {
 #ifndef CMHAR_ATTN_FWD_ONE_LAUNCH
 #define CMHAR_ATTN_FWD_ONE_LAUNCH 0
 #endif
-template <typename E, int QB>
+// OPT (optimistic running max, the default bulk launch; CMHAR_ATTN_FWD_OPT=0 at run time: one exact launch): after a
+// row's first 32 keys the running max m is frozen — no half-tile max, no rescale (16 max + a lane swap per q-block
+// and half: ~12 % of the VALU issue the forward is bound on).  The weights p = 2^(c·s − m) are then ≤ 2^64 for every
+// row whose later scores stay within 64 (log2 units) of its first keys' max; a row past that shows as a half-tile sum
+// above 2^64 (or not finite) on the MFMA row sum, its workgroup sets flag[wg], and a second launch of the exact
+// kernel (gate = flag) recomputes exactly the flagged workgroups (the others return at once) and clears their flags.
+// p ≤ 2^64 keeps l and O (fp32) far from overflow and bf16 P at full relative precision at any scale, so the result
+// is as accurate as the lazy-rescale form, not bit-identical to it (other weight scales); lse = m + log2 l is exact
+// either way.  Round 6 (tools/debug/attn_ab.py): 336.6 -> 289.1 us per layer (the optimistic kernel alone).
+#ifndef CMHAR_ATTN_FWD_OPT
+#define CMHAR_ATTN_FWD_OPT 1
+#endif
+template <typename E, int QB, bool OPT = false>
 __global__ __launch_bounds__(256, 3) void attn_fwd_bf16(int H, int Lq, int Lk, int q_base, const bf16* __restrict__ Q,
                                                         long ldq, const bf16* __restrict__ K, long ldk,
                                                         const bf16* __restrict__ V, long ldv, E* __restrict__ O,
                                                         long ldo, float* __restrict__ lse, float scale,
-                                                        int ntail, int q_tail0) {
+                                                        int ntail, int q_tail0, int* __restrict__ flag) {
+  static_assert(!OPT || CMHAR_ATTN_LSUM_MFMA, "the optimistic forward checks the MFMA row sums");
   __shared__ __attribute__((aligned(16))) char smem[4 * 8192 + 1024];   // +1 KB: a folded tail group's merge
 #define Ks(buf) (smem + 8192 * (buf))
 #define Vs(buf) (smem + 16384 + 8192 * (buf))
+  const int wg = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+  // exact kernel with a gate (the optimistic launch's flags): only the flagged workgroups run
+  if (!OPT && flag && flag[wg] == 0) return;
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6), h = lane >> 5;
   BlkIdx bi;
   if (tail_block(ntail, H, bi)) {   // ntail > 0: this workgroup is the 32-query tail group bi.blk of its head
@@ -550,6 +570,7 @@ __global__ __launch_bounds__(256, 3) void attn_fwd_bf16(int H, int Lq, int Lk, i
   float m[QB], l[QB];
 #pragma unroll
   for (int j = 0; j < QB; ++j) { m[j] = -INFINITY; l[j] = 0.f; }
+  bool bad = false;   // OPT: a row of this lane left the optimistic range
 
   const int nt = (Lk + 63) / 64;
   TileDma tk, tv;
@@ -606,6 +627,7 @@ __global__ __launch_bounds__(256, 3) void attn_fwd_bf16(int H, int Lq, int Lk, i
         bf16x8 pb[QB][2];
 #pragma unroll
         for (int j = 0; j < QB; ++j) {
+          if (!OPT || kbase + kb == 0) {
           float mt = -INFINITY;
 #pragma unroll
           for (int r = 0; r < 16; ++r) mt = fmaxf(mt, s[j][r]);
@@ -624,6 +646,7 @@ __global__ __launch_bounds__(256, 3) void attn_fwd_bf16(int H, int Lq, int Lk, i
 #pragma unroll
               for (int r = 0; r < 16; ++r) o[j][d][r] *= alpha;
           }
+          }
           const float mn = m[j];
 #pragma unroll
           for (int r = 0; r < 16; ++r) {
@@ -641,6 +664,7 @@ __global__ __launch_bounds__(256, 3) void attn_fwd_bf16(int H, int Lq, int Lk, i
             floatx4 ls = mma16<E>(lsel, pb[j][0], floatx4{0.f, 0.f, 0.f, 0.f});
             ls = mma16<E>(lsel, pb[j][1], ls);
             l[j] += ls[0];
+            if (OPT) bad = bad || !(ls[0] <= 0x1p64f);
           }
         }
         PRIO_HI();
@@ -671,6 +695,11 @@ __global__ __launch_bounds__(256, 3) void attn_fwd_bf16(int H, int Lq, int Lk, i
       store_row64<E>(O + ((long)b * Lq + q) * ldo + hd * 64, o[j], inv, h);
       if (h == 0) lse[((long)b * H + hd) * Lq + q] = m[j] + log2f(lj);   // log2-domain LSE of (scale*log2e)*s
     }
+  }
+  if (OPT) {
+    if (__builtin_amdgcn_ballot_w64(bad) != 0 && lane == 0) flag[wg] = 1;   // the exact launch redoes this workgroup
+  } else if (flag && tid == 0) {
+    flag[wg] = 0;   // gated rerun done (every wave read the flag before the tile loop's barriers)
   }
 }
 
@@ -1390,10 +1419,45 @@ static bool f32m_ok(int dtype, int D, float pdrop, std::initializer_list<std::pa
   return true;
 }
 
+// The optimistic forward's workgroup flags: one zeroed int block per (device, stream), grown (never freed: a launch
+// still in flight may hold the old one) to the largest bulk grid seen; every flag is 0 again after each forward
+// (set by the optimistic launch, cleared by the gated exact launch behind it on the same stream).
+static int* fwd_flags(hipStream_t st, long n) {
+  static std::mutex mu;
+  static std::map<std::pair<int, hipStream_t>, std::pair<int*, long>> blocks;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+  std::lock_guard<std::mutex> lk(mu);
+  auto& e = blocks[{dev, st}];
+  if (e.first && e.second >= n) return e.first;
+  void* p = nullptr;
+  if (hipMalloc(&p, n * sizeof(int)) != hipSuccess) return nullptr;
+  if (hipMemsetAsync(p, 0, n * sizeof(int), st) != hipSuccess) return nullptr;
+  e = {(int*)p, n};
+  return (int*)p;
+}
+static std::atomic<int> g_fwd_opt{-1};   // -1: CMHAR_ATTN_FWD_OPT from the environment (default: the build's)
+static bool fwd_opt_on() {
+  int v = g_fwd_opt.load();
+  if (v < 0) {
+    const char* s = getenv("CMHAR_ATTN_FWD_OPT");
+    v = s ? (atoi(s) != 0) : (CMHAR_ATTN_FWD_OPT != 0);
+    g_fwd_opt.store(v);
+  }
+  return v != 0;
+}
+
 // ----------------------------------------------------------------------------------------------------------------
 // C ABI.  Tensors are [B*L, ld] row-major with head h at columns h*D .. h*D+D-1.
 // lse / delta: fp32 [B*H*Lq] workspaces owned by the caller.
 // ----------------------------------------------------------------------------------------------------------------
+// The bf16 / fp16 flash forward's bulk launch: optimistic + gated exact (1) or one exact launch (0); mode < 0 only
+// queries.  Returns the previous mode.
+extern "C" int cmhar_attention_fwd_opt(int mode) {
+  const int prev = fwd_opt_on() ? 1 : 0;
+  if (mode >= 0) g_fwd_opt.store(mode != 0);
+  return prev;
+}
 extern "C" int cmhar_attention_fwd(int dtype, int B, int H, int Lq, int Lk, int D, const void* Q, long ldq,
                                    const void* K, long ldk, const void* V, long ldv, void* O, long ldo, float* lse,
                                    float scale, float pdrop, unsigned long long seed, hipStream_t st) {
@@ -1406,12 +1470,23 @@ extern "C" int cmhar_attention_fwd(int dtype, int B, int H, int Lq, int Lk, int 
     const bool tail = Lq > bulk && Lq - bulk <= CMHAR_ATTN_TAIL;
     // the tail's 32-query groups folded into the bulk launch (tail_block), or a launch of their own
     const int fold = tail && bulk > 0 && CMHAR_ATTN_FOLD_FWD ? cdiv(Lq - bulk, 32) : 0;
+    // the optimistic bulk launch and its gated exact rerun (see attn_fwd_bf16's OPT)
+    int* const flags = bulk > 0 && fwd_opt_on() ? fwd_flags(st, (long)(bulk / 256 + fold) * H * B) : nullptr;
 #define FL(E)                                                                                                    \
   do {                                                                                                           \
-    if (bulk > 0)                                                                                                \
+    if (bulk > 0 && flags) {                                                                                     \
+      attn_fwd_bf16<E, 2, true><<<dim3(bulk / 256 + fold, H, B), 256, 0, st>>>(                                  \
+          H, Lq, Lk, 0, (const bf16*)Q, ldq, (const bf16*)K, ldk, (const bf16*)V, ldv, (E*)O, ldo, lse, scale, fold, \
+          bulk, flags);                                                                                          \
       attn_fwd_bf16<E, 2><<<dim3(bulk / 256 + fold, H, B), 256, 0, st>>>(H, Lq, Lk, 0, (const bf16*)Q, ldq,         \
                                                                          (const bf16*)K, ldk, (const bf16*)V, ldv, \
-                                                                         (E*)O, ldo, lse, scale, fold, bulk);    \
+                                                                         (E*)O, ldo, lse, scale, fold, bulk,     \
+                                                                         flags);                                 \
+    } else if (bulk > 0)                                                                                         \
+      attn_fwd_bf16<E, 2><<<dim3(bulk / 256 + fold, H, B), 256, 0, st>>>(H, Lq, Lk, 0, (const bf16*)Q, ldq,         \
+                                                                         (const bf16*)K, ldk, (const bf16*)V, ldv, \
+                                                                         (E*)O, ldo, lse, scale, fold, bulk,     \
+                                                                         nullptr);                               \
     if (tail && !fold)                                                                                           \
       attn_fwd_tail_bf16<E><<<dim3(cdiv(Lq - bulk, 32), H, B), 256, 0, st>>>(H, Lq, Lk, bulk, (const bf16*)Q, ldq,   \
                                                                              (const bf16*)K, ldk,                \
@@ -1419,7 +1494,7 @@ extern "C" int cmhar_attention_fwd(int dtype, int B, int H, int Lq, int Lk, int 
     else if (Lq > bulk && !tail)   /* (folded tail groups: nothing left to launch) */                        \
       attn_fwd_bf16<E, 1><<<dim3(cdiv(Lq - bulk, 128), H, B), 256, 0, st>>>(H, Lq, Lk, bulk, (const bf16*)Q, ldq,   \
                                                                             (const bf16*)K, ldk, (const bf16*)V, ldv, \
-                                                                            (E*)O, ldo, lse, scale, 0, 0);       \
+                                                                            (E*)O, ldo, lse, scale, 0, 0, nullptr); \
   } while (0)
     if (dtype == CMHAR_F16) FL(f16); else FL(bf16);
 #undef FL

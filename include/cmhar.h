@@ -107,6 +107,10 @@ int cmhar_gemm_generic_splitk(int in_dtype, int out_dtype, int M, int N, int K, 
 int cmhar_attention_fwd(int dtype, int B, int H, int Lq, int Lk, int D, const void* Q, long ldq, const void* K,
                         long ldk, const void* V, long ldv, void* O, long ldo, float* lse, float scale, float pdrop,
                         unsigned long long seed, hipStream_t stream);
+/* The bf16 / fp16 D = 64 flash forward's bulk launch: 1 = optimistic running max (frozen after a row's first 32
+ * keys, no rescale) + an exact rerun of the workgroups whose rows left its range (the default; env
+ * CMHAR_ATTN_FWD_OPT), 0 = one exact lazy-rescale launch.  mode < 0 only queries.  Returns the previous mode. */
+int cmhar_attention_fwd_opt(int mode);
 int cmhar_attention_bwd(int dtype, int B, int H, int Lq, int Lk, int D, const void* Q, long ldq, const void* K,
                         long ldk, const void* V, long ldv, const void* O, long ldo, const void* dO, long lddo,
                         const float* lse, float* delta, void* dQ, long lddq, void* dK, long lddk, void* dV, long lddv,
