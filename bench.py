@@ -585,7 +585,8 @@ def main():
     torch.cuda.synchronize()
     first_loss = float(loss.float().mean().item()) if loss is not None else float('nan')
     # every traced label is one kernel symbol except the two-kernel attention backward entry
-    single = {k: v for k, v in breakdown.items() if '(' not in k}
+    # (the hipBLASLt label spans several vendor kernels, one per shape: not a single-kernel candidate)
+    single = {k: v for k, v in breakdown.items() if '(' not in k and k != 'hipblaslt_linear'}
     dominant = max(single.items(), key=lambda kv: kv[1][1])[0] if single else None
     if world > 1:
         dist.barrier()
