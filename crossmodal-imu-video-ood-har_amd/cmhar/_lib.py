@@ -135,8 +135,8 @@ _SIGS = {
     'cmhar_mt_transpose_bf16': (i32, [vp, i32, i32, vp]),
     'cmhar_mfma_peak_probe_flops': (i64, [i32, i32, i32]),
     'cmhar_mfma_peak_probe': (i32, [i32, i32, i32, vp, i32, vp, vp]),
-    'cmhar_blaslt_linear': (i32, [i32, i32, i32, vp, i64, vp, i64, vp, i64, vp, vp, i64, vp]),
-    'cmhar_blaslt_linear_ok': (i32, [i32, i32, i32, i64, i64, i64, i32, i32, i64]),
+    'cmhar_blaslt_linear': (i32, [i32, i32, i32, i32, vp, i64, vp, i64, vp, i64, vp, vp, i64, vp]),
+    'cmhar_blaslt_linear_ok': (i32, [i32, i32, i32, i32, i64, i64, i64, i32, i32, i64]),
 }
 
 EXPORTED = tuple(_SIGS)

@@ -149,7 +149,7 @@ def _generic_splits(M, N, K):
     return max(1, min(32, math.ceil(128 / tiles), K // 64))
 
 
-# Plain library GEMMs on hipBLASLt (`cmhar_blaslt_linear`): the forward-layout bf16 shapes listed in CMHAR_BLASLT
+# Plain library GEMMs on hipBLASLt (`cmhar_blaslt_linear`): the forward-layout bf16 / fp16 shapes listed in CMHAR_BLASLT
 # ("N,K" pairs separated by ';'; empty = none), with at most a bias and a residual in the epilogue and at least 4096
 # rows.  Default: the N = 768 launches of the VideoMAE step — attention output projection forward and input gradient
 # (768,768), FC2 forward and FC1 input gradient (768,3072), QKV input gradient (768,2304), the token-0 layer's K|V
@@ -162,9 +162,9 @@ _BLASLT = {tuple(int(v) for v in t.split(',')) for t in
            os.environ.get('CMHAR_BLASLT', '768,768;768,3072;768,2304;768,1536').split(';') if t.strip()}
 
 
-def _blaslt_route(layout, M, N, K, out, bias, residual, aux_in, aux_out, rowadd, act, alpha, beta, splits, pdrop,
+def _blaslt_route(layout, M, N, K, a, out, bias, residual, aux_in, aux_out, rowadd, act, alpha, beta, splits, pdrop,
                   rowsum, colscale, reduce_stream):
-    if not _BLASLT or layout != 0 or (N, K) not in _BLASLT or M < 4096 or out.dtype != torch.bfloat16:
+    if not _BLASLT or layout != 0 or (N, K) not in _BLASLT or M < 4096 or out.dtype != a.dtype:
         return False
     if (aux_in is not None or aux_out is not None or rowadd is not None or act != L.ACT_NONE or alpha != 1.0 or
             beta != 0.0 or splits is not None or pdrop > 0.0 or rowsum is not None or colscale is not None or
@@ -236,6 +236,15 @@ def gemm(layout: int, a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, *, bi
     epi = L.epilogue(bias, residual, aux_in, aux_out, rowadd, rowadd_mod, act, alpha, beta, pdrop, seed, rowsum,
                      rowsum_beta, colscale)
     st = L.stream(out.device)
+    if a.dtype in (torch.bfloat16, torch.float16) and _blaslt_route(layout, M, N, K, a, out, bias, residual, aux_in,
+                                                                     aux_out, rowadd, act, alpha, beta, splits, pdrop,
+                                                                     rowsum, colscale, reduce_stream):
+        ev = TRACE.begin('hipblaslt_linear') if TRACE.active else None
+        call('cmhar_blaslt_linear', L.dtype_code(a.dtype), M, N, K, ptr(a), a.stride(0), ptr(b), b.stride(0), ptr(out),
+             out.stride(0), ptr(bias), ptr(residual), residual.stride(0) if residual is not None else 0, st)
+        extra = out.element_size() * M * N if residual is not None else 0
+        TRACE.end(ev, 'hipblaslt_linear', 2 * M * N * K, 2 * (M * K + N * K) + out.element_size() * M * N + extra)
+        return out
     if a.dtype == torch.float16:
         # fp16 inference path (BASELINE config 5): the bf16 kernels on the fp16 MFMA, forward layout only
         if layout != 0 or rowsum is not None:
@@ -254,14 +263,6 @@ def gemm(layout: int, a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, *, bi
                 ws = workspace(n, out.device)
         call('cmhar_gemm_f16', layout, L.dtype_code(out.dtype), M, N, K, ptr(a), a.stride(0), ptr(b), b.stride(0),
              ptr(out), out.stride(0), C.byref(epi), s, ptr(ws), st)
-        return out
-    if a.dtype == torch.bfloat16 and _blaslt_route(layout, M, N, K, out, bias, residual, aux_in, aux_out, rowadd, act,
-                                                   alpha, beta, splits, pdrop, rowsum, colscale, reduce_stream):
-        ev = TRACE.begin('hipblaslt_linear') if TRACE.active else None
-        call('cmhar_blaslt_linear', M, N, K, ptr(a), a.stride(0), ptr(b), b.stride(0), ptr(out), out.stride(0),
-             ptr(bias), ptr(residual), residual.stride(0) if residual is not None else 0, st)
-        extra = out.element_size() * M * N if residual is not None else 0
-        TRACE.end(ev, 'hipblaslt_linear', 2 * M * N * K, 2 * (M * K + N * K) + out.element_size() * M * N + extra)
         return out
     if a.dtype == torch.bfloat16:
         _check_bf16_operand(a, 'A')

@@ -1,4 +1,4 @@
-// hipBLASLt for plain library GEMMs: out[M,N] (bf16) = A[M,K]·B[N,K]ᵀ (+ fp32 bias per column) (+ bf16 residual),
+// hipBLASLt for plain library GEMMs: out[M,N] (bf16 / fp16) = A[M,K]·B[N,K]ᵀ (+ fp32 bias per column) (+ bf16 residual),
 // fp32 accumulation.  Used where the vendor's stream-K kernel beats the hand-written 8-phase one — the N = 768,
 // K = 768 shapes (VideoMAE attention output projection forward and its input gradient on Wᵀ), where 588 tiles of
 // 256² fall on 256 CUs as 2.3 rounds and the vendor kernel runs 196 workgroups of exactly 3 tiles (DESIGN.md,
@@ -24,7 +24,7 @@ struct LtDev {
   hipblasLtHandle_t handle = nullptr;
   size_t ws_bytes = LT_WS_BYTES;
   std::map<hipStream_t, void*> ws;   // one workspace per stream: launches on two streams may run concurrently
-  std::map<std::tuple<int, int, int, long, long, long, long, int>, LtPlan> plans;
+  std::map<std::tuple<int, int, int, long, long, long, long, int, int>, LtPlan> plans;
 };
 
 std::mutex g_lt_mu;
@@ -53,8 +53,9 @@ void* lt_ws(LtDev* d, hipStream_t st) {
 
 // Column-major view: Dᵀ[N, M] = op_T(B as col-major [K, N]) · (A as col-major [K, M]); the bias (length N = rows of
 // Dᵀ) is the per-output-feature bias of the row-major product.
-LtPlan* lt_plan(LtDev* d, int M, int N, int K, long lda, long ldb, long ldr, long ldo, int epi) {
-  const auto key = std::make_tuple(M, N, K, lda, ldb, ldr, ldo, epi);
+LtPlan* lt_plan(LtDev* d, int dtype, int M, int N, int K, long lda, long ldb, long ldr, long ldo, int epi) {
+  const auto key = std::make_tuple(M, N, K, lda, ldb, ldr, ldo, epi, dtype);
+  const hipDataType dt = dtype == CMHAR_F16 ? HIP_R_16F : HIP_R_16BF;
   auto it = d->plans.find(key);
   if (it != d->plans.end()) return &it->second;
   LtPlan p;
@@ -68,10 +69,10 @@ LtPlan* lt_plan(LtDev* d, int M, int N, int K, long lda, long ldb, long ldr, lon
     ok = hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_EPILOGUE, &e, sizeof(e)) == HIPBLAS_STATUS_SUCCESS &&
          hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_BIAS_DATA_TYPE, &bt, sizeof(bt)) == HIPBLAS_STATUS_SUCCESS;
   }
-  ok = ok && hipblasLtMatrixLayoutCreate(&p.la, HIP_R_16BF, K, N, ldb) == HIPBLAS_STATUS_SUCCESS;
-  ok = ok && hipblasLtMatrixLayoutCreate(&p.lb, HIP_R_16BF, K, M, lda) == HIPBLAS_STATUS_SUCCESS;
-  ok = ok && hipblasLtMatrixLayoutCreate(&p.lc, HIP_R_16BF, N, M, (epi & 2) ? ldr : ldo) == HIPBLAS_STATUS_SUCCESS;
-  ok = ok && hipblasLtMatrixLayoutCreate(&p.ld, HIP_R_16BF, N, M, ldo) == HIPBLAS_STATUS_SUCCESS;
+  ok = ok && hipblasLtMatrixLayoutCreate(&p.la, dt, K, N, ldb) == HIPBLAS_STATUS_SUCCESS;
+  ok = ok && hipblasLtMatrixLayoutCreate(&p.lb, dt, K, M, lda) == HIPBLAS_STATUS_SUCCESS;
+  ok = ok && hipblasLtMatrixLayoutCreate(&p.lc, dt, N, M, (epi & 2) ? ldr : ldo) == HIPBLAS_STATUS_SUCCESS;
+  ok = ok && hipblasLtMatrixLayoutCreate(&p.ld, dt, N, M, ldo) == HIPBLAS_STATUS_SUCCESS;
   hipblasLtMatmulPreference_t pref = nullptr;
   ok = ok && hipblasLtMatmulPreferenceCreate(&pref) == HIPBLAS_STATUS_SUCCESS;
   const uint64_t wsb = d->ws_bytes;
@@ -94,15 +95,16 @@ LtPlan* lt_plan(LtDev* d, int M, int N, int K, long lda, long ldb, long ldr, lon
 
 }  // namespace
 
-extern "C" int cmhar_blaslt_linear(int M, int N, int K, const void* A, long lda, const void* B, long ldb, void* out,
+extern "C" int cmhar_blaslt_linear(int dtype, int M, int N, int K, const void* A, long lda, const void* B, long ldb, void* out,
                                    long ldo, const float* bias, const void* residual, long ldr, hipStream_t st) {
+  if (dtype != CMHAR_BF16 && dtype != CMHAR_F16) return 7;
   if (M <= 0 || N <= 0 || K <= 0) return 0;
   if (!A || !B || !out || lda < K || ldb < K || ldo < N || (residual && ldr < N)) return 1;
   std::lock_guard<std::mutex> lock(g_lt_mu);
   LtDev* d = lt_dev();
   if (!d) return 2;
   const int epi = (bias ? 1 : 0) | (residual ? 2 : 0);
-  LtPlan* p = lt_plan(d, M, N, K, lda, ldb, residual ? ldr : 0, ldo, epi);
+  LtPlan* p = lt_plan(d, dtype, M, N, K, lda, ldb, residual ? ldr : 0, ldo, epi);
   if (!p) return 3;
   void* ws = p->ws ? lt_ws(d, st) : nullptr;
   if (p->ws && !ws) return 6;
@@ -118,10 +120,11 @@ extern "C" int cmhar_blaslt_linear(int M, int N, int K, const void* A, long lda,
 }
 
 // 1 when the library finds an algorithm for this shape / epilogue (plans it on the current device), else 0.
-extern "C" int cmhar_blaslt_linear_ok(int M, int N, int K, long lda, long ldb, long ldo, int has_bias, int has_residual,
+extern "C" int cmhar_blaslt_linear_ok(int dtype, int M, int N, int K, long lda, long ldb, long ldo, int has_bias, int has_residual,
                                       long ldr) {
   std::lock_guard<std::mutex> lock(g_lt_mu);
   LtDev* d = lt_dev();
   if (!d) return 0;
-  return lt_plan(d, M, N, K, lda, ldb, has_residual ? ldr : 0, ldo, (has_bias ? 1 : 0) | (has_residual ? 2 : 0)) ? 1 : 0;
+  if (dtype != CMHAR_BF16 && dtype != CMHAR_F16) return 0;
+  return lt_plan(d, dtype, M, N, K, lda, ldb, has_residual ? ldr : 0, ldo, (has_bias ? 1 : 0) | (has_residual ? 2 : 0)) ? 1 : 0;
 }

@@ -410,12 +410,13 @@ int cmhar_mfma_peak_probe(int shape, int blocks, int iters, const void* ops, int
 
 /* ---- plain library GEMMs on hipBLASLt (replaces: the VideoMAE attention output projection `nn.Linear`,
  * modeling_videomae.py VideoMAESelfOutput.dense, and its input gradient; reached from models.py:199).
- * out[M,N] (bf16) = A[M,K]·B[N,K]ᵀ (+ bias[N] fp32) (+ residual[M,N] bf16), fp32 accumulation; row-major operands
+ * out[M,N] = A[M,K]·B[N,K]ᵀ (+ bias[N] fp32) (+ residual[M,N]), fp32 accumulation, dtype CMHAR_BF16 or CMHAR_F16
+ * (operands, residual and output); row-major operands
  * with leading dimensions lda / ldb / ldo / ldr (elements).  Plans (descriptor, layouts, heuristic algorithm) are
  * cached per shape and epilogue; a 128-MiB workspace per (device, stream), allocated on first use.  _ok: 1 when hipBLASLt has an algorithm for it. */
-int cmhar_blaslt_linear(int M, int N, int K, const void* A, long lda, const void* B, long ldb, void* out, long ldo,
+int cmhar_blaslt_linear(int dtype, int M, int N, int K, const void* A, long lda, const void* B, long ldb, void* out, long ldo,
                         const float* bias, const void* residual, long ldr, hipStream_t stream);
-int cmhar_blaslt_linear_ok(int M, int N, int K, long lda, long ldb, long ldo, int has_bias, int has_residual, long ldr);
+int cmhar_blaslt_linear_ok(int dtype, int M, int N, int K, long lda, long ldb, long ldo, int has_bias, int has_residual, long ldr);
 
 #ifdef __cplusplus
 }

@@ -26,7 +26,7 @@ def L():
 
 
 def blaslt(a, b, out, bias=None, residual=None):
-    L().call('cmhar_blaslt_linear', a.shape[0], b.shape[0], a.shape[1], a.data_ptr(), a.stride(0), b.data_ptr(),
+    L().call('cmhar_blaslt_linear', L().dtype_code(a.dtype), a.shape[0], b.shape[0], a.shape[1], a.data_ptr(), a.stride(0), b.data_ptr(),
              b.stride(0), out.data_ptr(), out.stride(0), L().ptr(bias), L().ptr(residual),
              residual.stride(0) if residual is not None else 0, L().stream())
     return out
@@ -129,12 +129,37 @@ def test_default_routing_list():
     saved = set(k._BLASLT)
     k._BLASLT.add((768, 768))
     try:
-        assert k._blaslt_route(0, 8192, 768, 768, act=k.L.ACT_NONE, **args)
-        assert not k._blaslt_route(0, 8192, 768, 768, act=k.L.ACT_GELU, **args)
-        assert not k._blaslt_route(1, 8192, 768, 768, act=k.L.ACT_NONE, **args)
-        assert not k._blaslt_route(0, 1024, 768, 768, act=k.L.ACT_NONE, **args)
+        a = torch.empty(8192, 768, dtype=torch.bfloat16, device=DEV)
+        assert k._blaslt_route(0, 8192, 768, 768, a, act=k.L.ACT_NONE, **args)
+        assert not k._blaslt_route(0, 8192, 768, 768, a, act=k.L.ACT_GELU, **args)
+        assert not k._blaslt_route(1, 8192, 768, 768, a, act=k.L.ACT_NONE, **args)
+        assert not k._blaslt_route(0, 1024, 768, 768, a, act=k.L.ACT_NONE, **args)
+        assert not k._blaslt_route(0, 8192, 768, 768, a.half(), act=k.L.ACT_NONE, **args)   # out bf16, A fp16
         args['rowadd'] = torch.zeros(1, 768, device=DEV)
-        assert not k._blaslt_route(0, 8192, 768, 768, act=k.L.ACT_NONE, **args)
+        assert not k._blaslt_route(0, 8192, 768, 768, a, act=k.L.ACT_NONE, **args)
     finally:
         k._BLASLT.clear()
         k._BLASLT.update(saved)
+
+
+@pytest.mark.parametrize('use_bias,use_res', [(True, True), (False, False)])
+def test_blaslt_linear_fp16(use_bias, use_res):
+    """fp16 operands / output (the config-5 inference path's N = 768 launches): integer operands bit-exact vs fp64,
+    random operands ≤ 1e-3 relative vs fp32 (fp16 output rounding, 2^-11)."""
+    M, N, Kd = 50176, 768, 768
+    g = torch.Generator(device=DEV).manual_seed(11)
+    a = torch.randint(-4, 5, (M, Kd), generator=g, device=DEV).half()
+    b = torch.randint(-4, 5, (N, Kd), generator=g, device=DEV).half()
+    bias = torch.randint(-64, 65, (N,), generator=g, device=DEV).float() if use_bias else None
+    res = torch.randint(-64, 65, (M, N), generator=g, device=DEV).half() if use_res else None
+    out = blaslt(a, b, torch.empty(M, N, dtype=torch.float16, device=DEV), bias, res)
+    torch.cuda.synchronize()
+    assert torch.equal(out, ref64(a, b, bias, res).half())
+    a = (torch.randn(M, Kd, generator=g, device=DEV) * 0.5).half()
+    b = (torch.randn(N, Kd, generator=g, device=DEV) / Kd ** 0.5).half()
+    if use_res:
+        res = torch.randn(M, N, generator=g, device=DEV).half()
+    out = blaslt(a, b, torch.empty(M, N, dtype=torch.float16, device=DEV), bias, res)
+    torch.cuda.synchronize()
+    ref = a.float() @ b.float().t() + (bias if bias is not None else 0) + (res.float() if res is not None else 0)
+    assert ((out.float() - ref).norm() / ref.norm()).item() <= 1e-3
