@@ -162,15 +162,27 @@ _BLASLT = {tuple(int(v) for v in t.split(',')) for t in
            os.environ.get('CMHAR_BLASLT', '768,768;768,3072;768,2304;768,1536').split(';') if t.strip()}
 
 
-def _blaslt_route(layout, M, N, K, a, out, bias, residual, aux_in, aux_out, rowadd, act, alpha, beta, splits, pdrop,
-                  rowsum, colscale, reduce_stream):
+_BLASLT_OK = {}
+
+
+def _blaslt_route(layout, M, N, K, a, b, out, bias, residual, aux_in, aux_out, rowadd, act, alpha, beta, splits,
+                  pdrop, rowsum, colscale, reduce_stream):
     if not _BLASLT or layout != 0 or (N, K) not in _BLASLT or M < 4096 or out.dtype != a.dtype:
         return False
     if (aux_in is not None or aux_out is not None or rowadd is not None or act != L.ACT_NONE or alpha != 1.0 or
             beta != 0.0 or splits is not None or pdrop > 0.0 or rowsum is not None or colscale is not None or
             reduce_stream is not None):
         return False
-    return residual is None or residual.stride(1) == 1
+    if residual is not None and residual.stride(1) != 1:
+        return False
+    # the library must have an algorithm for this exact call (planned once per shape / strides / epilogue); where it
+    # has none the hand-written kernels take the call
+    key = (L.dtype_code(a.dtype), M, N, K, a.stride(0), b.stride(0), out.stride(0), bias is not None,
+           residual is not None, residual.stride(0) if residual is not None else 0)
+    ok = _BLASLT_OK.get(key)
+    if ok is None:
+        ok = _BLASLT_OK[key] = bool(L.lib().cmhar_blaslt_linear_ok(*key[:7], int(key[7]), int(key[8]), key[9]))
+    return ok
 
 
 def _tail_ws(M, N, K):
@@ -236,7 +248,7 @@ def gemm(layout: int, a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, *, bi
     epi = L.epilogue(bias, residual, aux_in, aux_out, rowadd, rowadd_mod, act, alpha, beta, pdrop, seed, rowsum,
                      rowsum_beta, colscale)
     st = L.stream(out.device)
-    if a.dtype in (torch.bfloat16, torch.float16) and _blaslt_route(layout, M, N, K, a, out, bias, residual, aux_in,
+    if a.dtype in (torch.bfloat16, torch.float16) and _blaslt_route(layout, M, N, K, a, b, out, bias, residual, aux_in,
                                                                      aux_out, rowadd, act, alpha, beta, splits, pdrop,
                                                                      rowsum, colscale, reduce_stream):
         ev = TRACE.begin('hipblaslt_linear') if TRACE.active else None

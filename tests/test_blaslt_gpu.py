@@ -26,8 +26,8 @@ def L():
 
 
 def blaslt(a, b, out, bias=None, residual=None):
-    L().call('cmhar_blaslt_linear', L().dtype_code(a.dtype), a.shape[0], b.shape[0], a.shape[1], a.data_ptr(), a.stride(0), b.data_ptr(),
-             b.stride(0), out.data_ptr(), out.stride(0), L().ptr(bias), L().ptr(residual),
+    L().call('cmhar_blaslt_linear', L().dtype_code(a.dtype), a.shape[0], b.shape[0], a.shape[1], a.data_ptr(),
+             a.stride(0), b.data_ptr(), b.stride(0), out.data_ptr(), out.stride(0), L().ptr(bias), L().ptr(residual),
              residual.stride(0) if residual is not None else 0, L().stream())
     return out
 
@@ -130,13 +130,15 @@ def test_default_routing_list():
     k._BLASLT.add((768, 768))
     try:
         a = torch.empty(8192, 768, dtype=torch.bfloat16, device=DEV)
-        assert k._blaslt_route(0, 8192, 768, 768, a, act=k.L.ACT_NONE, **args)
-        assert not k._blaslt_route(0, 8192, 768, 768, a, act=k.L.ACT_GELU, **args)
-        assert not k._blaslt_route(1, 8192, 768, 768, a, act=k.L.ACT_NONE, **args)
-        assert not k._blaslt_route(0, 1024, 768, 768, a, act=k.L.ACT_NONE, **args)
-        assert not k._blaslt_route(0, 8192, 768, 768, a.half(), act=k.L.ACT_NONE, **args)   # out bf16, A fp16
+        w = torch.empty(768, 768, dtype=torch.bfloat16, device=DEV)
+        assert k._blaslt_route(0, 8192, 768, 768, a, w, act=k.L.ACT_NONE, **args)
+        assert not k._blaslt_route(0, 8192, 768, 768, a, w, act=k.L.ACT_GELU, **args)
+        assert not k._blaslt_route(1, 8192, 768, 768, a, w, act=k.L.ACT_NONE, **args)
+        assert not k._blaslt_route(0, 1024, 768, 768, a, w, act=k.L.ACT_NONE, **args)
+        # out bf16, A fp16
+        assert not k._blaslt_route(0, 8192, 768, 768, a.half(), w.half(), act=k.L.ACT_NONE, **args)
         args['rowadd'] = torch.zeros(1, 768, device=DEV)
-        assert not k._blaslt_route(0, 8192, 768, 768, a, act=k.L.ACT_NONE, **args)
+        assert not k._blaslt_route(0, 8192, 768, 768, a, w, act=k.L.ACT_NONE, **args)
     finally:
         k._BLASLT.clear()
         k._BLASLT.update(saved)
